@@ -1,0 +1,108 @@
+/*
+ * patmatch_hip.h -- C ABI of the MI355X PatMatch scan engine (libpatmatch_hip.so).
+ *
+ * The reference's only boundary on this path is a process boundary: the
+ * Flask service shells out to the prebuilt nrgrep_coords binary
+ *     nrgrep_coords -i -b 1600000 -k <k><ids> '<nrgrep pattern>' '<datafile>'
+ * (www/FlaskApp/FlaskApp/patmatch.py:733-742 for run_patmatch and :818-828
+ * for run_test) and parses its "[beg, end]: <match>" lines (:505-516).
+ * The entry points below replace that binary.  Pattern compilation (PatMatch
+ * syntax -> nrgrep syntax -> position automaton -> per-character bitmasks)
+ * stays on the host (patmatchdocker_amd/convert.py, regex.py); this library
+ * owns the device-resident sequence database and the scan kernels.
+ *
+ * Conventions: every function returns 0 on success and a negative PM_E_*
+ * code on failure; pm_last_error() then describes the failure (per thread).
+ * Positions are 0-based byte offsets into the FASTA file that was loaded,
+ * "end" is exclusive -- the same numbers nrgrep_coords prints.
+ * No function takes or returns framework (torch) types.
+ */
+#ifndef PATMATCH_HIP_H
+#define PATMATCH_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_OK 0
+#define PM_E_ARG (-1)      /* bad argument / unsupported shape            */
+#define PM_E_HIP (-2)      /* HIP runtime error                           */
+#define PM_E_NODEV (-3)    /* no usable GPU                               */
+#define PM_E_UNSUPPORTED (-4)
+
+#define PM_ALPHA_NUC 0     /* 2-bit A/C/G/T planes + sparse exceptions    */
+#define PM_ALPHA_BYTE 1    /* one folded byte per residue (peptides)      */
+
+#define PM_MAX_POSITIONS 64
+#define PM_MAX_K 3         /* substitutions handled by the GPU kernels    */
+
+typedef struct pm_db pm_db;        /* device-resident sequence database   */
+typedef struct pm_hits pm_hits;    /* device/host hit list of one scan    */
+
+const char* pm_last_error(void);
+const char* pm_version(void);
+int pm_device_count(int* count);
+
+/* --- database ----------------------------------------------------------
+ * Replaces nrgrep's per-call read of '<datafile>' (the file is uploaded once
+ * and stays in HBM).  `fasta` is the raw file content.  Header lines
+ * (/^>\S/, generate_sequence_index.pl:33) and '\n' become record breaks.
+ * `stream` is a hipStream_t (NULL = the library's own stream).          */
+int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device,
+                 void* stream, pm_db** out);
+/* Synthetic nucleotide database generated on the device: n_records records
+ * laid out like a FASTA file (">r%08u\n" header line, rec_len random bases,
+ * "\n"), bases from a counter-based hash of (seed, position).           */
+int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed,
+                           int device, void* stream, pm_db** out);
+int pm_db_destroy(pm_db* db);
+int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet,
+               uint64_t* n_exception_words, uint64_t* device_bytes);
+/* Decode positions [beg, beg+len) back to folded text (bench/debug). */
+int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
+
+/* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
+ * A batch of P linear patterns (sequences of classes, no ? * + |), matched
+ * with at most k substitutions.  The classes are numbered 0..n_classes-1:
+ *   class_acgt[c]     4-bit subset of {A,C,G,T} (bit0=A .. bit3=T)
+ *   class_bytes[8*c]  256-bit membership over folded bytes (for non-ACGT
+ *                     text bytes such as N)
+ *   class_is_any[c]   1 if the class is '.' (matches every non-break byte)
+ * pos_class[64*p + j] is the class of position j of pattern p, lengths[p]
+ * its length (1..64).  Hits are (pattern, beg) with end = beg + lengths[p].
+ * Replaces one nrgrep_coords run per pattern (per strand).              */
+int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths,
+                   const uint8_t* pos_class, int n_classes, const uint8_t* class_acgt,
+                   const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
+                   pm_hits** out);
+
+/* --- general patterns: Glushkov automaton (both alphabets) -------------
+ * m positions (1..64); byte_mask[256] = positions accepting each folded
+ * byte; follow[m] / first / last as produced by regex.py; max_len = the
+ * longest match (patterns with unbounded repetition are rejected with
+ * PM_E_UNSUPPORTED).  Reports, for every start with a match of <= k
+ * substitutions, the shortest end.  Hits carry pattern id `pattern_id`. */
+int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
+                uint64_t first, uint64_t last, int max_len, int k, int pattern_id,
+                pm_hits** out);
+
+/* --- hits --------------------------------------------------------------- */
+int pm_hits_count(const pm_hits* h, uint64_t* count);
+/* Copies hits sorted by (pattern, beg).  Any pointer may be NULL. */
+int pm_hits_copy(const pm_hits* h, int32_t* pattern, int64_t* beg, int64_t* end,
+                 uint64_t max_count);
+/* Milliseconds of the main scan kernel(s), measured with hipEvents on the
+ * stream the kernels were launched on. */
+int pm_hits_kernel_ms(const pm_hits* h, double* ms);
+int pm_hits_destroy(pm_hits* h);
+
+/* Raw device pointers of a hit list (uint64 keys = pattern<<48 | beg, and
+ * uint32 lengths), for a caller that gathers hits across GPUs itself.   */
+int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PATMATCH_HIP_H */

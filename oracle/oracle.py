@@ -1,0 +1,173 @@
+"""Python front-end of the CPU oracle.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module.  It wraps ``liboracle.so``
+(``pm_oracle.c``: per-start forward NFA simulation) and also carries a tiny
+pure-Python set-based restatement (``scan_py``) used to cross-check the C
+code on small inputs.  Parity of the scan against the reference binary is
+UNPINNED (``nrgrep_coords`` is prebuilt and cannot be run); the pattern
+converter and host logic are pinned by ``tests/golden``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+ERR_INS, ERR_DEL, ERR_SUB = 1, 2, 4
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "pm_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(build())
+        p64 = ctypes.POINTER(ctypes.c_int64)
+        pu64 = ctypes.POINTER(ctypes.c_uint64)
+        _LIB.pmo_scan.restype = ctypes.c_int64
+        _LIB.pmo_scan.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_uint64,
+                                  ctypes.c_uint64, pu64, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmo_index.restype = ctypes.c_int64
+        _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
+                                   ctypes.c_int64]
+    return _LIB
+
+
+def err_flags(types: str) -> int:
+    return (ERR_INS if "i" in types else 0) | (ERR_DEL if "d" in types else 0) | \
+           (ERR_SUB if "s" in types else 0)
+
+
+def header_spans(text: bytes):
+    """[beg, end) of every header line (/^>\\S/, generate_sequence_index.pl:33)."""
+    spans = []
+    for off, name in record_index(text):
+        if name.startswith(">"):
+            nl = text.find(b"\n", off)
+            spans.append((off, len(text) if nl < 0 else nl))
+    return spans
+
+
+def drop_header_hits(text: bytes, hits):
+    """Remove hits starting inside a header line: process_output discards them
+    (patmatch.py:548-550, records whose name starts with '>')."""
+    spans = header_spans(text)
+    if not spans:
+        return hits
+    import bisect
+    starts = [b for b, _ in spans]
+    out = []
+    for beg, end in hits:
+        i = bisect.bisect_right(starts, beg) - 1
+        if i >= 0 and spans[i][0] <= beg < spans[i][1]:
+            continue
+        out.append((beg, end))
+    return out
+
+
+def scan(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False):
+    """All (beg, end) hits of compiled program ``prog`` in ``text`` (what
+    nrgrep_coords prints); ``skip_headers`` drops the header-line hits that
+    the reference's process_output throws away."""
+    L = lib()
+    B = np.array(prog.byte_masks(), dtype=np.uint64)
+    F = np.array(prog.follow + [0], dtype=np.uint64)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = L.pmo_scan(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                       prog.first, prog.last, F.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                       prog.m, k, err_flags(types) if k else 0, 1 if prog.ignore_case else 0,
+                       beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                       end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("oracle rejected k=%d" % k)
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+def record_index(text: bytes):
+    """generate_sequence_index.pl restated: [(offset, name)] in file order."""
+    L = lib()
+    cap = max(16, text.count(b">") + 1)
+    arrs = [np.empty(cap, dtype=np.int64) for _ in range(4)]
+    n = L.pmo_index(text, len(text), *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) for a in arrs], cap)
+    out = []
+    hdr, data, nb, nl = (a[:n].tolist() for a in arrs)
+    for h, d, b, ln in zip(hdr, data, nb, nl):
+        name = text[b:b + ln].decode("latin-1")
+        out.append((h, ">" + name))
+        out.append((d, name))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# pure-Python restatement (explicit (position, errors) state sets), small n
+# ---------------------------------------------------------------------------
+
+def scan_py(text: bytes, prog, k: int = 0, types: str = "ids"):
+    types = types if k else ""
+    fold = (lambda c: c - 32 if 97 <= c <= 122 else c) if prog.ignore_case else (lambda c: c)
+    START = -1
+
+    def succ(state):
+        if state == START:
+            return [i for i in range(prog.m) if prog.first >> i & 1]
+        return [i for i in range(prog.m) if prog.follow[state] >> i & 1]
+
+    def closure(states):
+        out, todo = dict(states), list(states.items())
+        while todo:
+            st, e = todo.pop()
+            if "d" in types and e < k:
+                for nx in succ(st):
+                    if out.get(nx, k + 1) > e + 1:
+                        out[nx] = e + 1
+                        todo.append((nx, e + 1))
+        return out
+
+    hits = []
+    pos = 0
+    for line in text.split(b"\n"):
+        for s in range(len(line)):
+            cur = closure({START: 0})
+            for p in range(s, len(line)):
+                c = fold(line[p])
+                nxt = {}
+
+                def put(st, e):
+                    if e <= k and nxt.get(st, k + 1) > e:
+                        nxt[st] = e
+                for st, e in cur.items():
+                    for nx in succ(st):
+                        if c in prog.classes[nx]:
+                            put(nx, e)
+                        elif "s" in types:
+                            put(nx, e + 1)
+                    if "i" in types:
+                        put(st, e + 1)
+                cur = closure(nxt)
+                if any(st != START and prog.last >> st & 1 for st in cur):
+                    hits.append((pos + s, pos + p + 1))
+                    break
+                if not cur:
+                    break
+        pos += len(line) + 1
+    return hits

@@ -1,0 +1,253 @@
+"""Scan-pipeline dispatch: compiled patterns -> HIP kernels -> hits.
+
+This is the host half of the replacement for one or more
+``nrgrep_coords -i -b .. -k <k><types> '<pattern>' '<datafile>'`` runs
+(``www/FlaskApp/FlaskApp/patmatch.py:733-742``).  A
+:class:`SequenceDatabase` uploads a FASTA file into HBM once; :func:`scan`
+routes every compiled :class:`~patmatchdocker_amd.regex.Program` to a kernel:
+
+* ``linear`` -- fixed-length class sequences on a nucleotide database go to
+  the bit-sliced Hamming kernel (``pm_scan_linear``), all strands/patterns of
+  a query in ONE pass over the data;
+* ``nfa``    -- everything else with a bounded match length goes to the
+  Glushkov reverse-scan + verify kernels (``pm_scan_nfa``).
+
+Anything else (insertions/deletions with k > 0, unbounded ``*``/``+``,
+more than 64 positions, k > 3) raises :class:`UnsupportedOnGPU`; there is
+no CPU fallback by design.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import UnsupportedOnGPU, check
+from .regex import ALL_BYTES, Program, fold_byte
+
+ANY_FOLDED = frozenset(fold_byte(b) for b in ALL_BYTES)
+_ACGT = tuple(ord(c) for c in "ACGT")
+
+NUC = "nuc"
+BYTE = "byte"
+
+
+def choose_alphabet(data: bytes, sample: int = 1 << 22) -> str:
+    """Nucleotide planes when >= 90 % of the sampled sequence bytes are ACGTN."""
+    head = data[:sample]
+    seq = bytearray()
+    for line in head.split(b"\n"):
+        if not line.startswith(b">"):
+            seq += line
+    if not seq:
+        return NUC
+    arr = np.frombuffer(bytes(seq), dtype=np.uint8)
+    folded = np.where((arr >= 97) & (arr <= 122), arr - 32, arr)
+    good = np.isin(folded, np.frombuffer(b"ACGTN", dtype=np.uint8)).mean()
+    return NUC if good >= 0.9 else BYTE
+
+
+class SequenceDatabase:
+    """A FASTA file resident in the HBM of one GPU (``pm_db``)."""
+
+    def __init__(self, handle, alphabet: str, device: int, raw: Optional[bytes] = None):
+        self._h = handle
+        self.alphabet = alphabet
+        self.device = device
+        self.raw = raw
+
+    @classmethod
+    def from_bytes(cls, data: bytes, alphabet: Optional[str] = None, device: int = 0,
+                   stream: Optional[int] = None) -> "SequenceDatabase":
+        lib = _lib.load()
+        alphabet = alphabet or choose_alphabet(data)
+        code = _lib.PM_ALPHA_NUC if alphabet == NUC else _lib.PM_ALPHA_BYTE
+        h = ctypes.c_void_p()
+        check(lib.pm_db_create(data, len(data), code, device, stream, ctypes.byref(h)))
+        return cls(h, alphabet, device, raw=data)
+
+    @classmethod
+    def from_file(cls, path: str, alphabet: Optional[str] = None, device: int = 0) -> "SequenceDatabase":
+        with open(path, "rb") as fh:
+            return cls.from_bytes(fh.read(), alphabet, device)
+
+    @classmethod
+    def synthetic(cls, n_records: int, rec_len: int, seed: int = 1, device: int = 0,
+                  stream: Optional[int] = None) -> "SequenceDatabase":
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(lib.pm_db_create_synthetic(n_records, rec_len, seed, device, stream, ctypes.byref(h)))
+        return cls(h, NUC, device, raw=None)
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise ValueError("database closed")
+        return self._h
+
+    def info(self):
+        n, alpha, nx, nbytes = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.load().pm_db_info(self.handle, ctypes.byref(n), ctypes.byref(alpha), ctypes.byref(nx),
+                                     ctypes.byref(nbytes)))
+        return {"positions": n.value, "alphabet": NUC if alpha.value == 0 else BYTE,
+                "exception_words": nx.value, "device_bytes": nbytes.value}
+
+    def __len__(self):
+        return self.info()["positions"]
+
+    def decode(self, beg: int, length: int) -> bytes:
+        buf = ctypes.create_string_buffer(max(length, 1))
+        check(_lib.load().pm_db_decode(self.handle, beg, length, buf))
+        return buf.raw[:length]
+
+    def text(self, beg: int, end: int) -> bytes:
+        """Original (not case-folded) bytes when the file is held, else decoded."""
+        if self.raw is not None:
+            return self.raw[beg:end]
+        return self.decode(beg, end - beg)
+
+    def close(self):
+        if self._h is not None:
+            check(_lib.load().pm_db_destroy(self._h))
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class Hits:
+    """Hits of one scan call, sorted by (pattern, beg)."""
+
+    pattern: np.ndarray
+    beg: np.ndarray
+    end: np.ndarray
+    kernel_ms: float
+
+    def for_pattern(self, i: int):
+        sel = self.pattern == i
+        return self.beg[sel], self.end[sel]
+
+
+def _collect(handle) -> Hits:
+    lib = _lib.load()
+    try:
+        n = ctypes.c_uint64()
+        check(lib.pm_hits_count(handle, ctypes.byref(n)))
+        count = n.value
+        pat = np.empty(count, dtype=np.int32)
+        beg = np.empty(count, dtype=np.int64)
+        end = np.empty(count, dtype=np.int64)
+        if count:
+            check(lib.pm_hits_copy(handle, pat.ctypes.data, beg.ctypes.data, end.ctypes.data, count))
+        ms = ctypes.c_double()
+        check(lib.pm_hits_kernel_ms(handle, ctypes.byref(ms)))
+        return Hits(pat, beg, end, ms.value)
+    finally:
+        lib.pm_hits_destroy(handle)
+
+
+def parse_error_types(k: int, types: str) -> str:
+    return types if k else ""
+
+
+def route(prog: Program, alphabet: str, k: int, types: str) -> str:
+    """Which kernel handles ``prog``; raises UnsupportedOnGPU if none does."""
+    if k > _lib.PM_MAX_K:
+        raise UnsupportedOnGPU("k=%d > %d errors is not supported by the GPU kernels" % (k, _lib.PM_MAX_K))
+    if k and ("i" in types or "d" in types):
+        raise UnsupportedOnGPU("insertions/deletions (-k %d%s) are not supported by the GPU kernels yet"
+                               % (k, types))
+    if prog.m > 64:
+        raise UnsupportedOnGPU("patterns longer than 64 positions are not supported")
+    if prog.linear and alphabet == NUC:
+        return "linear"
+    if prog.max_len is None:
+        raise UnsupportedOnGPU("unbounded repetition (* or +) is not supported by the GPU scan yet")
+    if prog.max_len > 1024:
+        raise UnsupportedOnGPU("match length bound above 1024")
+    return "nfa"
+
+
+def _linear_tables(progs: Sequence[Program]):
+    classes, index = [], {}
+    pos_class = np.zeros((len(progs), 64), dtype=np.uint8)
+    lengths = np.zeros(len(progs), dtype=np.int32)
+    for p, prog in enumerate(progs):
+        lengths[p] = prog.m
+        for j, cls in enumerate(prog.classes):
+            if cls not in index:
+                index[cls] = len(classes)
+                classes.append(cls)
+            pos_class[p, j] = index[cls]
+    nc = len(classes)
+    acgt = np.zeros(nc, dtype=np.uint8)
+    is_any = np.zeros(nc, dtype=np.uint8)
+    bits = np.zeros((nc, 8), dtype=np.uint32)
+    for c, cls in enumerate(classes):
+        acgt[c] = sum(1 << i for i, b in enumerate(_ACGT) if b in cls)
+        is_any[c] = 1 if ANY_FOLDED <= cls else 0
+        for b in cls:
+            bits[c, b >> 5] |= np.uint32(1 << (b & 31))
+    return lengths, pos_class, nc, acgt, bits, is_any
+
+
+def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int) -> Hits:
+    lengths, pos_class, nc, acgt, bits, is_any = _linear_tables(progs)
+    out = ctypes.c_void_p()
+    check(_lib.load().pm_scan_linear(db.handle, len(progs), lengths.ctypes.data, pos_class.ctypes.data, nc,
+                                     acgt.ctypes.data, bits.ctypes.data, is_any.ctypes.data, k,
+                                     ctypes.byref(out)))
+    return _collect(out)
+
+
+def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0) -> Hits:
+    bm = np.array(prog.byte_masks(), dtype=np.uint64)
+    fol = np.array(prog.follow, dtype=np.uint64)
+    out = ctypes.c_void_p()
+    check(_lib.load().pm_scan_nfa(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
+                                  prog.max_len, k, pattern_id, ctypes.byref(out)))
+    return _collect(out)
+
+
+def _same_automaton(a: Program, b: Program) -> bool:
+    return a.classes == b.classes and a.follow == b.follow and a.first == b.first and a.last == b.last
+
+
+def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str = "ids"):
+    """Scan all programs; returns ([(beg, end) arrays per program], kernel_ms).
+
+    Programs equal as automata (a palindromic site and its reverse
+    complement, e.g. GAATTC) are scanned once and their hits reported for
+    each of them, as the reference's two nrgrep runs would.
+    """
+    types = parse_error_types(k, types)
+    routes = [route(p, db.alphabet, k, types) for p in progs]
+    canonical: List[int] = []
+    for i, p in enumerate(progs):
+        twin = next((j for j in range(i) if canonical[j] == j and _same_automaton(progs[j], p)), None)
+        canonical.append(i if twin is None else twin)
+    results: List[Optional[tuple]] = [None] * len(progs)
+    total_ms = 0.0
+    linear_ids = [i for i in range(len(progs)) if routes[i] == "linear" and canonical[i] == i]
+    if linear_ids:
+        hits = scan_linear(db, [progs[i] for i in linear_ids], k)
+        total_ms += hits.kernel_ms
+        for slot, i in enumerate(linear_ids):
+            results[i] = hits.for_pattern(slot)
+    for i in range(len(progs)):
+        if routes[i] == "nfa" and canonical[i] == i:
+            hits = scan_nfa(db, progs[i], k, 0)
+            total_ms += hits.kernel_ms
+            results[i] = (hits.beg, hits.end)
+    for i in range(len(progs)):
+        if results[i] is None:
+            results[i] = results[canonical[i]]
+    return results, total_ms

@@ -1,0 +1,573 @@
+"""PatMatch service functions with the GPU scan in place of nrgrep_coords.
+
+Drop-in for the functions of ``www/FlaskApp/FlaskApp/patmatch.py`` that the
+Flask endpoint (``www/FlaskApp/FlaskApp/__init__.py:24-42``) calls: same
+names, same argument meaning, same return shapes and the same error
+behaviour.  What changes is underneath:
+
+* ``process_pattern`` converts in-process (:mod:`.convert`) instead of
+  ``os.popen('patmatch_to_nrgrep.pl ...')`` (patmatch.py:270-316);
+* the two ``os.popen('nrgrep_coords ...')`` searches (patmatch.py:731-743)
+  become ONE pass of :func:`search_output` over the HBM-resident database,
+  both strands fused, producing the identical "[beg, end]: match" text;
+* ``get_record_offset`` indexes the file in-process instead of running
+  ``generate_sequence_index.pl`` (patmatch.py:197-215).
+
+``process_output`` and the small helpers keep the reference's observable
+behaviour, quirks included (see DESIGN.md "Host logic"), because hits,
+counts and row order depend on them.  S3 upload and temp-file cleanup are
+kept as the reference's no-S3 behaviour (no network here).
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import re
+import threading
+import time
+import traceback
+from bisect import bisect_right
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import engine
+from .convert import convert
+from .regex import RegexSyntaxError, compile_pattern
+
+MAX_BUFFER_SIZE = 1600000
+MIN_TOKEN = 3
+MINHITS = 500
+MAXHITS = 100000
+DEFAULT_MAXHITS = 500
+
+dataDir = "/data/patmatch/"
+binDir = "/var/www/bin/"
+tmpDir = "/var/www/tmp/"
+config_dir = "/var/www/conf/"
+
+day = 1
+
+_NUC_BAD = ("E", "F", "I", "J", "L", "O", "P", "Q", "Z")
+
+
+def _set_dirs_for_test(root_dir, root_data_dir):
+    """patmatch.py:54-66 (test hook): bin/conf under root_dir, tmp = cwd."""
+    global binDir, tmpDir, config_dir, dataDir
+    root = root_dir.rstrip("/")
+    binDir, tmpDir, config_dir, dataDir = root + "/www/bin/", "./", root + "/www/conf/", root_data_dir
+
+
+# ---------------------------------------------------------------------------
+# database residency: one SequenceDatabase per data file, kept in HBM
+# ---------------------------------------------------------------------------
+
+class _DatabaseCache:
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._dbs: Dict[Tuple[str, int], tuple] = {}
+
+    def get(self, path: str, device: int = 0):
+        st = os.stat(path)
+        key = (os.path.realpath(path), device)
+        with self._lock:
+            hit = self._dbs.get(key)
+            if hit and hit[0] == (st.st_mtime_ns, st.st_size):
+                return hit[1]
+            if hit:
+                hit[1].close()
+            db = engine.SequenceDatabase.from_file(path, device=device)
+            self._dbs[key] = ((st.st_mtime_ns, st.st_size), db)
+            return db
+
+    def clear(self):
+        with self._lock:
+            for _, db in self._dbs.values():
+                db.close()
+            self._dbs.clear()
+
+
+DATABASES = _DatabaseCache()
+
+
+# ---------------------------------------------------------------------------
+# the scan (replaces the nrgrep_coords processes)
+# ---------------------------------------------------------------------------
+
+def parse_error_option(option: str) -> Tuple[int, str]:
+    """'-k' argument '<err>[idst]' -> (k, types); no letters = all of them."""
+    m = re.fullmatch(r"(\d+)([idst]*)", option or "0")
+    if not m:
+        raise ValueError("<num>[idst] expected after -k")
+    return int(m.group(1)), (m.group(2) or "idst")
+
+
+def _format_hits(db: engine.SequenceDatabase, beg, end) -> str:
+    raw = db.raw
+    lines = []
+    for b, e in zip(beg.tolist(), end.tolist()):
+        text = (raw[b:e] if raw is not None else db.decode(b, e - b)).decode("latin-1")
+        lines.append("[%d, %d]: %s\n" % (b, e, text))
+    return "".join(lines)
+
+
+def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[str]:
+    """nrgrep_coords output text for each pattern, from one GPU pass.
+
+    A pattern nrgrep would reject ("Syntax error in pattern") yields ''.
+    """
+    k, types = parse_error_option(option)
+    progs, slots = [], []
+    for i, pat in enumerate(patterns):
+        try:
+            progs.append(compile_pattern(pat, ignore_case=True))
+            slots.append(i)
+        except RegexSyntaxError:
+            continue
+    outputs = [""] * len(patterns)
+    if not progs:
+        return outputs
+    db = DATABASES.get(datafile)
+    results, _ = engine.scan(db, progs, k=k, types=types)
+    for slot, (beg, end) in zip(slots, results):
+        outputs[slot] = _format_hits(db, beg, end)
+    return outputs
+
+
+# ---------------------------------------------------------------------------
+# helpers (patmatch.py:69-400)
+# ---------------------------------------------------------------------------
+
+def set_download_file(filename):
+    from flask import send_from_directory
+    return send_from_directory(tmpDir, filename, as_attachment=True, mimetype="application/text",
+                               attachment_filename=str(filename))
+
+
+def clean_up_temp_files():
+    cutoff = time.time() - day * 86400
+    for name in os.listdir(tmpDir):
+        path = os.path.join(tmpDir, name)
+        if os.path.isfile(path) and os.stat(path).st_mtime < cutoff:
+            os.remove(path)
+
+
+def get_downloadUrl(tmpFile):
+    """patmatch.py:125-154 as it behaves without S3 configured: the result
+    file is renamed to <md5>.txt and the URL is ''.  (Uploading to S3 is the
+    deployment's concern and out of scope here.)"""
+    path = Path(tmpDir + tmpFile)
+    if not path.exists():
+        return ""
+    digest = hashlib.md5(path.read_bytes()).hexdigest()
+    if digest:
+        os.rename(str(path), tmpDir + digest + ".txt")
+    return ""
+
+
+def get_config(conf):
+    name = conf or "patmatch"
+    if not name.endswith(".json"):
+        name += ".json"
+    with open(config_dir + name, encoding="utf-8") as fh:
+        return json.loads("".join(line.strip() for line in fh))
+
+
+def get_record_offset(datafile):
+    """(offset list, offset->name) as generate_sequence_index.pl + patmatch.py:197-215."""
+    with open(datafile, "rb") as fh:
+        data = fh.read()
+    offsets: List[int] = []
+    names: Dict[int, str] = {}
+    for m in re.finditer(rb"^>([^ \t\n\r\f\v]+)[^\n]*(?:\n|$)", data, re.M):
+        name = m.group(1).decode("latin-1")
+        for off, nm in ((m.start(), ">" + name), (m.end(), name)):
+            offsets.append(off)
+            names[off] = nm
+    return offsets, names
+
+
+def get_name_offset(offSet, recordOffSetList):
+    """Greatest record offset <= offSet, by the reference's binary search
+    (patmatch.py:218-238); offsets below the first record map to the first."""
+    lo, hi = 0, len(recordOffSetList) - 1
+    while hi > lo:
+        mid = (lo + hi) // 2
+        value = recordOffSetList[mid]
+        if value == offSet:
+            return offSet
+        if hi - lo == 1:
+            return recordOffSetList[hi] if offSet >= recordOffSetList[hi] else recordOffSetList[lo]
+        if value < offSet:
+            lo = mid
+        else:
+            hi = mid - 1
+    return recordOffSetList[lo]
+
+
+def check_pattern(pattern, seqtype):
+    """patmatch.py:241-267: alphabet check and MIN_TOKEN residues."""
+    if seqtype in ("pep", "protein"):
+        if "u" in pattern.lower():
+            return "Invalid peptide character found in pattern."
+    elif any(ch in pattern.upper() for ch in _NUC_BAD):
+        return "Invalid nucleotide character found in pattern."
+    tokens, counting = 0, True
+    for ch in pattern:
+        if ch in "([{":
+            tokens += 1 if counting else 0
+            counting = False
+        elif ch in ")]}":
+            counting = True
+        elif counting:
+            tokens += 1
+    if "{" in pattern:
+        return ""
+    if tokens < MIN_TOKEN:
+        return "Your pattern is shorter than the minimum number of " + str(MIN_TOKEN) + " residues."
+    return ""
+
+
+def process_pattern(pattern, seqtype, strand, insertion, deletion, substitution, mismatch):
+    """patmatch.py:270-316 -> (nrgrep pattern, reverse-complement pattern, '-k' option)."""
+    if seqtype is None:
+        seqtype = "pep"
+    if seqtype in ("pep", "protein"):
+        mode = "-p"
+    elif strand and "complement" in strand.lower():
+        mode = "-c"
+    else:
+        mode = "-n"
+    converted = convert(mode, pattern)
+    comp = ""
+    if seqtype.lower() in ("dna", "nuc") and (strand is None or strand.startswith("Both")):
+        comp = convert("-c", converted)
+    kinds = ""
+    for value, letter, word in ((insertion, "i", "insertion"), (deletion, "d", "deletion"),
+                                (substitution, "s", "substitution")):
+        if value and value.startswith(word):
+            kinds += letter
+    return converted, comp, str(0 if mismatch is None else mismatch) + (kinds or "ids")
+
+
+def get_sequence(dataset, seqname):
+    """patmatch.py:319-348: the sequence of one record, by name prefix.  A
+    later header with the same prefix restarts the defline and keeps
+    appending (as the reference's loop does)."""
+    if ".seq" not in dataset:
+        dataset += ".seq"
+    if "patmatch" not in dataset:
+        dataset = dataDir + dataset
+    defline, chunks, found = "", [], False
+    want = ">" + seqname.lower()
+    with open(dataset, encoding="utf-8") as fh:
+        for line in fh:
+            line = line.strip()
+            if line.lower().startswith(want):
+                found, defline = True, line
+            elif found:
+                if line.startswith(">"):
+                    break
+                chunks.append(line)
+    return {"defline": defline.replace('"', "'"), "seq": "".join(chunks)}
+
+
+def get_param(request, name, default=None):
+    value = request.args.get(name)
+    if value is None:
+        value = request.form.get(name)
+    return default if value is None else value
+
+
+_URL_ESCAPES = (("%28", "("), ("%29", ")"), ("%7B", "{"), ("%7D", "}"), ("%5B", "["), ("%5D", "]"),
+                ("%2C", ","), ("%5E", "^"))
+
+
+def cleanup_pattern(pattern):
+    for esc, ch in _URL_ESCAPES:
+        pattern = pattern.replace(esc, ch)
+    return pattern
+
+
+def set_seq_length(seqNm2length, datafile):
+    """patmatch.py:374-400: record lengths (a trailing '*' stop not counted)."""
+    has_stop: Dict[str, bool] = {}
+
+    def close(name, seq):
+        name = name.rstrip(",")
+        has_stop[name] = seq.endswith("*")
+        seqNm2length[name] = len(seq) - (1 if has_stop[name] else 0)
+
+    name, parts = "", []
+    with open(datafile, encoding="utf-8") as fh:
+        for line in fh:
+            if line.startswith(">"):
+                if name != "":
+                    close(name, "".join(parts))
+                name = line.replace(">", "").split(" ")[0].rstrip(",")
+                parts = []
+            else:
+                parts.append(line.strip())
+    seq = "".join(parts)
+    if name and seq:
+        close(name, seq)
+    return has_stop
+
+
+_TOKEN_RE = re.compile(r"\[[^\]]+\]|.(?:[*+?]|\{\d*(?:,\d*)?\})?")
+
+
+def find_exclusion_offset(pattern):
+    """patmatch.py:403-446.  Brackets count one residue; a quantified atom
+    counts its minimum repeat; a bare single character counts nothing (the
+    reference only adds inside its quantifier branch, :444)."""
+    tokens = _TOKEN_RE.findall(pattern)
+    first_neg = next((i for i, tok in enumerate(tokens) if tok.startswith("[^")), None)
+    if first_neg is None:
+        return None
+    offset = 0
+    for tok in tokens[:first_neg]:
+        if tok.startswith("["):
+            offset += 1
+        elif len(tok) > 1:
+            quant = tok[1:]
+            if quant in ("*", "?"):
+                continue
+            if quant.startswith("{"):
+                low = quant.strip("{}").split(",")[0]
+                offset += int(low) if low else 0
+            else:
+                offset += 1
+    return offset
+
+
+def _parse_hit_line(line):
+    """'[beg, end]: match' -> (beg, end, match) exactly as patmatch.py:507-516."""
+    pieces = line.replace("[", "").replace("]", "").replace(":", "").replace(",", "").split(" ")
+    if len(pieces) < 3:
+        return None
+    return int(pieces[0]), int(pieces[1]), pieces[2]
+
+
+def _resolve_maxhits(maxhits):
+    if maxhits is None:
+        return DEFAULT_MAXHITS
+    if str(maxhits).isdigit():
+        return int(maxhits)
+    if str(maxhits).lower() in ("no limit", "no+limit"):
+        return MAXHITS
+    return DEFAULT_MAXHITS
+
+
+def _locus_table():
+    table = {}
+    with open(dataDir + "locus.txt", encoding="utf-8") as fh:
+        for line in fh:
+            cols = line.strip().split("\t")
+            table[cols[0]] = (cols[1], cols[2], cols[3] if len(cols) > 3 else "")
+    return table
+
+
+def _intergenic_tables(datafile):
+    chrom, orfs = {}, {}
+    with open(datafile, encoding="utf-8") as fh:
+        for line in fh:
+            if not line.startswith(">"):
+                continue
+            words = line.strip().replace(">", "").split(" ")
+            name = words[0].replace(",", "")
+            chrom[name] = words[2]
+            orfs[name] = line.strip().split("between ")[1].replace("and", "-")
+    return chrom, orfs
+
+
+def process_output(recordOffSetList, seqNm4offSet, output, datafile, maxhits, begMatch, endMatch,
+                   downloadFile, original_pattern):
+    """patmatch.py:449-674: hits text -> (rows, uniqueHits, totalHits, error_message)."""
+    lengths: Dict[str, int] = {}
+    if endMatch == 1:
+        set_seq_length(lengths, datafile)
+    exclusions = [(find_exclusion_offset(original_pattern[:m.start()]), set(m.group(1)))
+                  for m in re.finditer(r"\[\^([^\]]+)\]", original_pattern)]
+    locus = _locus_table() if "orf_" in datafile else {}
+    intergenic = "Not" in datafile
+    chrom, orfs = _intergenic_tables(datafile) if intergenic else ({}, {})
+    limit = _resolve_maxhits(maxhits)
+
+    rows: List[str] = []
+    total = unique = 0
+    per_seq: Dict[str, int] = {}
+    for line in output.split("\n"):
+        if not line.startswith("["):
+            continue
+        parsed = _parse_hit_line(line)
+        if parsed is None:
+            continue
+        beg, end, match = parsed
+        if any(pos is not None and pos < len(match) and match[pos] in chars for pos, chars in exclusions):
+            continue
+        off = get_name_offset(beg, recordOffSetList)
+        seq_beg, seq_end = beg - off + 1, end - off
+        name = seqNm4offSet.get(off)
+        if name is None:
+            continue
+        if begMatch == 1 and seq_beg != 1:
+            continue
+        if endMatch == 1 and lengths.get(name) != seq_end:
+            continue
+        if name.startswith(">"):
+            continue
+        if name.endswith(","):
+            name = name.rstrip(name[-1])
+        if intergenic:
+            parts = name.split(":")
+            if len(parts) < 2:
+                continue
+            shift = int(parts[1].split("-")[0]) - 1
+            seq_beg, seq_end = seq_beg + shift, seq_end + shift
+            if name not in chrom or name not in orfs:
+                continue
+            row = "\t".join((str(orfs.get(name)), str(seq_beg), str(seq_end), match, str(chrom.get(name)), name))
+        else:
+            gene, sgdid, desc = locus.get(name, ("", "", ""))
+            row = "\t".join((name, str(seq_beg), str(seq_end), match, gene, sgdid, desc))
+        if name not in per_seq:
+            unique += 1
+        if total >= limit:
+            break
+        per_seq[name] = per_seq.get(name, 0) + 1
+        total += 1
+        rows.append(row)
+
+    if intergenic:
+        header = "Chromosome\tBetweenORFtoORF\tHitNumber\tMatchPattern\tMatchStartCoord\tMatchStopCoord\n"
+    elif "orf_" in datafile:
+        header = "Feature Name\tGene Name\tHitNumber\tMatchPattern\tMatchStartCoord\tMatchStopCoord\tLocusInfo\n"
+    else:
+        header = "Sequence Name\tHitNumber\tMatchPattern\tMatchStartCoord\tMatchStopCoord\n"
+    lines = [header]
+    data = []
+    error_message = ""
+    rows.sort()
+    for row in rows:
+        try:
+            cols = row.split("\t")
+            if intergenic:
+                orf_span, b, e, pat, chrom_name, name = cols
+                count = per_seq[name]
+                data.append({"orfs": orf_span.strip(), "chr": chrom_name, "beg": b, "end": e, "count": count,
+                             "seqname": name, "matchingPattern": pat})
+                # the reference builds but never writes intergenic file rows
+            else:
+                name, b, e, pat, gene, sgdid, desc = cols
+                count = per_seq.get(name, 0)
+                if sgdid != "":
+                    if gene == name:
+                        gene = ""
+                    data.append({"seqname": name, "beg": b, "end": e, "count": count, "matchingPattern": pat,
+                                 "gene_name": gene, "sgdid": sgdid, "desc": desc})
+                    lines.append("\t".join((name, gene, str(count), pat, b, e, desc)) + "\n")
+                else:
+                    data.append({"seqname": name, "gene_name": gene, "sgdid": sgdid, "beg": b, "end": e,
+                                 "count": count, "matchingPattern": pat, "desc": desc})
+                    lines.append("\t".join((name, str(count), pat, b, e)) + "\n")
+        except MemoryError as exc:
+            error_message += "Memory Error: " + str(exc) + "\n"
+            break
+        except OSError as exc:
+            error_message += "OS Error: " + str(exc) + "\n"
+        except (IndexError, ValueError) as exc:
+            error_message += "Error processing row: " + str(row) + "error: " + str(exc) + "\n"
+        except Exception as exc:  # pragma: no cover - mirrors the reference
+            error_message += "Unexpected error for row: " + str(row) + "error: " + str(exc) + "\n"
+            error_message += "Traceback: " + str(traceback.format_exc()) + "\n"
+    try:
+        with open(downloadFile, "w", encoding="utf-8") as fw:
+            fw.writelines(lines)
+    except MemoryError as exc:
+        error_message += "Memory Error during file writing: " + str(exc) + "\n"
+    except OSError as exc:
+        error_message += "OS Error during file writing: " + str(exc) + "\n"
+    except UnicodeEncodeError as exc:
+        error_message += "Unicode Encoding Error: " + str(exc) + "\n"
+    except Exception as exc:  # pragma: no cover
+        error_message += "Error writing to file " + downloadFile + ":" + str(exc)
+        error_message += "Traceback: " + str(traceback.format_exc()) + "\n"
+    return data, unique, total, error_message
+
+
+# ---------------------------------------------------------------------------
+# entry points (patmatch.py:677-839)
+# ---------------------------------------------------------------------------
+
+def _strip_anchors(pattern):
+    if pattern.startswith("<"):
+        return 1, 0, pattern.replace("<", "")
+    if pattern.endswith(">"):
+        return 0, 1, pattern.replace(">", "")
+    return 0, 0, pattern
+
+
+def _search_and_collect(pattern, comp_pattern, option, datafile, maxhits, begMatch, endMatch,
+                        downloadFile, original_pattern):
+    patterns = [pattern] + ([comp_pattern] if comp_pattern else [])
+    outputs = search_output(patterns, option, datafile)
+    output = outputs[0] + ("\n" + outputs[1] if comp_pattern else "")
+    offsets, names = get_record_offset(datafile)
+    return process_output(offsets, names, output, datafile, maxhits, begMatch, endMatch, downloadFile,
+                          original_pattern)
+
+
+def run_patmatch(request, id):
+    tmpFile = "patmatch." + id
+    downloadFile = tmpDir + tmpFile
+    dataset = get_param(request, "dataset")
+    seqtype = get_param(request, "seqtype")
+    if seqtype is None:
+        seqtype = "pep"
+    seqname = get_param(request, "seqname")
+    if dataset:
+        dataset += ".seq"
+    else:
+        dataset = "orf_dna.seq" if seqtype in ("dna", "nuc") else "orf_pep.seq"
+    datafile = dataDir + dataset
+    if seqname:
+        return get_sequence(datafile, seqname)
+    begMatch, endMatch, pattern = _strip_anchors(cleanup_pattern(get_param(request, "pattern")))
+    error = check_pattern(pattern, seqtype)
+    if error:
+        return {"error": error}
+    pattern, comp_pattern, option = process_pattern(
+        pattern, get_param(request, "seqtype"), get_param(request, "strand"),
+        get_param(request, "insertion"), get_param(request, "deletion"),
+        get_param(request, "substitution"), get_param(request, "mismatch"))
+    data, uniqueHits, totalHits, error_message = _search_and_collect(
+        pattern, comp_pattern, option, datafile, get_param(request, "max_hits"), begMatch, endMatch,
+        downloadFile, pattern)
+    downloadUrl = ""
+    if uniqueHits > 0:
+        try:
+            downloadUrl = get_downloadUrl(tmpFile)
+        except Exception as exc:
+            error_message = (error_message or "") + f" Error generating download URL: {exc}"
+    return {"hits": data, "uniqueHits": uniqueHits, "totalHits": totalHits, "downloadUrl": downloadUrl,
+            "error_message": error_message}
+
+
+def run_test(pattern, seqtype="pep", strand=None, insertion=None, deletion=None, substitution=None,
+             mismatch=None, max_hits=100, root_dir=None, root_data_dir=None):
+    """patmatch.py:768-838: local run on orf_pep.seq / orf_dna.seq, no Flask."""
+    if root_dir:
+        _set_dirs_for_test(root_dir, root_data_dir)
+    downloadFile = tmpDir + "patmatch.6688"
+    dataset = "orf_pep.seq" if seqtype in ("pep", "protein") else "orf_dna.seq"
+    datafile = dataDir + dataset
+    begMatch, endMatch, pattern = _strip_anchors(cleanup_pattern(pattern))
+    error = check_pattern(pattern, seqtype)
+    if error:
+        return [], 0, 0, error
+    pattern_conv, comp_pattern, option = process_pattern(pattern, seqtype, strand, insertion, deletion,
+                                                         substitution, mismatch)
+    return _search_and_collect(pattern_conv, comp_pattern, option, datafile, max_hits, begMatch, endMatch,
+                               downloadFile, pattern_conv)

@@ -1,0 +1,42 @@
+"""The C-ABI library loads and exports every symbol include/patmatch_hip.h
+declares (no GPU calls; those are in the gpu-marked tests)."""
+import ctypes
+import os
+import re
+
+from patmatchdocker_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "patmatch_hip.h")).read()
+    return sorted(set(re.findall(r"\b(pm_[a-z_]+)\s*\(", text)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_symbol():
+    from patmatchdocker_amd import build
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_version_without_gpu():
+    lib = _lib.load()
+    assert b"gfx950" in lib.pm_version()
+
+
+def test_no_fallback_when_library_missing(monkeypatch):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libpatmatch_hip.so")
+    try:
+        _lib.load()
+    except _lib.EngineUnavailable:
+        pass
+    else:
+        raise AssertionError("missing library must fail loudly")

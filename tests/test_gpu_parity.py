@@ -1,0 +1,125 @@
+"""GPU parity: the HIP kernels (through the C ABI) vs the CPU oracle.
+
+Bit-exact (beg, end) equality on seeded synthetic FASTA files, per strand
+pattern, for the linear (bit-sliced Hamming) and the Glushkov kernels.
+"""
+import numpy as np
+import pytest
+
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+from tests.fastagen import dna_fasta, pep_fasta
+
+pytestmark = pytest.mark.gpu
+
+DNA_PATTERNS = ["GAATTC", "TATAWAWR", "TGANTCAGNNNTGAC", "ACGTACGTACGTACGTACGTACGTACGTACGTACG",
+                "NNNGCNNN", "YYYYYYYYYYYYYYYYYYYYRRRRRRRRRRRRRRRRRRRRNNNNNNNNNNNNNNNNNNNNNNNN",
+                "CCAAT", "GGGCGG", "AN{2,3}TC", "GA(TC){1,2}A", "TTNNNN{0,3}AA"]
+PEP_PATTERNS = ["CX{2,4}CX{3}[LIVMFYWC]", "NXS", "RGD", "C{2}", "[ST]X[RK]", "LXXLL", "KDEL>",
+                "JOBZ", "W{1,3}Y", "P[^P]G"]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from patmatchdocker_amd import engine as eng
+    from patmatchdocker_amd import _lib
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+    return eng
+
+
+def _oracle_hits(oracle_mod, text, prog, k):
+    return oracle_mod.scan(text, prog, k, "s", skip_headers=True)
+
+
+def _gpu_pairs(res):
+    beg, end = res
+    return list(zip(beg.tolist(), end.tolist()))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_dna_patterns_both_strands(engine, oracle_mod, seed, k):
+    text = dna_fasta(seed, n_records=5, max_len=4000, width=(60 if seed == 3 else None))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in DNA_PATTERNS:
+            fwd = convert("-n", pat)
+            comp = convert("-c", fwd)
+            progs = [compile_pattern(fwd), compile_pattern(comp)]
+            res, _ = engine.scan(db, progs, k=k, types="s")
+            for prog, r in zip(progs, res):
+                want = _oracle_hits(oracle_mod, text, prog, k)
+                assert _gpu_pairs(r) == want, (pat, prog.source, k)
+    finally:
+        db.close()
+
+
+@pytest.mark.parametrize("k", [0, 1])
+def test_peptide_patterns(engine, oracle_mod, k):
+    text = pep_fasta(7, n_records=40)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE)
+    try:
+        for pat in PEP_PATTERNS:
+            prog = compile_pattern(convert("-p", pat))
+            res, _ = engine.scan(db, [prog], k=k, types="s")
+            assert _gpu_pairs(res[0]) == _oracle_hits(oracle_mod, text, prog, k), (pat, k)
+    finally:
+        db.close()
+
+
+def test_dna_db_through_nfa_kernel(engine, oracle_mod):
+    """Linear patterns forced through the Glushkov kernel on the 2-bit planes."""
+    text = dna_fasta(11, n_records=4, max_len=5000)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in ["GAATTC", "TATAWAWR", "NNGCNN"]:
+            prog = compile_pattern(convert("-n", pat))
+            for k in (0, 2):
+                r = engine.scan_nfa(db, prog, k)
+                assert list(zip(r.beg.tolist(), r.end.tolist())) == _oracle_hits(oracle_mod, text, prog, k)
+    finally:
+        db.close()
+
+
+def test_edge_cases(engine, oracle_mod):
+    cases = [b"", b">only header\n", b"GAATTC", b"gaattc\n", b">a\n\n\n>b\nGAATTCGAATTC\n",
+             b"GAATT\nC\n", b"> not a header GAATTC\nGAATTC", b"\n" * 100 + b"GAATTC",
+             b">x\n" + b"A" * 70000 + b"GAATTC\n"]
+    prog = compile_pattern("(GAATTC)")
+    for text in cases:
+        for alpha in (engine.NUC, engine.BYTE):
+            db = engine.SequenceDatabase.from_bytes(text, alphabet=alpha)
+            try:
+                for k in (0, 1):
+                    res, _ = engine.scan(db, [prog], k=k, types="s")
+                    assert _gpu_pairs(res[0]) == _oracle_hits(oracle_mod, text, prog, k), (text[:30], alpha, k)
+            finally:
+                db.close()
+
+
+def test_many_patterns_batch(engine, oracle_mod):
+    rng = np.random.default_rng(3)
+    text = dna_fasta(21, n_records=3, max_len=20000, noise=False)
+    pats = ["".join(rng.choice(list("ACGTRYN"), size=int(rng.integers(6, 20)))) for _ in range(13)]
+    progs = [compile_pattern(convert("-n", p)) for p in pats]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=1, types="s")
+        for prog, r in zip(progs, res):
+            assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, 1), prog.source
+    finally:
+        db.close()
+
+
+def test_synthetic_db_decode_and_scan(engine, oracle_mod):
+    db = engine.SequenceDatabase.synthetic(n_records=7, rec_len=30011, seed=5)
+    try:
+        n = db.info()["positions"]
+        text = db.decode(0, n)
+        assert text.count(b"\n") == 7 * 12
+        prog = compile_pattern(convert("-n", "TGANTCAG"))
+        res, _ = engine.scan(db, [prog], k=1, types="s")
+        assert _gpu_pairs(res[0]) == _oracle_hits(oracle_mod, text, prog, 1)
+    finally:
+        db.close()

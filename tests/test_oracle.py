@@ -1,0 +1,68 @@
+"""The CPU oracle (oracle/pm_oracle.c) cross-checked against two independent
+restatements: the pure-Python state-set simulation and, for k = 0, Python's
+own `re` engine (shortest full match from every start)."""
+import random
+import re
+
+import pytest
+
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+from tests.fastagen import dna_fasta, pep_fasta
+
+PATTERNS = ["(GAATTC)", "(TATA[AT]A[AT][AG])", "(C..?.?C...[LIVMFYWC])", "(A(CG)*T)", "(AC|GT.)", "(A[^C]G)",
+            "((GA)?TTC)", "(C?.?.TG)", "(A+C)", "(#A)"]
+
+
+def _to_python_re(source):
+    # nrgrep syntax used by these patterns is a subset of Python's
+    return source.replace("#", r"[^0-9A-Za-z\n]")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_oracle_vs_python_state_sets(oracle_mod, seed):
+    rng = random.Random(seed)
+    text = dna_fasta(seed, n_records=3, max_len=50) if seed % 2 else pep_fasta(seed, 3, 40)
+    for p in PATTERNS:
+        prog = compile_pattern(p)
+        for k, t in [(0, "ids"), (1, "s"), (1, "ids"), (2, "i"), (2, "d"), (1, "id"), (rng.randint(0, 3), "s")]:
+            assert oracle_mod.scan(text, prog, k, t) == oracle_mod.scan_py(text, prog, k, t), (p, k, t)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_vs_python_re_exact(oracle_mod, seed):
+    text = dna_fasta(seed + 10, n_records=3, max_len=120)
+    folded = text.upper()
+    for p in PATTERNS:
+        prog = compile_pattern(p)
+        rx = re.compile(_to_python_re(p).encode())
+        want = []
+        pos = 0
+        for line in folded.split(b"\n"):
+            for s in range(len(line)):
+                for e in range(s + 1, len(line) + 1):
+                    if rx.fullmatch(line, s, e):
+                        want.append((pos + s, pos + e))
+                        break
+            pos += len(line) + 1
+        assert oracle_mod.scan(text, prog, 0) == want, p
+
+
+def test_header_filter(oracle_mod):
+    t = b">a GAATTC\nGAATTC\n> b GAATTC\n"
+    p = compile_pattern("(GAATTC)")
+    assert oracle_mod.scan(t, p) == [(3, 9), (10, 16), (21, 27)]
+    assert oracle_mod.scan(t, p, skip_headers=True) == [(10, 16), (21, 27)]
+
+
+def test_record_index_restatement(oracle_mod):
+    assert oracle_mod.record_index(b">chrI a\nACGT\n>chrII\nAC\n>\n> x\nGG") == \
+        [(0, ">chrI"), (8, "chrI"), (13, ">chrII"), (20, "chrII")]
+
+
+def test_reverse_complement_strand(oracle_mod):
+    text = b">s\nAAGAATTCAA\nCTTTTATAGG\n"
+    fwd = compile_pattern(convert("-n", "TATAWAWR"))
+    rev = compile_pattern(convert("-c", convert("-n", "TATAWAWR")))
+    assert oracle_mod.scan(text, fwd) == []
+    assert oracle_mod.scan(text, rev) == [(14, 22)]     # CTTTTATA = revcomp of TATAAAAG

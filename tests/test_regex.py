@@ -1,0 +1,54 @@
+"""nrgrep-syntax compiler: Glushkov structure, bounds, classes, errors."""
+import pytest
+
+from patmatchdocker_amd.regex import RegexSyntaxError, compile_pattern
+
+
+def test_linear_pattern():
+    p = compile_pattern("(GAA[CT]TC)")
+    assert p.linear and p.m == 6 and p.min_len == p.max_len == 6
+    assert p.first == 1 and p.last == 1 << 5
+    assert p.follow == [2, 4, 8, 16, 32, 0]
+    assert p.classes[3] == frozenset(b"CT")
+
+
+def test_optional_and_groups():
+    p = compile_pattern("(GA(TC)(TC)?A)")
+    assert not p.linear and (p.min_len, p.max_len) == (5, 7)
+    assert p.follow[3] == (1 << 4) | (1 << 6)
+
+
+def test_star_unbounded():
+    p = compile_pattern("(A(CG)*T)")
+    assert p.max_len is None and p.min_len == 2
+    assert p.follow[2] & (1 << 1)          # loop back G -> C
+
+
+def test_case_folding_and_classes():
+    p = compile_pattern("(a[^c].)")
+    assert ord("A") in p.classes[0] and ord("a") not in p.classes[0]
+    assert ord("C") not in p.classes[1] and ord("G") in p.classes[1]
+    assert 10 not in p.classes[2]          # '.' never matches the delimiter
+
+
+def test_escapes_and_ranges():
+    p = compile_pattern(r"(\x41[0-2]\t\()")
+    assert p.classes[0] == frozenset([0x41])
+    assert p.classes[1] == frozenset(b"012")
+    assert p.classes[2] == frozenset([9]) and p.classes[3] == frozenset(b"(")
+
+
+def test_literal_anchor_characters():
+    p = compile_pattern("(ACG)$")
+    assert p.m == 4 and p.classes[3] == frozenset(b"$")
+
+
+@pytest.mark.parametrize("bad", ["", "()", "(?A)", "(A", "A)", "(*)", "[AC", "(A|)"])
+def test_syntax_errors(bad):
+    with pytest.raises(RegexSyntaxError):
+        compile_pattern(bad)
+
+
+def test_too_many_positions():
+    with pytest.raises(RegexSyntaxError):
+        compile_pattern("(" + "A" * 65 + ")")

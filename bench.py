@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""PatMatch scan benchmark (driver contract: one JSON line on rank 0).
+
+Workload (BASELINE.json configs[2]): a 15-nt degenerate DNA motif with k = 2
+mismatches, both strands (the reference's default "Both strands" search =
+pattern + reverse complement, two nrgrep_coords runs in patmatch.py:733-743)
+against 10 Gbp of synthetic random DNA per GPU laid out like a FASTA file
+(1 Mbp records with header lines).  A step = one query: both strands scanned
+in one pass of the bit-sliced Hamming kernel over the HBM-resident database,
+hits compacted + sorted on the device, copied into framework tensors and,
+for N > 1, gathered to rank 0 over RCCL and merged.  Weak scaling: every GPU
+owns its own 10 Gbp shard (records of one node-wide virtual FASTA).
+
+Reported beside the throughput:
+  roofline      k_linear's algorithmic bytes (2-bit planes + superblock flag
+                words) / its HIP-event duration vs the 8 TB/s HBM peak;
+                traffic = PMC HBM bytes per launch from profiles/ when a
+                counter run of this workload is committed there, else null;
+  cpu_baseline  the CPU oracle (oracle/pm_oracle.c, single thread) timed on a
+                bounded sample of the same database (decoded from HBM), which
+                is also a bit-exact parity spot check of the GPU hits.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
+ROUND = "r01"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gbp", type=float, default=10.0, help="Gbp of synthetic DNA per GPU")
+    ap.add_argument("--rec-len", type=int, default=1_000_000)
+    ap.add_argument("--motif", default=MOTIF)
+    ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--sample-mbp", type=float, default=48.0, help="CPU-baseline sample (Mbp)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def load_traffic(workload):
+    path = os.path.join(ROOT, "profiles", "%s_traffic.json" % ROUND)
+    try:
+        with open(path) as fh:
+            data = json.load(fh)
+        if data.get("workload") == workload:
+            return data.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(db, progs, k, sample_bp, gpu_hits):
+    """Oracle on the first `sample_bp` positions; returns (dict, parity_ok)."""
+    from oracle import oracle
+    text = db.decode(0, int(sample_bp))
+    t0 = time.perf_counter()
+    want = [oracle.scan(text, p, k, "s", skip_headers=True) for p in progs]
+    dt = time.perf_counter() - t0
+    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
+    ok = True
+    keys, lens = gpu_hits
+    keys = keys.cpu().tolist()
+    lens = lens.cpu().tolist()
+    for pid, w in enumerate(want):
+        got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
+               if (kk >> 48) == pid and (kk & ((1 << 48) - 1)) + ln <= len(text)]
+        ok &= got == w
+    return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "port",
+            "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, "
+                      "oracle/pm_oracle.c single thread, %.1f s" % (sample_bp / 1e6, dt)}, ok
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from patmatchdocker_amd import engine, shards
+    from patmatchdocker_amd.convert import convert
+    from patmatchdocker_amd.regex import compile_pattern
+
+    fwd = convert("-n", args.motif)
+    comp = convert("-c", fwd)
+    progs = [compile_pattern(fwd), compile_pattern(comp)]
+    batch = engine.LinearBatch(progs)
+
+    # node-wide virtual FASTA: rank r owns records [first, first+count)
+    per_rank_records = max(1, int(round(args.gbp * 1e9 / args.rec_len)))
+    total_records = per_rank_records * world
+    first, count = shards.shard_range(total_records, world, rank)
+    rec_bytes = 10 + 1 + args.rec_len + 1
+    db = engine.SequenceDatabase.synthetic(count, args.rec_len, seed=12345 + first, device=local)
+    info = db.info()
+    offset = first * rec_bytes
+    bases_local = count * args.rec_len
+
+    def step():
+        h = batch.launch(db, args.k)
+        try:
+            keys, lens = shards.hits_to_tensors(h, device)
+            ms = engine.kernel_ms(h)
+        finally:
+            engine.destroy_hits(h)
+        keys = shards.to_global(keys, offset)
+        out = shards.gather_hits(keys, lens)
+        return out, ms
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    result = None
+    for _ in range(args.steps):
+        result, ms = step()
+        kernel_ms.append(ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        bases_total = bases_local * world
+        ms_step = elapsed / args.steps * 1e3
+        value = bases_total * args.steps / elapsed / 1e9
+        mean_kms = sum(kernel_ms) / len(kernel_ms)
+        # k_linear algorithmic bytes per launch: hi+lo planes over the scanned
+        # words (0.25 B/position) + one superblock flag word per 1024 positions
+        positions = info["positions"]
+        scanned_words = -(-positions // 32)
+        alg_bytes = scanned_words * 8 + (-(-scanned_words // 32)) * 4
+        achieved = alg_bytes / (mean_kms * 1e-3) / 1e9
+        workload = "configs[2]: %s k=%d both strands vs %.0f Gbp synthetic DNA per GPU" % (
+            args.motif, args.k, args.gbp)
+        traffic = load_traffic(workload) if world == 1 else None
+        n_hits = int(result[0].numel()) if result is not None else 0
+        line = {
+            "metric": "Gbases/sec scanned (whole node)",
+            "value": round(value, 2),
+            "unit": "Gbases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (2-bit packed bases, bit-sliced)",
+            "data": "synthetic random DNA generated on device (FASTA layout, 1 Mbp records)",
+            "config": {"workload": workload, "motif": args.motif, "k_mismatches": args.k,
+                       "strands": 2, "gbp_per_gpu": args.gbp, "record_len": args.rec_len,
+                       "hits": n_hits, "parallelism": "shard-by-record x%d + RCCL hit gather" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_linear<2,2,1>", "kernel_ms": round(mean_kms, 4),
+                         "algorithmic_bytes_per_launch": alg_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb, ok = cpu_baseline(db, progs, args.k, args.sample_mbp * 1e6, result)
+            line["cpu_baseline"] = cb
+            line["parity_sample_bit_exact"] = ok
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    db.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

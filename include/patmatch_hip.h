@@ -98,6 +98,12 @@ int pm_hits_copy(const pm_hits* h, int32_t* pattern, int64_t* beg, int64_t* end,
 int pm_hits_kernel_ms(const pm_hits* h, double* ms);
 int pm_hits_destroy(pm_hits* h);
 
+/* Copies sorted keys (pattern<<48 | beg) and match lengths into caller-owned
+ * device buffers (e.g. a framework's tensors used for the cross-GPU gather);
+ * `stream` = hipStream_t to order the copy on (NULL = synchronous).      */
+int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst,
+                        uint64_t max_count, void* stream);
+
 /* Raw device pointers of a hit list (uint64 keys = pattern<<48 | beg, and
  * uint32 lengths), for a caller that gathers hits across GPUs itself.   */
 int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count);

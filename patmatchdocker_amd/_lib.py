@@ -23,7 +23,7 @@ EXPORTED = (
     "pm_last_error", "pm_version", "pm_device_count", "pm_db_create",
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
-    "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device",
+    "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
 )
 
 
@@ -66,6 +66,7 @@ def _declare(lib):
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]
     lib.pm_hits_destroy.argtypes = [P]
     lib.pm_hits_device.argtypes = [P, PP, PP, pu64]
+    lib.pm_hits_copy_device.argtypes = [P, P, P, u64, P]
     for name in EXPORTED:
         if name not in ("pm_last_error", "pm_version"):
             getattr(lib, name).restype = ctypes.c_int

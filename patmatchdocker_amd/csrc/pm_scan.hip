@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -70,9 +71,7 @@ void require(bool ok, const char* msg, int code = PM_E_ARG) {
     if (!ok) throw pm_failure(code, msg);
 }
 
-constexpr int WPL = 4;                 // words per lane per iteration in k_linear
-constexpr int WAVE_WORDS = 64 * WPL;   // words per wave iteration (8192 positions)
-constexpr int PAD_WORDS = 512;         // tail padding (16384 positions, all breaks)
+constexpr int PAD_WORDS = 1024;        // tail padding (32768 positions, all breaks)
 constexpr uint32_t NBINS = 1024;       // independent hit counters
 constexpr int MAX_NFA_CHUNK = 4096;    // positions per lane in k_nfa_rev
 
@@ -388,11 +387,19 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v, int lane) {
 // ---------------------------------------------------------------------------
 // k_linear: bit-sliced k-mismatch scan of fixed-length patterns
 // ---------------------------------------------------------------------------
-// Program (u32, device): prog[0] = number of classes nc; per class c a record
-// of 1 + P*MW words at 1 + c*(1+P*MW): [acgt-subset | byte-table index << 8]
-// then, for p in P, q in MW, the mask of shifts (j - 32q) at which pattern p
-// has class c in word offset q.  '.' positions never appear (they cannot
-// mismatch); breaks are handled through the exception path.
+// Program (u32, device, read through the scalar cache): prog[0] = number of
+// classes nc; class c has a record of linear_rec(P, MW) words at
+// 1 + c * REC: [acgt-subset | byte-table index << 8], then for p in P, q in
+// MW the mask of shifts (j - 32q) at which pattern p has class c in word
+// offset q.  '.' positions never appear (they cannot mismatch); breaks are
+// handled through the exception path.
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+typedef const __attribute__((address_space(4))) int32_t* ci32p;
+
+__host__ __device__ constexpr int linear_rec(int P, int MW) {
+    return (1 + P * MW) <= 2 ? 2 : (1 + P * MW) <= 4 ? 4 : (1 + P * MW) <= 8 ? 8 : 16;
+}
+
 struct LinearArgs {
     const uint32_t *hi, *lo, *sbflag, *sbbase, *xbrk, *xoth;
     const uint8_t* xbytes;
@@ -404,156 +411,303 @@ struct LinearArgs {
     Sink sink;
 };
 
-template <int P, int K, int MW>
+// index of flagged word w in the compacted exception side tables
+__device__ inline uint32_t exception_index(const uint32_t* sbflag, const uint32_t* sbbase, uint64_t w) {
+    const uint32_t f = sbflag[w >> 5];
+    const uint32_t wb = (uint32_t)(w & 31);
+    return sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
+}
+
+template <int WPL, int NW>
+struct LaneWords {
+    uint32_t H[NW], L[NW];
+    uint32_t f0, f1;   // superblock flag words covering w0 .. w0+NW-1
+    // bit i = word w0+i has exceptions (evaluated late, so a prefetch of the
+    // next iteration's words is not waited for)
+    __device__ uint64_t flags(uint64_t w0) const {
+        return ((((uint64_t)f1 << 32) | f0) >> (w0 & 31)) & ((1ull << NW) - 1);
+    }
+};
+
+template <int WPL, int NW>
+__device__ inline void load_lane_words(const LinearArgs& a, uint64_t w0, LaneWords<WPL, NW>& d) {
+    if constexpr (WPL == 2) {
+        const uint2 vh = *reinterpret_cast<const uint2*>(a.hi + w0);
+        const uint2 vl = *reinterpret_cast<const uint2*>(a.lo + w0);
+        d.H[0] = vh.x; d.H[1] = vh.y;
+        d.L[0] = vl.x; d.L[1] = vl.y;
+    } else {
+#pragma unroll
+        for (int v = 0; v < WPL / 4; ++v) {
+            const uint4 vh = *reinterpret_cast<const uint4*>(a.hi + w0 + 4 * v);
+            const uint4 vl = *reinterpret_cast<const uint4*>(a.lo + w0 + 4 * v);
+            d.H[4 * v] = vh.x; d.H[4 * v + 1] = vh.y; d.H[4 * v + 2] = vh.z; d.H[4 * v + 3] = vh.w;
+            d.L[4 * v] = vl.x; d.L[4 * v + 1] = vl.y; d.L[4 * v + 2] = vl.z; d.L[4 * v + 3] = vl.w;
+        }
+    }
+#pragma unroll
+    for (int i = WPL; i < NW; ++i) { d.H[i] = a.hi[w0 + i]; d.L[i] = a.lo[w0 + i]; }
+    // both flag words are loaded unconditionally (sbflag is padded) so no
+    // branch depends on the prefetched data
+    d.f0 = a.sbflag[w0 >> 5];
+    d.f1 = a.sbflag[(w0 >> 5) + 1];
+}
+
+// Per-window mismatch counters, bit-sliced over the 32 window starts of a
+// word.  Mismatch bits arrive one or two at a time; pairs go through a
+// carry-save adder (xor3 + majority, one v_bitop3 each) so the count is
+// o + 2*C with o in {0,1} and C tracked as a thermometer (c[0] = C>=1, ...).
+template <int K>
+struct Counter {
+    static constexpr int NC = K / 2 + 1;       // carry levels needed
+    uint32_t o, c[NC];
+    __device__ void clear() {
+        o = 0;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) c[i] = 0;
+    }
+    __device__ void carry_in(uint32_t cy) {
+#pragma unroll
+        for (int i = NC - 1; i > 0; --i) c[i] |= c[i - 1] & cy;
+        c[0] |= cy;
+    }
+    __device__ void add1(uint32_t x) {
+        if constexpr (K == 0) {
+            o |= x;
+        } else {
+            const uint32_t cy = o & x;
+            o ^= x;
+            carry_in(cy);
+        }
+    }
+    __device__ void add2(uint32_t x, uint32_t y) {
+        if constexpr (K == 0) {
+            o |= x | y;
+        } else {
+            const uint32_t cy = __builtin_amdgcn_bitop3_b32(o, x, y, 0xE8);   // majority
+            o = __builtin_amdgcn_bitop3_b32(o, x, y, 0x96);                  // xor3
+            carry_in(cy);
+        }
+    }
+    // windows with more than K mismatches
+    __device__ uint32_t dead() const {
+        if constexpr (K == 0) return o;
+        else if constexpr (K % 2 == 1) return c[NC - 1];              // C > K/2
+        else return c[NC - 1] | (c[NC - 2] & o);                     // C > K/2 or (C == K/2 and o)
+    }
+};
+
+// Mismatch word of one ACGT subset (bit0=A, bit1=C, bit2=G, bit3=T; codes
+// A=00 C=01 G=10 T=11 as (H,L)): one VALU op per word given H, L, ~H, ~L.
+template <int NW>
+__device__ inline void class_mismatch(uint32_t subset, const uint32_t (&H)[NW], const uint32_t (&L)[NW],
+                                      const uint32_t (&nH)[NW], const uint32_t (&nL)[NW], uint32_t (&X)[NW]) {
+#define PM_CASE(code, expr)                                   \
+    case code:                                                \
+        _Pragma("unroll") for (int i = 0; i < NW; ++i) X[i] = (expr); \
+        break;
+    switch (subset) {
+        PM_CASE(0x0, ~0u)
+        PM_CASE(0x1, H[i] | L[i])
+        PM_CASE(0x2, H[i] | nL[i])
+        PM_CASE(0x4, nH[i] | L[i])
+        PM_CASE(0x8, nH[i] | nL[i])
+        PM_CASE(0x3, H[i])
+        PM_CASE(0x5, L[i])
+        PM_CASE(0x9, H[i] ^ L[i])
+        PM_CASE(0x6, H[i] ^ nL[i])
+        PM_CASE(0xA, nL[i])
+        PM_CASE(0xC, nH[i])
+        PM_CASE(0x7, H[i] & L[i])
+        PM_CASE(0xB, H[i] & nL[i])
+        PM_CASE(0xD, nH[i] & L[i])
+        PM_CASE(0xE, nH[i] & nL[i])
+        default:
+            _Pragma("unroll") for (int i = 0; i < NW; ++i) X[i] = 0u;
+            break;
+    }
+#undef PM_CASE
+}
+
+// Mismatch counters of the WPL words of one lane.  EXC: some word of the
+// lane is flagged, so non-ACGT bytes are looked up and breaks kill windows.
+template <int P, int K, int MW, int WPL, bool EXC>
+__device__ inline void count_mismatches(const LinearArgs& a, const LaneWords<WPL, WPL + MW>& cur, uint64_t w0,
+                                        Counter<K> (&t)[P][WPL], uint32_t (&kill)[P][WPL],
+                                        const int (&len)[P], uint64_t fl) {
+    constexpr int NW = WPL + MW;
+    constexpr int REC = linear_rec(P, MW);
+    const cu32p prog = (cu32p)(uintptr_t)a.prog;
+    const uint32_t nc = prog[0];
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int r = 0; r < WPL; ++r) {
+            kill[p][r] = 0;
+            t[p][r].clear();
+        }
+    uint32_t nH[NW], nL[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) { nH[i] = ~cur.H[i]; nL[i] = ~cur.L[i]; }
+    uint32_t rec[REC], rec_next[REC];
+#pragma unroll
+    for (int i = 0; i < REC; ++i) rec[i] = prog[1 + i];
+    for (uint32_t c = 0; c < nc; ++c) {
+        const uint32_t cn = (c + 1 < nc) ? c + 1 : c;
+#pragma unroll
+        for (int i = 0; i < REC; ++i) rec_next[i] = prog[1 + cn * REC + i];
+        const uint32_t desc = rec[0];
+        uint32_t X[NW];
+        class_mismatch<NW>(desc & 15, cur.H, cur.L, nH, nL, X);
+        if constexpr (EXC) {
+            // non-ACGT bytes (N, other IUPAC letters, ...) of flagged words:
+            // membership from the class's 256-bit byte table (rare path,
+            // side-table words re-read from cache instead of held live)
+            const cu32p cb = (cu32p)(uintptr_t)a.class_bytes + 8 * (desc >> 8);
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                if (!((fl >> i) & 1)) continue;
+                const uint32_t idx = exception_index(a.sbflag, a.sbbase, w0 + i);
+                uint32_t o = a.xoth[idx];
+                const uint32_t oth = o;
+                uint32_t mem = 0;
+                while (o) {
+                    const int b = __builtin_ctz(o);
+                    o &= o - 1;
+                    const uint8_t ch = a.xbytes[(uint64_t)idx * 32 + b];
+                    if ((cb[ch >> 5] >> (ch & 31)) & 1) mem |= 1u << b;
+                }
+                X[i] = (X[i] & ~oth) | (oth & ~mem);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+#pragma unroll
+            for (int q = 0; q < MW; ++q) {
+                uint32_t sh = rec[1 + p * MW + q];
+                while (sh) {
+                    const int j = __builtin_ctz(sh);
+                    sh &= sh - 1;
+                    if (sh) {
+                        const int j2 = __builtin_ctz(sh);
+                        sh &= sh - 1;
+#pragma unroll
+                        for (int r = 0; r < WPL; ++r)
+                            t[p][r].add2(__builtin_amdgcn_alignbit(X[r + q + 1], X[r + q], j),
+                                         __builtin_amdgcn_alignbit(X[r + q + 1], X[r + q], j2));
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < WPL; ++r)
+                            t[p][r].add1(__builtin_amdgcn_alignbit(X[r + q + 1], X[r + q], j));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < REC; ++i) rec[i] = rec_next[i];
+    }
+    if constexpr (EXC) {
+        // windows overlapping a break (newline, header byte, tail padding)
+        uint32_t BRK[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            BRK[i] = ((fl >> i) & 1) ? a.xbrk[exception_index(a.sbflag, a.sbbase, w0 + i)] : 0u;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int r = 0; r < WPL; ++r) {
+                uint32_t k = 0;
+                for (int j = 0; j < len[p]; ++j) {
+                    const int q = j >> 5;
+                    uint32_t lo_w = 0, hi_w = 0;
+#pragma unroll
+                    for (int qq = 0; qq < MW; ++qq)
+                        if (q == qq) { lo_w = BRK[r + qq]; hi_w = BRK[r + qq + 1]; }
+                    k |= __builtin_amdgcn_alignbit(hi_w, lo_w, j & 31);
+                }
+                kill[p][r] = k;
+            }
+    }
+}
+
+// Counts one lane-iteration and emits its hits.
+template <int P, int K, int MW, int WPL>
+__device__ inline void linear_iteration(const LinearArgs& a, const LaneWords<WPL, WPL + MW>& cur, uint64_t w0,
+                                        const int (&len)[P], int lane, uint64_t wave) {
+    Counter<K> t[P][WPL];
+    uint32_t kill[P][WPL];
+    const uint64_t fl = cur.flags(w0);
+    if (fl == 0) count_mismatches<P, K, MW, WPL, false>(a, cur, w0, t, kill, len, fl);
+    else count_mismatches<P, K, MW, WPL, true>(a, cur, w0, t, kill, len, fl);
+    uint32_t hits[P][WPL];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int r = 0; r < WPL; ++r) {
+            hits[p][r] = ~t[p][r].dead() & ~kill[p][r];
+            cnt += __popc(hits[p][r]);
+        }
+    if (__ballot(cnt != 0)) {
+        const uint32_t incl = wave_incl_scan(cnt, lane);
+        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t bin = (uint32_t)(wave % NBINS);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&a.sink.bin_cnt[bin], total);
+        base = __shfl(base, 0, 64);
+        uint32_t o = base + incl - cnt;
+        uint64_t* dst = a.sink.out + (uint64_t)bin * a.sink.cap;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+#pragma unroll
+            for (int r = 0; r < WPL; ++r) {
+                uint32_t h = hits[p][r];
+                while (h) {
+                    const int b = __builtin_ctz(h);
+                    h &= h - 1;
+                    if (o < a.sink.cap) dst[o] = ((uint64_t)(a.pattern_base + p) << 48) | ((w0 + r) * 32 + b);
+                    ++o;
+                }
+            }
+        }
+    }
+}
+
+// Grid-stride over wave iterations (64 lanes x WPL consecutive words each).
+// DBUF: unrolled by two with alternating register buffers, so the planes of
+// the next iteration are in flight while this one computes; the prefetch
+// address is clamped instead of predicated so the compiler can count its
+// loads (no vmcnt(0) drain).
+template <int P, int K, int MW, int WPL, bool DBUF>
 __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
     constexpr int NW = WPL + MW;
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = (gridDim.x * (uint64_t)blockDim.x) >> 6;
-    const uint32_t nc = a.prog[0];
-    constexpr int REC = 1 + P * MW;
+    if (wave >= a.n_iter) return;
     int len[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) len[p] = a.lengths[p];
-
-    for (uint64_t it = wave; it < a.n_iter; it += nwaves) {
-        const uint64_t w0 = (it * 64 + lane) * WPL;
-        uint32_t H[NW], L[NW];
-        {
-            const uint4 vh = *reinterpret_cast<const uint4*>(a.hi + w0);
-            const uint4 vl = *reinterpret_cast<const uint4*>(a.lo + w0);
-            H[0] = vh.x; H[1] = vh.y; H[2] = vh.z; H[3] = vh.w;
-            L[0] = vl.x; L[1] = vl.y; L[2] = vl.z; L[3] = vl.w;
-#pragma unroll
-            for (int i = WPL; i < NW; ++i) { H[i] = a.hi[w0 + i]; L[i] = a.lo[w0 + i]; }
+    for (int p = 0; p < P; ++p) len[p] = ((ci32p)(uintptr_t)a.lengths)[p];
+    const uint64_t last = a.n_iter - 1;
+    auto words_of = [&](uint64_t it) { return (std::min(it, last) * 64 + lane) * WPL; };
+    LaneWords<WPL, NW> A, B;
+    uint64_t it = wave;
+    if constexpr (DBUF) {
+        load_lane_words<WPL, NW>(a, words_of(it), A);
+        while (true) {
+            load_lane_words<WPL, NW>(a, words_of(it + nwaves), B);
+            linear_iteration<P, K, MW, WPL>(a, A, words_of(it), len, lane, wave);
+            it += nwaves;
+            if (it >= a.n_iter) break;
+            load_lane_words<WPL, NW>(a, words_of(it + nwaves), A);
+            linear_iteration<P, K, MW, WPL>(a, B, words_of(it), len, lane, wave);
+            it += nwaves;
+            if (it >= a.n_iter) break;
         }
-        // exception flags of words w0 .. w0+NW-1 (at most two superblocks)
-        const uint64_t wl = w0 + NW - 1;
-        const uint32_t f0 = a.sbflag[w0 >> 5];
-        const uint32_t f1 = ((wl >> 5) != (w0 >> 5)) ? a.sbflag[wl >> 5] : 0u;
-        const uint32_t s0 = (uint32_t)(w0 & 31);
-        uint64_t fl = ((uint64_t)f1 << 32 | f0) >> s0;   // bit i = word w0+i flagged
-        fl &= (1ull << NW) - 1;
-        const bool exc = fl != 0;
-        uint32_t BRK[NW], OTH[NW];
-        uint32_t XI[NW];
-        if (exc) {
-#pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                BRK[i] = 0; OTH[i] = 0; XI[i] = 0;
-                if ((fl >> i) & 1) {
-                    const uint64_t w = w0 + i;
-                    const uint32_t f = a.sbflag[w >> 5];
-                    const uint32_t wb = (uint32_t)(w & 31);
-                    const uint32_t idx = a.sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
-                    XI[i] = idx; BRK[i] = a.xbrk[idx]; OTH[i] = a.xoth[idx];
-                }
-            }
-        }
-
-        uint32_t t[P][WPL][K + 1];
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-#pragma unroll
-            for (int r = 0; r < WPL; ++r)
-#pragma unroll
-                for (int e = 0; e <= K; ++e) t[p][r][e] = 0;
-
-        for (uint32_t c = 0; c < nc; ++c) {
-            const uint32_t* rec = a.prog + 1 + c * REC;
-            const uint32_t desc = rec[0];
-            const uint32_t m0 = (desc & 1) ? ~0u : 0u, m1 = (desc & 2) ? ~0u : 0u;
-            const uint32_t m2 = (desc & 4) ? ~0u : 0u, m3 = (desc & 8) ? ~0u : 0u;
-            uint32_t X[NW];
-#pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                // member(code) with code = (H,L): bfi(sel, a, b) = sel ? a : b
-                const uint32_t hi_half = (L[i] & m3) | (~L[i] & m2);
-                const uint32_t lo_half = (L[i] & m1) | (~L[i] & m0);
-                X[i] = ~((H[i] & hi_half) | (~H[i] & lo_half));
-            }
-            if (exc) {
-                const uint32_t* cb = a.class_bytes + 8 * (desc >> 8);
-#pragma unroll
-                for (int i = 0; i < NW; ++i) {
-                    uint32_t o = OTH[i];
-                    uint32_t mem = 0;
-                    while (o) {
-                        const int b = __builtin_ctz(o);
-                        o &= o - 1;
-                        const uint8_t ch = a.xbytes[(uint64_t)XI[i] * 32 + b];
-                        if ((cb[ch >> 5] >> (ch & 31)) & 1) mem |= 1u << b;
-                    }
-                    X[i] = (X[i] & ~OTH[i]) | (OTH[i] & ~mem);
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-#pragma unroll
-                for (int q = 0; q < MW; ++q) {
-                    uint32_t sh = rec[1 + p * MW + q];
-                    while (sh) {
-                        const int j = __builtin_ctz(sh);
-                        sh &= sh - 1;
-#pragma unroll
-                        for (int r = 0; r < WPL; ++r) {
-                            const uint32_t x = __builtin_amdgcn_alignbit(X[r + q + 1], X[r + q], j);
-#pragma unroll
-                            for (int e = K; e > 0; --e) t[p][r][e] |= t[p][r][e - 1] & x;
-                            t[p][r][0] |= x;
-                        }
-                    }
-                }
-            }
-        }
-
-        // surviving window starts; breaks (incl. tail padding) kill windows
-        uint32_t hits[P][WPL];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-#pragma unroll
-            for (int r = 0; r < WPL; ++r) {
-                uint32_t h = ~t[p][r][K];
-                if (exc) {
-                    uint32_t kill = 0;
-                    for (int j = 0; j < len[p]; ++j) {
-                        const int q = j >> 5;
-                        uint32_t lo_w = 0, hi_w = 0;
-#pragma unroll
-                        for (int qq = 0; qq < MW; ++qq)
-                            if (q == qq) { lo_w = BRK[r + qq]; hi_w = BRK[r + qq + 1]; }
-                        kill |= __builtin_amdgcn_alignbit(hi_w, lo_w, j & 31);
-                    }
-                    h &= ~kill;
-                }
-                hits[p][r] = h;
-                cnt += __popc(h);
-            }
-        }
-        if (__ballot(cnt != 0)) {
-            const uint32_t incl = wave_incl_scan(cnt, lane);
-            const uint32_t total = __shfl(incl, 63, 64);
-            const uint32_t bin = (uint32_t)(wave % NBINS);
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.sink.bin_cnt[bin], total);
-            base = __shfl(base, 0, 64);
-            uint32_t o = base + incl - cnt;
-            uint64_t* dst = a.sink.out + (uint64_t)bin * a.sink.cap;
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-#pragma unroll
-                for (int r = 0; r < WPL; ++r) {
-                    uint32_t h = hits[p][r];
-                    while (h) {
-                        const int b = __builtin_ctz(h);
-                        h &= h - 1;
-                        if (o < a.sink.cap)
-                            dst[o] = ((uint64_t)(a.pattern_base + p) << 48) | ((w0 + r) * 32 + b);
-                        ++o;
-                    }
-                }
-            }
+    } else {
+        for (; it < a.n_iter; it += nwaves) {
+            load_lane_words<WPL, NW>(a, words_of(it), A);
+            linear_iteration<P, K, MW, WPL>(a, A, words_of(it), len, lane, wave);
         }
     }
 }
@@ -919,33 +1073,61 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, uint64_t total, int key_
 }
 
 // --- linear-scan dispatch ----------------------------------------------------
-template <int P, int K, int MW>
+// Lane shape (words per lane, double buffering).  The default is the
+// measured best; PM_LINEAR_SHAPE=<wpl><d|s> selects the experimental shapes
+// (instantiated for the two-pattern batch only).
+struct LinearShape {
+    int wpl = 4;
+    bool dbuf = true;
+};
+
+LinearShape linear_shape() {
+    LinearShape sh;
+    if (const char* e = getenv("PM_LINEAR_SHAPE")) {
+        if (e[0] == '2' || e[0] == '4' || e[0] == '8') sh.wpl = e[0] - '0';
+        if (e[0] && e[1] == 's') sh.dbuf = false;
+    }
+    return sh;
+}
+
+template <int P, int K, int MW, int WPL, bool DBUF>
 void launch_linear(const LinearArgs& a, hipStream_t s) {
     const uint64_t blocks = std::min<uint64_t>((a.n_iter + 3) / 4, 256 * 16);
-    hipLaunchKernelGGL((k_linear<P, K, MW>), dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_linear<P, K, MW, WPL, DBUF>), dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256),
+                       0, s, a);
+}
+
+template <int P, int K, int MW>
+void launch_linear_shape(const LinearShape& sh, const LinearArgs& a, hipStream_t s) {
+    if constexpr (P == 2 && K == 2 && MW == 1) {
+        if (sh.wpl == 2) { sh.dbuf ? launch_linear<P, K, MW, 2, true>(a, s) : launch_linear<P, K, MW, 2, false>(a, s); return; }
+        if (sh.wpl == 8) { sh.dbuf ? launch_linear<P, K, MW, 8, true>(a, s) : launch_linear<P, K, MW, 8, false>(a, s); return; }
+        if (!sh.dbuf) { launch_linear<P, K, MW, 4, false>(a, s); return; }
+    }
+    launch_linear<P, K, MW, 4, true>(a, s);
 }
 
 template <int P, int K>
-void launch_linear_mw(int mw, const LinearArgs& a, hipStream_t s) {
-    if (mw == 1) launch_linear<P, K, 1>(a, s);
-    else launch_linear<P, K, 2>(a, s);
+void launch_linear_mw(int mw, const LinearShape& sh, const LinearArgs& a, hipStream_t s) {
+    if (mw == 1) launch_linear_shape<P, K, 1>(sh, a, s);
+    else launch_linear_shape<P, K, 2>(sh, a, s);
 }
 
 template <int P>
-void launch_linear_k(int k, int mw, const LinearArgs& a, hipStream_t s) {
+void launch_linear_k(int k, int mw, const LinearShape& sh, const LinearArgs& a, hipStream_t s) {
     switch (k) {
-        case 0: launch_linear_mw<P, 0>(mw, a, s); break;
-        case 1: launch_linear_mw<P, 1>(mw, a, s); break;
-        case 2: launch_linear_mw<P, 2>(mw, a, s); break;
-        default: launch_linear_mw<P, 3>(mw, a, s); break;
+        case 0: launch_linear_mw<P, 0>(mw, sh, a, s); break;
+        case 1: launch_linear_mw<P, 1>(mw, sh, a, s); break;
+        case 2: launch_linear_mw<P, 2>(mw, sh, a, s); break;
+        default: launch_linear_mw<P, 3>(mw, sh, a, s); break;
     }
 }
 
-void launch_linear_any(int P, int k, int mw, const LinearArgs& a, hipStream_t s) {
+void launch_linear_any(int P, int k, int mw, const LinearShape& sh, const LinearArgs& a, hipStream_t s) {
     switch (P) {
-        case 1: launch_linear_k<1>(k, mw, a, s); break;
-        case 2: launch_linear_k<2>(k, mw, a, s); break;
-        default: launch_linear_k<4>(k, mw, a, s); break;
+        case 1: launch_linear_k<1>(k, mw, sh, a, s); break;
+        case 2: launch_linear_k<2>(k, mw, sh, a, s); break;
+        default: launch_linear_k<4>(k, mw, sh, a, s); break;
     }
 }
 
@@ -1158,9 +1340,11 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         }
         DeviceGuard g(db->device);
         hipStream_t s = db->stream;
+        const LinearShape shape = linear_shape();
+        const uint64_t wave_words = 64ull * shape.wpl;
         const uint64_t start_words = (db->n + 31) / 32;
-        const uint64_t n_iter = (start_words + WAVE_WORDS - 1) / WAVE_WORDS;
-        require(n_iter * WAVE_WORDS + 4 <= db->nwords, "internal: padding too small");
+        const uint64_t n_iter = (start_words + wave_words - 1) / wave_words;
+        require(n_iter * wave_words + 64 <= db->nwords, "internal: padding too small");
 
         // one upload: class byte tables, lengths, then one program per chunk
         struct Chunk { int base, P, MW; size_t off; };
@@ -1182,8 +1366,8 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                     slot[c] = (int)used.size();
                     used.push_back(c);
                 }
-            const int REC = 1 + P * MW;
-            std::vector<uint32_t> prog(1 + used.size() * REC, 0);
+            const int REC = linear_rec(P, MW);
+            std::vector<uint32_t> prog(1 + (used.size() + 1) * REC, 0);   // +1: prefetch slack
             prog[0] = (uint32_t)used.size();
             for (size_t u = 0; u < used.size(); ++u)
                 prog[1 + u * REC] = (uint32_t)(class_acgt[used[u]] & 15) | ((uint32_t)used[u] << 8);
@@ -1215,7 +1399,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 a.n_iter = n_iter;
                 a.pattern_base = ch.base;
                 a.sink = Sink{sb.out, sb.cnt, sb.cap};
-                launch_linear_any(ch.P, k, ch.MW, a, s);
+                launch_linear_any(ch.P, k, ch.MW, shape, a, s);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(hipEventRecord(ev.b, s));
@@ -1363,6 +1547,20 @@ int pm_hits_copy(const pm_hits* h, int32_t* pattern, int64_t* beg, int64_t* end,
             if (beg) beg[i] = b;
             if (end) end[i] = b + (int64_t)lens[i];
         }
+    });
+}
+
+int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst, uint64_t max_count,
+                        void* stream) {
+    return guarded([&] {
+        require(h != nullptr, "hits is NULL");
+        const uint64_t n = std::min<uint64_t>(h->count, max_count);
+        if (n == 0) return;
+        DeviceGuard g(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        if (keys_dst) HIPCHK(hipMemcpyAsync(keys_dst, h->keys, n * 8, hipMemcpyDeviceToDevice, s));
+        if (lens_dst) HIPCHK(hipMemcpyAsync(lens_dst, h->lens, n * 4, hipMemcpyDeviceToDevice, s));
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
     });
 }
 

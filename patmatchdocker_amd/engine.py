@@ -199,13 +199,38 @@ def _linear_tables(progs: Sequence[Program]):
     return lengths, pos_class, nc, acgt, bits, is_any
 
 
+class LinearBatch:
+    """Pre-built class/position tables of a batch of linear programs."""
+
+    def __init__(self, progs: Sequence[Program]):
+        for p in progs:
+            if not p.linear:
+                raise ValueError("LinearBatch needs linear programs: %s" % p.source)
+        self.lengths, self.pos_class, self.nc, self.acgt, self.bits, self.is_any = _linear_tables(progs)
+        self.n = len(progs)
+
+    def launch(self, db: SequenceDatabase, k: int):
+        """Run pm_scan_linear; returns the raw pm_hits handle (caller destroys)."""
+        out = ctypes.c_void_p()
+        check(_lib.load().pm_scan_linear(db.handle, self.n, self.lengths.ctypes.data,
+                                         self.pos_class.ctypes.data, self.nc, self.acgt.ctypes.data,
+                                         self.bits.ctypes.data, self.is_any.ctypes.data, k,
+                                         ctypes.byref(out)))
+        return out
+
+
+def kernel_ms(handle) -> float:
+    ms = ctypes.c_double()
+    check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))
+    return ms.value
+
+
+def destroy_hits(handle):
+    check(_lib.load().pm_hits_destroy(handle))
+
+
 def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int) -> Hits:
-    lengths, pos_class, nc, acgt, bits, is_any = _linear_tables(progs)
-    out = ctypes.c_void_p()
-    check(_lib.load().pm_scan_linear(db.handle, len(progs), lengths.ctypes.data, pos_class.ctypes.data, nc,
-                                     acgt.ctypes.data, bits.ctypes.data, is_any.ctypes.data, k,
-                                     ctypes.byref(out)))
-    return _collect(out)
+    return _collect(LinearBatch(progs).launch(db, k))
 
 
 def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0) -> Hits:

@@ -24,6 +24,7 @@ EXPORTED = (
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
+    "pm_linear_jit_compile",
 )
 
 
@@ -67,6 +68,7 @@ def _declare(lib):
     lib.pm_hits_destroy.argtypes = [P]
     lib.pm_hits_device.argtypes = [P, PP, PP, pu64]
     lib.pm_hits_copy_device.argtypes = [P, P, P, u64, P]
+    lib.pm_linear_jit_compile.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, P, ctypes.c_int, pu64]
     for name in EXPORTED:
         if name not in ("pm_last_error", "pm_version"):
             getattr(lib, name).restype = ctypes.c_int

@@ -20,7 +20,7 @@ ARCH = os.environ.get("PM_OFFLOAD_ARCH", "gfx950")
 
 def command(out: str = OUT):
     return [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-            "-I" + os.path.join(ROOT, "include"), "-o", out, SRC]
+            "-I" + os.path.join(ROOT, "include"), "-o", out, SRC, "-lhiprtc"]
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -32,7 +32,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     tmp = OUT + ".tmp"
-    subprocess.run(cmd[:-3] + ["-o", tmp, SRC], check=True)
+    subprocess.run(cmd[:-4] + ["-o", tmp, SRC, "-lhiprtc"], check=True)
     os.replace(tmp, OUT)
     return OUT
 

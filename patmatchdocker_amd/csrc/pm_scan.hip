@@ -24,9 +24,13 @@
 //    independent bins (no single hot counter), are compacted and radix
 //    sorted by (pattern, beg) on the device.
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <sstream>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -1072,6 +1076,300 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, uint64_t total, int key_
     return h;
 }
 
+// --- runtime-specialized k_linear (hipRTC) -----------------------------------
+// For large databases the batch's patterns are compiled into the kernel:
+// every shift is an immediate of v_alignbit, every class word a single op
+// on (H, L, ~H, ~L), all positions of a pattern are paired through the
+// carry-save counter, and no scalar loop or program load is left in the
+// hot loop.  Code objects are cached per generated source and device.
+const char* kJitCommon = R"JIT(
+typedef unsigned int u32;
+typedef unsigned long long u64;
+struct JArgs {
+    const u32 *hi, *lo, *sbflag, *sbbase, *xbrk, *xoth;
+    const unsigned char* xbytes;
+    const u32* cb;
+    u64 n_iter;
+    u64* out;
+    u32* bin_cnt;
+    u32 cap;
+    int pattern_base;
+};
+#define NBINS 1024u
+#define AL(h, l, s) __builtin_amdgcn_alignbit((h), (l), (s))
+template <int K>
+struct Ctr {
+    static constexpr int NC = K / 2 + 1;
+    u32 o, c[NC];
+    __device__ __forceinline__ void clear() { o = 0; for (int i = 0; i < NC; ++i) c[i] = 0; }
+    __device__ __forceinline__ void carry(u32 cy) {
+        for (int i = NC - 1; i > 0; --i) c[i] |= c[i - 1] & cy;
+        c[0] |= cy;
+    }
+    __device__ __forceinline__ void add1(u32 x) {
+        if constexpr (K == 0) { o |= x; } else { const u32 cy = o & x; o ^= x; carry(cy); }
+    }
+    __device__ __forceinline__ void add2(u32 x, u32 y) {
+        if constexpr (K == 0) { o |= x | y; }
+        else {
+            const u32 cy = __builtin_amdgcn_bitop3_b32(o, x, y, 0xE8);
+            o = __builtin_amdgcn_bitop3_b32(o, x, y, 0x96);
+            carry(cy);
+        }
+    }
+    __device__ __forceinline__ u32 dead() const {
+        if constexpr (K == 0) return o;
+        else if constexpr (K % 2 == 1) return c[NC - 1];
+        else return c[NC - 1] | (c[NC - 2] & o);
+    }
+};
+__device__ __forceinline__ u32 exc_index(const u32* sbflag, const u32* sbbase, u64 w) {
+    const u32 f = sbflag[w >> 5];
+    const u32 wb = (u32)(w & 31);
+    return sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
+}
+// non-ACGT bytes of a flagged word: class membership from the byte table
+__device__ __forceinline__ u32 fix_class(const JArgs& a, u32 x, u64 w, int cls) {
+    const u32 idx = exc_index(a.sbflag, a.sbbase, w);
+    u32 o = a.xoth[idx];
+    const u32 oth = o;
+    u32 mem = 0;
+    while (o) {
+        const int b = __builtin_ctz(o);
+        o &= o - 1;
+        const unsigned char ch = a.xbytes[(u64)idx * 32 + b];
+        if ((a.cb[8 * cls + (ch >> 5)] >> (ch & 31)) & 1) mem |= 1u << b;
+    }
+    return (x & ~oth) | (oth & ~mem);
+}
+__device__ __forceinline__ u32 wave_incl_scan(u32 v, int lane) {
+    for (int d = 1; d < 64; d <<= 1) {
+        u32 o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+)JIT";
+
+struct JitKernel {
+    hipModule_t module = nullptr;
+    hipFunction_t fn = nullptr;
+};
+
+std::mutex g_jit_mu;
+std::map<std::pair<int, std::string>, JitKernel> g_jit_cache;
+
+struct JArgsHost {           // must match JArgs in kJitCommon
+    const uint32_t *hi, *lo, *sbflag, *sbbase, *xbrk, *xoth;
+    const uint8_t* xbytes;
+    const uint32_t* cb;
+    uint64_t n_iter;
+    uint64_t* out;
+    uint32_t* bin_cnt;
+    uint32_t cap;
+    int pattern_base;
+};
+
+const char* subset_expr(int subset) {
+    switch (subset & 15) {
+        case 0x0: return "~0u";
+        case 0x1: return "H[i] | L[i]";
+        case 0x2: return "H[i] | nL[i]";
+        case 0x4: return "nH[i] | L[i]";
+        case 0x8: return "nH[i] | nL[i]";
+        case 0x3: return "H[i]";
+        case 0x5: return "L[i]";
+        case 0x9: return "H[i] ^ L[i]";
+        case 0x6: return "H[i] ^ nL[i]";
+        case 0xA: return "nL[i]";
+        case 0xC: return "nH[i]";
+        case 0x7: return "H[i] & L[i]";
+        case 0xB: return "H[i] & nL[i]";
+        case 0xD: return "nH[i] & L[i]";
+        case 0xE: return "nH[i] & nL[i]";
+        default: return "0u";
+    }
+}
+
+// Source of the specialized kernel for patterns [base, base+P).
+std::string gen_linear_source(int P, int K, int MW, const int32_t* lengths, const uint8_t* pos_class,
+                              const uint8_t* class_acgt, const uint8_t* class_is_any) {
+    constexpr int W = 4;                      // words per lane
+    const int NW = W + MW;
+    std::vector<int> used;
+    std::map<int, int> slot;
+    for (int p = 0; p < P; ++p)
+        for (int j = 0; j < lengths[p]; ++j) {
+            const int c = pos_class[64 * p + j];
+            if (!class_is_any[c] && !slot.count(c)) { slot[c] = (int)used.size(); used.push_back(c); }
+        }
+    std::ostringstream o;
+    o << kJitCommon;
+    o << "#define P " << P << "\n#define K " << K << "\n#define W " << W << "\n#define NW " << NW << "\n";
+    o << "__device__ __forceinline__ void body(const JArgs& a, const u32 (&H)[NW], const u32 (&L)[NW], u32 f0, "
+         "u32 f1, u64 w0, int lane, u64 wave) {\n";
+    o << "  const u64 fl = ((((u64)f1 << 32) | f0) >> (w0 & 31)) & ((1ull << NW) - 1);\n";
+    o << "  u32 nH[NW], nL[NW];\n#pragma unroll\n  for (int i = 0; i < NW; ++i) { nH[i] = ~H[i]; nL[i] = ~L[i]; }\n";
+    for (size_t u = 0; u < used.size(); ++u) {
+        o << "  u32 X" << u << "[NW];\n#pragma unroll\n  for (int i = 0; i < NW; ++i) X" << u << "[i] = "
+          << subset_expr(class_acgt[used[u]]) << ";\n";
+    }
+    o << "  if (fl) {\n#pragma unroll\n    for (int i = 0; i < NW; ++i) if ((fl >> i) & 1) {\n";
+    for (size_t u = 0; u < used.size(); ++u)
+        o << "      X" << u << "[i] = fix_class(a, X" << u << "[i], w0 + i, " << used[u] << ");\n";
+    o << "    }\n  }\n";
+    o << "  Ctr<K> t[P][W];\n#pragma unroll\n  for (int p = 0; p < P; ++p)\n#pragma unroll\n"
+         "    for (int r = 0; r < W; ++r) t[p][r].clear();\n";
+    o << "#pragma unroll\n  for (int r = 0; r < W; ++r) {\n";
+    for (int p = 0; p < P; ++p) {
+        std::vector<std::pair<int, int>> pos;   // (shift, slot)
+        for (int j = 0; j < lengths[p]; ++j) {
+            const int c = pos_class[64 * p + j];
+            if (!class_is_any[c]) pos.push_back({j, slot[c]});
+        }
+        auto term = [&](const std::pair<int, int>& e) {
+            std::ostringstream t;
+            const int q = e.first >> 5, sh = e.first & 31;
+            t << "AL(X" << e.second << "[r + " << q + 1 << "], X" << e.second << "[r + " << q << "], " << sh << ")";
+            return t.str();
+        };
+        size_t i = 0;
+        for (; i + 1 < pos.size(); i += 2)
+            o << "    t[" << p << "][r].add2(" << term(pos[i]) << ", " << term(pos[i + 1]) << ");\n";
+        if (i < pos.size()) o << "    t[" << p << "][r].add1(" << term(pos[i]) << ");\n";
+    }
+    o << "  }\n";
+    // windows overlapping breaks (newline, header bytes, tail padding)
+    o << "  u32 kill[P][W];\n#pragma unroll\n  for (int p = 0; p < P; ++p)\n#pragma unroll\n"
+         "    for (int r = 0; r < W; ++r) kill[p][r] = 0;\n";
+    o << "  if (fl) {\n    u32 B[NW + 1];\n#pragma unroll\n    for (int i = 0; i < NW; ++i) B[i] = ((fl >> i) & 1) ? "
+         "a.xbrk[exc_index(a.sbflag, a.sbbase, w0 + i)] : 0u;\n    B[NW] = 0;\n";
+    for (int p = 0; p < P; ++p)
+        o << "#pragma unroll\n    for (int r = 0; r < W; ++r) {\n      u32 k = 0;\n#pragma unroll\n"
+             "      for (int j = 0; j < " << lengths[p] << "; ++j) k |= AL(B[r + (j >> 5) + 1], B[r + (j >> 5)], j & 31);\n"
+             "      kill[" << p << "][r] = k;\n    }\n";
+    o << "  }\n";
+    o << R"JIT(  u32 hits[P][W];
+  u32 cnt = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int r = 0; r < W; ++r) { hits[p][r] = ~t[p][r].dead() & ~kill[p][r]; cnt += __popc(hits[p][r]); }
+  if (__ballot(cnt != 0)) {
+    const u32 incl = wave_incl_scan(cnt, lane);
+    const u32 total = __shfl(incl, 63, 64);
+    const u32 bin = (u32)(wave % NBINS);
+    u32 base = 0;
+    if (lane == 0) base = atomicAdd(&a.bin_cnt[bin], total);
+    base = __shfl(base, 0, 64);
+    u32 o = base + incl - cnt;
+    u64* dst = a.out + (u64)bin * a.cap;
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        u32 h = hits[p][r];
+        while (h) {
+          const int b = __builtin_ctz(h);
+          h &= h - 1;
+          if (o < a.cap) dst[o] = ((u64)(a.pattern_base + p) << 48) | ((w0 + r) * 32 + b);
+          ++o;
+        }
+      }
+  }
+}
+__device__ __forceinline__ void load(const JArgs& a, u64 w0, u32 (&H)[NW], u32 (&L)[NW], u32& f0, u32& f1) {
+  const uint4 vh = *reinterpret_cast<const uint4*>(a.hi + w0);
+  const uint4 vl = *reinterpret_cast<const uint4*>(a.lo + w0);
+  H[0] = vh.x; H[1] = vh.y; H[2] = vh.z; H[3] = vh.w;
+  L[0] = vl.x; L[1] = vl.y; L[2] = vl.z; L[3] = vl.w;
+#pragma unroll
+  for (int i = W; i < NW; ++i) { H[i] = a.hi[w0 + i]; L[i] = a.lo[w0 + i]; }
+  f0 = a.sbflag[w0 >> 5];
+  f1 = a.sbflag[(w0 >> 5) + 1];
+}
+extern "C" __global__ __launch_bounds__(256) void pm_linear_jit(JArgs a) {
+  const int lane = threadIdx.x & 63;
+  const u64 wave = (blockIdx.x * (u64)blockDim.x + threadIdx.x) >> 6;
+  const u64 nwaves = (gridDim.x * (u64)blockDim.x) >> 6;
+  if (wave >= a.n_iter) return;
+  const u64 last = a.n_iter - 1;
+  u32 HA[NW], LA[NW], HB[NW], LB[NW], fa0, fa1, fb0, fb1;
+  u64 it = wave;
+  load(a, (it * 64 + lane) * W, HA, LA, fa0, fa1);
+  while (true) {
+    u64 nx = it + nwaves < last ? it + nwaves : last;
+    load(a, (nx * 64 + lane) * W, HB, LB, fb0, fb1);
+    body(a, HA, LA, fa0, fa1, (it * 64 + lane) * W, lane, wave);
+    it += nwaves;
+    if (it >= a.n_iter) break;
+    nx = it + nwaves < last ? it + nwaves : last;
+    load(a, (nx * 64 + lane) * W, HA, LA, fa0, fa1);
+    body(a, HB, LB, fb0, fb1, (it * 64 + lane) * W, lane, wave);
+    it += nwaves;
+    if (it >= a.n_iter) break;
+  }
+}
+)JIT";
+    return o.str();
+}
+
+#define RTCCHK(expr)                                                                     \
+    do {                                                                                 \
+        hiprtcResult r_ = (expr);                                                        \
+        if (r_ != HIPRTC_SUCCESS)                                                        \
+            throw pm_failure(PM_E_HIP, std::string(#expr) + ": " + hiprtcGetErrorString(r_)); \
+    } while (0)
+
+// Compiles (cached) and returns the code object of `src`.
+std::vector<char> jit_compile(const std::string& src) {
+    if (const char* dump = getenv("PM_JIT_DUMP")) {      // debugging: keep the generated source
+        if (FILE* f = fopen(dump, "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+    }
+    hiprtcProgram prog;
+    RTCCHK(hiprtcCreateProgram(&prog, src.c_str(), "pm_linear_jit.hip", 0, nullptr, nullptr));
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        throw pm_failure(PM_E_HIP, "hipRTC compile failed: " + log.substr(0, 2000));
+    }
+    size_t n = 0;
+    RTCCHK(hiprtcGetCodeSize(prog, &n));
+    std::vector<char> code(n);
+    RTCCHK(hiprtcGetCode(prog, code.data()));
+    hiprtcDestroyProgram(&prog);
+    return code;
+}
+
+hipFunction_t jit_function(int device, const std::string& src) {
+    std::lock_guard<std::mutex> lk(g_jit_mu);
+    auto key = std::make_pair(device, src);
+    auto it = g_jit_cache.find(key);
+    if (it != g_jit_cache.end()) return it->second.fn;
+    std::vector<char> code = jit_compile(src);
+    JitKernel jk;
+    HIPCHK(hipModuleLoadData(&jk.module, code.data()));
+    HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
+    g_jit_cache[key] = jk;
+    return jk.fn;
+}
+
+// PM_JIT: "0" never, "1" always, default: databases of >= 64 Mi positions
+bool use_jit(const pm_db* db) {
+    const char* e = getenv("PM_JIT");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return db->n >= (64ull << 20);
+}
+
 // --- linear-scan dispatch ----------------------------------------------------
 // Lane shape (words per lane, double buffering).  The default is the
 // measured best; PM_LINEAR_SHAPE=<wpl><d|s> selects the experimental shapes
@@ -1347,8 +1645,9 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         require(n_iter * wave_words + 64 <= db->nwords, "internal: padding too small");
 
         // one upload: class byte tables, lengths, then one program per chunk
-        struct Chunk { int base, P, MW; size_t off; };
+        struct Chunk { int base, P, MW; size_t off; hipFunction_t jit; };
         std::vector<Chunk> chunks;
+        const bool jit = use_jit(db);
         Upload up;
         const size_t o_cb = up.add(class_bytes, (size_t)n_classes * 32);
         const size_t o_len = up.add(lengths, (size_t)n_patterns * 4);
@@ -1376,10 +1675,15 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                     const int c = pos_class[64 * (base + p) + j];
                     if (!class_is_any[c]) prog[1 + slot[c] * REC + 1 + p * MW + (j >> 5)] |= 1u << (j & 31);
                 }
-            chunks.push_back({base, P, MW, up.add(prog.data(), prog.size() * 4)});
+            hipFunction_t fn = nullptr;
+            if (jit)
+                fn = jit_function(db->device, gen_linear_source(P, k, MW, lengths + base, pos_class + 64 * base,
+                                                                class_acgt, class_is_any));
+            chunks.push_back({base, P, MW, up.add(prog.data(), prog.size() * 4), fn});
             base += P;
         }
         uint8_t* d_up = up.commit(db);
+        const uint64_t jit_iter = (start_words + 255) / 256;        // W = 4 words per lane
 
         uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
         SinkBuffers sb;
@@ -1390,6 +1694,15 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             sb = make_sink(db, expected);
             HIPCHK(hipEventRecord(ev.a, s));
             for (const Chunk& ch : chunks) {
+                if (ch.jit) {
+                    JArgsHost ja{db->hi, db->lo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xbytes,
+                                 reinterpret_cast<const uint32_t*>(d_up + o_cb), jit_iter, sb.out, sb.cnt, sb.cap,
+                                 ch.base};
+                    void* params[] = {&ja};
+                    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((jit_iter + 3) / 4, 256 * 16));
+                    HIPCHK(hipModuleLaunchKernel(ch.jit, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr));
+                    continue;
+                }
                 LinearArgs a{};
                 a.hi = db->hi; a.lo = db->lo; a.sbflag = db->sbflag; a.sbbase = db->sbbase;
                 a.xbrk = db->xbrk; a.xoth = db->xoth; a.xbytes = db->xbytes;
@@ -1421,6 +1734,25 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         }
         HIPCHK(hipStreamSynchronize(s));
         *out = h;
+    });
+}
+
+int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
+                          const uint8_t* class_acgt, const uint8_t* class_is_any, int k, uint64_t* code_bytes) {
+    return guarded([&] {
+        require(lengths && pos_class && class_acgt && class_is_any, "null argument");
+        require(n_patterns >= 1 && n_patterns <= 4, "n_patterns out of range for one specialized kernel");
+        require(n_classes >= 1 && n_classes <= 256, "n_classes out of range");
+        require(k >= 0 && k <= PM_MAX_K, "k out of range", PM_E_UNSUPPORTED);
+        int maxlen = 0;
+        for (int p = 0; p < n_patterns; ++p) {
+            require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
+            maxlen = std::max(maxlen, (int)lengths[p]);
+        }
+        const std::string src = gen_linear_source(n_patterns, k, maxlen > 32 ? 2 : 1, lengths, pos_class,
+                                                  class_acgt, class_is_any);
+        const std::vector<char> code = jit_compile(src);
+        if (code_bytes) *code_bytes = code.size();
     });
 }
 

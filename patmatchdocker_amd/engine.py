@@ -219,6 +219,16 @@ class LinearBatch:
         return out
 
 
+def jit_compile(progs: Sequence[Program], k: int) -> int:
+    """Generate + hipRTC-compile the specialized linear kernel (no GPU needed);
+    returns the code-object size in bytes."""
+    t = LinearBatch(progs)
+    nbytes = ctypes.c_uint64()
+    check(_lib.load().pm_linear_jit_compile(t.n, t.lengths.ctypes.data, t.pos_class.ctypes.data, t.nc,
+                                            t.acgt.ctypes.data, t.is_any.ctypes.data, k, ctypes.byref(nbytes)))
+    return nbytes.value
+
+
 def kernel_ms(handle) -> float:
     ms = ctypes.c_double()
     check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))

@@ -40,3 +40,16 @@ def test_no_fallback_when_library_missing(monkeypatch):
         pass
     else:
         raise AssertionError("missing library must fail loudly")
+
+
+def test_specialized_kernel_compiles_without_gpu():
+    """hipRTC generation + gfx950 compile of the pattern-specialized kernel."""
+    from patmatchdocker_amd import engine
+    from patmatchdocker_amd.convert import convert
+    from patmatchdocker_amd.regex import compile_pattern
+    fwd = convert("-n", "TGCTGASTCAGCANW")
+    progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+    for k in (0, 2):
+        assert engine.jit_compile(progs, k) > 1000
+    long_pat = [compile_pattern(convert("-n", "ACGT" * 12))]
+    assert engine.jit_compile(long_pat, 1) > 1000

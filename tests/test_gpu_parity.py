@@ -123,3 +123,37 @@ def test_synthetic_db_decode_and_scan(engine, oracle_mod):
         assert _gpu_pairs(res[0]) == _oracle_hits(oracle_mod, text, prog, 1)
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_specialized_linear_kernel(engine, oracle_mod, monkeypatch, k):
+    """The hipRTC pattern-specialized k_linear (PM_JIT=1) vs the oracle,
+    including N runs, lowercase, wrapped lines and 33..64-position patterns."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = dna_fasta(31 + k, n_records=5, max_len=6000, width=(70 if k % 2 else None))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in ["GAATTC", "TATAWAWR", "TGCTGASTCAGCANW", "ACGTACGTACGTACGTACGTACGTACGTACGTACG",
+                    "YYYYYYYYYYYYYYYYYYYYRRRRRRRRRRRRRRRRRRRRNNNNNNNNNNNNNNNNNNNNNNNN"]:
+            fwd = convert("-n", pat)
+            progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+            res, _ = engine.scan(db, progs, k=k, types="s")
+            for prog, r in zip(progs, res):
+                assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, k), (pat, prog.source, k)
+    finally:
+        db.close()
+
+
+def test_specialized_matches_generic_on_synthetic(engine, monkeypatch):
+    db = engine.SequenceDatabase.synthetic(n_records=40, rec_len=100_003, seed=9)
+    try:
+        fwd = convert("-n", "TGCTGASTCAGCANW")
+        progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+        monkeypatch.setenv("PM_JIT", "0")
+        generic, _ = engine.scan(db, progs, k=2, types="s")
+        monkeypatch.setenv("PM_JIT", "1")
+        special, _ = engine.scan(db, progs, k=2, types="s")
+        for g, s_ in zip(generic, special):
+            assert _gpu_pairs(g) == _gpu_pairs(s_)
+    finally:
+        db.close()

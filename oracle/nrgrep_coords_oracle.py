@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""CPU oracle behind an nrgrep_coords-style command line.  TEST INFRASTRUCTURE
+ONLY: used by tests/golden/make_e2e.py to run the reference's own Python
+pipeline (www/FlaskApp/FlaskApp/patmatch.py run_test) with this oracle in
+place of the prebuilt binary.  Prints "[beg, end]: match" lines."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from oracle import oracle  # noqa: E402
+from patmatchdocker_amd.regex import RegexSyntaxError, compile_pattern  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("-i", action="store_true")
+    ap.add_argument("-b")
+    ap.add_argument("-k", default="0")
+    ap.add_argument("pattern")
+    ap.add_argument("files", nargs="+")
+    a = ap.parse_args()
+    k = int("".join(ch for ch in a.k if ch.isdigit()) or 0)
+    types = "".join(ch for ch in a.k if ch in "idst") or "idst"
+    try:
+        prog = compile_pattern(a.pattern)
+    except RegexSyntaxError:
+        print("Syntax error in pattern %s" % a.pattern, file=sys.stderr)
+        return 1
+    for path in a.files:
+        text = open(path, "rb").read()
+        for b, e in oracle.scan(text, prog, k, types):
+            sys.stdout.write("[%d, %d]: %s\n" % (b, e, text[b:e].decode("latin-1")))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,79 @@
+"""End-to-end fixtures: the REFERENCE's run_test (www/FlaskApp/FlaskApp/
+patmatch.py:768-838, its Perl converter and generate_sequence_index.pl, its
+process_output) with oracle/nrgrep_coords_oracle.py standing in for the
+prebuilt nrgrep_coords binary.  Run in the dev container (needs
+/root/reference); writes tests/golden/e2e.json (inputs + outputs only)."""
+import importlib.util
+import json
+import os
+import shutil
+import sys
+import tempfile
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from tests.fastagen import dna_fasta, pep_fasta  # noqa: E402
+
+QUERIES = [
+    # pattern, seqtype, strand, insertion, deletion, substitution, mismatch, max_hits
+    ("GAATTC", "dna", None, None, None, None, None, 500),
+    ("TATAWAWR", "dna", "Both strands", None, None, None, None, "no limit"),
+    ("GAN{2,3}TC", "dna", None, None, None, None, None, 50),
+    ("<ATG", "dna", None, None, None, None, None, 500),
+    ("TAA>", "dna", None, None, None, None, None, 500),
+    ("CCAAT", "dna", "Watson strand", None, None, "substitution", "1", 100),
+    ("TGANTCA", "dna", "Reverse complement", None, None, "substitution", "2", 100),
+    ("GGNCC", "dna", None, None, None, "substitution", "1", 7),
+    ("CX{2,4}CX{3}[LIVMFYWC]", "pep", None, None, None, None, None, 500),
+    ("NXS", "pep", None, None, None, None, None, "no limit"),
+    ("[^P]CX", "pep", None, None, None, None, None, 500),
+    ("KDEL>", "pep", None, None, None, None, None, 500),
+    ("<MSK", "protein", None, None, None, None, None, 20),
+    ("<ATGNNN", "dna", "Both strands", None, None, None, None, 500),
+    ("NNNTAA>", "dna", None, None, None, None, None, 500),
+    ("RGD", "pep", None, None, None, "substitution", "1", 200),
+    ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
+    ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
+]
+
+
+def main():
+    tmp = tempfile.mkdtemp()
+    try:
+        files = {"orf_dna.seq": dna_fasta(101, 12, max_len=2500, noise=True)
+                 + b">orfA orfA desc\nATGAAACCCGGGAATTCTTTTAA\n>orfB\nATGCATGCTAA\n>orfC x\natgtataaaagtaa\n",
+                 "orf_pep.seq": pep_fasta(102, 60, max_len=500)
+                 + b">YPX1 X SGDID:S1, p\nMSKCAACGGGCLNASKDEL*\n>YPX2\nMSKDEL\n"}
+        for name, data in files.items():
+            open(os.path.join(tmp, name), "wb").write(data)
+        locus = "".join("YP%04d\tG%d\tS%06d\tprotein %d\n" % (r, r, r, r) for r in range(60))
+        locus += "".join("seq%d\tGENE%d\tS9%05d\tdna record %d\n" % (r, r, r, r) for r in range(0, 12, 2))
+        open(os.path.join(tmp, "locus.txt"), "w").write(locus)
+        spec = importlib.util.spec_from_file_location("ref_patmatch", REF + "/www/FlaskApp/FlaskApp/patmatch.py")
+        ref = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(ref)
+        ref.dataDir = tmp + "/"
+        ref.tmpDir = tmp + "/"
+        ref.patternConvertScript = REF + "/www/bin/patmatch_to_nrgrep.pl"
+        ref.seqIndexCreateScript = REF + "/www/bin/generate_sequence_index.pl"
+        ref.searchScript = os.path.join(ROOT, "oracle", "nrgrep_coords_oracle.py")
+        cases = []
+        for q in QUERIES:
+            pattern, seqtype, strand, ins, dele, sub, mm, maxhits = q
+            res = ref.run_test(pattern, seqtype=seqtype, strand=strand, insertion=ins, deletion=dele,
+                               substitution=sub, mismatch=mm, max_hits=maxhits)
+            dl = os.path.join(tmp, "patmatch.6688")
+            cases.append({"query": list(q), "result": list(res),
+                          "file": open(dl).read() if os.path.exists(dl) else None})
+            if os.path.exists(dl):
+                os.remove(dl)
+        json.dump({"files": {k: v.decode("latin-1") for k, v in files.items()}, "locus": locus, "cases": cases},
+                  open(os.path.join(HERE, "e2e.json"), "w"), indent=0)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

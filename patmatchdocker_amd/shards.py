@@ -44,8 +44,7 @@ def gather_hits(keys: torch.Tensor, lens: torch.Tensor, group=None, dst: int = 0
     Non-destination ranks return None.
     """
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        order = torch.argsort(keys)
-        return keys[order], lens[order]
+        return keys, lens          # one rank: the engine already sorted them
     world = dist.get_world_size(group)
     count = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
     counts = [torch.zeros_like(count) for _ in range(world)]

@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
-ROUND = "r01"
+ROUND = "r01b"
 
 
 def parse_args():
@@ -153,11 +153,12 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = bases_total * args.steps / elapsed / 1e9
         mean_kms = sum(kernel_ms) / len(kernel_ms)
-        # k_linear algorithmic bytes per launch: hi+lo planes over the scanned
-        # words (0.25 B/position) + one superblock flag word per 1024 positions
+        # algorithmic bytes per launch: the 2-bit code of every position of
+        # the file (hi + lo bit planes, 0.25 B/position); the stream tiles'
+        # halo words (+3.1 %) and lane flags are layout overhead, counted in
+        # `traffic` but not here
         positions = info["positions"]
-        scanned_words = -(-positions // 32)
-        alg_bytes = scanned_words * 8 + (-(-scanned_words // 32)) * 4
+        alg_bytes = -(-positions // 32) * 8
         achieved = alg_bytes / (mean_kms * 1e-3) / 1e9
         workload = "configs[2]: %s k=%d both strands vs %.0f Gbp synthetic DNA per GPU" % (
             args.motif, args.k, args.gbp)
@@ -181,9 +182,11 @@ def main():
                        "hits": n_hits, "parallelism": "shard-by-record x%d + RCCL hit gather" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": ("pm_linear_jit (hipRTC-specialized k_linear)" if jit else "k_linear<2,2,1>"),
+                         "kernel": ("pm_linear_jit (hipRTC-specialized, stream tiles + LDS-DMA ring)" if jit
+                                    else "k_linear_generic"),
                          "kernel_ms": round(mean_kms, 4),
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "note": "VALU-issue bound (see DESIGN.md §4)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             cb, ok = cpu_baseline(db, progs, args.k, args.sample_mbp * 1e6, result)

@@ -1,0 +1,509 @@
+// pm_db.hip -- the device-resident sequence database (pm_db_* entry points).
+//
+// Replaces nrgrep_coords' per-call read of '<datafile>'
+// (www/FlaskApp/FlaskApp/patmatch.py:733-742): the FASTA file is uploaded
+// once and kept in HBM in the stream-tile layout described in pm_internal.h
+// (nucleotides) or as folded bytes (peptides).  Header lines (/^>\S/, the
+// record names of generate_sequence_index.pl:33) and '\n' are record breaks.
+#include <hipcub/hipcub.hpp>
+
+#include "pm_internal.h"
+
+namespace pm {
+
+thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+namespace {
+
+// code of a folded byte: 0..3 = A C G T, 4 = delimiter, 5 = other
+__constant__ uint8_t c_code[256];
+
+void init_code_table() {
+    static bool done = false;
+    if (done) return;
+    uint8_t t[256];
+    for (int i = 0; i < 256; ++i) t[i] = 5;
+    t[(int)'A'] = 0; t[(int)'C'] = 1; t[(int)'G'] = 2; t[(int)'T'] = 3;
+    t[(int)'a'] = 0; t[(int)'c'] = 1; t[(int)'g'] = 2; t[(int)'t'] = 3;
+    t[(int)'\n'] = 4;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_code), t, sizeof(t)));
+    done = true;
+}
+
+// ---------------------------------------------------------------------------
+// packing kernels (one thread per logical word of the 2048 main words of a
+// tile; halo words are derived afterwards by k_fill_halo)
+// ---------------------------------------------------------------------------
+__global__ void k_pack_nuc(const uint8_t* __restrict__ raw, uint64_t n, uint64_t ntiles,
+                           uint2* __restrict__ hl, uint2* __restrict__ bo) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (g >= ntiles * STREAM) return;
+    const uint64_t t = g / STREAM;
+    const uint32_t w = (uint32_t)(g % STREAM);
+    uint32_t h = 0, l = 0, br = 0, ot = 0;
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint64_t p = pos_of(t, w, b);
+        const uint32_t c = p < n ? c_code[raw[p]] : 4u;
+        if (c < 4) {
+            h |= (c >> 1) << b;
+            l |= (c & 1) << b;
+        } else if (c == 4) {
+            br |= 1u << b;
+        } else {
+            ot |= 1u << b;
+        }
+    }
+    const uint64_t pw = phys_word(t, w);
+    hl[pw] = make_uint2(h, l);
+    bo[pw] = make_uint2(br, ot);
+}
+
+__device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+constexpr uint64_t SYN_HDR = 10;  // ">r%08u" then '\n'
+
+// Synthetic FASTA-shaped text: records of SYN_HDR header bytes + '\n' +
+// rec_len bases + '\n'; bases from a counter-based hash of (seed, word).
+__global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint64_t seed,
+                             uint2* __restrict__ hl, uint2* __restrict__ bo) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (g >= ntiles * STREAM) return;
+    const uint64_t t = g / STREAM;
+    const uint32_t w = (uint32_t)(g % STREAM);
+    const uint64_t stride = SYN_HDR + 1 + rec_len + 1;
+    const uint64_t r = mix64(seed * 0x9e3779b97f4a7c15ull + g);
+    uint32_t br = 0;
+    const uint64_t p0 = pos_of(t, w, 0);
+    uint64_t q = p0 % stride;
+    const uint64_t d = STREAM % stride;
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint64_t p = p0 + (uint64_t)b * STREAM;
+        const bool is_base = p < n && q >= SYN_HDR + 1 && q < SYN_HDR + 1 + rec_len;
+        if (!is_base) br |= 1u << b;
+        q += d;
+        if (q >= stride) q -= stride;
+    }
+    const uint64_t pw = phys_word(t, w);
+    hl[pw] = make_uint2((uint32_t)(r >> 32) & ~br, (uint32_t)r & ~br);
+    bo[pw] = make_uint2(br, 0u);
+}
+
+// Header lines become breaks: one thread per [beg, end) range.
+__global__ void k_mark_ranges(const uint64_t* __restrict__ ranges, uint64_t nr, uint2* __restrict__ bo) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= nr) return;
+    for (uint64_t p = ranges[2 * i]; p < ranges[2 * i + 1]; ++p) {
+        const Loc l = loc_of(p);
+        atomicOr(&bo[l.word].x, 1u << l.bit);
+    }
+}
+
+// Halo word i of tile t: bit b = bit b+1 of main word i (b < 31), bit 31 =
+// bit 0 of main word i of tile t+1 (a break past the last tile).
+__global__ void k_fill_halo(uint64_t ntiles, uint2* __restrict__ hl, uint2* __restrict__ bo) {
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (g >= ntiles * HALO) return;
+    const uint64_t t = g / HALO;
+    const uint32_t i = (uint32_t)(g % HALO);
+    const uint64_t src = phys_word(t, i);
+    const uint64_t dst = phys_word(t, (uint32_t)STREAM + i);
+    const bool last = t + 1 >= ntiles;
+    const uint64_t nxt = last ? src : phys_word(t + 1, i);
+    auto shift_in = [](uint32_t cur, uint32_t next_bit) { return (cur >> 1) | (next_bit << 31); };
+    const uint2 a = hl[src], b = bo[src];
+    const uint2 an = last ? make_uint2(0u, 0u) : hl[nxt];
+    const uint2 bn = last ? make_uint2(1u, 0u) : bo[nxt];
+    hl[dst] = make_uint2(shift_in(a.x, an.x & 1u), shift_in(a.y, an.y & 1u));
+    bo[dst] = make_uint2(shift_in(b.x, bn.x & 1u), shift_in(b.y, bn.y & 1u));
+}
+
+// superblock flags (32 physical words each)
+__global__ void k_sb_flags(const uint2* __restrict__ bo, uint64_t nsb, uint32_t* __restrict__ sbflag,
+                           uint32_t* __restrict__ sbcnt) {
+    const uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (s >= nsb) return;
+    uint32_t f = 0;
+    for (int i = 0; i < 32; ++i) {
+        const uint64_t w = s * 32 + i;
+        const uint2 e = bo[w];
+        if (e.x | e.y) f |= 1u << i;
+    }
+    sbflag[s] = f;
+    sbcnt[s] = __popc(f);
+}
+
+__global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, uint64_t nwords,
+                                  const uint2* __restrict__ bo,
+                                  const uint32_t* __restrict__ sbflag, const uint32_t* __restrict__ sbbase,
+                                  uint32_t* __restrict__ xbrk, uint32_t* __restrict__ xoth,
+                                  uint64_t* __restrict__ xword, uint8_t* __restrict__ xbytes) {
+    const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    const uint32_t f = sbflag[w >> 5];
+    const uint32_t bit = (uint32_t)(w & 31);
+    if (!((f >> bit) & 1)) return;
+    const uint64_t idx = sbbase[w >> 5] + __popc(f & ((1u << bit) - 1));
+    const uint2 e = bo[w];
+    const uint32_t br = e.x, ot = e.y & ~br;
+    xbrk[idx] = br;
+    xoth[idx] = ot;
+    xword[idx] = w;
+    const uint64_t t = w / TILE_WORDS;
+    const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
+    for (uint32_t i = 0; i < 32; ++i) {
+        const uint64_t p = pos_of(t, lw, i);
+        uint8_t c = '\n';
+        if (((ot >> i) & 1) && raw != nullptr && p < n) c = fold(raw[p]);
+        xbytes[idx * 32 + i] = c;
+    }
+}
+
+// oth = oth & ~brk everywhere (a header byte is a break, not an "other")
+__global__ void k_clean_oth(uint64_t nwords, uint2* __restrict__ bo) {
+    const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (w < nwords) bo[w].y &= ~bo[w].x;
+}
+
+// lflag[t] bit l: lane l of tile t sees brk|oth in logical words
+// [32 l, 32 l + 32 + HALO - 1).  One wave per tile.
+__global__ void k_lane_flags(uint64_t ntiles, const uint2* __restrict__ bo, uint64_t* __restrict__ lflag) {
+    const uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (t >= ntiles) return;
+    bool any = false;
+    for (uint32_t i = 0; i < LANE_WORDS + HALO - 1; ++i) {
+        const uint32_t w = lane * LANE_WORDS + i;
+        if (w >= TILE_WORDS) break;
+        const uint2 e = bo[phys_word(t, w)];
+        any |= (e.x | e.y) != 0;
+    }
+    const uint64_t bal = __ballot(any);
+    if (lane == 0) lflag[t] = bal;
+}
+
+__global__ void k_pack_bytes(const uint8_t* __restrict__ raw, uint64_t n, uint64_t nalloc,
+                             uint8_t* __restrict__ out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= nalloc) return;
+    out[i] = i < n ? fold(raw[i]) : (uint8_t)'\n';
+}
+
+__global__ void k_mark_ranges_bytes(const uint64_t* __restrict__ ranges, uint64_t nr, uint8_t* __restrict__ bytes) {
+    const uint64_t i = blockIdx.x;
+    if (i >= nr) return;
+    const uint64_t b = ranges[2 * i], e = ranges[2 * i + 1];
+    for (uint64_t p = b + threadIdx.x; p < e; p += blockDim.x) bytes[p] = '\n';
+}
+
+__global__ void k_decode(NucView v, uint64_t beg, uint32_t len, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < len) out[i] = nuc_char_at(v, beg + i);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <class T>
+T* dalloc(pm_db* db, uint64_t count) {
+    void* p = nullptr;
+    if (count == 0) count = 1;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    db->device_bytes += count * sizeof(T);
+    return static_cast<T*>(p);
+}
+
+template <class T>
+T* tmp_alloc(std::vector<void*>& owned, uint64_t count) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, std::max<uint64_t>(count, 1) * sizeof(T)));
+    owned.push_back(p);
+    return static_cast<T*>(p);
+}
+
+void free_all(pm_db* db, std::vector<void*>& owned) {
+    HIPCHK(hipStreamSynchronize(db->stream));
+    for (void* p : owned) HIPCHK(hipFree(p));
+    owned.clear();
+}
+
+// header lines (/^>\S/) as [beg, end) ranges, end excluding the '\n'
+std::vector<uint64_t> header_ranges(const uint8_t* t, uint64_t n) {
+    std::vector<uint64_t> r;
+    uint64_t p = 0;
+    while (p < n) {
+        const void* nl = memchr(t + p, '\n', n - p);
+        const uint64_t e = nl ? (uint64_t)((const uint8_t*)nl - t) : n;
+        if (t[p] == '>' && p + 1 < e) {
+            const uint8_t c = t[p + 1];
+            const bool space = c == ' ' || c == '\t' || c == '\r' || c == '\f' || c == '\v';
+            if (!space) { r.push_back(p); r.push_back(e); }
+        }
+        p = e + 1;
+    }
+    return r;
+}
+
+// Tiles cover the file plus room for the longest NFA halo after the last
+// chunk; every position >= n is a break.
+uint64_t tiles_for(uint64_t n) { return (n + MAX_NFA_CHUNK + 2048 + TILE_POS - 1) / TILE_POS; }
+
+void alloc_planes(pm_db* db) {
+    db->ntiles = tiles_for(db->n);
+    db->nwords = db->ntiles * TILE_WORDS;
+    db->nsb = db->nwords / 32;
+    db->hl = dalloc<uint2>(db, db->nwords + 128);   // + LDS-DMA over-read of the last tile
+    db->bo = dalloc<uint2>(db, db->nwords);
+    db->lflag = dalloc<uint64_t>(db, db->ntiles);
+}
+
+// halo words, flags, compacted exception side tables, lane flags
+void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw) {
+    hipStream_t s = db->stream;
+    hipLaunchKernelGGL(k_clean_oth, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, db->nwords, db->bo);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fill_halo, dim3(blocks_for(db->ntiles * HALO, 256)), dim3(256), 0, s, db->ntiles, db->hl,
+                       db->bo);
+    HIPCHK(hipGetLastError());
+    db->sbflag = dalloc<uint32_t>(db, db->nsb);
+    db->sbbase = dalloc<uint32_t>(db, db->nsb);
+    uint32_t* sbcnt = tmp_alloc<uint32_t>(owned, db->nsb);
+    hipLaunchKernelGGL(k_sb_flags, dim3(blocks_for(db->nsb, 256)), dim3(256), 0, s, db->bo, db->nsb, db->sbflag,
+                       sbcnt);
+    HIPCHK(hipGetLastError());
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
+    void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
+    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
+    HIPCHK(hipMemcpyAsync(h, db->sbbase + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + 1, sbcnt + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    db->nflag = (uint64_t)h[0] + h[1];
+    db->xbrk = dalloc<uint32_t>(db, db->nflag);
+    db->xoth = dalloc<uint32_t>(db, db->nflag);
+    db->xword = dalloc<uint64_t>(db, db->nflag);
+    db->xbytes = dalloc<uint8_t>(db, db->nflag * 32);
+    hipLaunchKernelGGL(k_fill_exceptions, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, d_raw, db->n,
+                       db->nwords, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword,
+                       db->xbytes);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_lane_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
+                       db->lflag);
+    HIPCHK(hipGetLastError());
+}
+
+void init_stream(pm_db* db, void* stream) {
+    if (stream) {
+        db->stream = (hipStream_t)stream;
+    } else {
+        HIPCHK(hipStreamCreate(&db->stream));   // blocking: ordered with the null stream
+        db->own_stream = true;
+    }
+}
+
+void free_db(pm_db* db) {
+    if (!db) return;
+    if (db->stream) (void)hipStreamSynchronize(db->stream);
+    void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
+                    db->lflag, db->bytes, db->ws_tab.p, db->ws_sink.p, db->ws_post.p};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (db->pin_up.p) (void)hipHostFree(db->pin_up.p);
+    if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
+    if (db->own_stream && db->stream) (void)hipStreamDestroy(db->stream);
+    delete db;
+}
+
+void check_device(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw failure(PM_E_NODEV, "no HIP device");
+    require(device >= 0 && device < ndev, "device out of range");
+}
+
+}  // namespace
+
+// Grow a workspace.  Growing waits for the stream first, so no queued work
+// can still reference the old allocation.
+void* reserve(pm_db* db, pm_devbuf& b, size_t bytes) {
+    if (b.cap < bytes) {
+        HIPCHK(hipStreamSynchronize(db->stream));
+        if (b.p) HIPCHK(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+        HIPCHK(hipMalloc(&b.p, want));
+        b.cap = want;
+    }
+    return b.p;
+}
+
+void* reserve_host(pm_db* db, pm_hostbuf& b, size_t bytes) {
+    if (b.cap < bytes) {
+        HIPCHK(hipStreamSynchronize(db->stream));
+        if (b.p) HIPCHK(hipHostFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+        HIPCHK(hipHostMalloc(&b.p, want, hipHostMallocDefault));
+        b.cap = want;
+    }
+    return b.p;
+}
+
+uint8_t* Upload::commit(pm_db* db) {
+    uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_tab, std::max<size_t>(blob.size(), 256)));
+    uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_up, std::max<size_t>(blob.size(), 256)));
+    memcpy(h, blob.data(), blob.size());
+    HIPCHK(hipMemcpyAsync(d, h, blob.size(), hipMemcpyHostToDevice, db->stream));
+    return d;
+}
+
+NucView nuc_view(const pm_db* db) {
+    return NucView{db->hl, db->bo, db->sbflag, db->sbbase, db->xbytes};
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+const char* pm_last_error(void) { return g_err.c_str(); }
+const char* pm_version(void) { return "patmatch_hip 0.3 (gfx950, stream-tile layout)"; }
+
+int pm_device_count(int* count) {
+    return guarded([&] {
+        require(count != nullptr, "count is NULL");
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        *count = c;
+    });
+}
+
+int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, void* stream, pm_db** out) {
+    pm_db* db = nullptr;
+    std::vector<void*> owned;
+    int rc = guarded([&] {
+        require(out != nullptr && (fasta != nullptr || n == 0), "null argument");
+        require(alphabet == PM_ALPHA_NUC || alphabet == PM_ALPHA_BYTE, "unknown alphabet");
+        check_device(device);
+        DeviceGuard g(device);
+        init_code_table();
+        db = new pm_db();
+        db->device = device;
+        db->alphabet = alphabet;
+        db->n = n;
+        init_stream(db, stream);
+        hipStream_t s = db->stream;
+        const std::vector<uint64_t> ranges = header_ranges(fasta, n);
+        const uint64_t nr = ranges.size() / 2;
+        uint64_t* d_ranges = tmp_alloc<uint64_t>(owned, ranges.size());
+        if (nr) HIPCHK(hipMemcpy(d_ranges, ranges.data(), ranges.size() * 8, hipMemcpyHostToDevice));
+        uint8_t* d_raw = tmp_alloc<uint8_t>(owned, n + 64);
+        if (n) HIPCHK(hipMemcpy(d_raw, fasta, n, hipMemcpyHostToDevice));
+        if (alphabet == PM_ALPHA_NUC) {
+            alloc_planes(db);
+            hipLaunchKernelGGL(k_pack_nuc, dim3(blocks_for(db->ntiles * STREAM, 256)), dim3(256), 0, s, d_raw, n,
+                               db->ntiles, db->hl, db->bo);
+            HIPCHK(hipGetLastError());
+            if (nr) {
+                hipLaunchKernelGGL(k_mark_ranges, dim3(blocks_for(nr, 64)), dim3(64), 0, s, d_ranges, nr, db->bo);
+                HIPCHK(hipGetLastError());
+            }
+            finish_nuc(db, owned, d_raw);
+        } else {
+            db->nbytes_alloc = round_up(n + BYTE_PAD, 4096);
+            db->bytes = dalloc<uint8_t>(db, db->nbytes_alloc);
+            hipLaunchKernelGGL(k_pack_bytes, dim3(blocks_for(db->nbytes_alloc, 256)), dim3(256), 0, s, d_raw, n,
+                               db->nbytes_alloc, db->bytes);
+            HIPCHK(hipGetLastError());
+            if (nr) {
+                hipLaunchKernelGGL(k_mark_ranges_bytes, dim3((uint32_t)nr), dim3(256), 0, s, d_ranges, nr, db->bytes);
+                HIPCHK(hipGetLastError());
+            }
+        }
+        free_all(db, owned);
+        *out = db;
+    });
+    if (rc != PM_OK) {
+        if (db && db->stream) (void)hipStreamSynchronize(db->stream);
+        for (void* p : owned) (void)hipFree(p);
+        free_db(db);
+    }
+    return rc;
+}
+
+int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, int device, void* stream,
+                           pm_db** out) {
+    pm_db* db = nullptr;
+    std::vector<void*> owned;
+    int rc = guarded([&] {
+        require(out != nullptr && n_records > 0 && rec_len > 0, "bad synthetic shape");
+        check_device(device);
+        DeviceGuard g(device);
+        init_code_table();
+        db = new pm_db();
+        db->device = device;
+        db->alphabet = PM_ALPHA_NUC;
+        db->n = n_records * (SYN_HDR + 1 + rec_len + 1);
+        init_stream(db, stream);
+        alloc_planes(db);
+        hipLaunchKernelGGL(k_pack_synth, dim3(blocks_for(db->ntiles * STREAM, 256)), dim3(256), 0, db->stream,
+                           db->n, db->ntiles, rec_len, seed, db->hl, db->bo);
+        HIPCHK(hipGetLastError());
+        finish_nuc(db, owned, nullptr);
+        free_all(db, owned);
+        *out = db;
+    });
+    if (rc != PM_OK) {
+        if (db && db->stream) (void)hipStreamSynchronize(db->stream);
+        for (void* p : owned) (void)hipFree(p);
+        free_db(db);
+    }
+    return rc;
+}
+
+int pm_db_destroy(pm_db* db) {
+    return guarded([&] {
+        if (!db) return;
+        DeviceGuard g(db->device);
+        free_db(db);
+    });
+}
+
+int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet, uint64_t* n_exception_words,
+               uint64_t* device_bytes) {
+    return guarded([&] {
+        require(db != nullptr, "db is NULL");
+        if (n_positions) *n_positions = db->n;
+        if (alphabet) *alphabet = db->alphabet;
+        if (n_exception_words) *n_exception_words = db->nflag;
+        if (device_bytes) *device_bytes = db->device_bytes;
+    });
+}
+
+int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out) {
+    return guarded([&] {
+        require(db != nullptr && out != nullptr, "null argument");
+        require(beg + len <= db->n, "decode range outside the database");
+        if (len == 0) return;
+        DeviceGuard g(db->device);
+        uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_post, len));
+        if (db->alphabet == PM_ALPHA_NUC) {
+            hipLaunchKernelGGL(k_decode, dim3(blocks_for(len, 256)), dim3(256), 0, db->stream, nuc_view(db), beg, len, d);
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipMemcpyAsync(d, db->bytes + beg, len, hipMemcpyDeviceToDevice, db->stream));
+        }
+        HIPCHK(hipStreamSynchronize(db->stream));
+        HIPCHK(hipMemcpy(out, d, len, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

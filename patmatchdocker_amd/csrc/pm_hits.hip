@@ -1,0 +1,313 @@
+// pm_hits.hip -- hit collection: bins -> one sorted (pattern, beg) list, and
+// the pm_hits_* entry points.
+//
+// The reference reads hits as nrgrep_coords' "[beg, end]: match" lines, one
+// run per pattern/strand, each in increasing beg order (parsed at
+// www/FlaskApp/FlaskApp/patmatch.py:505-531).  Here every scan kernel pushes
+// 64-bit keys (pattern << 48 | beg) into bins that partition (pattern,
+// position) space in increasing order; each bin is sorted in LDS by one
+// workgroup and written at its exclusive offset, which yields the same
+// order as the reference's concatenated runs without a global sort.  Bins
+// too large for LDS fall back to a device radix sort of everything.
+#include <hipcub/hipcub.hpp>
+
+#include <map>
+#include <mutex>
+
+#include "pm_internal.h"
+
+namespace pm {
+namespace {
+
+// bin counters -> exclusive offsets; one block of 1024 threads, each owning a
+// contiguous run of bins
+__global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict__ cnt, uint32_t nbins,
+                                                      uint32_t cap, uint64_t* __restrict__ off) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nbins + 1023) / 1024;
+    const uint32_t b0 = t * per, b1 = min(nbins, b0 + per);
+    uint64_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += min(cnt[b], cap);
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t acc = part[t] - s;
+    for (uint32_t b = b0; b < b1; ++b) {
+        off[b] = acc;
+        acc += min(cnt[b], cap);
+    }
+}
+
+// One workgroup per bin: bitonic sort in LDS, write at the bin's offset.
+__global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
+                                                   const uint64_t* __restrict__ off, uint32_t cap,
+                                                   uint64_t* __restrict__ dst) {
+    __shared__ uint64_t s[LDS_SORT_CAP];
+    const uint32_t bin = blockIdx.x;
+    const uint32_t c = min(cnt[bin], cap);
+    if (c == 0) return;
+    const uint64_t* src = out + (uint64_t)bin * cap;
+    uint64_t* d = dst + off[bin];
+    if (c == 1) {
+        if (threadIdx.x == 0) d[0] = src[0];
+        return;
+    }
+    uint32_t n2 = 2;
+    while (n2 < c) n2 <<= 1;
+    for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) s[i] = i < c ? src[i] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += blockDim.x) {
+                const uint32_t ix = i ^ j;
+                if (ix > i) {
+                    const uint64_t a = s[i], b = s[ix];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { s[i] = b; s[ix] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) d[i] = s[i];
+}
+
+__global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
+                              const uint64_t* __restrict__ off, uint32_t cap, uint64_t* __restrict__ dst) {
+    const uint32_t bin = blockIdx.x;
+    const uint32_t c = min(cnt[bin], cap);
+    const uint64_t o = off[bin];
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = out[(uint64_t)bin * cap + i];
+}
+
+std::mutex g_pool_mu;
+std::map<std::pair<int, size_t>, std::vector<void*>> g_pool;   // (device, capacity) -> free buffers
+
+}  // namespace
+
+void* pool_get(int device, size_t bytes, size_t* cap) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    *cap = c;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto it = g_pool.find({device, c});
+        if (it != g_pool.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            return p;
+        }
+    }
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, c));
+    return p;
+}
+
+void hits_ready(pm_db* db, pm_hits* h) {
+    if (!h->ready) HIPCHK(hipEventCreateWithFlags(&h->ready, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->ready, db->stream));
+}
+
+void pool_put(int device, void* p, size_t cap) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto& v = g_pool[{device, cap}];
+    if (v.size() < 8) v.push_back(p);
+    else (void)hipFree(p);
+}
+
+SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected) {
+    SinkBuffers sb;
+    require(n_slots >= 1 && (uint32_t)n_slots <= MAX_BINS, "internal: too many pattern slots");
+    sb.bins_per_pattern = std::max<uint32_t>(1, NBINS / (uint32_t)n_slots);
+    sb.pos_shift = 0;
+    const uint64_t last = std::max<uint64_t>(n_positions, 1) - 1;
+    while ((last >> sb.pos_shift) >= sb.bins_per_pattern) ++sb.pos_shift;
+    sb.nbins = (uint32_t)n_slots * sb.bins_per_pattern;
+    uint64_t cap = std::max<uint64_t>(1024, (expected + sb.nbins - 1) / sb.nbins * 2);
+    cap = std::min<uint64_t>(cap, 1ull << 26);
+    sb.cap = (uint32_t)cap;
+    Carve c;
+    const size_t o_out = c.take((uint64_t)sb.nbins * sb.cap * sizeof(uint64_t));
+    const size_t o_cnt = c.take(sb.nbins * sizeof(uint32_t));
+    uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
+    sb.out = reinterpret_cast<uint64_t*>(base + o_out);
+    sb.cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    HIPCHK(hipMemsetAsync(sb.cnt, 0, sb.nbins * sizeof(uint32_t), db->stream));
+    return sb;
+}
+
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, uint32_t cap) {
+    SinkBuffers sb;
+    require(n_slots >= 1 && per_slot >= 1, "internal: bad segment shape");
+    sb.bins_per_pattern = per_slot;
+    sb.pos_shift = 0;
+    sb.nbins = (uint32_t)n_slots * per_slot;
+    sb.cap = cap;
+    Carve c;
+    const size_t o_out = c.take((uint64_t)sb.nbins * sb.cap * sizeof(uint64_t));
+    const size_t o_cnt = c.take(sb.nbins * sizeof(uint32_t));
+    uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
+    sb.out = reinterpret_cast<uint64_t*>(base + o_out);
+    sb.cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    HIPCHK(hipMemsetAsync(sb.cnt, 0, sb.nbins * sizeof(uint32_t), db->stream));
+    return sb;
+}
+
+uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow) {
+    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, sb.nbins * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(h, sb.cnt, sb.nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, db->stream));
+    HIPCHK(hipStreamSynchronize(db->stream));
+    counts.assign(h, h + sb.nbins);
+    uint64_t total = 0;
+    overflow = false;
+    for (uint32_t c : counts) {
+        total += c;
+        overflow |= c > sb.cap;
+    }
+    return total;
+}
+
+pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total) {
+    hipStream_t s = db->stream;
+    pm_hits* h = new pm_hits();
+    h->device = db->device;
+    h->count = total;
+    try {
+        h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(total, 1) * sizeof(uint64_t),
+                                                  &h->keys_cap));
+        h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(total, 1) * sizeof(uint32_t),
+                                                  &h->lens_cap));
+        if (total == 0) return h;
+        const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
+        const bool lds = maxc <= LDS_SORT_CAP;
+        size_t sort_bytes = 0;
+        if (!lds)
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                     (int)total, 0, 64, s));
+        Carve c;
+        const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
+        const size_t o_uns = lds ? 0 : c.take(total * sizeof(uint64_t));
+        const size_t o_tmp = lds ? 0 : c.take(sort_bytes);
+        uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
+        uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
+        hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sb.cap, d_off);
+        HIPCHK(hipGetLastError());
+        if (lds) {
+            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sb.cap, h->keys);
+            HIPCHK(hipGetLastError());
+        } else {
+            uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
+            hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sb.cap,
+                               unsorted);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0, 64,
+                                                     s));
+        }
+    } catch (...) {
+        pool_put(h->device, h->keys, h->keys_cap);
+        pool_put(h->device, h->lens, h->lens_cap);
+        delete h;
+        throw;
+    }
+    return h;
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" {
+
+int pm_hits_count(const pm_hits* h, uint64_t* count) {
+    return guarded([&] {
+        require(h != nullptr && count != nullptr, "null argument");
+        *count = h->count;
+    });
+}
+
+int pm_hits_copy(const pm_hits* h, int32_t* pattern, int64_t* beg, int64_t* end, uint64_t max_count) {
+    return guarded([&] {
+        require(h != nullptr, "hits is NULL");
+        const uint64_t n = std::min<uint64_t>(h->count, max_count);
+        if (n == 0) return;
+        DeviceGuard g(h->device);
+        std::vector<uint64_t> keys(n);
+        std::vector<uint32_t> lens(n);
+        if (h->ready) HIPCHK(hipEventSynchronize(h->ready));
+        HIPCHK(hipMemcpy(keys.data(), h->keys, n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(lens.data(), h->lens, n * 4, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n; ++i) {
+            const int64_t b = (int64_t)(keys[i] & ((1ull << 48) - 1));
+            if (pattern) pattern[i] = (int32_t)(keys[i] >> 48);
+            if (beg) beg[i] = b;
+            if (end) end[i] = b + (int64_t)lens[i];
+        }
+    });
+}
+
+int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst, uint64_t max_count,
+                        void* stream) {
+    return guarded([&] {
+        require(h != nullptr, "hits is NULL");
+        const uint64_t n = std::min<uint64_t>(h->count, max_count);
+        if (n == 0) return;
+        DeviceGuard g(h->device);
+        hipStream_t s = (hipStream_t)stream;
+        if (h->ready && s) HIPCHK(hipStreamWaitEvent(s, h->ready, 0));
+        if (h->ready && !s) HIPCHK(hipEventSynchronize(h->ready));
+        if (keys_dst) HIPCHK(hipMemcpyAsync(keys_dst, h->keys, n * 8, hipMemcpyDeviceToDevice, s));
+        if (lens_dst) HIPCHK(hipMemcpyAsync(lens_dst, h->lens, n * 4, hipMemcpyDeviceToDevice, s));
+        if (!stream) {
+            HIPCHK(hipStreamSynchronize(s));
+        } else {   // pm_hits_destroy waits for this copy before recycling the buffers
+            pm_hits* hm = const_cast<pm_hits*>(h);
+            if (!hm->last_use) HIPCHK(hipEventCreateWithFlags(&hm->last_use, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(hm->last_use, s));
+        }
+    });
+}
+
+int pm_hits_kernel_ms(const pm_hits* h, double* ms) {
+    return guarded([&] {
+        require(h != nullptr && ms != nullptr, "null argument");
+        *ms = h->kernel_ms;
+    });
+}
+
+int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count) {
+    return guarded([&] {
+        require(h != nullptr, "hits is NULL");
+        if (keys) *keys = h->keys;
+        if (lens) *lens = h->lens;
+        if (count) *count = h->count;
+    });
+}
+
+int pm_hits_destroy(pm_hits* h) {
+    return guarded([&] {
+        if (!h) return;
+        DeviceGuard g(h->device);
+        // the producing stream's work and any async copy out must be done
+        // before the buffers go back to the pool
+        if (h->ready) {
+            HIPCHK(hipEventSynchronize(h->ready));
+            (void)hipEventDestroy(h->ready);
+        }
+        if (h->last_use) {
+            HIPCHK(hipEventSynchronize(h->last_use));
+            (void)hipEventDestroy(h->last_use);
+        }
+        pool_put(h->device, h->keys, h->keys_cap);
+        pool_put(h->device, h->lens, h->lens_cap);
+        delete h;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,327 @@
+// pm_internal.h -- shared internals of libpatmatch_hip.so (not part of the ABI).
+//
+// The public boundary is include/patmatch_hip.h; everything here is private
+// to the library's translation units (pm_db.hip, pm_hits.hip, pm_linear.hip,
+// pm_nfa.hip).
+//
+// Nucleotide database layout ("stream tiles")
+// ---------------------------------------------------------
+// The file is cut into tiles of TILE_POS = 65536 positions.  Inside a tile,
+// bit b (0..31) of logical word w (0..2047) holds position
+//        T * 65536 + b * 2048 + w,
+// i.e. each of the 32 bits of a word walks its own 2048-position "stream".
+// Consequence: the window starting at (w, b) reads its j-th position from
+// bit b of word w + j -- no bit shifts at all in the scan kernels, a pattern
+// position is just a register index.  The logical words of a tile are stored
+// lane-interleaved (physical (w % 32) * 64 + w / 32), so a wave whose lane l
+// owns logical words [32 l, 32 l + 32) loads them with perfectly coalesced
+// dword loads.  A tile stores HALO more logical words 2048..2111 (the
+// continuation of every stream into the next one: bit b of word 2048 + i is
+// position T * 65536 + (b + 1) * 2048 + i), so windows near a stream end need
+// no neighbour-tile access.  The formula pos = T * 65536 + b * 2048 + w holds
+// for halo words too.
+//
+// Planes per physical word, stored as two uint2 arrays: hl = {hi, lo} (2-bit
+// code A=00 C=01 G=10 T=11, folded case) and bo = {brk, oth}: brk = the
+// position is a record break ('\n', a header-line byte, or past the end of
+// the file), oth = any other non-ACGT byte (N, IUPAC letters, '\r', ...).
+// One dwordx2 load per word gives both bits of every base.  Sparse side tables give the exact byte of every
+// exception position: sbflag (1 bit per physical word with brk|oth, 32 words
+// per u32), sbbase (exclusive prefix), xbrk/xoth masks, the physical word
+// index (xword) and 32 folded bytes per flagged word.  lflag has one u64 per
+// tile: bit l = lane l of the tile sees an exception among its 32 words and
+// the HALO-1 words after them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "patmatch_hip.h"
+
+namespace pm {
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+struct failure : std::runtime_error {
+    int code;
+    failure(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            throw ::pm::failure(PM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+void set_error(const std::string& msg);
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return PM_OK;
+    } catch (const failure& e) {
+        set_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return PM_E_ARG;
+    }
+}
+
+inline void require(bool ok, const char* msg, int code = PM_E_ARG) {
+    if (!ok) throw failure(code, msg);
+}
+
+// ---------------------------------------------------------------------------
+// layout constants
+// ---------------------------------------------------------------------------
+constexpr int LANE_WORDS = 32;                       // logical words per lane
+constexpr int TILE_LANES = 64;                       // one wave per tile
+constexpr uint64_t STREAM = LANE_WORDS * TILE_LANES; // 2048 positions per stream
+constexpr uint64_t TILE_POS = 32 * STREAM;           // 65536 positions per tile
+constexpr int HALO = 64;                             // halo words per tile (63 used)
+constexpr uint64_t TILE_WORDS = STREAM + HALO;       // 2112 physical words per tile
+constexpr int MAX_WINDOW = HALO;                     // longest linear pattern (64)
+constexpr uint32_t NBINS = 1024;                     // hit bins (at least)
+constexpr uint32_t MAX_BINS = 8192;
+constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_nfa_rev
+constexpr uint32_t LDS_SORT_CAP = 4096;              // keys per bin sorted in LDS (32 KB)
+constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
+
+__host__ __device__ inline uint8_t fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// physical word index of logical word w (0 <= w < TILE_WORDS) of tile t
+__host__ __device__ inline uint64_t phys_word(uint64_t tile, uint32_t w) {
+    return tile * TILE_WORDS + (w < STREAM ? (uint64_t)((w & 31u) * 64u + (w >> 5)) : (uint64_t)w);
+}
+// logical word of physical offset r (0 <= r < TILE_WORDS) inside its tile
+__host__ __device__ inline uint32_t logical_word(uint32_t r) {
+    return r < STREAM ? (r & 63u) * 32u + (r >> 6) : r;
+}
+// file position of bit b of logical word w of tile t (valid for halo words)
+__host__ __device__ inline uint64_t pos_of(uint64_t tile, uint32_t w, uint32_t b) {
+    return tile * TILE_POS + (uint64_t)b * STREAM + w;
+}
+struct Loc {
+    uint64_t word;   // physical word
+    uint32_t bit;
+};
+__host__ __device__ inline Loc loc_of(uint64_t p) {
+    const uint64_t t = p / TILE_POS;
+    const uint32_t q = (uint32_t)(p % TILE_POS);
+    return Loc{phys_word(t, q % (uint32_t)STREAM), q / (uint32_t)STREAM};
+}
+
+inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+inline uint32_t blocks_for(uint64_t n, uint32_t threads) {
+    return (uint32_t)std::max<uint64_t>(1, (n + threads - 1) / threads);
+}
+
+// ---------------------------------------------------------------------------
+// device views
+// ---------------------------------------------------------------------------
+struct NucView {
+    const uint2 *hl, *bo;
+    const uint32_t *sbflag, *sbbase;
+    const uint8_t* xbytes;
+};
+
+// index of flagged physical word w in the compacted side tables
+__device__ inline uint32_t exception_index(const uint32_t* sbflag, const uint32_t* sbbase, uint64_t w) {
+    const uint32_t f = sbflag[w >> 5];
+    const uint32_t wb = (uint32_t)(w & 31);
+    return sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
+}
+
+// folded byte at file position p ('\n' for breaks and the tail padding)
+__device__ inline uint8_t nuc_char_at(const NucView& v, uint64_t p) {
+    const Loc l = loc_of(p);
+    const uint2 e = v.bo[l.word];
+    if ((e.x >> l.bit) & 1) return (uint8_t)'\n';
+    if ((e.y >> l.bit) & 1) {
+        const uint32_t idx = exception_index(v.sbflag, v.sbbase, l.word);
+        return v.xbytes[(uint64_t)idx * 32 + l.bit];
+    }
+    const uint2 d = v.hl[l.word];
+    const uint32_t code = (((d.x >> l.bit) & 1) << 1) | ((d.y >> l.bit) & 1);
+    return (uint8_t)((0x54474341u >> (8 * code)) & 0xff);   // "ACGT"
+}
+
+// Hit sink: NBINS bins of `cap` keys.  Bins are ranges of (pattern, position)
+// in increasing order, so sorting every bin sorts the whole list.
+struct Sink {
+    uint64_t* out;       // [NBINS * cap]
+    uint32_t* bin_cnt;   // [NBINS]
+    uint32_t cap;
+    uint32_t bins_per_pattern;
+    uint32_t pos_shift;  // bin within a pattern = position >> pos_shift
+    __device__ uint32_t bin_of(uint32_t pattern_slot, uint64_t pos) const {
+        return pattern_slot * bins_per_pattern + (uint32_t)(pos >> pos_shift);
+    }
+    __device__ void push(uint32_t bin, uint64_t key) const {
+        const uint32_t o = atomicAdd(&bin_cnt[bin], 1u);
+        if (o < cap) out[(uint64_t)bin * cap + o] = key;
+    }
+};
+
+__device__ inline uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+}  // namespace pm
+
+// ---------------------------------------------------------------------------
+// opaque ABI types
+// ---------------------------------------------------------------------------
+struct pm_devbuf {       // device buffer grown on demand, reused across calls
+    void* p = nullptr;
+    size_t cap = 0;
+};
+struct pm_hostbuf {      // pinned host staging buffer
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct pm_db {
+    int device = 0;
+    int alphabet = PM_ALPHA_NUC;
+    uint64_t n = 0;          // positions (file bytes)
+    uint64_t ntiles = 0;     // NUC: tiles (incl. break-only padding tiles)
+    uint64_t nwords = 0;     // NUC: physical words (ntiles * TILE_WORDS)
+    uint64_t nsb = 0;        // NUC: superblocks (32 physical words)
+    uint64_t nflag = 0;      // NUC: exception words
+    uint64_t nbytes_alloc = 0;
+    uint2 *hl = nullptr, *bo = nullptr;   // NUC planes {hi, lo}, {brk, oth}
+    uint32_t *sbflag = nullptr, *sbbase = nullptr;
+    uint32_t *xbrk = nullptr, *xoth = nullptr;
+    uint8_t* xbytes = nullptr;
+    uint64_t* xword = nullptr;   // NUC: physical word of each flagged word
+    uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
+    uint8_t* bytes = nullptr;    // BYTE alphabet
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // per-call workspaces (never stream-ordered allocations)
+    pm_devbuf ws_tab, ws_sink, ws_post;
+    pm_hostbuf pin_up, pin_down;
+    uint64_t device_bytes = 0;
+};
+
+struct pm_hits {
+    int device = 0;
+    uint64_t count = 0;
+    uint64_t* keys = nullptr;   // sorted, pattern << 48 | beg
+    uint32_t* lens = nullptr;
+    size_t keys_cap = 0, lens_cap = 0;
+    double kernel_ms = 0.0;
+    hipEvent_t ready = nullptr;     // recorded after the last kernel writing keys/lens
+    hipEvent_t last_use = nullptr;  // recorded by pm_hits_copy_device on the caller's stream
+};
+
+namespace pm {
+
+// ---------------------------------------------------------------------------
+// host helpers (pm_db.hip)
+// ---------------------------------------------------------------------------
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        HIPCHK(hipGetDevice(&prev));
+        if (prev != dev) HIPCHK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+void* reserve(pm_db* db, pm_devbuf& b, size_t bytes);
+// Per-device pool of hit-list buffers (sizes rounded to powers of two):
+// scans allocate their result from it and pm_hits_destroy returns it, so a
+// query costs no hipMalloc/hipFree (hipFree synchronizes the device).
+void* pool_get(int device, size_t bytes, size_t* cap);
+void pool_put(int device, void* p, size_t cap);
+void* reserve_host(pm_db* db, pm_hostbuf& b, size_t bytes);
+NucView nuc_view(const pm_db* db);
+
+// Carves 256-byte aligned pieces out of one buffer.
+struct Carve {
+    size_t off = 0;
+    size_t take(size_t bytes) {
+        size_t at = off;
+        off += (bytes + 255) / 256 * 256;
+        return at;
+    }
+};
+
+// Host blob staged through pinned memory and uploaded in one copy.
+struct Upload {
+    std::vector<uint8_t> blob;
+    size_t add(const void* src, size_t bytes) {
+        size_t at = (blob.size() + 255) / 256 * 256;
+        blob.resize(at + bytes);
+        if (bytes) memcpy(blob.data() + at, src, bytes);
+        return at;
+    }
+    uint8_t* commit(pm_db* db);   // uploads into db->ws_tab; returns its device base
+};
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    EventPair() {
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+    }
+    ~EventPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+    double ms() {
+        float v = 0.f;
+        HIPCHK(hipEventElapsedTime(&v, a, b));
+        return v;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// hit collection (pm_hits.hip)
+// ---------------------------------------------------------------------------
+struct SinkBuffers {
+    uint64_t* out = nullptr;
+    uint32_t* cnt = nullptr;
+    uint32_t cap = 0;
+    uint32_t bins_per_pattern = NBINS;
+    uint32_t pos_shift = 0;
+    uint32_t nbins = NBINS;
+    Sink sink() const { return Sink{out, cnt, cap, bins_per_pattern, pos_shift}; }
+};
+
+// Bins for `n_slots` pattern slots over positions [0, n_positions);
+// `expected` sizes the per-bin capacity.
+SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected);
+// Bins filled by the producer itself: n_slots x per_slot segments of `cap`
+// keys, each a position range in increasing order (pm_linear_jit).
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, uint32_t cap);
+// Reads bin counters; returns total, sets `overflow` if a bin exceeded cap.
+uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
+// bins -> one sorted key list (pattern << 48 | pos) owned by the returned
+// hits; lens are left for the caller to fill.
+pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total);
+// records h->ready on the db stream: call after the last kernel filling h
+void hits_ready(pm_db* db, pm_hits* h);
+
+}  // namespace pm

@@ -53,3 +53,21 @@ def test_specialized_kernel_compiles_without_gpu():
         assert engine.jit_compile(progs, k) > 1000
     long_pat = [compile_pattern(convert("-n", "ACGT" * 12))]
     assert engine.jit_compile(long_pat, 1) > 1000
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("pat", ["GAATTC", "TATAWAWR", "TGCTGASTCAGCANW",
+                                 "YYYYYYYYYYYYYYYYYYYYRRRRRRRRRRRRRRRRRRRRNNNNNNNNNNNNNNNNNNNNNNNN"])
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_specialized_kernel_matrix_compiles(pat, k):
+    """Every (pattern, k, strands) shape the GPU parity tests run generates
+    valid gfx950 code (hipRTC, no GPU)."""
+    from patmatchdocker_amd import engine
+    from patmatchdocker_amd.convert import convert
+    from patmatchdocker_amd.regex import compile_pattern
+    fwd = convert("-n", pat)
+    progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+    assert engine.jit_compile(progs, k) > 1000
+    assert engine.jit_compile(progs[:1], k) > 1000

@@ -157,3 +157,43 @@ def test_specialized_matches_generic_on_synthetic(engine, monkeypatch):
             assert _gpu_pairs(g) == _gpu_pairs(s_)
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("jit", ["0", "1"])
+def test_multi_tile_stream_layout(engine, oracle_mod, monkeypatch, jit):
+    """~450 KB over 7+ stream tiles: records crossing stream and tile
+    boundaries, wrapped lines, N runs and lowercase, generic and specialized
+    kernels, k = 0..3, against the oracle."""
+    monkeypatch.setenv("PM_JIT", jit)
+    text = dna_fasta(77, n_records=9, min_len=20000, max_len=90000, width=(None if jit == "1" else 80))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        assert len(db) > 6 * 65536
+        for pat, ks in [("TGCTGASTCAGCANW", (0, 2, 3)), ("GAATTC", (0, 1)), ("TATAWAWR", (1,)),
+                        ("ACGTACGTACGTACGTACGTACGTACGTACGTACG", (3,))]:
+            fwd = convert("-n", pat)
+            progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+            for k in ks:
+                res, _ = engine.scan(db, progs, k=k, types="s")
+                for prog, r in zip(progs, res):
+                    assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, k), (pat, prog.source, k)
+    finally:
+        db.close()
+
+
+def test_decode_roundtrip_multi_tile(engine):
+    """pm_db_decode(0, n) reproduces the folded file (breaks -> '\\n')."""
+    text = dna_fasta(78, n_records=5, min_len=30000, max_len=60000, width=61)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        got = db.decode(0, len(text))
+    finally:
+        db.close()
+    want = bytearray()
+    for line in text.split(b"\n"):
+        if line.startswith(b">") and len(line) > 1 and line[1:2] not in (b" ", b"\t", b"\r", b"\f", b"\v"):
+            want += b"\n" * len(line)
+        else:
+            want += line.upper()
+        want += b"\n"
+    assert got == bytes(want[:len(text)])

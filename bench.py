@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
-ROUND = "r01b"
+ROUND = "r01c"
 
 
 def parse_args():

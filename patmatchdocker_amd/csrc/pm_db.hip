@@ -311,7 +311,7 @@ void free_db(pm_db* db) {
     if (!db) return;
     if (db->stream) (void)hipStreamSynchronize(db->stream);
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->bytes, db->ws_tab.p, db->ws_sink.p, db->ws_post.p};
+                    db->lflag, db->bytes, db->ws_tab.p, db->ws_sink.p, db->ws_post.p, db->ws_rec.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_up.p) (void)hipHostFree(db->pin_up.p);

@@ -217,7 +217,7 @@ struct pm_db {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // per-call workspaces (never stream-ordered allocations)
-    pm_devbuf ws_tab, ws_sink, ws_post;
+    pm_devbuf ws_tab, ws_sink, ws_post, ws_rec;
     pm_hostbuf pin_up, pin_down;
     uint64_t device_bytes = 0;
 };

@@ -27,6 +27,7 @@
 #include <hip/hiprtc.h>
 
 #include <deque>
+#include <memory>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -199,6 +200,72 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     }
 }
 
+constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
+
+// Hit records of pm_linear_jit -> hit keys.  A record is (tile, lane, step,
+// pattern) and the live mask of that window word, exact for the ACGT fast
+// path; windows overlapping an exception are dropped here (breaks kill,
+// windows with an "other" byte belong to k_linear_others), which needs the
+// exception planes only for lanes the tile's lane flags mark.  One block per
+// pm_linear_jit workgroup, wave w takes the records of that workgroup's wave
+// w; slots of the (pattern, workgroup) output segments are reserved with LDS
+// atomics and the segment counts written once at the end (k_linear_others,
+// launched after, appends to them with global atomics).
+struct ExpandArgs {
+    const uint2* bo;
+    const uint64_t* lflag;
+    const uint2* rec;
+    const uint32_t* rec_cnt;
+    uint32_t* rec_over;   // max record count seen above rcap (0: none)
+    uint32_t rcap;
+    uint64_t ntiles, n;
+    const int32_t* lengths;
+    int P, pattern_base;
+    uint64_t* out;
+    uint32_t* seg_cnt;
+    uint32_t cap, nwg, tiles_per_wg;
+};
+
+__global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
+    __shared__ uint32_t cnt_p[4];
+    const uint32_t wg = blockIdx.x, part = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
+    if (threadIdx.x < 4) cnt_p[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t seg = wg * 4 + part;
+    uint32_t cnt = a.rec_cnt[seg];
+    if (cnt > a.rcap) {
+        if (lane_t == 0) atomicMax(a.rec_over, cnt);
+        cnt = a.rcap;
+    }
+    for (uint32_t i = lane_t; i < cnt; i += 64) {
+        const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
+        const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 11);
+        const uint32_t lane = (r.x >> 5) & 63, s = (r.x >> 2) & 7, p = r.x & 3;
+        if (tile >= a.ntiles) continue;
+        const uint32_t w0 = 32u * lane + part * JIT_STEPS + s;
+        uint32_t live = r.y;
+        if ((a.lflag[tile] >> lane) & 1) {
+            uint32_t kill = 0;
+            const int len = a.lengths[p];
+            for (int j = 0; j < len; ++j) {
+                const uint2 e = a.bo[phys_word(tile, w0 + j)];
+                kill |= e.x | e.y;
+            }
+            live &= ~kill;
+        }
+        const uint32_t slot = (uint32_t)a.pattern_base + p;
+        const uint64_t sg = (uint64_t)slot * a.nwg + wg;
+        for (; live; live &= live - 1) {
+            const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
+            if (pos >= a.n) continue;
+            const uint32_t o = atomicAdd(&cnt_p[p], 1u);
+            if (o < a.cap) a.out[sg * a.cap + o] = ((uint64_t)slot << 48) | pos;
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < a.P) a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nwg + wg] = cnt_p[threadIdx.x];
+}
+
 __global__ void k_linear_lens(const uint64_t* __restrict__ keys, uint64_t n, const int32_t* __restrict__ lengths,
                               uint32_t* __restrict__ lens) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -213,52 +280,27 @@ const char* kJitCommon = R"JIT(
 typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
+// Hit records: one uint2 per (tile, lane, step, pattern) with a live window:
+// x = (tile - first tile of the workgroup) << 11 | lane << 5 | step << 2 |
+// pattern, y = the live mask (bit b = the window of stream b).  Staged per
+// wave in LDS and flushed to the wave's global segment, so the scan loop
+// never waits on a global store; k_linear_expand turns records into keys.
 struct JArgs {
-    const uint2 *hl, *bo;
-    const u64* lflag;
-    const u8* pos_class;    // [P][64]
-    const u8* class_any;    // [nc]
-    const u8* class_acgt;   // [nc]
-    u64 ntiles, n;
-    u64* out;               // [slot][nwg][cap] hit keys, one segment per (pattern, workgroup)
-    u32* seg_cnt;           // [slot][nwg]
-    u64* dummy;             // [nwg] sink of the always-issued flush stores
-    u32 cap, nwg, tiles_per_wg;
-    int pattern_base;
+    const uint2* hl;
+    uint2* rec;             // [nwg * 4][rcap]
+    u32* rec_cnt;           // [nwg * 4]
+    u64 ntiles;
+    u32 rcap, tiles_per_wg;
 };
 #define STREAM 2048u
 #define TILE_POS 65536ull
 #define TILE_WORDS 2112ull
 #define B3(a, b, c, t) ((u32)__builtin_amdgcn_bitop3_b32((a), (b), (c), (t)))
-__device__ __forceinline__ u64 phys_word(u64 tile, u32 w) {
-    return tile * TILE_WORDS + (w < STREAM ? (u64)((w & 31u) * 64u + (w >> 5)) : (u64)w);
-}
-// Hit output (rare path, out of line: inlined, even never-executed emission
-// code perturbs the allocation and schedule of the 16-step fast path).  A
-// slot of the (pattern, workgroup) segment is reserved with an LDS atomic
-// (lgkmcnt; a returning global atomic would be waited for on vmcnt, which
-// retires in order and would drain the tile prefetch in flight).  Workgroups
-// own contiguous tile ranges, so each segment is a position range.
-typedef __attribute__((address_space(3))) u32 lds_u32;
-typedef __attribute__((address_space(3))) const uint2 lds_uint2;
-struct HitStage {
-    u32 cnt[4];      // per pattern: next slot of this workgroup's segment
-};
-// the kernel arguments the rare path needs, passed by value (no struct copy
-// to scratch)
-typedef __attribute__((address_space(1))) const uint2 glb_uint2;
-typedef __attribute__((address_space(1))) u64 glb_u64;
-struct RareArgs {
-    glb_uint2* bo;   // global address space: flat accesses would also count in lgkmcnt
-    glb_u64* out;
-    u32 cap, nwg;
-    int pattern_base;
-};
-__device__ __forceinline__ void emit(const RareArgs& a, lds_u32* cnt, int p, u64 pos) {
-    const u32 slot = (u32)(a.pattern_base + p);
-    const u32 o = __atomic_fetch_add(cnt + p, 1u, __ATOMIC_RELAXED);
-    if (o < a.cap) a.out[((u64)slot * a.nwg + blockIdx.x) * a.cap + o] = ((u64)slot << 48) | pos;
-}
+// pins a class word in a register: the compiler would otherwise re-derive it
+// from the plane words at every step that uses it
+#define PIN(x) asm("" : "+v"(x))
+typedef __attribute__((address_space(1))) uint2 glb_uint2;
+typedef __attribute__((address_space(3))) uint2 lds_uint2;
 )JIT";
 
 struct JitKernel {
@@ -270,18 +312,18 @@ std::mutex g_jit_mu;
 std::map<std::pair<int, std::string>, JitKernel> g_jit_cache;
 
 struct JArgsHost {           // must match JArgs in kJitCommon
-    const uint2 *hl, *bo;
-    const uint64_t* lflag;
-    const uint8_t* pos_class;
-    const uint8_t* class_any;
-    const uint8_t* class_acgt;
-    uint64_t ntiles, n;
-    uint64_t* out;
-    uint32_t* seg_cnt;
-    uint64_t* dummy;
-    uint32_t cap, nwg, tiles_per_wg;
-    int pattern_base;
+    const uint2* hl;
+    uint2* rec;
+    uint32_t* rec_cnt;
+    uint64_t ntiles;
+    uint32_t rcap, tiles_per_wg;
 };
+constexpr int JIT_REC_LDS = 96;       // hit records staged per wave in LDS (3 workgroups per CU)
+// workgroups resident per CU (PM_JIT_WAVES: experiment override, e.g. 4 with PM_JIT_RING=2)
+int jit_wg_per_cu() {
+    const char* e = getenv("PM_JIT_WAVES");
+    return e ? std::max(1, atoi(e)) : 3;
+}
 
 // mismatch of an ACGT subset as an expression of the plane words h, l
 std::string subset_expr(int subset, const std::string& h, const std::string& l) {
@@ -377,36 +419,34 @@ std::string emit_dead_network(std::ostringstream& o, const std::vector<std::stri
     return acc;
 }
 
-#define PROF_TAIL                                                                              \
-    "#ifdef PM_PROF\n  if (lane == 0) { u64* pr = a.dummy + (u64)gridDim.x + (blockIdx.x * 4 + wid) * 3;\n" \
-    "    pr[0] = c_wait; pr[1] = c_bar; pr[2] = c_rest; }\n#endif\n"
-
 // Source of the specialized kernel for a batch of P <= 4 patterns.
 //
-// Workgroup = 4 waves = one tile at a time: wave w scans pattern w % P over
-// the step range part w / P (4 / P parts of the tile's 32 steps).  Tiles
+// Workgroup = 4 waves = one tile at a time: wave w scans steps
+// [8 w, 8 w + 8) of the tile for EVERY pattern of the batch, so the class
+// words X_c(word) of a word are derived once and shared by both strands
+// (they are pinned in registers: one VALU op per (word, class)).  Tiles
 // arrive in a 3-deep LDS ring by global_load_lds_dwordx4 (LDS-DMA, no
 // VGPRs, 1 KiB per wave-instruction): while the workgroup computes tile i
-// the DMAs of tiles i+1 and i+2 are in flight (~104 KB per CU at 3
+// the DMAs of tiles i+1 and i+2 are in flight (~100 KB per CU at 3
 // workgroups/CU), so HBM latency is off the critical path and every tile is
-// read from HBM once however many waves scan it.  Per wave, lane l walks its
-// window words t; the class words X_c(w) of the wave's pattern live in a
-// register ring from first to last use and each step is a straight-line
-// Wallace tree.  The steps are one basic block (no branch): hits are rare,
-// so the fast path only records which steps had a live window (hs) and the
-// XOR of the live masks (acc); the rare path emits them.
+// read from HBM once however many waves scan it.  Each step is a
+// straight-line Wallace tree per pattern ending in a "dead" word; the fast
+// path only ANDs them.  When some lane has a live window (rare: the branch
+// is wave-uniform), every (step, pattern) with live windows leaves an 8-byte
+// record with its live mask (wave ballot + mbcnt into an LDS stage, flushed
+// rarely); k_linear_expand turns records into hit keys.
 std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                               const uint8_t* class_acgt, const uint8_t* class_is_any) {
-    const int PARTS = 4 / P;                   // step ranges per pattern
-    const int STEPS = LANE_WORDS / PARTS;      // steps per wave
-    int RING = 3;                              // LDS tile buffers
+    constexpr int PARTS = LANE_WORDS / JIT_STEPS;   // == 4 waves
+    int RING = 3;                                   // LDS tile buffers
     if (const char* e = getenv("PM_JIT_RING")) RING = atoi(e);   // experiment: 2 or 3
     const int TILE_BYTES = (int)(TILE_WORDS * 8);         // 16896: 16.5 KiB
     const int DMA_PIECES = (TILE_BYTES + 1023) / 1024;   // 1 KiB per glds wave-instruction (last one half)
     const int LDS_TILE = TILE_BYTES;
     std::ostringstream o;
     o << kJitCommon;
-    o << "#define P " << P << "\n#define K " << K << "\n";
+    o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define STEPS "
+      << JIT_STEPS << "\n";
     auto word_off = [&](int i) {   // physical word of logical word 32 lane + i, relative to the tile
         std::ostringstream s;
         if (i < LANE_WORDS) s << (i * 64) << " + lane";
@@ -414,113 +454,56 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
         else s << "hb2 + " << (i - 64) << " * hs2";
         return s.str();
     };
-    int max_est = 0;
-    for (int p = 0; p < P; ++p) {
-        const int L = lengths[p];
-        const uint8_t* pc = pos_class + 64 * p;
-        std::vector<int> used;
-        std::map<int, int> slot;
-        std::map<int, std::pair<int, int>> span;
-        for (int j = 0; j < L; ++j) {
-            if (class_is_any[pc[j]]) continue;
-            if (!slot.count(pc[j])) { slot[pc[j]] = (int)used.size(); used.push_back(pc[j]); span[pc[j]] = {j, j}; }
-            span[pc[j]].second = j;
-        }
-        int ring = 0;
-        for (auto& kv : span) ring += kv.second.second - kv.second.first + 1;
-        max_est = std::max(max_est, ring + 2 * L + 32);
-        // --- rare path: emit the live windows of step t (exception-free ones
-        // for a lane that sees exceptions; k_linear_others owns the rest)
-        o << "__device__ __forceinline__ void emit_hits" << p
-          << "(const RareArgs& a, lds_u32* cnt, u64 tile, u32 lane, u32 t, u64 lf, u32 lv) {\n"
-             "  const u32 w0 = 32u * lane + t;\n"
-             "  if ((lf >> lane) & 1) {\n    glb_uint2* bo = a.bo + tile * TILE_WORDS;\n    u32 ex = 0;\n"
-             "#pragma unroll\n    for (int j = 0; j < " << L << "; ++j) {\n"
-             "      const u32 w = w0 + j;\n      const uint2 v = bo[w < STREAM ? (w & 31u) * 64u + (w >> 5) : w];\n"
-             "      ex |= v.x | v.y;\n    }\n    lv &= ~ex;\n  }\n"
-             "  for (u32 h = lv; h; h &= h - 1) emit(a, cnt, " << p
-          << ", tile * TILE_POS + (u64)__builtin_ctz(h) * STREAM + w0);\n}\n";
-        // --- rare path: re-evaluate step t (several live steps in a lane)
-        o << "__device__ __forceinline__ void recompute_step" << p
-          << "(const RareArgs& a, lds_u32* cnt, lds_uint2* hl, u64 tile, u32 lane, u32 t, u64 lf) {\n"
-             "  const u32 w0 = 32u * lane + t;\n"
-             "  uint2 v[" << L << "];\n#pragma unroll\n  for (int j = 0; j < " << L << "; ++j) {\n"
-             "    const u32 w = w0 + j;\n    v[j] = hl[w < STREAM ? (w & 31u) * 64u + (w >> 5) : w];\n  }\n";
-        {
-            int ruid = 0;
-            std::vector<std::string> in;
-            for (int j = 0; j < L; ++j) {
-                if (class_is_any[pc[j]]) continue;
-                const std::string nm = "r" + std::to_string(ruid++);
-                o << "  const u32 " << nm << " = "
-                  << subset_expr(class_acgt[pc[j]], "v[" + std::to_string(j) + "].x", "v[" + std::to_string(j) + "].y")
-                  << ";\n";
-                in.push_back(nm);
+    int Lmax = 0;
+    for (int p = 0; p < P; ++p) Lmax = std::max(Lmax, (int)lengths[p]);
+    for (int part = 0; part < PARTS; ++part) {
+        const int t0 = part * JIT_STEPS, t1 = t0 + JIT_STEPS;
+        const int wend = t1 + Lmax - 1;   // words [t0, wend)
+        o << "__device__ __forceinline__ void tile_body" << part
+          << "(const uint2* __restrict__ sw, int lane, u32 hb1, u32 hs1, u32 hb2, u32 hs2, u32 (&dd)[STEPS][P]) {\n";
+        std::vector<bool> loaded(wend, false);
+        std::map<std::pair<int, int>, std::string> cw;   // (word, ACGT subset) -> class word
+        auto class_word = [&](int i, int subset) {
+            const auto key = std::make_pair(i, subset);
+            auto it = cw.find(key);
+            if (it != cw.end()) return it->second;
+            if (!loaded[i]) {
+                loaded[i] = true;
+                o << "  const uint2 v" << i << " = sw[" << word_off(i) << "];\n";
             }
-            const std::string d = emit_dead_network(o, in, K, ruid, "  ");
-            o << "  emit_hits" << p << "(a, cnt, tile, lane, t, lf, ~" << d << ");\n}\n";
-        }
-        o << "__device__ __noinline__ void rare" << p << "(u32 hs, u32 acc, u64 tile, u32 lane, u64 lf, u32 sw_addr, "
-             "u32 cnt_addr, const uint2* bo, u64* out, u32 cap, u32 nwg, int pattern_base) {\n"
-             "  const RareArgs a{(glb_uint2*)bo, (glb_u64*)out, cap, nwg, pattern_base};\n"
-             "  lds_u32* cnt = (lds_u32*)(size_t)cnt_addr;\n  lds_uint2* sw = (lds_uint2*)(size_t)sw_addr;\n"
-             "  if ((hs & (hs - 1)) == 0) emit_hits" << p << "(a, cnt, tile, lane, __builtin_ctz(hs), lf, acc);\n"
-             "  else for (u32 h = hs; h; h &= h - 1) recompute_step" << p << "(a, cnt, sw, tile, lane, __builtin_ctz(h), lf);\n}\n";
-        // --- fast path over steps [t0, t1) of one tile, words from LDS
-        for (int part = 0; part < PARTS; ++part) {
-            const int t0 = part * STEPS, t1 = t0 + STEPS;
-            const int wend = t1 + L - 1;   // words [t0, wend)
-            o << "__device__ __forceinline__ void tile_body" << p << "_" << part
-              << "(const JArgs& a, u32 sw_addr, u32 cnt_addr, const uint2* __restrict__ sw, u64 tile, int lane, u32 hb1, "
-                 "u32 hs1, u32 hb2, u32 hs2, u64 lf) {\n  u32 hs = 0, acc = 0;\n";
-            std::vector<bool> loaded(wend, false);
-            std::vector<std::vector<bool>> done(wend, std::vector<bool>(used.size(), false));
-            auto ensure_class = [&](int i, int u) {
-                if (!loaded[i]) {
-                    loaded[i] = true;
-                    o << "  const uint2 v" << i << " = sw[" << word_off(i) << "];\n";
-                }
-                if (done[i][u]) return;
-                done[i][u] = true;
-                o << "  const u32 x" << u << "_" << i << " = "
-                  << subset_expr(class_acgt[used[u]], "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y")
-                  << ";\n";
-            };
-            int uid = 0;
-            for (int t = t0; t < t1; ++t) {
+            const std::string nm = "x" + std::to_string(subset) + "_" + std::to_string(i);
+            o << "  u32 " << nm << " = "
+              << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << "; PIN(" << nm
+              << ");\n";
+            cw[key] = nm;
+            return nm;
+        };
+        int uid = 0;
+        for (int t = t0; t < t1; ++t) {
+            for (int p = 0; p < P; ++p) {
+                const uint8_t* pc = pos_class + 64 * p;
                 std::vector<std::string> in;
-                for (int j = 0; j < L; ++j) {
+                for (int j = 0; j < lengths[p]; ++j) {
                     if (class_is_any[pc[j]]) continue;
-                    ensure_class(t + j, slot[pc[j]]);
-                    in.push_back("x" + std::to_string(slot[pc[j]]) + "_" + std::to_string(t + j));
+                    in.push_back(class_word(t + j, class_acgt[pc[j]] & 15));
                 }
-                o << "  {  // step " << t << "\n";
+                o << "  {  // step " << t << ", pattern " << p << "\n";
                 const std::string d = emit_dead_network(o, in, K, uid, "    ");
-                o << "    hs |= min(~" << d << ", 1u) << " << t << ";\n    acc ^= ~" << d << ";\n  }\n";
+                o << "    dd[" << (t - t0) << "][" << p << "] = " << d << ";\n  }\n";
             }
-            if (getenv("PM_JIT_EMIT") && getenv("PM_JIT_EMIT")[0] == '0')   // experiment: no emission
-                o << "  if (hs == 0x12345678u && acc == 0x9abcdef0u) a.seg_cnt[0] = 1;\n  hs = 0;\n";
-            if (getenv("PM_JIT_EMIT") && getenv("PM_JIT_EMIT")[0] == '2')   // experiment: code present, never taken
-                o << "  if (hs == 0x12345678u && acc == 0x9abcdef0u) a.seg_cnt[1] = 1;\n  if (lf != 0x1234567812345678ull) hs = 0;\n";
-            o << "  if (hs) rare" << p << "(hs, acc, tile, lane, lf, sw_addr, cnt_addr, a.bo, a.out, a.cap, a.nwg, "
-                 "a.pattern_base);\n}\n";
         }
+        o << "}\n";
     }
-    // Occupancy target from the widest body's register ring; LDS allows 3
-    // workgroups (12 waves) per CU.
-    int waves = 1;
-    while (waves < 3 && 512 / (waves + 1) >= max_est * 5 / 4) ++waves;
-    if (const char* e = getenv("PM_JIT_WAVES")) waves = atoi(e);   // experiment override
+    const int waves = jit_wg_per_cu();   // workgroups per CU (LDS allows 3 with a 3-tile ring)
     o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << DMA_PIECES << "\n";
-    // experiment knobs: PM_JIT_NODMA=1 computes on whatever is in LDS (no
-    // staging), PM_JIT_NOCOMPUTE=1 only streams the tiles
-    const bool nodma = getenv("PM_JIT_NODMA") && getenv("PM_JIT_NODMA")[0] == '1';
+    // experiment knobs: PM_JIT_NOCOMPUTE=1 only streams the tiles,
+    // PM_JIT_NODMA=1 computes on whatever the LDS ring holds (no HBM reads)
     const bool nocompute = getenv("PM_JIT_NOCOMPUTE") && getenv("PM_JIT_NOCOMPUTE")[0] == '1';
-    if (nodma) o << "#define PM_NODMA 1\n";
-    o << R"JIT(// Raw barrier: __syncthreads()'s release fence would wait vmcnt(0) for the
-// hit stores and with them drain the tile prefetch in flight.  LDS writes
-// (hit counters, register-staged tiles) are complete at lgkmcnt(0); the
-// empty asm statements keep the compiler from moving memory accesses across.
+    if (getenv("PM_JIT_NODMA") && getenv("PM_JIT_NODMA")[0] == '1') o << "#define PM_NODMA 1\n";
+    o << R"JIT(// Raw barrier: __syncthreads()'s release fence would wait vmcnt(0) and
+// drain the tile prefetch in flight.  LDS writes are complete at
+// lgkmcnt(0); the empty asm statements keep the compiler from moving memory
+// accesses across.
 #define BARRIER()                                                   \
   do {                                                              \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              \
@@ -547,24 +530,21 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
                  : "=&s"(keep) : "v"(src + (q + wid) * 1024), "s"(dst) : "memory");
   }
 }
-)JIT";
-    // PM_JIT_PROF=1: per-wave s_memtime totals (wait / barrier / rest of the
-    // iteration) into the dummy buffer, for tools/jit_sweep.py
-    const bool prof = getenv("PM_JIT_PROF") && getenv("PM_JIT_PROF")[0] == '1';
-    if (prof) o << "#define PM_PROF 1\n";
-    o << R"JIT(#ifdef PM_PROF
-#define PT(v) const u64 v = __builtin_amdgcn_s_memtime()
-#else
-#define PT(v)
-#endif
+// Moves the wave's staged records to its global segment.  Rare; ends with
+// vmcnt(0), so the DMA wait arithmetic of the main loop stays exact whatever
+// order stores and loads retire in.
+__device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2* g,
+                                           u32 gcnt, u32 rcap, int lane) {
+  for (u32 r = lane; r < n; r += 64)
+    if (gcnt + r < rcap) g[gcnt + r] = st[r];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 )JIT";
     o << "extern \"C\" __global__ __launch_bounds__(256, " << waves << ") void pm_linear_jit(JArgs a) {\n"
          "  __shared__ __attribute__((aligned(1024))) unsigned char lds[RING * LDS_TILE];\n"
-         "  __shared__ HitStage hsg;\n"
+         "  __shared__ uint2 rst[4][REC_LDS];\n"
          "  const int lane = threadIdx.x & 63;\n"
          "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-         "  const u32 pat = wid % " << P << ", part = wid / " << P << ";\n"
-         "  if (threadIdx.x < 4) hsg.cnt[threadIdx.x] = 0;\n"
          "  // pieces this wave DMAs per tile (its share of DMA_PIECES)\n"
          "  const u32 mine = (DMA_PIECES - wid + 3) / 4;\n"
          "  // halo word offsets (logical words 32 lane + 32 g + r, r < 32)\n"
@@ -574,43 +554,60 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
          "  // this workgroup's contiguous tile range\n"
          "  const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
          "  const u64 tend = t0 + a.tiles_per_wg < a.ntiles ? t0 + a.tiles_per_wg : a.ntiles;\n"
+         "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * 4 + wid) * a.rcap);\n"
+         "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
+         "  u32 scnt = 0, gcnt = 0;   // staged / flushed records (wave-uniform)\n"
          "  stage(a, lds_base, t0, tend, wid, lane);\n"
          "  stage(a, lds_base + LDS_TILE, t0 + 1, tend, wid, lane);\n"
          "  u32 slot = 0;\n"
-         "  const u32 cnt_addr = (u32)reinterpret_cast<u64>(&hsg.cnt[0]);\n"
-         "#ifdef PM_PROF\n  u64 c_wait = 0, c_bar = 0, c_rest = 0;\n#endif\n"
          "  for (u64 tile = t0; tile < tend; ++tile) {\n"
-         "    PT(ta);\n"
          "    // wait for this tile's pieces (own DMAs; the next tile's stay in\n"
          "    // flight: vmcnt retires in order), then the barrier makes everyone's\n"
          "    // pieces visible and frees the previous tile's slot\n"
-         "    if (tile + 1 < tend) {\n"
+         "    if (RING > 2 && tile + 1 < tend) {\n"
          "      if (mine == 5) asm volatile(\"s_waitcnt vmcnt(5)\" ::: \"memory\");\n"
          "      else asm volatile(\"s_waitcnt vmcnt(4)\" ::: \"memory\");\n"
          "    } else {\n"
          "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
          "    }\n"
-         "    PT(tb);\n"
          "    BARRIER();\n"
-         "    PT(tc);\n"
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
-         "    u64 lf;   // scalar load (lgkmcnt): a vector load's vmcnt wait would drain the DMAs\n"
-         "    asm volatile(\"s_load_dwordx2 %0, %1, 0x0\\n\\ts_waitcnt lgkmcnt(0)\" : \"=s\"(lf) : \"s\"(a.lflag + tile) : \"memory\");\n"
-         "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n";
-    bool first = true;
-    if (nocompute) o << "    if (lf == 0x123456789ull) a.seg_cnt[0] = sw[lane].x;\n";
-    for (int p = 0; p < P && !nocompute; ++p)
-        for (int part = 0; part < PARTS; ++part) {
-            o << "    " << (first ? "" : "else ") << "if (pat == " << p << " && part == " << part << ") tile_body" << p
-              << "_" << part << "(a, (u32)reinterpret_cast<u64>(sw), cnt_addr, sw, tile, lane, hb1, hs1, hb2, hs2, lf);\n";
-            first = false;
-        }
-    o << "#ifdef PM_PROF\n    { PT(td); c_wait += tb - ta; c_bar += tc - tb; c_rest += td - tc; }\n#endif\n";
-    o << "    slot = slot == RING - 1 ? 0 : slot + 1;\n  }\n"
-         "  BARRIER();\n"
-         "  if (threadIdx.x < " << P << ") a.seg_cnt[(u64)(a.pattern_base + threadIdx.x) * a.nwg + blockIdx.x] = "
-         "hsg.cnt[threadIdx.x];\n"
-         PROF_TAIL "}\n";
+         "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
+         "    u32 dd[STEPS][P];   // dead windows per step and pattern\n"
+         "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) dd[s][p] = ~0u;\n";
+    if (nocompute) {
+        o << "    if (sw[lane].x == 0x12345u && lane == 99) dd[0][0] = 0u;   // keeps the tile reads\n";
+    } else {
+        for (int part = 0; part < PARTS; ++part)
+            o << "    " << (part ? "else " : "") << "if (wid == " << part << ") tile_body" << part
+              << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
+    }
+    o << "    u32 all = ~0u;\n"
+         "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
+         "    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {   // wave-uniform, rare\n"
+         "#pragma unroll\n"
+         "      for (int s = 0; s < STEPS; ++s) {\n"
+         "#pragma unroll\n"
+         "        for (int p = 0; p < P; ++p) {\n"
+         "          const u32 lv = ~dd[s][p];\n"
+         "          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);\n"
+         "          if (m) {\n"
+         "            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));\n"
+         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 11 | (u32)lane << 5 | (u32)s << 2 | (u32)p, lv);\n"
+         "            scnt += (u32)__builtin_popcountll(m);\n"
+         "            if (scnt > REC_LDS - 64) {\n"
+         "              flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
+         "              gcnt += scnt;\n"
+         "              scnt = 0;\n"
+         "            }\n"
+         "          }\n"
+         "        }\n"
+         "      }\n"
+         "    }\n"
+         "    slot = slot == RING - 1 ? 0 : slot + 1;\n  }\n"
+         "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
+         "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * 4 + wid] = gcnt + scnt;\n"
+         "}\n";
     return o.str();
 }
 
@@ -669,8 +666,7 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
         }
         sig += "]";
     }
-    for (const char* knob : {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_EMIT", "PM_JIT_NODMA", "PM_JIT_NOCOMPUTE",
-                             "PM_JIT_PROF"})
+    for (const char* knob : {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA"})
         if (const char* e = getenv(knob)) sig += std::string(";") + knob + "=" + e;
     return sig;
 }
@@ -745,26 +741,47 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         std::vector<uint32_t> counts;
         uint64_t total = 0;
         EventPair ev;
+        std::vector<std::unique_ptr<EventPair>> jev;   // per specialized launch
         bool done = false;
         if (jit) {
             // one output segment per (pattern, workgroup); workgroups own
             // contiguous tile ranges (3 per CU resident)
-            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256 * 3);
+            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * jit_wg_per_cu());
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
+            const uint64_t nseg = nwg * 4;   // one lane-record segment per wave
             uint32_t cap = 1024;
             while (cap > 256 && (uint64_t)n_patterns * nwg * cap * 8 > (1ull << 30)) cap /= 2;
-            const uint64_t dummy_words = nwg + nwg * 4 * 3;   // flush sink + PM_JIT_PROF counters
-            uint64_t* dummy = static_cast<uint64_t*>(reserve(db, db->ws_post, dummy_words * sizeof(uint64_t)));
-            if (getenv("PM_JIT_PROF")) HIPCHK(hipMemsetAsync(dummy, 0, dummy_words * sizeof(uint64_t), s));
-            for (int attempt = 0; attempt < 2 && !done; ++attempt) {
+            // records per wave: at most tiles_per_wg * 64 lanes * 8 steps * 4 patterns
+            const uint64_t rec_max = tpw * 64 * JIT_STEPS * 4;
+            uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, 512);
+            uint32_t* h_over = static_cast<uint32_t*>(reserve_host(db, db->pin_up, sizeof(uint32_t)));
+            for (int attempt = 0; attempt < 3 && !done; ++attempt) {
+                Carve cv;
+                const size_t o_rec = cv.take(nseg * rcap * sizeof(uint2));
+                const size_t o_rcnt = cv.take(nseg * sizeof(uint32_t));
+                const size_t o_over = cv.take(sizeof(uint32_t));
+                uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
+                uint2* d_rec = reinterpret_cast<uint2*>(rbase + o_rec);
+                uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
+                uint32_t* d_over = reinterpret_cast<uint32_t*>(rbase + o_over);
+                HIPCHK(hipMemsetAsync(d_over, 0, sizeof(uint32_t), s));
                 sb = make_sink_segments(db, n_patterns, (uint32_t)nwg, cap);
-                HIPCHK(hipEventRecord(ev.a, s));
+                // kernel_ms = the scan passes over the database (pm_linear_jit
+                // launches); record expansion and the rest are not included
+                jev.clear();
                 for (const Chunk& ch : chunks) {
-                    JArgsHost ja{db->hl, db->bo, db->lflag, d_up + o_pc + 64 * ch.base, d_up + o_any, d_up + o_acgt,
-                                 db->ntiles, db->n, sb.out, sb.cnt, dummy, sb.cap, (uint32_t)nwg, (uint32_t)tpw, ch.base};
+                    JArgsHost ja{db->hl, d_rec, d_rcnt, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
+                    jev.emplace_back(new EventPair());
+                    HIPCHK(hipEventRecord(jev.back()->a, s));
                     HIPCHK(hipModuleLaunchKernel(ch.jit, (uint32_t)nwg, 1, 1, 256, 1, 1, 0, s, params, nullptr));
+                    HIPCHK(hipEventRecord(jev.back()->b, s));
+                    ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
+                                  reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
+                                  sb.cap, (uint32_t)nwg, (uint32_t)tpw};
+                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nwg), dim3(256), 0, s, xa);
+                    HIPCHK(hipGetLastError());
                     if (db->nflag) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
@@ -774,24 +791,17 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                         HIPCHK(hipGetLastError());
                     }
                 }
-                HIPCHK(hipEventRecord(ev.b, s));
+                HIPCHK(hipMemcpyAsync(h_over, d_over, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
                 bool overflow = false;
-                total = sink_total(db, sb, counts, overflow);
-                if (getenv("PM_JIT_PROF") && getenv("PM_JIT_PROF")[0] == '1') {
-                    std::vector<uint64_t> pr(nwg * 4 * 3);
-                    HIPCHK(hipMemcpy(pr.data(), dummy + nwg, pr.size() * 8, hipMemcpyDeviceToHost));
-                    double w[4][3] = {};
-                    for (uint64_t b = 0; b < nwg; ++b)
-                        for (int wv = 0; wv < 4; ++wv)
-                            for (int c = 0; c < 3; ++c) w[wv][c] += (double)pr[(b * 4 + wv) * 3 + c] / nwg;
-                    for (int wv = 0; wv < 4; ++wv)
-                        fprintf(stderr, "PM_JIT_PROF wave %d: wait %.0f  barrier %.0f  rest %.0f cycles/workgroup\n", wv,
-                                w[wv][0], w[wv][1], w[wv][2]);
+                total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
+                const uint32_t rec_need = *h_over;
+                if (!overflow && rec_need == 0) { done = true; break; }
+                if (rec_need) rcap = std::max<uint32_t>(rcap, rec_need);
+                if (overflow) {
+                    const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
+                    if (maxc > LDS_SORT_CAP) break;   // pathological hit density: generic kernels below
+                    while (cap < maxc) cap *= 2;
                 }
-                if (!overflow) { done = true; break; }
-                const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
-                if (maxc > LDS_SORT_CAP) break;   // pathological hit density: generic kernels below
-                while (cap < maxc) cap *= 2;
             }
         }
         if (!done) {
@@ -824,7 +834,11 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
             }
         }
-        const double kms = ev.ms();
+        double kms = 0.0;
+        if (done && jit)
+            for (auto& e : jev) kms += e->ms();
+        else
+            kms = ev.ms();
         pm_hits* h = sink_to_hits(db, sb, counts, total);
         h->kernel_ms = kms;
         if (total) {

@@ -36,7 +36,7 @@ extern "C" {
 #define PM_ALPHA_BYTE 1    /* one folded byte per residue (peptides)      */
 
 #define PM_MAX_POSITIONS 64
-#define PM_MAX_K 3         /* substitutions handled by the GPU kernels    */
+#define PM_MAX_K 3         /* errors handled by the GPU kernels           */
 
 typedef struct pm_db pm_db;        /* device-resident sequence database   */
 typedef struct pm_hits pm_hits;    /* device/host hit list of one scan    */
@@ -94,6 +94,22 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
 int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
                 uint64_t first, uint64_t last, int max_len, int k, int pattern_id,
                 pm_hits** out);
+
+/* Error types of nrgrep's `-k <k>[ids]` (patmatch.py:299-314 builds the
+ * letters; all three when none is chosen). */
+#define PM_ERR_INS 1       /* i: an extra text character                  */
+#define PM_ERR_DEL 2       /* d: a pattern position with no text character */
+#define PM_ERR_SUB 4       /* s: a substituted character                  */
+
+/* pm_scan_nfa with an explicit error-type mask `errs` (PM_ERR_*) -- the
+ * general `nrgrep_coords -k <k><ids>` scan.  min_len = the shortest match
+ * length of the pattern (regex.py); with PM_ERR_DEL it must exceed k
+ * (otherwise PM_E_UNSUPPORTED).  Insertions let a match run to
+ * max_len + k characters.  pm_scan_nfa(...) == pm_scan_nfa_errs(..., 0, k,
+ * PM_ERR_SUB, ...). */
+int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
+                     uint64_t first, uint64_t last, int max_len, int min_len, int k, int errs,
+                     int pattern_id, pm_hits** out);
 
 /* --- hits --------------------------------------------------------------- */
 int pm_hits_count(const pm_hits* h, uint64_t* count);

@@ -17,6 +17,7 @@ PM_ALPHA_NUC = 0
 PM_ALPHA_BYTE = 1
 PM_E_UNSUPPORTED = -4
 PM_MAX_K = 3
+PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -24,7 +25,7 @@ EXPORTED = (
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
-    "pm_linear_jit_compile",
+    "pm_linear_jit_compile", "pm_scan_nfa_errs",
 )
 
 
@@ -62,6 +63,8 @@ def _declare(lib):
     lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, PP]
     lib.pm_scan_nfa.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, PP]
+    lib.pm_scan_nfa_errs.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, PP]
     lib.pm_hits_count.argtypes = [P, pu64]
     lib.pm_hits_copy.argtypes = [P, P, P, P, u64]
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]

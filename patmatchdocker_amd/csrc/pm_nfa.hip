@@ -9,6 +9,17 @@
 // k_nfa_verify runs the forward automaton from each start and records the
 // shortest end -- the hit nrgrep_coords prints for that start (oracle/
 // pm_oracle.c).
+//
+// Error model: `-k <k><ids>` (patmatch.py:299-314; the web form's default
+// when mismatches > 0 is all three).  Row j holds the positions reached with
+// j errors; substitution (any non-break char consumes a position), insertion
+// (a text char consumed, the state kept) and deletion (a position skipped
+// without text: a closure over the rows after every step) are each enabled by
+// a bit of `errs`.  The reverse scan is the forward recurrence of
+// pm_oracle.c:55-94 mirrored (prec for follow, last for first) in search
+// mode: a fresh start config -- init row 0, insertion rows when INS, and its
+// deletion closure, precomputed on the host as rev_pre[j] / rev_ins[j] -- is
+// injected before every character.
 #include "pm_internal.h"
 
 namespace pm {
@@ -28,6 +39,10 @@ struct NfaArgs {
     uint64_t nchunks;
     int pattern_id;
     Sink sink;
+    int errs;                 // PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB
+    uint64_t rev_pre[4];      // reverse: prec(S[j]) | (I[j] ? last : 0) for the injected start config
+    uint64_t rev_ins[4];      // reverse: S[j] (insertion source rows of the injected config)
+    uint64_t fwd_del[4];      // forward: deletion closure of the start config (rows of R)
     // verify
     const uint64_t* starts;
     uint64_t nstarts;
@@ -35,19 +50,42 @@ struct NfaArgs {
     int max_len;
 };
 
+__device__ inline uint64_t table_or(const uint64_t* __restrict__ tab, uint64_t set, int nt) {
+    uint64_t acc = 0;
+    for (int t = 0; t < nt; ++t) acc |= tab[t * 256 + ((set >> (8 * t)) & 255)];
+    return acc;
+}
+
+// One character of the reverse search (right to left).  Substitution-only
+// patterns (the common case) take the short form.
 template <int K>
 __device__ inline void nfa_rev_step(uint64_t (&R)[K + 1], uint64_t bc, uint64_t nb,
-                                    const uint64_t* __restrict__ s_prec, int nt, uint64_t last) {
+                                    const uint64_t* __restrict__ s_prec, const NfaArgs& a) {
     uint64_t A[K + 1];
 #pragma unroll
+    for (int j = 0; j <= K; ++j) A[j] = table_or(s_prec, R[j], a.nt) | a.rev_pre[j];
+    if (a.errs == PM_ERR_SUB) {
+#pragma unroll
+        for (int j = K; j >= 0; --j) R[j] = (A[j] & bc) | (j > 0 ? (A[j - 1] & nb) : 0ull);
+        return;
+    }
+    uint64_t N[K + 1];
+#pragma unroll
     for (int j = 0; j <= K; ++j) {
-        uint64_t acc = last;
-        const uint64_t d = R[j];
-        for (int t = 0; t < nt; ++t) acc |= s_prec[t * 256 + ((d >> (8 * t)) & 255)];
-        A[j] = acc;
+        N[j] = A[j] & bc;
+        if (j > 0) {
+            if (a.errs & PM_ERR_SUB) N[j] |= A[j - 1] & nb;
+            if (a.errs & PM_ERR_INS) N[j] |= (R[j - 1] | a.rev_ins[j - 1]) & nb;
+        }
+    }
+    if (a.errs & PM_ERR_DEL) {
+        // ninit[j] (j >= 1) = an insertion-kept start; row 0's init is consumed
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            N[j + 1] |= table_or(s_prec, N[j], a.nt) | ((j >= 1 && (a.errs & PM_ERR_INS) && nb) ? a.last : 0ull);
     }
 #pragma unroll
-    for (int j = K; j >= 0; --j) R[j] = (A[j] & bc) | (j > 0 ? (A[j - 1] & nb) : 0ull);
+    for (int j = 0; j <= K; ++j) R[j] = N[j];
 }
 
 template <bool NUC>
@@ -76,7 +114,7 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
         const uint8_t ch = char_at<NUC>(a, p);
         const uint64_t bc = s_b[ch];
         const uint64_t nb = ch == '\n' ? 0ull : ~0ull;
-        nfa_rev_step<K>(R, bc, nb, s_prec, a.nt, a.last);
+        nfa_rev_step<K>(R, bc, nb, s_prec, a);
         uint64_t any = 0;
 #pragma unroll
         for (int j = 0; j <= K; ++j) any |= R[j];
@@ -96,30 +134,52 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= a.nstarts) return;
     const uint64_t s = a.starts[i] & ((1ull << 48) - 1);
+    // pm_oracle.c match_from(): rows R[j] and the "before the first position"
+    // state init[j] (kept alive by insertions), deletion closures after every
+    // step; the first accepting step gives the shortest end
     uint64_t R[K + 1];
+    bool init[K + 1];
 #pragma unroll
-    for (int j = 0; j <= K; ++j) R[j] = 0;
+    for (int j = 0; j <= K; ++j) {
+        R[j] = a.fwd_del[j];
+        init[j] = j == 0;
+    }
     uint32_t len = 0;
     for (int d = 0; d < a.max_len; ++d) {
         const uint8_t ch = char_at<NUC>(a, s + d);
         const uint64_t bc = s_b[ch];
         const uint64_t nb = ch == '\n' ? 0ull : ~0ull;
-        uint64_t A[K + 1];
+        uint64_t A[K + 1], N[K + 1];
+        bool ninit[K + 1];
+#pragma unroll
+        for (int j = 0; j <= K; ++j) A[j] = table_or(s_fol, R[j], a.nt) | (init[j] ? a.first : 0ull);
 #pragma unroll
         for (int j = 0; j <= K; ++j) {
-            uint64_t acc = (d == 0 && j == 0) ? a.first : 0ull;
-            const uint64_t v = R[j];
-            for (int t = 0; t < a.nt; ++t) acc |= s_fol[t * 256 + ((v >> (8 * t)) & 255)];
-            A[j] = acc;
+            N[j] = A[j] & bc;
+            ninit[j] = false;
+            if (j > 0) {
+                if (a.errs & PM_ERR_SUB) N[j] |= A[j - 1] & nb;
+                if (a.errs & PM_ERR_INS) {
+                    N[j] |= R[j - 1] & nb;
+                    ninit[j] = init[j - 1] && nb;
+                }
+            }
+        }
+        if (a.errs & PM_ERR_DEL) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) N[j + 1] |= table_or(s_fol, N[j], a.nt) | (ninit[j] ? a.first : 0ull);
         }
         uint64_t any = 0;
+        bool alive = false;
 #pragma unroll
-        for (int j = K; j >= 0; --j) {
-            R[j] = (A[j] & bc) | (j > 0 ? (A[j - 1] & nb) : 0ull);
+        for (int j = 0; j <= K; ++j) {
+            R[j] = N[j];
+            init[j] = ninit[j];
             any |= R[j];
+            alive |= init[j];
         }
         if (any & a.last) { len = d + 1; break; }
-        if (!any) break;
+        if (!any && !alive) break;
     }
     a.lens[i] = len;   // 0 = no match (cannot happen for a start found by k_nfa_rev)
 }
@@ -151,6 +211,12 @@ using namespace pm;
 
 extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow, uint64_t first,
                            uint64_t last, int max_len, int k, int pattern_id, pm_hits** out) {
+    return pm_scan_nfa_errs(db, m, byte_mask, follow, first, last, max_len, 0, k, PM_ERR_SUB, pattern_id, out);
+}
+
+extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow, uint64_t first,
+                                uint64_t last, int max_len, int min_len, int k, int errs, int pattern_id,
+                                pm_hits** out) {
     return guarded([&] {
         require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");
         require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range");
@@ -159,6 +225,15 @@ extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const ui
         require(k >= 0 && k <= PM_MAX_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
         require(pattern_id >= 0 && pattern_id < 65536, "pattern_id out of range");
         require(first != 0 && last != 0, "empty automaton");
+        require((errs & ~(PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB)) == 0, "bad error-type mask");
+        if (k == 0) errs = PM_ERR_SUB;   // no errors: the type letters are irrelevant
+        // a match must consume a pattern position (pm_oracle.c reports
+        // non-empty matches only): with deletions that needs min_len > k
+        require(!(errs & PM_ERR_DEL) || min_len > k,
+                "deletions with k >= the shortest match length are not supported by the GPU scan",
+                PM_E_UNSUPPORTED);
+        const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
+        require(max_len + ins_extra <= 1024 + PM_MAX_K, "max_len above 1024", PM_E_UNSUPPORTED);
         DeviceGuard g(db->device);
         hipStream_t s = db->stream;
         const int nt = (m + 7) / 8;
@@ -174,6 +249,28 @@ extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const ui
                         tf[t * 256 + v] |= follow[t * 8 + b];
                         tp[t * 256 + v] |= prec[t * 8 + b];
                     }
+        // start configurations (see the kernel comment): forward deletion
+        // closure of the start, and the reverse search's injected config
+        auto set_or = [&](const std::vector<uint64_t>& per_pos, uint64_t set) {
+            uint64_t acc = 0;
+            for (int i = 0; i < m; ++i)
+                if ((set >> i) & 1) acc |= per_pos[i];
+            return acc;
+        };
+        const std::vector<uint64_t> fol_v(follow, follow + m);
+        uint64_t fwd_del[4] = {0, 0, 0, 0}, rev_pre[4] = {0, 0, 0, 0}, rev_ins[4] = {0, 0, 0, 0};
+        {
+            uint64_t S[4] = {0, 0, 0, 0};
+            const bool del = errs & PM_ERR_DEL, ins = errs & PM_ERR_INS;
+            for (int j = 0; j < k && del; ++j) {
+                fwd_del[j + 1] = set_or(fol_v, fwd_del[j]) | (j == 0 ? first : 0);
+                S[j + 1] = set_or(prec, S[j]) | ((j == 0 || ins) ? last : 0);
+            }
+            for (int j = 0; j <= k; ++j) {
+                rev_ins[j] = S[j];
+                rev_pre[j] = set_or(prec, S[j]) | ((j == 0 || ins) ? last : 0);
+            }
+        }
         std::vector<uint64_t> bm(byte_mask, byte_mask + 256);
         bm['\n'] = 0;   // records never span the delimiter
         Upload up;
@@ -191,7 +288,13 @@ extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const ui
         a.first = first;
         a.last = last;
         a.nt = nt;
-        a.halo = max_len - 1;
+        a.halo = max_len + ins_extra - 1;
+        a.errs = errs;
+        for (int j = 0; j < 4; ++j) {
+            a.rev_pre[j] = rev_pre[j];
+            a.rev_ins[j] = rev_ins[j];
+            a.fwd_del[j] = fwd_del[j];
+        }
         a.n = db->n;
         a.pattern_id = pattern_id;
         // chunk per lane: a power of two (so that on the nucleotide layout
@@ -233,7 +336,7 @@ extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const ui
             a.starts = h->keys;
             a.nstarts = total;
             a.lens = h->lens;
-            a.max_len = max_len;
+            a.max_len = max_len + ins_extra;
             EventPair ev2;
             HIPCHK(hipEventRecord(ev2.a, s));
             if (nuc) launch_nfa_verify<true>(k, a, blocks_for(total, 256), s);

@@ -12,9 +12,11 @@ routes every compiled :class:`~patmatchdocker_amd.regex.Program` to a kernel:
 * ``nfa``    -- everything else with a bounded match length goes to the
   Glushkov reverse-scan + verify kernels (``pm_scan_nfa``).
 
-Anything else (insertions/deletions with k > 0, unbounded ``*``/``+``,
-more than 64 positions, k > 3) raises :class:`UnsupportedOnGPU`; there is
-no CPU fallback by design.
+Queries with insertions/deletions (``-k <k>ids``, the web form's default
+when mismatches > 0) go to the Glushkov kernels with the error-type mask.
+Anything else (unbounded ``*``/``+``, more than 64 positions, k > 3,
+deletions with k >= the shortest match) raises :class:`UnsupportedOnGPU`;
+there is no CPU fallback by design.
 """
 
 from __future__ import annotations
@@ -155,19 +157,20 @@ def _collect(handle) -> Hits:
 
 
 def parse_error_types(k: int, types: str) -> str:
-    return types if k else ""
+    return (types or "ids") if k else ""
 
 
 def route(prog: Program, alphabet: str, k: int, types: str) -> str:
     """Which kernel handles ``prog``; raises UnsupportedOnGPU if none does."""
     if k > _lib.PM_MAX_K:
         raise UnsupportedOnGPU("k=%d > %d errors is not supported by the GPU kernels" % (k, _lib.PM_MAX_K))
-    if k and ("i" in types or "d" in types):
-        raise UnsupportedOnGPU("insertions/deletions (-k %d%s) are not supported by the GPU kernels yet"
-                               % (k, types))
     if prog.m > 64:
         raise UnsupportedOnGPU("patterns longer than 64 positions are not supported")
-    if prog.linear and alphabet == NUC:
+    indel = bool(k) and ("i" in types or "d" in types)
+    if indel and "d" in types and prog.min_len <= k:
+        raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
+                               % (k, prog.min_len))
+    if prog.linear and alphabet == NUC and not indel:
         return "linear"
     if prog.max_len is None:
         raise UnsupportedOnGPU("unbounded repetition (* or +) is not supported by the GPU scan yet")
@@ -243,12 +246,19 @@ def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int) -> Hits:
     return _collect(LinearBatch(progs).launch(db, k))
 
 
-def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0) -> Hits:
+def error_mask(types: str) -> int:
+    """'-k' type letters -> PM_ERR_* mask (patmatch.py:299-309)."""
+    return ((_lib.PM_ERR_INS if "i" in types else 0) | (_lib.PM_ERR_DEL if "d" in types else 0)
+            | (_lib.PM_ERR_SUB if "s" in types else 0))
+
+
+def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s") -> Hits:
     bm = np.array(prog.byte_masks(), dtype=np.uint64)
     fol = np.array(prog.follow, dtype=np.uint64)
+    errs = error_mask(types) if k else _lib.PM_ERR_SUB
     out = ctypes.c_void_p()
-    check(_lib.load().pm_scan_nfa(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
-                                  prog.max_len, k, pattern_id, ctypes.byref(out)))
+    check(_lib.load().pm_scan_nfa_errs(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
+                                       prog.max_len, prog.min_len, k, errs, pattern_id, ctypes.byref(out)))
     return _collect(out)
 
 
@@ -279,7 +289,7 @@ def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str 
             results[i] = hits.for_pattern(slot)
     for i in range(len(progs)):
         if routes[i] == "nfa" and canonical[i] == i:
-            hits = scan_nfa(db, progs[i], k, 0)
+            hits = scan_nfa(db, progs[i], k, 0, types)
             total_ms += hits.kernel_ms
             results[i] = (hits.beg, hits.end)
     for i in range(len(progs)):

@@ -34,6 +34,14 @@ QUERIES = [
     ("<ATGNNN", "dna", "Both strands", None, None, None, None, 500),
     ("NNNTAA>", "dna", None, None, None, None, None, 500),
     ("RGD", "pep", None, None, None, "substitution", "1", 200),
+    # insertions / deletions (-k <k><ids>; no checkbox = all three, patmatch.py:308)
+    ("GAATTC", "dna", None, None, None, None, "1", 300),
+    ("TATAWAWR", "dna", "Both strands", "insertion", "deletion", None, "1", "no limit"),
+    ("CCAAT", "dna", None, None, "deletion", "substitution", "1", 100),
+    ("GGNCC", "dna", "Watson strand", "insertion", None, None, "2", 50),
+    ("CX{2,4}CX{3}[LIVMFYWC]", "pep", None, "insertion", None, None, "1", 500),
+    ("RGD", "pep", None, None, None, None, "2", 200),
+    ("KDEL>", "pep", None, None, "deletion", None, "1", 500),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]

@@ -71,3 +71,21 @@ def test_specialized_kernel_matrix_compiles(pat, k):
     progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
     assert engine.jit_compile(progs, k) > 1000
     assert engine.jit_compile(progs[:1], k) > 1000
+
+
+def test_route_indels():
+    """-k with insertions/deletions routes to the Glushkov kernels; deletions
+    with k >= the shortest match are refused loudly (no CPU fallback)."""
+    from patmatchdocker_amd import engine
+    from patmatchdocker_amd._lib import UnsupportedOnGPU
+    from patmatchdocker_amd.regex import compile_pattern
+    lin = compile_pattern("(GAATTC)")
+    assert engine.route(lin, engine.NUC, 2, "s") == "linear"
+    assert engine.route(lin, engine.NUC, 2, "ids") == "nfa"
+    assert engine.route(lin, engine.NUC, 2, "i") == "nfa"
+    assert engine.route(lin, engine.NUC, 0, "") == "linear"
+    assert engine.parse_error_types(2, "") == "ids"
+    assert engine.error_mask("ids") == 7 and engine.error_mask("d") == 2
+    with pytest.raises(UnsupportedOnGPU):
+        engine.route(compile_pattern("(RGD)"), engine.BYTE, 3, "d")
+    assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 2, "d") == "nfa"

@@ -197,3 +197,62 @@ def test_decode_roundtrip_multi_tile(engine):
             want += line.upper()
         want += b"\n"
     assert got == bytes(want[:len(text)])
+
+
+INDEL_DNA = ["GAATTC", "TATAWAWR", "TGANTCAG", "AN{2,3}TC", "GA(TC){1,2}A", "CCAATNNNNNGG",
+             "ACGTACGTACGTACGTACGTACGTACGTACGTACG"]
+INDEL_PEP = ["CX{2,4}CX{3}[LIVMFYWC]", "NXS", "RGDX", "LXXLL", "KDEL>", "W{1,3}YP", "P[^P]GA"]
+
+
+@pytest.mark.parametrize("types", ["ids", "i", "d", "id", "is", "ds"])
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_indel_scan_dna(engine, oracle_mod, types, k):
+    """-k <k><types> with insertions/deletions (the web default when
+    mismatches > 0) through the Glushkov kernels, both strands, vs the oracle
+    (pm_oracle.c's forward recurrence; parity of the binary itself unpinned)."""
+    text = dna_fasta(200 + k, n_records=4, max_len=3000, width=(70 if k == 2 else None))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in INDEL_DNA:
+            fwd = convert("-n", pat)
+            progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+            if "d" in types and min(p.min_len for p in progs) <= k:
+                continue
+            res, _ = engine.scan(db, progs, k=k, types=types)
+            for prog, r in zip(progs, res):
+                want = oracle_mod.scan(text, prog, k, types, skip_headers=True)
+                assert _gpu_pairs(r) == want, (pat, prog.source, k, types)
+    finally:
+        db.close()
+
+
+@pytest.mark.parametrize("types", ["ids", "id", "s", "d"])
+@pytest.mark.parametrize("k", [1, 2])
+def test_indel_scan_peptide(engine, oracle_mod, types, k):
+    text = pep_fasta(300 + k, n_records=30)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE)
+    try:
+        for pat in INDEL_PEP:
+            prog = compile_pattern(convert("-p", pat))
+            if "d" in types and prog.min_len <= k:
+                continue
+            res, _ = engine.scan(db, [prog], k=k, types=types)
+            want = oracle_mod.scan(text, prog, k, types, skip_headers=True)
+            assert _gpu_pairs(res[0]) == want, (pat, k, types)
+    finally:
+        db.close()
+
+
+def test_indel_multi_tile(engine, oracle_mod):
+    """Insertions/deletions across stream and tile boundaries of the
+    nucleotide layout (~330 KB, wrapped lines, N runs)."""
+    text = dna_fasta(404, n_records=6, min_len=30000, max_len=80000, width=60)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        assert len(db) > 4 * 65536
+        for pat, k in [("TGCTGASTCAGCANW", 2), ("GAATTC", 1), ("TATAWAWR", 1)]:
+            prog = compile_pattern(convert("-n", pat))
+            res, _ = engine.scan(db, [prog], k=k, types="ids")
+            assert _gpu_pairs(res[0]) == oracle_mod.scan(text, prog, k, "ids", skip_headers=True), pat
+    finally:
+        db.close()

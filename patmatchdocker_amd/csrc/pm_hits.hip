@@ -284,6 +284,8 @@ int pm_hits_kernel_ms(const pm_hits* h, double* ms) {
 int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count) {
     return guarded([&] {
         require(h != nullptr, "hits is NULL");
+        DeviceGuard g(h->device);
+        if (h->ready) HIPCHK(hipEventSynchronize(h->ready));   // the pointers are read by foreign streams
         if (keys) *keys = h->keys;
         if (lens) *lens = h->lens;
         if (count) *count = h->count;

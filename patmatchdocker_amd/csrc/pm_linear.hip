@@ -207,8 +207,9 @@ constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 wav
 // path; windows overlapping an exception are dropped here (breaks kill,
 // windows with an "other" byte belong to k_linear_others), which needs the
 // exception planes only for lanes the tile's lane flags mark.  One block per
-// pm_linear_jit workgroup, wave w takes the records of that workgroup's wave
-// w; slots of the (pattern, workgroup) output segments are reserved with LDS
+// output segment (`group` consecutive pm_linear_jit workgroups, i.e. a
+// contiguous tile range), wave w takes the records of those workgroups'
+// waves w; slots of the (pattern, segment) hit lists are reserved with LDS
 // atomics and the segment counts written once at the end (k_linear_others,
 // launched after, appends to them with global atomics).
 struct ExpandArgs {
@@ -223,47 +224,50 @@ struct ExpandArgs {
     int P, pattern_base;
     uint64_t* out;
     uint32_t* seg_cnt;
-    uint32_t cap, nwg, tiles_per_wg;
+    uint32_t cap, nwg, nout, group, tiles_per_wg;
 };
 
 __global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
     __shared__ uint32_t cnt_p[4];
-    const uint32_t wg = blockIdx.x, part = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
+    const uint32_t og = blockIdx.x, part = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
     if (threadIdx.x < 4) cnt_p[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t seg = wg * 4 + part;
-    uint32_t cnt = a.rec_cnt[seg];
-    if (cnt > a.rcap) {
-        if (lane_t == 0) atomicMax(a.rec_over, cnt);
-        cnt = a.rcap;
-    }
-    for (uint32_t i = lane_t; i < cnt; i += 64) {
-        const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-        const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 11);
-        const uint32_t lane = (r.x >> 5) & 63, s = (r.x >> 2) & 7, p = r.x & 3;
-        if (tile >= a.ntiles) continue;
-        const uint32_t w0 = 32u * lane + part * JIT_STEPS + s;
-        uint32_t live = r.y;
-        if ((a.lflag[tile] >> lane) & 1) {
-            uint32_t kill = 0;
-            const int len = a.lengths[p];
-            for (int j = 0; j < len; ++j) {
-                const uint2 e = a.bo[phys_word(tile, w0 + j)];
-                kill |= e.x | e.y;
-            }
-            live &= ~kill;
+    const uint32_t wg_end = min(a.nwg, (og + 1) * a.group);
+    for (uint32_t wg = og * a.group; wg < wg_end; ++wg) {
+        const uint32_t seg = wg * 4 + part;
+        uint32_t cnt = a.rec_cnt[seg];
+        if (cnt > a.rcap) {
+            if (lane_t == 0) atomicMax(a.rec_over, cnt);
+            cnt = a.rcap;
         }
-        const uint32_t slot = (uint32_t)a.pattern_base + p;
-        const uint64_t sg = (uint64_t)slot * a.nwg + wg;
-        for (; live; live &= live - 1) {
-            const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
-            if (pos >= a.n) continue;
-            const uint32_t o = atomicAdd(&cnt_p[p], 1u);
-            if (o < a.cap) a.out[sg * a.cap + o] = ((uint64_t)slot << 48) | pos;
+        for (uint32_t i = lane_t; i < cnt; i += 64) {
+            const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
+            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 11);
+            const uint32_t lane = (r.x >> 5) & 63, s = (r.x >> 2) & 7, p = r.x & 3;
+            if (tile >= a.ntiles) continue;
+            const uint32_t w0 = 32u * lane + part * JIT_STEPS + s;
+            uint32_t live = r.y;
+            if ((a.lflag[tile] >> lane) & 1) {
+                uint32_t kill = 0;
+                const int len = a.lengths[p];
+                for (int j = 0; j < len; ++j) {
+                    const uint2 e = a.bo[phys_word(tile, w0 + j)];
+                    kill |= e.x | e.y;
+                }
+                live &= ~kill;
+            }
+            const uint32_t slot = (uint32_t)a.pattern_base + p;
+            const uint64_t sg = (uint64_t)slot * a.nout + og;
+            for (; live; live &= live - 1) {
+                const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
+                if (pos >= a.n) continue;
+                const uint32_t o = atomicAdd(&cnt_p[p], 1u);
+                if (o < a.cap) a.out[sg * a.cap + o] = ((uint64_t)slot << 48) | pos;
+            }
         }
     }
     __syncthreads();
-    if ((int)threadIdx.x < a.P) a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nwg + wg] = cnt_p[threadIdx.x];
+    if ((int)threadIdx.x < a.P) a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nout + og] = cnt_p[threadIdx.x];
 }
 
 __global__ void k_linear_lens(const uint64_t* __restrict__ keys, uint64_t n, const int32_t* __restrict__ lengths,
@@ -351,7 +355,9 @@ std::string subset_expr(int subset, const std::string& h, const std::string& l) 
 // returns the name of the result.  Columns of equal weight are compressed
 // with full adders (xor3 + majority, one v_bitop3 each); carries whose
 // weight exceeds K go straight into the dead mask, the few bits left are
-// compared with K at the end.  ~1.6 ops per input for K = 2.
+// compared with K at the end.  ~1.4 ops per input for K = 2.  Three-way ORs
+// are emitted as v_bitop3 0xFE: v_or3_b32 issues ~1.5x slower on gfx950
+// (profiles/r01c_valu_rates.txt).
 std::string emit_dead_network(std::ostringstream& o, const std::vector<std::string>& in, int K, int& uid,
                               const std::string& ind) {
     auto fresh = [&](const char* pfx) { return std::string(pfx) + std::to_string(uid++); };
@@ -361,7 +367,7 @@ std::string emit_dead_network(std::ostringstream& o, const std::vector<std::stri
         size_t i = 1;
         for (; i + 1 < in.size(); i += 2) {
             const std::string v = fresh("d");
-            o << ind << "const u32 " << v << " = " << acc << " | " << in[i] << " | " << in[i + 1] << ";\n";
+            o << ind << "const u32 " << v << " = B3(" << acc << ", " << in[i] << ", " << in[i + 1] << ", 0xFE);\n";
             acc = v;
         }
         if (i < in.size()) {
@@ -408,7 +414,7 @@ std::string emit_dead_network(std::ostringstream& o, const std::vector<std::stri
     size_t i = 1;
     for (; i + 1 < terms.size(); i += 2) {
         const std::string v = fresh("d");
-        o << ind << "const u32 " << v << " = " << acc << " | " << terms[i] << " | " << terms[i + 1] << ";\n";
+        o << ind << "const u32 " << v << " = B3(" << acc << ", " << terms[i] << ", " << terms[i + 1] << ", 0xFE);\n";
         acc = v;
     }
     if (i < terms.size()) {
@@ -746,15 +752,28 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         if (jit) {
             // one output segment per (pattern, workgroup); workgroups own
             // contiguous tile ranges (3 per CU resident)
-            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * jit_wg_per_cu());
+            // more workgroups than resident slots (PM_JIT_SPLIT x): the
+            // dispatcher hands the next one to whichever CU frees a slot, so
+            // an unevenly loaded CU does not hold up the whole launch
+            const char* split_env = getenv("PM_JIT_SPLIT");
+            const uint64_t split = split_env ? std::max(1, atoi(split_env)) : 16;
+            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * jit_wg_per_cu() * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
             const uint64_t nseg = nwg * 4;   // one lane-record segment per wave
-            uint32_t cap = 1024;
-            while (cap > 256 && (uint64_t)n_patterns * nwg * cap * 8 > (1ull << 30)) cap /= 2;
+            // segment capacities scale with the tiles a workgroup owns (a
+            // random 15-mer at k = 2 leaves ~1.4 hits per tile and strand);
+            // an overflow re-runs with the counts seen
+            uint32_t cap = 256;
+            // output segments: `split` consecutive workgroups share one
+            // (pattern, segment) hit list, so the sort sees ~768 segments
+            const uint64_t group = split;
+            const uint64_t nout = (nwg + group - 1) / group;
+            while (cap < 4096 && cap < 16 * tpw * group) cap *= 2;
+            while (cap > 256 && (uint64_t)n_patterns * nout * cap * 8 > (1ull << 30)) cap /= 2;
             // records per wave: at most tiles_per_wg * 64 lanes * 8 steps * 4 patterns
             const uint64_t rec_max = tpw * 64 * JIT_STEPS * 4;
-            uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, 512);
+            uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, std::max<uint64_t>(128, 8 * tpw));
             uint32_t* h_over = static_cast<uint32_t*>(reserve_host(db, db->pin_up, sizeof(uint32_t)));
             for (int attempt = 0; attempt < 3 && !done; ++attempt) {
                 Carve cv;
@@ -766,7 +785,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
                 uint32_t* d_over = reinterpret_cast<uint32_t*>(rbase + o_over);
                 HIPCHK(hipMemsetAsync(d_over, 0, sizeof(uint32_t), s));
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nwg, cap);
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, cap);
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
                 jev.clear();
@@ -779,14 +798,14 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                     HIPCHK(hipEventRecord(jev.back()->b, s));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
-                                  sb.cap, (uint32_t)nwg, (uint32_t)tpw};
-                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nwg), dim3(256), 0, s, xa);
+                                  sb.cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group, (uint32_t)tpw};
+                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(256), 0, s, xa);
                     HIPCHK(hipGetLastError());
                     if (db->nflag) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                      sb.out, sb.cnt, sb.cap, (uint32_t)nwg, (uint32_t)tpw};
+                                      sb.out, sb.cnt, sb.cap, (uint32_t)nout, (uint32_t)(tpw * group)};
                         hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, s, oa);
                         HIPCHK(hipGetLastError());
                     }
@@ -846,7 +865,8 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                                reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
             HIPCHK(hipGetLastError());
         }
-        HIPCHK(hipStreamSynchronize(s));
+        // no host sync here: consumers wait on h->ready (pm_hits_copy*,
+        // pm_hits_device, pm_hits_destroy)
         hits_ready(db, h);
         *out = h;
     });

@@ -77,5 +77,7 @@ def hits_to_tensors(hits_handle, device: torch.device):
     keys = torch.empty(n.value, dtype=torch.int64, device=device)
     lens = torch.empty(n.value, dtype=torch.int32, device=device)
     if n.value:
-        _lib.check(lib.pm_hits_copy_device(hits_handle, keys.data_ptr(), lens.data_ptr(), n.value, None))
+        # ordered on torch's current stream after the scan (no host sync)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream) if keys.is_cuda else None
+        _lib.check(lib.pm_hits_copy_device(hits_handle, keys.data_ptr(), lens.data_ptr(), n.value, stream))
     return keys, lens

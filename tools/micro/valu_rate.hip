@@ -4,6 +4,7 @@
 // lane-ops/s and cycles per wave-instruction per SIMD at the nominal 2.4 GHz.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define A3(ins) asm volatile(ins " %0, %1, %2, %3" : "=v"(a[i]) : "v"(a[i]), "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]))
 #define A2(ins) asm volatile(ins " %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "v"(a[(i + 1) & 7]))
@@ -39,9 +40,11 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed, int iters
     if (r == 0x12345678u) out[0] = r;
 }
 
+static int g_wps = 8;   // blocks per CU = waves per SIMD (256-thread blocks)
+
 template <int OP>
 void run(const char* name, unsigned* out, hipEvent_t e0, hipEvent_t e1) {
-    const int blocks = 256 * 8, iters = 4096;
+    const int blocks = 256 * g_wps, iters = 4096;
     float ms = 0;
     for (int rep = 0; rep < 2; ++rep) {
         hipEventRecord(e0);
@@ -55,7 +58,9 @@ void run(const char* name, unsigned* out, hipEvent_t e0, hipEvent_t e1) {
            wave_instr * 64 / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.4e9 / (wave_instr / 1024));
 }
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1) g_wps = atoi(argv[1]);
+    printf("waves per SIMD: %d\n", g_wps);
     unsigned* out;
     (void)hipMalloc(&out, 4);
     hipEvent_t e0, e1;

@@ -316,6 +316,7 @@ void free_db(pm_db* db) {
         if (p) (void)hipFree(p);
     if (db->pin_up.p) (void)hipHostFree(db->pin_up.p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
+    if (db->pin_slots.p) (void)hipHostFree(db->pin_slots.p);
     if (db->own_stream && db->stream) (void)hipStreamDestroy(db->stream);
     delete db;
 }

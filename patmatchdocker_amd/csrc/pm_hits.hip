@@ -21,14 +21,25 @@ namespace {
 
 // bin counters -> exclusive offsets; one block of 1024 threads, each owning a
 // contiguous run of bins
+struct BinShape {
+    const uint64_t* slot_base;
+    const uint32_t* slot_cap;
+    uint32_t bins_per_slot;
+    __device__ uint32_t cap(uint32_t bin) const { return slot_cap[bin / bins_per_slot]; }
+    __device__ const uint64_t* src(const uint64_t* out, uint32_t bin) const {
+        const uint32_t sl = bin / bins_per_slot;
+        return out + slot_base[sl] + (uint64_t)(bin % bins_per_slot) * slot_cap[sl];
+    }
+};
+
 __global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict__ cnt, uint32_t nbins,
-                                                      uint32_t cap, uint64_t* __restrict__ off) {
+                                                      BinShape sh, uint64_t* __restrict__ off) {
     __shared__ uint64_t part[1024];
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nbins + 1023) / 1024;
     const uint32_t b0 = t * per, b1 = min(nbins, b0 + per);
     uint64_t s = 0;
-    for (uint32_t b = b0; b < b1; ++b) s += min(cnt[b], cap);
+    for (uint32_t b = b0; b < b1; ++b) s += min(cnt[b], sh.cap(b));
     part[t] = s;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {
@@ -40,19 +51,19 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict
     uint64_t acc = part[t] - s;
     for (uint32_t b = b0; b < b1; ++b) {
         off[b] = acc;
-        acc += min(cnt[b], cap);
+        acc += min(cnt[b], sh.cap(b));
     }
 }
 
 // One workgroup per bin: bitonic sort in LDS, write at the bin's offset.
 __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
-                                                   const uint64_t* __restrict__ off, uint32_t cap,
+                                                   const uint64_t* __restrict__ off, BinShape sh,
                                                    uint64_t* __restrict__ dst) {
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
-    const uint32_t c = min(cnt[bin], cap);
+    const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0) return;
-    const uint64_t* src = out + (uint64_t)bin * cap;
+    const uint64_t* src = sh.src(out, bin);
     uint64_t* d = dst + off[bin];
     if (c == 1) {
         if (threadIdx.x == 0) d[0] = src[0];
@@ -79,11 +90,12 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
 }
 
 __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
-                              const uint64_t* __restrict__ off, uint32_t cap, uint64_t* __restrict__ dst) {
+                              const uint64_t* __restrict__ off, BinShape sh, uint64_t* __restrict__ dst) {
     const uint32_t bin = blockIdx.x;
-    const uint32_t c = min(cnt[bin], cap);
+    const uint32_t c = min(cnt[bin], sh.cap(bin));
     const uint64_t o = off[bin];
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = out[(uint64_t)bin * cap + i];
+    const uint64_t* src = sh.src(out, bin);
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = src[i];
 }
 
 std::mutex g_pool_mu;
@@ -122,41 +134,59 @@ void pool_put(int device, void* p, size_t cap) {
     else (void)hipFree(p);
 }
 
-SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected) {
+// Allocates out/cnt/slot arrays for n_slots slots of `per_slot` bins with
+// per-slot capacities; counters zeroed, slot tables uploaded.
+static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& caps) {
     SinkBuffers sb;
-    require(n_slots >= 1 && (uint32_t)n_slots <= MAX_BINS, "internal: too many pattern slots");
-    sb.bins_per_pattern = std::max<uint32_t>(1, NBINS / (uint32_t)n_slots);
-    sb.pos_shift = 0;
-    const uint64_t last = std::max<uint64_t>(n_positions, 1) - 1;
-    while ((last >> sb.pos_shift) >= sb.bins_per_pattern) ++sb.pos_shift;
-    sb.nbins = (uint32_t)n_slots * sb.bins_per_pattern;
-    uint64_t cap = std::max<uint64_t>(1024, (expected + sb.nbins - 1) / sb.nbins * 2);
-    cap = std::min<uint64_t>(cap, 1ull << 26);
-    sb.cap = (uint32_t)cap;
+    require(n_slots >= 1 && per_slot >= 1 && caps.size() == (size_t)n_slots, "internal: bad sink shape");
+    sb.bins_per_pattern = per_slot;
+    sb.nbins = (uint32_t)n_slots * per_slot;
+    sb.slot_cap_h = caps;
+    std::vector<uint64_t> base(n_slots);
+    uint64_t total = 0;
+    sb.cap = 0;
+    for (int i = 0; i < n_slots; ++i) {
+        base[i] = total;
+        total += (uint64_t)per_slot * caps[i];
+        sb.cap = std::max(sb.cap, caps[i]);
+    }
     Carve c;
-    const size_t o_out = c.take((uint64_t)sb.nbins * sb.cap * sizeof(uint64_t));
+    const size_t o_out = c.take(total * sizeof(uint64_t));
     const size_t o_cnt = c.take(sb.nbins * sizeof(uint32_t));
-    uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
-    sb.out = reinterpret_cast<uint64_t*>(base + o_out);
-    sb.cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    const size_t o_base = c.take(n_slots * sizeof(uint64_t));
+    const size_t o_cap = c.take(n_slots * sizeof(uint32_t));
+    uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
+    sb.out = reinterpret_cast<uint64_t*>(d + o_out);
+    sb.cnt = reinterpret_cast<uint32_t*>(d + o_cnt);
+    sb.slot_base = reinterpret_cast<uint64_t*>(d + o_base);
+    sb.slot_cap = reinterpret_cast<uint32_t*>(d + o_cap);
+    // slot tables staged through pinned memory (ordered on the db stream)
+    uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_slots, n_slots * 12 + 16));
+    memcpy(h, base.data(), n_slots * 8);
+    memcpy(h + n_slots * 8, caps.data(), n_slots * 4);
+    HIPCHK(hipMemcpyAsync(sb.slot_base, h, n_slots * 8, hipMemcpyHostToDevice, db->stream));
+    HIPCHK(hipMemcpyAsync(sb.slot_cap, h + n_slots * 8, n_slots * 4, hipMemcpyHostToDevice, db->stream));
     HIPCHK(hipMemsetAsync(sb.cnt, 0, sb.nbins * sizeof(uint32_t), db->stream));
     return sb;
 }
 
-SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, uint32_t cap) {
-    SinkBuffers sb;
-    require(n_slots >= 1 && per_slot >= 1, "internal: bad segment shape");
-    sb.bins_per_pattern = per_slot;
+SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected) {
+    require(n_slots >= 1 && (uint32_t)n_slots <= MAX_BINS, "internal: too many pattern slots");
+    const uint32_t bpp = std::max<uint32_t>(1, NBINS / (uint32_t)n_slots);
+    uint32_t shift = 0;
+    const uint64_t last = std::max<uint64_t>(n_positions, 1) - 1;
+    while ((last >> shift) >= bpp) ++shift;
+    const uint32_t nbins = (uint32_t)n_slots * bpp;
+    uint64_t cap = std::max<uint64_t>(1024, (expected + nbins - 1) / nbins * 2);
+    cap = std::min<uint64_t>(cap, 1ull << 26);
+    SinkBuffers sb = alloc_sink(db, n_slots, bpp, std::vector<uint32_t>(n_slots, (uint32_t)cap));
+    sb.pos_shift = shift;   // uniform capacity: bin b lives at out + b * cap (Sink::push)
+    return sb;
+}
+
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps) {
+    SinkBuffers sb = alloc_sink(db, n_slots, per_slot, slot_caps);
     sb.pos_shift = 0;
-    sb.nbins = (uint32_t)n_slots * per_slot;
-    sb.cap = cap;
-    Carve c;
-    const size_t o_out = c.take((uint64_t)sb.nbins * sb.cap * sizeof(uint64_t));
-    const size_t o_cnt = c.take(sb.nbins * sizeof(uint32_t));
-    uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
-    sb.out = reinterpret_cast<uint64_t*>(base + o_out);
-    sb.cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
-    HIPCHK(hipMemsetAsync(sb.cnt, 0, sb.nbins * sizeof(uint32_t), db->stream));
     return sb;
 }
 
@@ -167,9 +197,9 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
     counts.assign(h, h + sb.nbins);
     uint64_t total = 0;
     overflow = false;
-    for (uint32_t c : counts) {
-        total += c;
-        overflow |= c > sb.cap;
+    for (uint32_t b = 0; b < sb.nbins; ++b) {
+        total += counts[b];
+        overflow |= counts[b] > sb.slot_cap_h[b / sb.bins_per_pattern];
     }
     return total;
 }
@@ -197,14 +227,15 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         const size_t o_tmp = lds ? 0 : c.take(sort_bytes);
         uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
-        hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sb.cap, d_off);
+        const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
+        hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sh, d_off);
         HIPCHK(hipGetLastError());
         if (lds) {
-            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sb.cap, h->keys);
+            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh, h->keys);
             HIPCHK(hipGetLastError());
         } else {
             uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
-            hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sb.cap,
+            hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh,
                                unsorted);
             HIPCHK(hipGetLastError());
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0, 64,

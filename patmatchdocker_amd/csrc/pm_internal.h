@@ -218,7 +218,7 @@ struct pm_db {
     bool own_stream = false;
     // per-call workspaces (never stream-ordered allocations)
     pm_devbuf ws_tab, ws_sink, ws_post, ws_rec;
-    pm_hostbuf pin_up, pin_down;
+    pm_hostbuf pin_up, pin_down, pin_slots;
     uint64_t device_bytes = 0;
 };
 
@@ -303,7 +303,12 @@ struct EventPair {
 struct SinkBuffers {
     uint64_t* out = nullptr;
     uint32_t* cnt = nullptr;
-    uint32_t cap = 0;
+    uint32_t cap = 0;              // uniform capacity (make_sink) / the largest slot capacity
+    // per pattern slot: bin b of slot p = b / bins_per_pattern holds up to
+    // slot_cap[p] keys at out + slot_base[p] + (b % bins_per_pattern) * slot_cap[p]
+    uint64_t* slot_base = nullptr;
+    uint32_t* slot_cap = nullptr;
+    std::vector<uint32_t> slot_cap_h;
     uint32_t bins_per_pattern = NBINS;
     uint32_t pos_shift = 0;
     uint32_t nbins = NBINS;
@@ -315,7 +320,7 @@ struct SinkBuffers {
 SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected);
 // Bins filled by the producer itself: n_slots x per_slot segments of `cap`
 // keys, each a position range in increasing order (pm_linear_jit).
-SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, uint32_t cap);
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps);
 // Reads bin counters; returns total, sets `overflow` if a bin exceeded cap.
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
 // bins -> one sorted key list (pattern << 48 | pos) owned by the returned

@@ -155,9 +155,11 @@ struct OthersArgs {
     const uint8_t* class_any;
     const uint32_t* class_bytes;
     int P, k, pattern_base;
-    uint64_t* out;       // the specialized kernel's (pattern, workgroup) segments
+    uint64_t* out;       // the specialized kernel's (pattern, segment) hit lists
     uint32_t* seg_cnt;
-    uint32_t cap, nwg, tiles_per_wg;
+    const uint64_t* slot_base;
+    const uint32_t* slot_cap;
+    uint32_t nwg, tiles_per_wg;
 };
 
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
@@ -191,9 +193,9 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
                 }
                 if (ok) {
                     const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                    const uint64_t seg = (uint64_t)slot * a.nwg + (s / TILE_POS) / a.tiles_per_wg;
-                    const uint32_t o = atomicAdd(&a.seg_cnt[seg], 1u);
-                    if (o < a.cap) a.out[seg * a.cap + o] = ((uint64_t)slot << 48) | s;
+                    const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
+                    const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
+                    if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
                 }
             }
         }
@@ -224,7 +226,9 @@ struct ExpandArgs {
     int P, pattern_base;
     uint64_t* out;
     uint32_t* seg_cnt;
-    uint32_t cap, nwg, nout, group, tiles_per_wg;
+    const uint64_t* slot_base;
+    const uint32_t* slot_cap;
+    uint32_t nwg, nout, group, tiles_per_wg;
 };
 
 __global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
@@ -257,12 +261,13 @@ __global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
                 live &= ~kill;
             }
             const uint32_t slot = (uint32_t)a.pattern_base + p;
-            const uint64_t sg = (uint64_t)slot * a.nout + og;
+            const uint32_t cap = a.slot_cap[slot];
+            uint64_t* dst = a.out + a.slot_base[slot] + (uint64_t)og * cap;
             for (; live; live &= live - 1) {
                 const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
                 if (pos >= a.n) continue;
                 const uint32_t o = atomicAdd(&cnt_p[p], 1u);
-                if (o < a.cap) a.out[sg * a.cap + o] = ((uint64_t)slot << 48) | pos;
+                if (o < cap) dst[o] = ((uint64_t)slot << 48) | pos;
             }
         }
     }
@@ -691,6 +696,11 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     return jk.fn;
 }
 
+// Segment / record capacities per (database, batch) that held all hits
+// last time.
+std::mutex g_cap_mu;
+std::map<std::pair<const pm_db*, std::string>, std::pair<std::vector<uint32_t>, uint32_t>> g_cap_hint;
+
 // PM_JIT: "0" never, "1" always, default: databases of >= 64 Mi positions
 bool use_jit(const pm_db* db) {
     const char* e = getenv("PM_JIT");
@@ -771,11 +781,27 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             const uint64_t nout = (nwg + group - 1) / group;
             while (cap < 4096 && cap < 16 * tpw * group) cap *= 2;
             while (cap > 256 && (uint64_t)n_patterns * nout * cap * 8 > (1ull << 30)) cap /= 2;
+            // per-pattern capacities: a dense pattern (many hits) gets its own
+            // larger segments on the retry, the others keep theirs
+            std::vector<uint32_t> slot_caps(n_patterns, cap);
             // records per wave: at most tiles_per_wg * 64 lanes * 8 steps * 4 patterns
             const uint64_t rec_max = tpw * 64 * JIT_STEPS * 4;
             uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, std::max<uint64_t>(128, 8 * tpw));
+            // capacities that sufficed for the same batch on this database
+            // last time (a repeated query does not pay the overflow retry)
+            std::string cap_key;
+            for (const Chunk& ch : chunks)
+                cap_key += jit_signature(ch.P, k, lengths + ch.base, pos_class + 64 * ch.base, class_acgt, class_is_any) + "|";
+            {
+                std::lock_guard<std::mutex> lk(g_cap_mu);
+                auto it = g_cap_hint.find({db, cap_key});
+                if (it != g_cap_hint.end() && it->second.first.size() == slot_caps.size()) {
+                    slot_caps = it->second.first;
+                    rcap = std::max(rcap, it->second.second);
+                }
+            }
             uint32_t* h_over = static_cast<uint32_t*>(reserve_host(db, db->pin_up, sizeof(uint32_t)));
-            for (int attempt = 0; attempt < 3 && !done; ++attempt) {
+            for (int attempt = 0; attempt < 4 && !done; ++attempt) {
                 Carve cv;
                 const size_t o_rec = cv.take(nseg * rcap * sizeof(uint2));
                 const size_t o_rcnt = cv.take(nseg * sizeof(uint32_t));
@@ -785,7 +811,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
                 uint32_t* d_over = reinterpret_cast<uint32_t*>(rbase + o_over);
                 HIPCHK(hipMemsetAsync(d_over, 0, sizeof(uint32_t), s));
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, cap);
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps);
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
                 jev.clear();
@@ -798,14 +824,16 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                     HIPCHK(hipEventRecord(jev.back()->b, s));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
-                                  sb.cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group, (uint32_t)tpw};
+                                  sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
+                                  (uint32_t)tpw};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(256), 0, s, xa);
                     HIPCHK(hipGetLastError());
                     if (db->nflag) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                      sb.out, sb.cnt, sb.cap, (uint32_t)nout, (uint32_t)(tpw * group)};
+                                      sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout,
+                                      (uint32_t)(tpw * group)};
                         hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, s, oa);
                         HIPCHK(hipGetLastError());
                     }
@@ -814,12 +842,24 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t rec_need = *h_over;
-                if (!overflow && rec_need == 0) { done = true; break; }
+                if (!overflow && rec_need == 0) {
+                    done = true;
+                    std::lock_guard<std::mutex> lk(g_cap_mu);
+                    if (g_cap_hint.size() > 256) g_cap_hint.clear();
+                    g_cap_hint[{db, cap_key}] = {slot_caps, rcap};
+                    break;
+                }
                 if (rec_need) rcap = std::max<uint32_t>(rcap, rec_need);
                 if (overflow) {
-                    const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
-                    if (maxc > LDS_SORT_CAP) break;   // pathological hit density: generic kernels below
-                    while (cap < maxc) cap *= 2;
+                    uint64_t keys_total = 0;
+                    for (int p = 0; p < n_patterns; ++p) {
+                        const uint32_t* c = counts.data() + (uint64_t)p * nout;
+                        const uint32_t m = *std::max_element(c, c + nout);
+                        while (slot_caps[p] < m) slot_caps[p] *= 2;
+                        keys_total += (uint64_t)slot_caps[p] * nout;
+                    }
+                    require(keys_total * 8 <= (16ull << 30), "hit list larger than 16 GB of segments",
+                            PM_E_UNSUPPORTED);
                 }
             }
         }

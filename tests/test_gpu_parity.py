@@ -256,3 +256,37 @@ def test_indel_multi_tile(engine, oracle_mod):
             assert _gpu_pairs(res[0]) == oracle_mod.scan(text, prog, k, "ids", skip_headers=True), pat
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("k", [0, 2])
+def test_specialized_batch_chunks(engine, oracle_mod, monkeypatch, k):
+    """A batch of 11 patterns through the specialized kernel (chunks of 4, 4
+    and 3 -> 4 + 4 + 2 + 1 launches), record expansion per chunk, vs oracle."""
+    monkeypatch.setenv("PM_JIT", "1")
+    rng = np.random.default_rng(17 + k)
+    text = dna_fasta(91 + k, n_records=5, min_len=30000, max_len=70000, width=None)
+    pats = ["".join(rng.choice(list("ACGTACGTRYSWN"), size=int(rng.integers(8, 16)))) for _ in range(11)]
+    progs = [compile_pattern(convert("-n", p)) for p in pats]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=k, types="s")
+        for prog, r in zip(progs, res):
+            assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, k), (prog.source, k)
+    finally:
+        db.close()
+
+
+def test_specialized_dense_hits(engine, oracle_mod, monkeypatch):
+    """Patterns matching a large fraction of all windows (records overflow
+    the first guess, per-pattern segment capacities grow on the retry, LDS
+    sort replaced by the radix sort) next to a sparse one, vs the oracle."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = dna_fasta(131, n_records=4, min_len=60000, max_len=90000, width=None)
+    progs = [compile_pattern(convert("-n", p)) for p in ["NNNNNANN", "TGCTGASTCAGCANW", "RRYY", "GAATTC"]]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=1, types="s")
+        for prog, r in zip(progs, res):
+            assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, 1), prog.source
+    finally:
+        db.close()

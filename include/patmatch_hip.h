@@ -88,8 +88,8 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
 /* --- general patterns: Glushkov automaton (both alphabets) -------------
  * m positions (1..64); byte_mask[256] = positions accepting each folded
  * byte; follow[m] / first / last as produced by regex.py; max_len = the
- * longest match (patterns with unbounded repetition are rejected with
- * PM_E_UNSUPPORTED).  Reports, for every start with a match of <= k
+ * longest match, 0 = unbounded (`*`, `+`: a match may run to the end of
+ * its record).  Reports, for every start with a match of <= k
  * substitutions, the shortest end.  Hits carry pattern id `pattern_id`. */
 int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
                 uint64_t first, uint64_t last, int max_len, int k, int pattern_id,

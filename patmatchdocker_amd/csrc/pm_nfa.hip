@@ -43,6 +43,9 @@ struct NfaArgs {
     uint64_t rev_pre[4];      // reverse: prec(S[j]) | (I[j] ? last : 0) for the injected start config
     uint64_t rev_ins[4];      // reverse: S[j] (insertion source rows of the injected config)
     uint64_t fwd_del[4];      // forward: deletion closure of the start config (rows of R)
+    // unbounded patterns: reverse state entering each chunk from the right
+    // (rows at stride 4), found by k_nfa_carry; null = start from the halo
+    const uint64_t* in_state;
     // verify
     const uint64_t* starts;
     uint64_t nstarts;
@@ -109,7 +112,8 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
     const uint64_t top = c1 + a.halo;           // process (top .. c0], padded storage
     uint64_t R[K + 1];
 #pragma unroll
-    for (int j = 0; j <= K; ++j) R[j] = 0;
+    for (int j = 0; j <= K; ++j)
+        R[j] = (a.in_state && chunk_id + 1 < a.nchunks) ? a.in_state[(chunk_id + 1) * 4 + j] : 0ull;
     for (uint64_t p = top; p-- > c0;) {
         const uint8_t ch = char_at<NUC>(a, p);
         const uint64_t bc = s_b[ch];
@@ -121,6 +125,53 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
         if (live && p < c1 && p < a.n && (any & a.first))
             a.sink.push(a.sink.bin_of(0, p), ((uint64_t)a.pattern_id << 48) | p);
     }
+}
+
+// Unbounded patterns (`*`, `+`: a match may run to the end of its record):
+// chunk i's reverse scan must start from the true state entering it from the
+// right, which is chunk i+1's state after its leftmost position.  One
+// relaxation round: every chunk rescans itself from its right neighbour's
+// state of the previous round (from zero initially); the transfer is
+// monotone, so the states only grow and the rounds stop when none changed
+// (at most the chunks per record; a record break kills every state, so
+// patterns that die quickly converge in 1-2 rounds).  Chunks whose input did
+// not change since the previous round copy their old output.
+template <int K, bool NUC>
+__global__ __launch_bounds__(256) void k_nfa_carry(NfaArgs a, const uint64_t* __restrict__ st_old,
+                                                   uint64_t* __restrict__ st_new, const uint64_t* __restrict__ in_seen,
+                                                   uint64_t* __restrict__ in_now, uint32_t* changed) {
+    __shared__ uint64_t s_prec[8 * 256];
+    __shared__ uint64_t s_b[256];
+    for (int i = threadIdx.x; i < a.nt * 256; i += blockDim.x) s_prec[i] = a.prec[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_b[i] = a.bmask[i];
+    __syncthreads();
+    const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (gid >= a.nchunks) return;
+    const uint64_t c0 = gid * a.chunk, c1 = c0 + a.chunk;
+    uint64_t R[K + 1];
+    bool same = true;
+#pragma unroll
+    for (int j = 0; j <= K; ++j) {
+        R[j] = gid + 1 < a.nchunks ? st_old[(gid + 1) * 4 + j] : 0ull;
+        same &= R[j] == in_seen[gid * 4 + j];
+        in_now[gid * 4 + j] = R[j];
+    }
+    if (same) {   // input unchanged: output unchanged
+#pragma unroll
+        for (int j = 0; j <= K; ++j) st_new[gid * 4 + j] = st_old[gid * 4 + j];
+        return;
+    }
+    for (uint64_t p = c1; p-- > c0;) {
+        const uint8_t ch = char_at<NUC>(a, p);
+        nfa_rev_step<K>(R, s_b[ch], ch == '\n' ? 0ull : ~0ull, s_prec, a);
+    }
+    bool diff = false;
+#pragma unroll
+    for (int j = 0; j <= K; ++j) {
+        diff |= R[j] != st_old[gid * 4 + j];
+        st_new[gid * 4 + j] = R[j];
+    }
+    if (diff) atomicOr(changed, 1u);
 }
 
 // k_nfa_verify: one lane per start, forward automaton -> shortest end.
@@ -145,7 +196,11 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
         init[j] = j == 0;
     }
     uint32_t len = 0;
-    for (int d = 0; d < a.max_len; ++d) {
+    // max_len == 0: unbounded pattern; every start came with a match inside
+    // its record, and the record break ('\n', also the tail padding) kills
+    // every state, so the loop ends at the shortest end
+    const uint64_t steps = a.max_len ? (uint64_t)a.max_len : a.n - s + 1;
+    for (uint64_t d = 0; d < steps; ++d) {
         const uint8_t ch = char_at<NUC>(a, s + d);
         const uint64_t bc = s_b[ch];
         const uint64_t nb = ch == '\n' ? 0ull : ~0ull;
@@ -178,7 +233,7 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
             any |= R[j];
             alive |= init[j];
         }
-        if (any & a.last) { len = d + 1; break; }
+        if (any & a.last) { len = (uint32_t)(d + 1); break; }
         if (!any && !alive) break;
     }
     a.lens[i] = len;   // 0 = no match (cannot happen for a start found by k_nfa_rev)
@@ -191,6 +246,17 @@ void launch_nfa_rev(int k, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
         case 1: hipLaunchKernelGGL((k_nfa_rev<1, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
         case 2: hipLaunchKernelGGL((k_nfa_rev<2, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL((k_nfa_rev<3, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
+    }
+}
+
+template <bool NUC>
+void launch_nfa_carry(int k, const NfaArgs& a, uint32_t blocks, hipStream_t s, const uint64_t* o, uint64_t* n,
+                      const uint64_t* seen, uint64_t* now, uint32_t* changed) {
+    switch (k) {
+        case 0: hipLaunchKernelGGL((k_nfa_carry<0, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
+        case 1: hipLaunchKernelGGL((k_nfa_carry<1, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
+        case 2: hipLaunchKernelGGL((k_nfa_carry<2, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
+        default: hipLaunchKernelGGL((k_nfa_carry<3, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
     }
 }
 
@@ -220,7 +286,8 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
     return guarded([&] {
         require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");
         require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range");
-        require(max_len >= 1, "unbounded patterns (*, +) are not supported by the GPU scan yet", PM_E_UNSUPPORTED);
+        require(max_len >= 0, "max_len < 0");
+        const bool unbounded = max_len == 0;   // '*' / '+': matches may run to the record end
         require(max_len <= 1024, "max_len above 1024", PM_E_UNSUPPORTED);
         require(k >= 0 && k <= PM_MAX_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
         require(pattern_id >= 0 && pattern_id < 65536, "pattern_id out of range");
@@ -288,7 +355,7 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         a.first = first;
         a.last = last;
         a.nt = nt;
-        a.halo = max_len + ins_extra - 1;
+        a.halo = unbounded ? 0 : max_len + ins_extra - 1;
         a.errs = errs;
         for (int j = 0; j < 4; ++j) {
             a.rev_pre[j] = rev_pre[j];
@@ -316,6 +383,40 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         uint64_t total = 0;
         EventPair ev;
         const uint32_t blocks = blocks_for(a.nchunks, 256);
+        double carry_ms = 0.0;
+        if (unbounded) {
+            // relaxation rounds (k_nfa_carry) until no chunk's state changes
+            Carve c;
+            const size_t st_bytes = a.nchunks * 4 * sizeof(uint64_t);
+            const size_t o_a = c.take(st_bytes), o_b = c.take(st_bytes), o_s = c.take(st_bytes),
+                         o_n = c.take(st_bytes), o_f = c.take(sizeof(uint32_t));
+            uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_rec, c.off));
+            uint64_t* st[2] = {reinterpret_cast<uint64_t*>(base + o_a), reinterpret_cast<uint64_t*>(base + o_b)};
+            uint64_t* in_seen = reinterpret_cast<uint64_t*>(base + o_s);
+            uint64_t* in_now = reinterpret_cast<uint64_t*>(base + o_n);
+            uint32_t* changed = reinterpret_cast<uint32_t*>(base + o_f);
+            HIPCHK(hipMemsetAsync(st[0], 0, st_bytes, s));
+            HIPCHK(hipMemsetAsync(in_seen, 0xff, st_bytes, s));   // no chunk has been scanned yet
+            uint32_t* h_changed = static_cast<uint32_t*>(reserve_host(db, db->pin_slots, 64));
+            int cur = 0;
+            EventPair cev;
+            HIPCHK(hipEventRecord(cev.a, s));
+            for (uint64_t round = 0; round <= a.nchunks; ++round) {
+                HIPCHK(hipMemsetAsync(changed, 0, sizeof(uint32_t), s));
+                if (nuc) launch_nfa_carry<true>(k, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+                else launch_nfa_carry<false>(k, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+                HIPCHK(hipGetLastError());
+                std::swap(in_seen, in_now);
+                cur ^= 1;
+                HIPCHK(hipMemcpyAsync(h_changed, changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                if (!*h_changed) break;
+            }
+            HIPCHK(hipEventRecord(cev.b, s));
+            HIPCHK(hipEventSynchronize(cev.b));
+            carry_ms = cev.ms();
+            a.in_state = st[cur];
+        }
         for (int attempt = 0; attempt < 2; ++attempt) {
             sb = make_sink(db, 1, db->n, expected);
             a.sink = sb.sink();
@@ -330,13 +431,13 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
             require(attempt == 0, "internal: hit bins overflowed twice");
             expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
         }
-        double kms = ev.ms();
+        double kms = ev.ms() + carry_ms;
         pm_hits* h = sink_to_hits(db, sb, counts, total);
         if (total) {
             a.starts = h->keys;
             a.nstarts = total;
             a.lens = h->lens;
-            a.max_len = max_len + ins_extra;
+            a.max_len = unbounded ? 0 : max_len + ins_extra;
             EventPair ev2;
             HIPCHK(hipEventRecord(ev2.a, s));
             if (nuc) launch_nfa_verify<true>(k, a, blocks_for(total, 256), s);

@@ -14,8 +14,10 @@ routes every compiled :class:`~patmatchdocker_amd.regex.Program` to a kernel:
 
 Queries with insertions/deletions (``-k <k>ids``, the web form's default
 when mismatches > 0) go to the Glushkov kernels with the error-type mask.
-Anything else (unbounded ``*``/``+``, more than 64 positions, k > 3,
-deletions with k >= the shortest match) raises :class:`UnsupportedOnGPU`;
+Unbounded ``*``/``+`` (``{m,}``) also run there (chunk states relaxed
+across chunks, :func:`scan_nfa`).  Anything else (more than 64 positions,
+k > 3, deletions with k >= the shortest match, a bounded match longer
+than 1024) raises :class:`UnsupportedOnGPU`;
 there is no CPU fallback by design.
 """
 
@@ -172,9 +174,7 @@ def route(prog: Program, alphabet: str, k: int, types: str) -> str:
                                % (k, prog.min_len))
     if prog.linear and alphabet == NUC and not indel:
         return "linear"
-    if prog.max_len is None:
-        raise UnsupportedOnGPU("unbounded repetition (* or +) is not supported by the GPU scan yet")
-    if prog.max_len > 1024:
+    if prog.max_len is not None and prog.max_len > 1024:
         raise UnsupportedOnGPU("match length bound above 1024")
     return "nfa"
 
@@ -258,7 +258,7 @@ def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, t
     errs = error_mask(types) if k else _lib.PM_ERR_SUB
     out = ctypes.c_void_p()
     check(_lib.load().pm_scan_nfa_errs(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
-                                       prog.max_len, prog.min_len, k, errs, pattern_id, ctypes.byref(out)))
+                                       prog.max_len or 0, prog.min_len, k, errs, pattern_id, ctypes.byref(out)))
     return _collect(out)
 
 

@@ -42,6 +42,9 @@ QUERIES = [
     ("CX{2,4}CX{3}[LIVMFYWC]", "pep", None, "insertion", None, None, "1", 500),
     ("RGD", "pep", None, None, None, None, "2", 200),
     ("KDEL>", "pep", None, None, "deletion", None, "1", 500),
+    # unbounded repeats ({m,} -> nrgrep '*')
+    ("GA{2,}TC", "dna", None, None, None, None, None, 500),
+    ("CX{3,}C", "pep", None, None, None, "substitution", "1", 300),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]

@@ -290,3 +290,37 @@ def test_specialized_dense_hits(engine, oracle_mod, monkeypatch):
             assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, 1), prog.source
     finally:
         db.close()
+
+
+UNBOUNDED_DNA = ["GA{2,}T", "A(TC){1,}G", "TATA{1,}GG", "GN{3,}CC", "C{4,}"]
+UNBOUNDED_PEP = ["CX{3,}C", "W{2,}Y", "KX{1,}DEL", "R{2,}GD", "NX{0,}S{2,}"]
+
+
+@pytest.mark.parametrize("k,types", [(0, ""), (1, "s"), (1, "ids"), (2, "id")])
+def test_unbounded_repeats(engine, oracle_mod, k, types):
+    """{m,} repeats (nrgrep '*'): matches may run to the end of their record;
+    chunk states are relaxed across chunks (k_nfa_carry) before the emitting
+    reverse scan, on both layouts, multi-tile, vs the oracle."""
+    text = dna_fasta(500 + k, n_records=5, min_len=20000, max_len=60000, width=(None if k else 90))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in UNBOUNDED_DNA:
+            prog = compile_pattern(convert("-n", pat))
+            assert prog.max_len is None
+            if "d" in types and prog.min_len <= k:
+                continue
+            res, _ = engine.scan(db, [prog], k=k, types=types)
+            assert _gpu_pairs(res[0]) == oracle_mod.scan(text, prog, k, types or "s", skip_headers=True), (pat, k)
+    finally:
+        db.close()
+    text = pep_fasta(600 + k, n_records=40, max_len=3000)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE)
+    try:
+        for pat in UNBOUNDED_PEP:
+            prog = compile_pattern(convert("-p", pat))
+            if "d" in types and prog.min_len <= k:
+                continue
+            res, _ = engine.scan(db, [prog], k=k, types=types)
+            assert _gpu_pairs(res[0]) == oracle_mod.scan(text, prog, k, types or "s", skip_headers=True), (pat, k)
+    finally:
+        db.close()

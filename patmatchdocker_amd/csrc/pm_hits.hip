@@ -58,13 +58,18 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict
 // One workgroup per bin: bitonic sort in LDS, write at the bin's offset.
 __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
                                                    const uint64_t* __restrict__ off, BinShape sh,
-                                                   uint64_t* __restrict__ dst) {
+                                                   uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
+                                                   uint32_t* __restrict__ lens) {
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0) return;
     const uint64_t* src = sh.src(out, bin);
     uint64_t* d = dst + off[bin];
+    if (slot_len) {   // every key of a bin has its slot's fixed length
+        const uint32_t len = (uint32_t)slot_len[bin / sh.bins_per_slot];
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) lens[off[bin] + i] = len;
+    }
     if (c == 1) {
         if (threadIdx.x == 0) d[0] = src[0];
         return;
@@ -152,7 +157,7 @@ static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const s
     }
     Carve c;
     const size_t o_out = c.take(total * sizeof(uint64_t));
-    const size_t o_cnt = c.take(sb.nbins * sizeof(uint32_t));
+    const size_t o_cnt = c.take((sb.nbins + 1) * sizeof(uint32_t));   // + the aux counter
     const size_t o_base = c.take(n_slots * sizeof(uint64_t));
     const size_t o_cap = c.take(n_slots * sizeof(uint32_t));
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_sink, c.off));
@@ -160,13 +165,22 @@ static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const s
     sb.cnt = reinterpret_cast<uint32_t*>(d + o_cnt);
     sb.slot_base = reinterpret_cast<uint64_t*>(d + o_base);
     sb.slot_cap = reinterpret_cast<uint32_t*>(d + o_cap);
-    // slot tables staged through pinned memory (ordered on the db stream)
-    uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_slots, n_slots * 12 + 16));
-    memcpy(h, base.data(), n_slots * 8);
-    memcpy(h + n_slots * 8, caps.data(), n_slots * 4);
-    HIPCHK(hipMemcpyAsync(sb.slot_base, h, n_slots * 8, hipMemcpyHostToDevice, db->stream));
-    HIPCHK(hipMemcpyAsync(sb.slot_cap, h + n_slots * 8, n_slots * 4, hipMemcpyHostToDevice, db->stream));
-    HIPCHK(hipMemsetAsync(sb.cnt, 0, sb.nbins * sizeof(uint32_t), db->stream));
+    // slot tables staged through pinned memory (ordered on the db stream);
+    // the layout is a function of (buffer, per_slot, caps), so an identical
+    // repeat finds them in place
+    if (db->slot_cache_p != (void*)d || db->slot_cache_per != per_slot || db->slot_cache_caps != caps) {
+        static_assert(sizeof(uint64_t) == 8, "");
+        uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_slots, (size_t)n_slots * 12 + 16));
+        memcpy(h, base.data(), n_slots * 8);
+        memcpy(h + (size_t)n_slots * 8, caps.data(), n_slots * 4);
+        // o_base and o_cap are adjacent (8-byte entries then 4-byte ones, 256-aligned carve)
+        HIPCHK(hipMemcpyAsync(sb.slot_base, h, n_slots * 8, hipMemcpyHostToDevice, db->stream));
+        HIPCHK(hipMemcpyAsync(sb.slot_cap, h + (size_t)n_slots * 8, n_slots * 4, hipMemcpyHostToDevice, db->stream));
+        db->slot_cache_p = d;
+        db->slot_cache_per = per_slot;
+        db->slot_cache_caps = caps;
+    }
+    HIPCHK(hipMemsetAsync(sb.cnt, 0, (sb.nbins + 1) * sizeof(uint32_t), db->stream));
     return sb;
 }
 
@@ -191,10 +205,11 @@ SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const 
 }
 
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow) {
-    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, sb.nbins * sizeof(uint32_t)));
-    HIPCHK(hipMemcpyAsync(h, sb.cnt, sb.nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, db->stream));
+    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, (sb.nbins + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(h, sb.cnt, (sb.nbins + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, db->stream));
     HIPCHK(hipStreamSynchronize(db->stream));
     counts.assign(h, h + sb.nbins);
+    const_cast<SinkBuffers&>(sb).aux = h[sb.nbins];
     uint64_t total = 0;
     overflow = false;
     for (uint32_t b = 0; b < sb.nbins; ++b) {
@@ -204,7 +219,9 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
     return total;
 }
 
-pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total) {
+pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,
+                      const int32_t* slot_len, bool* lens_done) {
+    if (lens_done) *lens_done = false;
     hipStream_t s = db->stream;
     pm_hits* h = new pm_hits();
     h->device = db->device;
@@ -231,7 +248,9 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sh, d_off);
         HIPCHK(hipGetLastError());
         if (lds) {
-            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh, h->keys);
+            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh, h->keys,
+                               slot_len, h->lens);
+            if (lens_done) *lens_done = slot_len != nullptr;
             HIPCHK(hipGetLastError());
         } else {
             uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);

@@ -219,6 +219,10 @@ struct pm_db {
     // per-call workspaces (never stream-ordered allocations)
     pm_devbuf ws_tab, ws_sink, ws_post, ws_rec;
     pm_hostbuf pin_up, pin_down, pin_slots;
+    // slot tables last uploaded into ws_sink (skip the copy when unchanged)
+    void* slot_cache_p = nullptr;
+    uint32_t slot_cache_per = 0;
+    std::vector<uint32_t> slot_cache_caps;
     uint64_t device_bytes = 0;
 };
 
@@ -309,6 +313,9 @@ struct SinkBuffers {
     uint64_t* slot_base = nullptr;
     uint32_t* slot_cap = nullptr;
     std::vector<uint32_t> slot_cap_h;
+    // cnt[nbins]: one auxiliary device counter zeroed and read back with the
+    // bin counters (pm_linear: the record-overflow maximum); sink_total sets aux
+    uint32_t aux = 0;
     uint32_t bins_per_pattern = NBINS;
     uint32_t pos_shift = 0;
     uint32_t nbins = NBINS;
@@ -325,7 +332,10 @@ SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const 
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
 // bins -> one sorted key list (pattern << 48 | pos) owned by the returned
 // hits; lens are left for the caller to fill.
-pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total);
+// slot_len (device, per slot, optional): fixed match length of every key of
+// a slot -- the LDS sort writes h->lens with the keys.
+pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,
+                      const int32_t* slot_len = nullptr, bool* lens_done = nullptr);
 // records h->ready on the db stream: call after the last kernel filling h
 void hits_ready(pm_db* db, pm_hits* h);
 

@@ -208,12 +208,12 @@ constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 wav
 // pattern) and the live mask of that window word, exact for the ACGT fast
 // path; windows overlapping an exception are dropped here (breaks kill,
 // windows with an "other" byte belong to k_linear_others), which needs the
-// exception planes only for lanes the tile's lane flags mark.  One block per
-// output segment (`group` consecutive pm_linear_jit workgroups, i.e. a
-// contiguous tile range), wave w takes the records of those workgroups'
-// waves w; slots of the (pattern, segment) hit lists are reserved with LDS
-// atomics and the segment counts written once at the end (k_linear_others,
-// launched after, appends to them with global atomics).
+// exception planes only for lanes the tile's lane flags mark.  One
+// 1024-thread block per output segment (`group` consecutive pm_linear_jit
+// workgroups, a contiguous tile range); its 16 waves take the (workgroup,
+// wave) record lists in turn, reserve slots of the (pattern, segment) hit
+// lists with LDS atomics and write the segment counts once at the end
+// (k_linear_others, launched after, appends with global atomics).
 struct ExpandArgs {
     const uint2* bo;
     const uint64_t* lflag;
@@ -231,13 +231,16 @@ struct ExpandArgs {
     uint32_t nwg, nout, group, tiles_per_wg;
 };
 
-__global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
+constexpr int EXPAND_THREADS = 1024;
+
+__global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) {
     __shared__ uint32_t cnt_p[4];
-    const uint32_t og = blockIdx.x, part = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
+    const uint32_t og = blockIdx.x, wave = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
     if (threadIdx.x < 4) cnt_p[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t wg_end = min(a.nwg, (og + 1) * a.group);
-    for (uint32_t wg = og * a.group; wg < wg_end; ++wg) {
+    const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * 4;
+    for (uint32_t q = wave; q < pairs; q += EXPAND_THREADS / 64) {
+        const uint32_t wg = wg0 + q / 4, part = q % 4;
         const uint32_t seg = wg * 4 + part;
         uint32_t cnt = a.rec_cnt[seg];
         if (cnt > a.rcap) {
@@ -272,6 +275,7 @@ __global__ __launch_bounds__(256) void k_linear_expand(ExpandArgs a) {
         }
     }
     __syncthreads();
+    // k_linear_others (launched after) appends to the same counters
     if ((int)threadIdx.x < a.P) a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nout + og] = cnt_p[threadIdx.x];
 }
 
@@ -800,7 +804,6 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                     rcap = std::max(rcap, it->second.second);
                 }
             }
-            uint32_t* h_over = static_cast<uint32_t*>(reserve_host(db, db->pin_up, sizeof(uint32_t)));
             for (int attempt = 0; attempt < 4 && !done; ++attempt) {
                 Carve cv;
                 const size_t o_rec = cv.take(nseg * rcap * sizeof(uint2));
@@ -809,9 +812,9 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
                 uint2* d_rec = reinterpret_cast<uint2*>(rbase + o_rec);
                 uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
-                uint32_t* d_over = reinterpret_cast<uint32_t*>(rbase + o_over);
-                HIPCHK(hipMemsetAsync(d_over, 0, sizeof(uint32_t), s));
+                (void)o_over;
                 sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps);
+                uint32_t* d_over = sb.cnt + sb.nbins;   // the sink's aux counter
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
                 jev.clear();
@@ -826,7 +829,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
                                   (uint32_t)tpw};
-                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(256), 0, s, xa);
+                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, s, xa);
                     HIPCHK(hipGetLastError());
                     if (db->nflag) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
@@ -838,10 +841,9 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                         HIPCHK(hipGetLastError());
                     }
                 }
-                HIPCHK(hipMemcpyAsync(h_over, d_over, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
-                const uint32_t rec_need = *h_over;
+                const uint32_t rec_need = sb.aux;
                 if (!overflow && rec_need == 0) {
                     done = true;
                     std::lock_guard<std::mutex> lk(g_cap_mu);
@@ -898,9 +900,10 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             for (auto& e : jev) kms += e->ms();
         else
             kms = ev.ms();
-        pm_hits* h = sink_to_hits(db, sb, counts, total);
+        bool lens_done = false;
+        pm_hits* h = sink_to_hits(db, sb, counts, total, reinterpret_cast<const int32_t*>(d_up + o_len), &lens_done);
         h->kernel_ms = kms;
-        if (total) {
+        if (total && !lens_done) {
             hipLaunchKernelGGL(k_linear_lens, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
                                reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
             HIPCHK(hipGetLastError());

@@ -6,9 +6,10 @@ into contiguous runs of whole records, one run per GPU (one process per
 GPU, ``torch.distributed`` over RCCL/xGMI).  Every rank scans only its own
 records -- there is no data-path collective -- and the (small) hit lists
 are gathered to rank 0 once per query: counts first, then the padded key and
-length vectors with one ``all_gather`` each, then one device sort on rank 0.
-Keys are ``pattern << 48 | global_beg``, so concatenation + sort reproduces
-the single-GPU order exactly.
+length vectors with one ``all_gather`` each, then an O(n) merge on rank 0
+(ranks own increasing position ranges, so each pattern's hits are the
+ranks' sorted slices in rank order).  Keys are ``pattern << 48 |
+global_beg``, so the result is exactly the single-GPU order.
 """
 
 from __future__ import annotations
@@ -61,10 +62,39 @@ def gather_hits(keys: torch.Tensor, lens: torch.Tensor, group=None, dst: int = 0
     dist.all_gather(all_l, pl, group=group)
     if dist.get_rank(group) != dst:
         return None
-    k = torch.cat([t[:n] for t, n in zip(all_k, sizes)])
+    parts = [t[:n] for t, n in zip(all_k, sizes)]
+    k = torch.cat(parts)
     ln = torch.cat([t[:n] for t, n in zip(all_l, sizes)])
-    order = torch.argsort(k)
-    return k[order], ln[order]
+    if k.numel() == 0:
+        return k, ln
+    return _merge(parts, k, ln)
+
+
+def _merge(parts, k, ln):
+    """Rank-major concatenation -> (pattern, beg) order without a sort: each
+    rank's list is sorted and ranks own increasing position ranges, so the
+    output is, pattern by pattern, the ranks' pattern slices in rank order.
+    Every element's destination is computed from per-(rank, pattern) counts
+    (torch.searchsorted) and scattered once."""
+    dev = k.device
+    npat = int((k >> POS_BITS).max().item()) + 1
+    bounds = torch.arange(npat + 1, device=dev, dtype=torch.int64) << POS_BITS
+    start = torch.stack([torch.searchsorted(t, bounds) for t in parts])   # [world, npat + 1]
+    cnt = start[:, 1:] - start[:, :-1]                                    # [world, npat]
+    # destination base of (rank, pattern): all earlier patterns, then earlier ranks
+    per_pat = cnt.sum(0)
+    pat_base = torch.cumsum(per_pat, 0) - per_pat                         # [npat]
+    rank_off = torch.cumsum(cnt, 0) - cnt                                 # [world, npat]
+    base = pat_base.unsqueeze(0) + rank_off - start[:, :-1]               # dest = base[r, p] + index in rank
+    sizes = torch.tensor([t.numel() for t in parts], device=dev)
+    rank = torch.repeat_interleave(torch.arange(len(parts), device=dev), sizes)
+    idx = torch.arange(k.numel(), device=dev) - (torch.cumsum(sizes, 0) - sizes)[rank]
+    dest = base[rank, k >> POS_BITS] + idx
+    out_k = torch.empty_like(k)
+    out_l = torch.empty_like(ln)
+    out_k[dest] = k
+    out_l[dest] = ln
+    return out_k, out_l
 
 
 def hits_to_tensors(hits_handle, device: torch.device):

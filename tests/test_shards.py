@@ -42,7 +42,7 @@ def _worker(rank, world, port, results):
         g = torch.Generator().manual_seed(rank)
         n = 3 + 4 * rank
         pos = torch.randint(0, 1000, (n,), generator=g) 
-        pat = torch.randint(0, 2, (n,), generator=g)
+        pat = torch.randint(0, 3, (n,), generator=g)
         keys = (pat << 48) | pos
         order = torch.argsort(keys)
         keys, lens = keys[order], torch.full((n,), 15, dtype=torch.int32)
@@ -55,9 +55,9 @@ def _worker(rank, world, port, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(120)
-def test_gather_two_ranks_gloo():
-    world = 2
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_ranks_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,7 +74,7 @@ def test_gather_two_ranks_gloo():
         g = torch.Generator().manual_seed(rank)
         n = 3 + 4 * rank
         pos = torch.randint(0, 1000, (n,), generator=g)
-        pat = torch.randint(0, 2, (n,), generator=g)
+        pat = torch.randint(0, 3, (n,), generator=g)
         want += (((pat << 48) | pos) + rank * 1000).tolist()
     assert keys == sorted(want)
     assert lens == [15] * len(want)

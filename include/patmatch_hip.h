@@ -79,7 +79,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths,
                    pm_hits** out);
 
 /* Generates and compiles (hipRTC, gfx950) the pattern-specialized linear
- * kernel for up to 4 patterns without launching it: a host-only check that
+ * kernel for up to 8 patterns without launching it: a host-only check that
  * needs no GPU (used by the CPU tests and to pre-warm the code cache). */
 int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t* pos_class,
                           int n_classes, const uint8_t* class_acgt, const uint8_t* class_is_any,

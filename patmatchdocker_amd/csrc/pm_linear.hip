@@ -28,6 +28,7 @@
 
 #include <deque>
 #include <memory>
+#include <set>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -136,7 +137,8 @@ void launch_generic(int P, const LinearArgs& a, hipStream_t s) {
     switch (P) {
         case 1: hipLaunchKernelGGL(k_linear_generic<1>, dim3(blocks), dim3(256), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_linear_generic<2>, dim3(blocks), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_linear_generic<4>, dim3(blocks), dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_linear_generic<4>, dim3(blocks), dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_linear_generic<8>, dim3(blocks), dim3(256), 0, s, a); break;
     }
 }
 
@@ -203,6 +205,7 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
 }
 
 constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
+constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 
 // Hit records of pm_linear_jit -> hit keys.  A record is (tile, lane, step,
 // pattern) and the live mask of that window word, exact for the ACGT fast
@@ -234,9 +237,9 @@ struct ExpandArgs {
 constexpr int EXPAND_THREADS = 1024;
 
 __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) {
-    __shared__ uint32_t cnt_p[4];
+    __shared__ uint32_t cnt_p[JIT_MAX_P];
     const uint32_t og = blockIdx.x, wave = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
-    if (threadIdx.x < 4) cnt_p[threadIdx.x] = 0;
+    if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * 4;
     for (uint32_t q = wave; q < pairs; q += EXPAND_THREADS / 64) {
@@ -249,8 +252,8 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
         }
         for (uint32_t i = lane_t; i < cnt; i += 64) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 11);
-            const uint32_t lane = (r.x >> 5) & 63, s = (r.x >> 2) & 7, p = r.x & 3;
+            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 12);
+            const uint32_t lane = (r.x >> 6) & 63, s = (r.x >> 3) & 7, p = r.x & 7;
             if (tile >= a.ntiles) continue;
             const uint32_t w0 = 32u * lane + part * JIT_STEPS + s;
             uint32_t live = r.y;
@@ -294,7 +297,7 @@ typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
 // Hit records: one uint2 per (tile, lane, step, pattern) with a live window:
-// x = (tile - first tile of the workgroup) << 11 | lane << 5 | step << 2 |
+// x = (tile - first tile of the workgroup) << 12 | lane << 6 | step << 3 |
 // pattern, y = the live mask (bit b = the window of stream b).  Staged per
 // wave in LDS and flushed to the wave's global segment, so the scan loop
 // never waits on a global store; k_linear_expand turns records into keys.
@@ -434,7 +437,7 @@ std::string emit_dead_network(std::ostringstream& o, const std::vector<std::stri
     return acc;
 }
 
-// Source of the specialized kernel for a batch of P <= 4 patterns.
+// Source of the specialized kernel for a batch of P <= 8 patterns.
 //
 // Workgroup = 4 waves = one tile at a time: wave w scans steps
 // [8 w, 8 w + 8) of the tile for EVERY pattern of the batch, so the class
@@ -471,6 +474,22 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     };
     int Lmax = 0;
     for (int p = 0; p < P; ++p) Lmax = std::max(Lmax, (int)lengths[p]);
+    // Class words are pinned in registers (derived once per row); unpinned,
+    // the compiler re-derives them per use and keeps the plane words of every
+    // row alive instead, which measured worse for every shape (experiment
+    // knob PM_JIT_PIN_LIMIT: most class words per wave that are pinned).
+    int max_words = 0;
+    for (int part = 0; part < PARTS; ++part) {
+        std::set<std::pair<int, int>> need;
+        for (int t = part * JIT_STEPS; t < (part + 1) * JIT_STEPS; ++t)
+            for (int p = 0; p < P; ++p)
+                for (int j = 0; j < lengths[p]; ++j)
+                    if (!class_is_any[pos_class[64 * p + j]]) need.insert({t + j, class_acgt[pos_class[64 * p + j]] & 15});
+        max_words = std::max(max_words, (int)need.size());
+    }
+    int pin_limit = 1 << 30;
+    if (const char* e = getenv("PM_JIT_PIN_LIMIT")) pin_limit = atoi(e);   // experiment knob
+    const bool pin = max_words <= pin_limit;
     for (int part = 0; part < PARTS; ++part) {
         const int t0 = part * JIT_STEPS, t1 = t0 + JIT_STEPS;
         const int wend = t1 + Lmax - 1;   // words [t0, wend)
@@ -488,8 +507,8 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
             }
             const std::string nm = "x" + std::to_string(subset) + "_" + std::to_string(i);
             o << "  u32 " << nm << " = "
-              << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << "; PIN(" << nm
-              << ");\n";
+              << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << ";"
+              << (pin ? " PIN(" + nm + ");" : "") << "\n";
             cw[key] = nm;
             return nm;
         };
@@ -608,7 +627,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);\n"
          "          if (m) {\n"
          "            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));\n"
-         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 11 | (u32)lane << 5 | (u32)s << 2 | (u32)p, lv);\n"
+         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 12 | (u32)lane << 6 | (u32)s << 3 | (u32)p, lv);\n"
          "            scnt += (u32)__builtin_popcountll(m);\n"
          "            if (scnt > REC_LDS - 64) {\n"
          "              flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
@@ -681,7 +700,7 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
         }
         sig += "]";
     }
-    for (const char* knob : {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA"})
+    for (const char* knob : {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT"})
         if (const char* e = getenv(knob)) sig += std::string(";") + knob + "=" + e;
     return sig;
 }
@@ -748,10 +767,21 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         std::vector<Chunk> chunks;
         for (int base = 0; base < n_patterns;) {
             const int rem = n_patterns - base;
-            const int P = rem >= 4 ? 4 : (rem >= 2 ? 2 : 1);   // instantiated widths
+            // instantiated widths; a specialized kernel takes up to 8 (class
+            // words shared by more patterns, one pass over HBM for all of them)
+            int P = (jit && rem >= 8) ? 8 : rem >= 4 ? 4 : (rem >= 2 ? 2 : 1);
             hipFunction_t fn = nullptr;
-            if (jit)
-                fn = jit_function(db->device, P, k, lengths + base, pos_class + 64 * base, class_acgt, class_is_any);
+            if (jit) {
+                // halve the width while the compiled kernel spills registers
+                // to scratch (long patterns at high k with many patterns)
+                for (;;) {
+                    fn = jit_function(db->device, P, k, lengths + base, pos_class + 64 * base, class_acgt, class_is_any);
+                    int scratch = 0;
+                    HIPCHK(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn));
+                    if (scratch == 0 || P == 1) break;
+                    P /= 2;
+                }
+            }
             chunks.push_back({base, P, fn});
             base += P;
         }
@@ -789,7 +819,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             // larger segments on the retry, the others keep theirs
             std::vector<uint32_t> slot_caps(n_patterns, cap);
             // records per wave: at most tiles_per_wg * 64 lanes * 8 steps * 4 patterns
-            const uint64_t rec_max = tpw * 64 * JIT_STEPS * 4;
+            const uint64_t rec_max = tpw * 64 * JIT_STEPS * JIT_MAX_P;
             uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, std::max<uint64_t>(128, 8 * tpw));
             // capacities that sufficed for the same batch on this database
             // last time (a repeated query does not pay the overflow retry)
@@ -919,7 +949,7 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
                           const uint8_t* class_acgt, const uint8_t* class_is_any, int k, uint64_t* code_bytes) {
     return guarded([&] {
         require(lengths && pos_class && class_acgt && class_is_any, "null argument");
-        require(n_patterns >= 1 && n_patterns <= 4, "n_patterns out of range for one specialized kernel");
+        require(n_patterns >= 1 && n_patterns <= JIT_MAX_P, "n_patterns out of range for one specialized kernel");
         require(n_classes >= 1 && n_classes <= 256, "n_classes out of range");
         require(k >= 0 && k <= PM_MAX_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)

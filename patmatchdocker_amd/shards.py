@@ -46,6 +46,9 @@ def gather_hits(keys: torch.Tensor, lens: torch.Tensor, group=None, dst: int = 0
     """
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return keys, lens          # one rank: the engine already sorted them
+    if dist.get_backend(group) == "gloo" and keys.is_cuda:   # gloo gathers host tensors
+        out = gather_hits(keys.cpu(), lens.cpu(), group, dst)
+        return None if out is None else (out[0].to(keys.device), out[1].to(lens.device))
     world = dist.get_world_size(group)
     count = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
     counts = [torch.zeros_like(count) for _ in range(world)]

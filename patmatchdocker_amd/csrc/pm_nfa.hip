@@ -46,6 +46,10 @@ struct NfaArgs {
     // unbounded patterns: reverse state entering each chunk from the right
     // (rows at stride 4), found by k_nfa_carry; null = start from the halo
     const uint64_t* in_state;
+    // a plain class sequence (follow(i) = {i+1}): transitions are shifts
+    // instead of table lookups; mmask = the m position bits
+    int shift_only;
+    uint64_t mmask;
     // verify
     const uint64_t* starts;
     uint64_t nstarts;
@@ -58,6 +62,13 @@ __device__ inline uint64_t table_or(const uint64_t* __restrict__ tab, uint64_t s
     for (int t = 0; t < nt; ++t) acc |= tab[t * 256 + ((set >> (8 * t)) & 255)];
     return acc;
 }
+// positions preceding / following a set (reverse / forward transitions)
+__device__ inline uint64_t prec_of(const NfaArgs& a, const uint64_t* __restrict__ s_prec, uint64_t set) {
+    return a.shift_only ? set >> 1 : table_or(s_prec, set, a.nt);
+}
+__device__ inline uint64_t fol_of(const NfaArgs& a, const uint64_t* __restrict__ s_fol, uint64_t set) {
+    return a.shift_only ? (set << 1) & a.mmask : table_or(s_fol, set, a.nt);
+}
 
 // One character of the reverse search (right to left).  Substitution-only
 // patterns (the common case) take the short form.
@@ -66,7 +77,7 @@ __device__ inline void nfa_rev_step(uint64_t (&R)[K + 1], uint64_t bc, uint64_t 
                                     const uint64_t* __restrict__ s_prec, const NfaArgs& a) {
     uint64_t A[K + 1];
 #pragma unroll
-    for (int j = 0; j <= K; ++j) A[j] = table_or(s_prec, R[j], a.nt) | a.rev_pre[j];
+    for (int j = 0; j <= K; ++j) A[j] = prec_of(a, s_prec, R[j]) | a.rev_pre[j];
     if (a.errs == PM_ERR_SUB) {
 #pragma unroll
         for (int j = K; j >= 0; --j) R[j] = (A[j] & bc) | (j > 0 ? (A[j - 1] & nb) : 0ull);
@@ -85,7 +96,7 @@ __device__ inline void nfa_rev_step(uint64_t (&R)[K + 1], uint64_t bc, uint64_t 
         // ninit[j] (j >= 1) = an insertion-kept start; row 0's init is consumed
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            N[j + 1] |= table_or(s_prec, N[j], a.nt) | ((j >= 1 && (a.errs & PM_ERR_INS) && nb) ? a.last : 0ull);
+            N[j + 1] |= prec_of(a, s_prec, N[j]) | ((j >= 1 && (a.errs & PM_ERR_INS) && nb) ? a.last : 0ull);
     }
 #pragma unroll
     for (int j = 0; j <= K; ++j) R[j] = N[j];
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
         uint64_t A[K + 1], N[K + 1];
         bool ninit[K + 1];
 #pragma unroll
-        for (int j = 0; j <= K; ++j) A[j] = table_or(s_fol, R[j], a.nt) | (init[j] ? a.first : 0ull);
+        for (int j = 0; j <= K; ++j) A[j] = fol_of(a, s_fol, R[j]) | (init[j] ? a.first : 0ull);
 #pragma unroll
         for (int j = 0; j <= K; ++j) {
             N[j] = A[j] & bc;
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
         }
         if (a.errs & PM_ERR_DEL) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) N[j + 1] |= table_or(s_fol, N[j], a.nt) | (ninit[j] ? a.first : 0ull);
+            for (int j = 0; j < K; ++j) N[j + 1] |= fol_of(a, s_fol, N[j]) | (ninit[j] ? a.first : 0ull);
         }
         uint64_t any = 0;
         bool alive = false;
@@ -356,6 +367,10 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         a.last = last;
         a.nt = nt;
         a.halo = unbounded ? 0 : max_len + ins_extra - 1;
+        a.mmask = m == 64 ? ~0ull : ((1ull << m) - 1);
+        a.shift_only = first == 1 && last == (1ull << (m - 1));
+        for (int i = 0; i < m && a.shift_only; ++i)
+            a.shift_only = follow[i] == (i + 1 < m ? (1ull << (i + 1)) : 0ull);
         a.errs = errs;
         for (int j = 0; j < 4; ++j) {
             a.rev_pre[j] = rev_pre[j];

@@ -338,7 +338,7 @@ constexpr int JIT_REC_LDS = 96;       // hit records staged per wave in LDS (3 w
 // workgroups resident per CU (PM_JIT_WAVES: experiment override, e.g. 4 with PM_JIT_RING=2)
 int jit_wg_per_cu() {
     const char* e = getenv("PM_JIT_WAVES");
-    return e ? std::max(1, atoi(e)) : 3;
+    return e ? std::max(1, atoi(e)) : 4;
 }
 
 // mismatch of an ACGT subset as an expression of the plane words h, l
@@ -454,9 +454,12 @@ std::string emit_dead_network(std::ostringstream& o, const std::vector<std::stri
 // record with its live mask (wave ballot + mbcnt into an LDS stage, flushed
 // rarely); k_linear_expand turns records into hit keys.
 std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
-                              const uint8_t* class_acgt, const uint8_t* class_is_any) {
+                              const uint8_t* class_acgt, const uint8_t* class_is_any, int waves) {
     constexpr int PARTS = LANE_WORDS / JIT_STEPS;   // == 4 waves
-    int RING = 3;                                   // LDS tile buffers
+    // LDS tile buffers: 2 (the next tile streams in while this one is
+    // scanned) leave room for 4 workgroups per CU, which measured 10 %
+    // faster than 3 buffers at 3 workgroups per CU (profiles/r01c_ring_sweep.txt)
+    int RING = 2;
     if (const char* e = getenv("PM_JIT_RING")) RING = atoi(e);   // experiment: 2 or 3
     const int TILE_BYTES = (int)(TILE_WORDS * 8);         // 16896: 16.5 KiB
     const int DMA_PIECES = (TILE_BYTES + 1023) / 1024;   // 1 KiB per glds wave-instruction (last one half)
@@ -528,7 +531,8 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
         }
         o << "}\n";
     }
-    const int waves = jit_wg_per_cu();   // workgroups per CU (LDS allows 3 with a 3-tile ring)
+    // `waves`: __launch_bounds__ minimum workgroups per CU (4 -> at most
+    // 128 VGPRs; jit_function falls back to 3 when that would spill)
     o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << DMA_PIECES << "\n";
     // experiment knobs: PM_JIT_NOCOMPUTE=1 only streams the tiles,
     // PM_JIT_NODMA=1 computes on whatever the LDS ring holds (no HBM reads)
@@ -711,10 +715,19 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);
     if (it != g_jit_cache.end()) return it->second.fn;
-    std::vector<char> code = jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any));
+    // 4 workgroups per CU when the kernel fits 128 VGPRs without spilling,
+    // else 3 (up to 168 VGPRs)
     JitKernel jk;
-    HIPCHK(hipModuleLoadData(&jk.module, code.data()));
-    HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
+    for (int waves = jit_wg_per_cu(); waves >= 1; --waves) {
+        std::vector<char> code =
+            jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves));
+        if (jk.module) HIPCHK(hipModuleUnload(jk.module));
+        HIPCHK(hipModuleLoadData(&jk.module, code.data()));
+        HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
+        int scratch = 0;
+        HIPCHK(hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, jk.fn));
+        if (scratch == 0 || waves <= 3) break;
+    }
     g_jit_cache[key] = jk;
     return jk.fn;
 }
@@ -800,7 +813,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             // dispatcher hands the next one to whichever CU frees a slot, so
             // an unevenly loaded CU does not hold up the whole launch
             const char* split_env = getenv("PM_JIT_SPLIT");
-            const uint64_t split = split_env ? std::max(1, atoi(split_env)) : 16;
+            const uint64_t split = split_env ? std::max(1, atoi(split_env)) : 8;
             uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * jit_wg_per_cu() * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
@@ -810,7 +823,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             // an overflow re-runs with the counts seen
             uint32_t cap = 256;
             // output segments: `split` consecutive workgroups share one
-            // (pattern, segment) hit list, so the sort sees ~768 segments
+            // (pattern, segment) hit list, so the sort sees ~1024 segments
             const uint64_t group = split;
             const uint64_t nout = (nwg + group - 1) / group;
             while (cap < 4096 && cap < 16 * tpw * group) cap *= 2;
@@ -954,7 +967,7 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
         require(k >= 0 && k <= PM_MAX_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
-        const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any);
+        const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4);
         const std::vector<char> code = jit_compile(src);
         if (code_bytes) *code_bytes = code.size();
     });

@@ -1,11 +1,14 @@
 """Times the specialized linear kernel on the bench workload under env-var
 variants of the generator (PM_JIT_* knobs), e.g.
     python tools/jit_sweep.py 10 TGCTGASTCAGCANW 2 "" "PM_JIT_EMIT=0" "PM_JIT_WAVES=3"
-Each variant is a comma-separated list of NAME=VALUE."""
+Each variant is a comma-separated list of NAME=VALUE.  PM_SWEEP_GAP_MS=<ms>
+idles between launches so that every variant is timed at the recovered
+clock (back-to-back launches settle ~15 % slower: power limit)."""
 import ctypes
 import os
 import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from patmatchdocker_amd import _lib, engine  # noqa: E402
@@ -25,7 +28,10 @@ for var in variants:
     saved = {kk: os.environ.get(kk) for kk in env}
     os.environ.update(env)
     times, count = [], None
+    gap = float(os.environ.get("PM_SWEEP_GAP_MS", "0")) * 1e-3   # idle between launches (clock recovery)
+    time.sleep(10 * gap)
     for i in range(6):
+        time.sleep(gap)
         h = batch.launch(db, k)
         times.append(engine.kernel_ms(h))
         n = ctypes.c_uint64()

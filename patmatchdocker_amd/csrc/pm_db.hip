@@ -142,7 +142,8 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
                                   const uint2* __restrict__ bo,
                                   const uint32_t* __restrict__ sbflag, const uint32_t* __restrict__ sbbase,
                                   uint32_t* __restrict__ xbrk, uint32_t* __restrict__ xoth,
-                                  uint64_t* __restrict__ xword, uint8_t* __restrict__ xbytes) {
+                                  uint64_t* __restrict__ xword, uint8_t* __restrict__ xbytes,
+                                  uint32_t* __restrict__ n_oth_words) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (w >= nwords) return;
     const uint32_t f = sbflag[w >> 5];
@@ -153,6 +154,7 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
     const uint32_t br = e.x, ot = e.y & ~br;
     xbrk[idx] = br;
     xoth[idx] = ot;
+    if (ot) atomicAdd(n_oth_words, 1u);
     xword[idx] = w;
     const uint64_t t = w / TILE_WORDS;
     const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
@@ -289,10 +291,15 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw) {
     db->xoth = dalloc<uint32_t>(db, db->nflag);
     db->xword = dalloc<uint64_t>(db, db->nflag);
     db->xbytes = dalloc<uint8_t>(db, db->nflag * 32);
+    uint32_t* d_noth = static_cast<uint32_t*>(reserve(db, db->ws_post, sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(d_noth, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_fill_exceptions, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, d_raw, db->n,
                        db->nwords, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword,
-                       db->xbytes);
+                       db->xbytes, d_noth);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, d_noth, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    db->n_oth_words = h[0];   // 0: scans skip the "other byte" pass
     hipLaunchKernelGGL(k_lane_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
                        db->lflag);
     HIPCHK(hipGetLastError());

@@ -64,11 +64,26 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
     const uint32_t bin = blockIdx.x;
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0) return;
+    uint64_t base;
+    if (off) {
+        base = off[bin];
+    } else {   // few bins: the block sums the counts before it (no offsets pass)
+        uint64_t acc = 0;
+        for (uint32_t b = threadIdx.x; b < bin; b += blockDim.x) acc += min(cnt[b], sh.cap(b));
+        s[threadIdx.x] = acc;
+        __syncthreads();
+        for (uint32_t d2 = blockDim.x / 2; d2 > 0; d2 >>= 1) {
+            if (threadIdx.x < d2) s[threadIdx.x] += s[threadIdx.x + d2];
+            __syncthreads();
+        }
+        base = s[0];
+        __syncthreads();
+    }
     const uint64_t* src = sh.src(out, bin);
-    uint64_t* d = dst + off[bin];
+    uint64_t* d = dst + base;
     if (slot_len) {   // every key of a bin has its slot's fixed length
         const uint32_t len = (uint32_t)slot_len[bin / sh.bins_per_slot];
-        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) lens[off[bin] + i] = len;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) lens[base + i] = len;
     }
     if (c == 1) {
         if (threadIdx.x == 0) d[0] = src[0];
@@ -245,11 +260,15 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sh, d_off);
-        HIPCHK(hipGetLastError());
+        // up to 4096 bins each sort block sums the counts before it itself
+        const bool inline_off = lds && sb.nbins <= 4096;
+        if (!inline_off) {
+            hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sh, d_off);
+            HIPCHK(hipGetLastError());
+        }
         if (lds) {
-            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh, h->keys,
-                               slot_len, h->lens);
+            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt,
+                               inline_off ? nullptr : d_off, sh, h->keys, slot_len, h->lens);
             if (lens_done) *lens_done = slot_len != nullptr;
             HIPCHK(hipGetLastError());
         } else {

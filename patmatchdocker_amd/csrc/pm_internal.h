@@ -206,6 +206,7 @@ struct pm_db {
     uint64_t nwords = 0;     // NUC: physical words (ntiles * TILE_WORDS)
     uint64_t nsb = 0;        // NUC: superblocks (32 physical words)
     uint64_t nflag = 0;      // NUC: exception words
+    uint64_t n_oth_words = ~0ull;   // NUC: words holding an "other" byte (~0: not counted)
     uint64_t nbytes_alloc = 0;
     uint2 *hl = nullptr, *bo = nullptr;   // NUC planes {hi, lo}, {brk, oth}
     uint32_t *sbflag = nullptr, *sbbase = nullptr;

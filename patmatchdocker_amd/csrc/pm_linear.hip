@@ -874,7 +874,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                                   (uint32_t)tpw};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, s, xa);
                     HIPCHK(hipGetLastError());
-                    if (db->nflag) {
+                    if (db->nflag && db->n_oth_words) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,

@@ -535,7 +535,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // 128 VGPRs; jit_function falls back to 3 when that would spill)
     o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << DMA_PIECES << "\n";
     // experiment knobs: PM_JIT_NOCOMPUTE=1 only streams the tiles,
-    // PM_JIT_NODMA=1 computes on whatever the LDS ring holds (no HBM reads)
+    // PM_JIT_NODMA=1 rescans each workgroup's first tiles (no HBM stream)
     const bool nocompute = getenv("PM_JIT_NOCOMPUTE") && getenv("PM_JIT_NOCOMPUTE")[0] == '1';
     if (getenv("PM_JIT_NODMA") && getenv("PM_JIT_NODMA")[0] == '1') o << "#define PM_NODMA 1\n";
     o << R"JIT(// Raw barrier: __syncthreads()'s release fence would wait vmcnt(0) and
@@ -553,19 +553,20 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
 // Inline asm so that the compiler's wait bookkeeping does not drain it
 // before the ds_reads of the slot being computed; waited for explicitly.
 __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 tend, u32 wid, int lane) {
-#ifdef PM_NODMA
-  return;
-#endif
   if (tile >= tend) return;
-  const unsigned char* src = reinterpret_cast<const unsigned char*>(a.hl + tile * TILE_WORDS) + lane * 16;
+  // scalar base (SGPR pair, SALU arithmetic) + the lane's constant 16-byte
+  // offset: no VALU address math per piece
+  const unsigned char* tb = reinterpret_cast<const unsigned char*>(a.hl + tile * TILE_WORDS);
+  const u32 voff = (u32)lane * 16u;
 #pragma unroll
   for (int q = 0; q < DMA_PIECES; q += 4) {
     if (q + (int)wid >= DMA_PIECES) break;
     if ((q + (int)wid + 1) * 1024 > LDS_TILE && lane * 16 >= LDS_TILE % 1024) continue;   // half last piece
     const u32 dst = __builtin_amdgcn_readfirstlane(dst0 + (q + wid) * 1024);
+    const unsigned char* pb = tb + (q + wid) * 1024;
     u32 keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src + (q + wid) * 1024), "s"(dst) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(pb), "s"(dst) : "memory");
   }
 }
 // Moves the wave's staged records to its global segment.  Rare; ends with
@@ -609,7 +610,9 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
          "    }\n"
          "    BARRIER();\n"
+         "#ifndef PM_NODMA   // experiment: keep scanning the workgroup's first tiles (compute only)\n"
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
+         "#endif\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
          "    u32 dd[STEPS][P];   // dead windows per step and pattern\n"
          "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) dd[s][p] = ~0u;\n";

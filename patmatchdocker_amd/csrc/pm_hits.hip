@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
     const uint32_t c = min(cnt[bin], sh.cap(bin));
-    if (c == 0) return;
+    if (c == 0 || c > LDS_SORT_CAP) return;   // (a speculative sort's caller redoes such lists)
     uint64_t base;
     if (off) {
         base = off[bin];
@@ -232,6 +232,33 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
         overflow |= counts[b] > sb.slot_cap_h[b / sb.bins_per_pattern];
     }
     return total;
+}
+
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len) {
+    require(sb.nbins <= 4096, "internal: speculative sort needs <= 4096 bins");
+    uint64_t cap_total = 0;
+    for (uint32_t c : sb.slot_cap_h) cap_total += (uint64_t)c * sb.bins_per_pattern;
+    pm_hits* h = new pm_hits();
+    h->device = db->device;
+    try {
+        h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
+        h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
+        const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
+        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, db->stream, sb.out, sb.cnt, nullptr, sh,
+                           h->keys, slot_len, h->lens);
+        HIPCHK(hipGetLastError());
+    } catch (...) {
+        discard_hits(h);
+        throw;
+    }
+    return h;
+}
+
+void discard_hits(pm_hits* h) {
+    if (!h) return;
+    pool_put(h->device, h->keys, h->keys_cap);
+    pool_put(h->device, h->lens, h->lens_cap);
+    delete h;
 }
 
 pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,

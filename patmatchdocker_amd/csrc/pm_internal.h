@@ -333,6 +333,12 @@ SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const 
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
 // bins -> one sorted key list (pattern << 48 | pos) owned by the returned
 // hits; lens are left for the caller to fill.
+// Sorts every bin (<= 4096 bins, lists <= LDS_SORT_CAP keys) into a list
+// sized for all capacities BEFORE the counts reach the host, so a scan needs
+// one host sync; count unset -- the caller validates the counts it reads
+// afterwards and keeps the result (count = total) or discards it.
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len);
+void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // slot_len (device, per slot, optional): fixed match length of every key of
 // a slot -- the LDS sort writes h->lens with the keys.
 pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,

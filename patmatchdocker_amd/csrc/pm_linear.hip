@@ -808,6 +808,8 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         uint64_t total = 0;
         EventPair ev;
         std::vector<std::unique_ptr<EventPair>> jev;   // per specialized launch
+        pm_hits* spec = nullptr;       // speculatively sorted hit list
+        pm_hits* hit_list = nullptr;   // accepted speculative list
         bool done = false;
         if (jit) {
             // one output segment per (pattern, workgroup); workgroups own
@@ -887,16 +889,27 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                         HIPCHK(hipGetLastError());
                     }
                 }
+                if (sb.nbins <= 4096)   // sort before the host sees the counts (one sync per scan)
+                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len));
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t rec_need = sb.aux;
                 if (!overflow && rec_need == 0) {
                     done = true;
+                    if (spec && total && *std::max_element(counts.begin(), counts.end()) <= LDS_SORT_CAP) {
+                        spec->count = total;
+                        hit_list = spec;
+                    } else {
+                        discard_hits(spec);
+                    }
+                    spec = nullptr;
                     std::lock_guard<std::mutex> lk(g_cap_mu);
                     if (g_cap_hint.size() > 256) g_cap_hint.clear();
                     g_cap_hint[{db, cap_key}] = {slot_caps, rcap};
                     break;
                 }
+                discard_hits(spec);
+                spec = nullptr;
                 if (rec_need) rcap = std::max<uint32_t>(rcap, rec_need);
                 if (overflow) {
                     uint64_t keys_total = 0;
@@ -946,8 +959,10 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
             for (auto& e : jev) kms += e->ms();
         else
             kms = ev.ms();
-        bool lens_done = false;
-        pm_hits* h = sink_to_hits(db, sb, counts, total, reinterpret_cast<const int32_t*>(d_up + o_len), &lens_done);
+        bool lens_done = hit_list != nullptr;
+        pm_hits* h = hit_list ? hit_list
+                              : sink_to_hits(db, sb, counts, total, reinterpret_cast<const int32_t*>(d_up + o_len),
+                                             &lens_done);
         h->kernel_ms = kms;
         if (total && !lens_done) {
             hipLaunchKernelGGL(k_linear_lens, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,

@@ -363,78 +363,78 @@ std::string subset_expr(int subset, const std::string& h, const std::string& l) 
     }
 }
 
-// Emits a bit-sliced "count > K" network over `in` (mismatch words) and
-// returns the name of the result.  Columns of equal weight are compressed
-// with full adders (xor3 + majority, one v_bitop3 each); carries whose
-// weight exceeds K go straight into the dead mask, the few bits left are
-// compared with K at the end.  ~1.4 ops per input for K = 2.  Three-way ORs
-// are emitted as v_bitop3 0xFE: v_or3_b32 issues ~1.5x slower on gfx950
-// (profiles/r01c_valu_rates.txt).
-std::string emit_dead_network(std::ostringstream& o, const std::vector<std::string>& in, int K, int& uid,
-                              const std::string& ind) {
-    auto fresh = [&](const char* pfx) { return std::string(pfx) + std::to_string(uid++); };
-    if (in.empty()) return "0u";
-    if (K == 0) {
-        std::string acc = in[0];
-        size_t i = 1;
-        for (; i + 1 < in.size(); i += 2) {
-            const std::string v = fresh("d");
-            o << ind << "const u32 " << v << " = B3(" << acc << ", " << in[i] << ", " << in[i + 1] << ", 0xFE);\n";
-            acc = v;
-        }
-        if (i < in.size()) {
-            const std::string v = fresh("d");
-            o << ind << "const u32 " << v << " = " << acc << " | " << in[i] << ";\n";
-            acc = v;
-        }
-        return acc;
-    }
-    const int lmax = K >= 2 ? 1 : 0;   // highest column whose weight is <= K
-    std::deque<std::string> col[3];
-    col[0].assign(in.begin(), in.end());
-    // compress every column to at most 2 bits with full adders; carries of
-    // weight > K go straight into the dead mask
-    for (int L = 0; L <= lmax; ++L) {
-        auto& c = col[L];
-        while (c.size() > 2) {
-            const std::string a = c.front(); c.pop_front();
-            const std::string b = c.front(); c.pop_front();
-            const std::string d = c.front(); c.pop_front();
-            const std::string s = fresh("s"), cy = fresh("c");
-            o << ind << "const u32 " << s << " = B3(" << a << ", " << b << ", " << d << ", 0x96);\n";
-            o << ind << "const u32 " << cy << " = B3(" << a << ", " << b << ", " << d << ", 0xE8);\n";
-            c.push_back(s);
-            col[L + 1].push_back(cy);
-        }
-    }
-    std::vector<std::string> terms(col[lmax + 1].begin(), col[lmax + 1].end());
-    // what is left: a, b (weight 1) and, for K >= 2, c, d (weight 2)
-    auto at = [&](int L, size_t i) { return i < col[L].size() ? col[L][i] : std::string("0u"); };
-    if (K == 1) {
-        if (col[0].size() == 2) terms.push_back("(" + at(0, 0) + " & " + at(0, 1) + ")");
-    } else if (!col[1].empty()) {
-        // count = a + b + 2 (c + d) (+ 4 per dead carry):
-        //   K = 2: dead iff c & d, or (c | d) & (a | b)  = maj(c, d, a | b)
-        //   K = 3: dead iff c & d, or (c | d) & a & b    = maj(c, d, a & b)
-        const std::string ab = col[0].size() < 2 ? at(0, 0)
-                               : "(" + at(0, 0) + (K == 2 ? " | " : " & ") + at(0, 1) + ")";
-        if (K == 3 && col[0].size() < 2) terms.push_back("(" + at(1, 0) + " & " + at(1, 1) + ")");
-        else terms.push_back("B3(" + at(1, 0) + ", " + at(1, 1) + ", " + ab + ", 0xE8)");
-    }
+// Carry-save state of a partial mismatch count: column 0 (weight 1) and, for
+// K >= 2, column 1 (weight 2); every carry whose weight exceeds K is a dead
+// term (the window is dead whatever the other inputs are).
+struct CountNet {
+    std::deque<std::string> col[2];
+    std::vector<std::string> dead;
+};
+
+// ORs `terms` into one word (three-way ORs as v_bitop3 0xFE: v_or3_b32
+// issues ~1.5x slower on gfx950, profiles/r01c_valu_rates.txt).
+std::string emit_or(std::ostringstream& o, const std::vector<std::string>& terms, int& uid, const std::string& ind) {
     if (terms.empty()) return "0u";
     std::string acc = terms[0];
     size_t i = 1;
     for (; i + 1 < terms.size(); i += 2) {
-        const std::string v = fresh("d");
+        const std::string v = "d" + std::to_string(uid++);
         o << ind << "const u32 " << v << " = B3(" << acc << ", " << terms[i] << ", " << terms[i + 1] << ", 0xFE);\n";
         acc = v;
     }
     if (i < terms.size()) {
-        const std::string v = fresh("d");
+        const std::string v = "d" + std::to_string(uid++);
         o << ind << "const u32 " << v << " = " << acc << " | " << terms[i] << ";\n";
         acc = v;
     }
     return acc;
+}
+
+// Adds mismatch words to a count and compresses every column to at most 2
+// bits with full adders (xor3 + majority, one v_bitop3 each); carries of
+// weight > K go straight into the dead terms.  K = 0: every input is dead.
+void net_add(std::ostringstream& o, CountNet& n, const std::vector<std::string>& in, int K, int& uid,
+             const std::string& ind) {
+    if (K == 0) {
+        n.dead.insert(n.dead.end(), in.begin(), in.end());
+        return;
+    }
+    n.col[0].insert(n.col[0].end(), in.begin(), in.end());
+    const int lmax = K >= 2 ? 1 : 0;   // highest column whose weight is <= K
+    for (int L = 0; L <= lmax; ++L) {
+        auto& c = n.col[L];
+        while (c.size() > 2) {
+            const std::string a = c.front(); c.pop_front();
+            const std::string b = c.front(); c.pop_front();
+            const std::string d = c.front(); c.pop_front();
+            const std::string s = "s" + std::to_string(uid), cy = "c" + std::to_string(uid);
+            ++uid;
+            o << ind << "const u32 " << s << " = B3(" << a << ", " << b << ", " << d << ", 0x96);\n";
+            o << ind << "const u32 " << cy << " = B3(" << a << ", " << b << ", " << d << ", 0xE8);\n";
+            c.push_back(s);
+            if (L < lmax) n.col[L + 1].push_back(cy);
+            else n.dead.push_back(cy);
+        }
+    }
+}
+
+// "count > K" of a compressed count: the dead terms OR the comparison of
+// what is left -- a, b (weight 1) and, for K >= 2, c, d (weight 2).
+std::string net_dead(std::ostringstream& o, const CountNet& n, int K, int& uid, const std::string& ind) {
+    std::vector<std::string> terms = n.dead;
+    auto at = [&](int L, size_t i) { return i < n.col[L].size() ? n.col[L][i] : std::string("0u"); };
+    if (K == 1) {
+        if (n.col[0].size() == 2) terms.push_back("(" + at(0, 0) + " & " + at(0, 1) + ")");
+    } else if (K >= 2 && !n.col[1].empty()) {
+        // count = a + b + 2 (c + d) (+ 4 per dead carry):
+        //   K = 2: dead iff c & d, or (c | d) & (a | b)  = maj(c, d, a | b)
+        //   K = 3: dead iff c & d, or (c | d) & a & b    = maj(c, d, a & b)
+        const std::string ab = n.col[0].size() < 2 ? at(0, 0)
+                               : "(" + at(0, 0) + (K == 2 ? " | " : " & ") + at(0, 1) + ")";
+        if (K == 3 && n.col[0].size() < 2) terms.push_back("(" + at(1, 0) + " & " + at(1, 1) + ")");
+        else terms.push_back("B3(" + at(1, 0) + ", " + at(1, 1) + ", " + ab + ", 0xE8)");
+    }
+    return emit_or(o, terms, uid, ind);
 }
 
 // Source of the specialized kernel for a batch of P <= 8 patterns.
@@ -493,6 +493,44 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     int pin_limit = 1 << 30;
     if (const char* e = getenv("PM_JIT_PIN_LIMIT")) pin_limit = atoi(e);   // experiment knob
     const bool pin = max_words <= pin_limit;
+    // Shared blocks.  Two patterns whose class sequences agree on a run of
+    // positions at some offset -- the strands of a (near-)palindromic motif:
+    // TGCTGA[GC]TCAGCA.[AT] and its reverse complement agree on 13 positions
+    // at offset 2, restriction sites on all of them -- read the same
+    // (row, class) words for those positions at steps `off` apart, so the
+    // carry-save count of the block is built once per row and both windows
+    // only add their own positions (a 13-position block at k = 2: 17 ops
+    // once, then 3 per window, instead of 19 per window).  Greedy pairing,
+    // each pattern in at most one pair; a pair pays when the block is large
+    // and the offset small against the wave's 8 steps.
+    std::vector<std::vector<int>> block(P);   // positions of pattern p in its shared block
+    {
+        std::vector<bool> used(P, false);
+        auto cls = [&](int p, int j) { return class_is_any[pos_class[64 * p + j]] ? -1 : class_acgt[pos_class[64 * p + j]] & 15; };
+        for (;;) {
+            int bp = -1, bq = -1, boff = 0, best = 0;
+            for (int p = 0; p < P; ++p)
+                for (int q = p + 1; q < P; ++q) {
+                    if (used[p] || used[q]) continue;
+                    for (int off = -(JIT_STEPS / 2); off <= JIT_STEPS / 2; ++off) {
+                        // position j of p meets position j - off of q
+                        int n = 0;
+                        for (int j = 0; j < lengths[p]; ++j)
+                            n += j - off >= 0 && j - off < lengths[q] && cls(p, j) >= 0 && cls(p, j) == cls(q, j - off);
+                        // ops saved ~ 1.3 per shared input and shared step, a block per extra step
+                        const int gain = n * (JIT_STEPS - 2 * std::abs(off));
+                        if (n >= 6 && gain > best) { best = gain; bp = p; bq = q; boff = off; }
+                    }
+                }
+            if (bp < 0 || getenv("PM_JIT_NOSHARE")) break;
+            used[bp] = used[bq] = true;
+            for (int j = 0; j < lengths[bp]; ++j)
+                if (j - boff >= 0 && j - boff < lengths[bq] && cls(bp, j) >= 0 && cls(bp, j) == cls(bq, j - boff)) {
+                    block[bp].push_back(j);
+                    block[bq].push_back(j - boff);
+                }
+        }
+    }
     for (int part = 0; part < PARTS; ++part) {
         const int t0 = part * JIT_STEPS, t1 = t0 + JIT_STEPS;
         const int wend = t1 + Lmax - 1;   // words [t0, wend)
@@ -516,16 +554,32 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
             return nm;
         };
         int uid = 0;
+        std::map<std::vector<std::string>, CountNet> blocks;   // block inputs -> its compressed count
         for (int t = t0; t < t1; ++t) {
             for (int p = 0; p < P; ++p) {
                 const uint8_t* pc = pos_class + 64 * p;
-                std::vector<std::string> in;
-                for (int j = 0; j < lengths[p]; ++j) {
+                std::vector<std::string> in, bin;
+                for (int j = 0, b = 0; j < lengths[p]; ++j) {
                     if (class_is_any[pc[j]]) continue;
-                    in.push_back(class_word(t + j, class_acgt[pc[j]] & 15));
+                    const bool shared = b < (int)block[p].size() && block[p][b] == j;
+                    b += shared;
+                    (shared ? bin : in).push_back(class_word(t + j, class_acgt[pc[j]] & 15));
+                }
+                CountNet n;
+                if (!bin.empty()) {   // the block's count, at function scope (the partner reuses it)
+                    auto it = blocks.find(bin);
+                    if (it == blocks.end()) {
+                        o << "  // shared block, rows " << t + block[p].front() << ".." << t + block[p].back() << "\n";
+                        CountNet b;
+                        net_add(o, b, bin, K, uid, "  ");
+                        if (b.dead.size() > 1) b.dead = {emit_or(o, b.dead, uid, "  ")};
+                        it = blocks.emplace(bin, b).first;
+                    }
+                    n = it->second;
                 }
                 o << "  {  // step " << t << ", pattern " << p << "\n";
-                const std::string d = emit_dead_network(o, in, K, uid, "    ");
+                net_add(o, n, in, K, uid, "    ");
+                const std::string d = net_dead(o, n, K, uid, "    ");
                 o << "    dd[" << (t - t0) << "][" << p << "] = " << d << ";\n  }\n";
             }
         }
@@ -707,7 +761,8 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
         }
         sig += "]";
     }
-    for (const char* knob : {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT"})
+    for (const char* knob :
+         {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT", "PM_JIT_NOSHARE"})
         if (const char* e = getenv(knob)) sig += std::string(";") + knob + "=" + e;
     return sig;
 }

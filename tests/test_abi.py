@@ -73,6 +73,35 @@ def test_specialized_kernel_matrix_compiles(pat, k):
     assert engine.jit_compile(progs[:1], k) > 1000
 
 
+SHARED_BLOCK_BATCH = ["ACGGTCATTGCAGT", "TTACGGTCATTGCA", "GGTCATTGCAGTCCAA", "ACGGTCATTGCAGT"]
+
+
+def test_specialized_kernel_shares_strand_blocks(tmp_path, monkeypatch):
+    """The generator builds one carry-save block per row for patterns that
+    agree on a run of classes at a small offset: both strands of the
+    near-palindromic bench motif (13 positions at offset 2) and a batch of
+    shifted copies (offsets -2, +2, 0); unrelated strands share nothing."""
+    from patmatchdocker_amd import engine
+    from patmatchdocker_amd.convert import convert
+    from patmatchdocker_amd.regex import compile_pattern
+
+    def n_blocks(pats, k, strands):
+        dump = tmp_path / "k.hip"
+        monkeypatch.setenv("PM_JIT_DUMP", str(dump))
+        fwd = [convert("-n", p) for p in pats]
+        progs = [compile_pattern(f) for f in fwd]
+        if strands:
+            progs += [compile_pattern(convert("-c", f)) for f in fwd]
+        assert engine.jit_compile(progs, k) > 1000
+        return dump.read_text().count("// shared block")
+
+    # 4 waves x (8 + 2) blocks for the bench motif at every k
+    for k in (0, 1, 2, 3):
+        assert n_blocks(["TGCTGASTCAGCANW"], k, True) == 40
+    assert n_blocks(SHARED_BLOCK_BATCH, 2, False) > 0
+    assert n_blocks(["AAAAAACCCCCC"], 2, True) == 0   # strands agree nowhere
+
+
 def test_route_indels():
     """-k with insertions/deletions routes to the Glushkov kernels; deletions
     with k >= the shortest match are refused loudly (no CPU fallback)."""

@@ -144,6 +144,29 @@ def test_specialized_linear_kernel(engine, oracle_mod, monkeypatch, k):
         db.close()
 
 
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_specialized_shared_blocks(engine, oracle_mod, monkeypatch, k):
+    """Patterns whose class runs agree at small offsets (shared carry-save
+    blocks in the generated kernel): shifted copies, strands of palindromic
+    and near-palindromic motifs, and a degenerate pair with N inside, vs the
+    oracle."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = dna_fasta(211 + k, n_records=4, min_len=40000, max_len=80000, width=None)
+    pats = ["ACGGTCATTGCAGT", "TTACGGTCATTGCA", "GGTCATTGCAGTCCAA", "ACGGTCATTGCAGT",
+            "GAATTC", "TGCTGASTCAGCANW", "RGCCNNNNNGGCY", "ACGTTGCAAGGC"]
+    progs = [compile_pattern(convert("-n", p)) for p in pats[:4]]
+    for p in pats[4:]:
+        fwd = convert("-n", p)
+        progs += [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=k, types="s")
+        for prog, r in zip(progs, res):
+            assert _gpu_pairs(r) == _oracle_hits(oracle_mod, text, prog, k), (prog.source, k)
+    finally:
+        db.close()
+
+
 def test_specialized_matches_generic_on_synthetic(engine, monkeypatch):
     db = engine.SequenceDatabase.synthetic(n_records=40, rec_len=100_003, seed=9)
     try:

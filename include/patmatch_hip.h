@@ -78,6 +78,19 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths,
                    const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
                    pm_hits** out);
 
+/* pm_scan_linear without a host synchronization: launches the scan and
+ * returns a hit list that resolves on first use (pm_hits_count, _copy*,
+ * _device, _kernel_ms wait for it; pm_hits_destroy does not).  A server
+ * launches query i+1 before collecting query i, so host-side work overlaps
+ * the GPU scan.  Same results as pm_scan_linear: when the hit counts
+ * overflow the speculative layout, resolution re-runs the query
+ * synchronously.  The database must outlive the list's resolution
+ * (pm_db_destroy resolves pending lists first).                       */
+int pm_scan_linear_async(pm_db* db, int n_patterns, const int32_t* lengths,
+                         const uint8_t* pos_class, int n_classes, const uint8_t* class_acgt,
+                         const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
+                         pm_hits** out);
+
 /* Generates and compiles (hipRTC, gfx950) the pattern-specialized linear
  * kernel for up to 8 patterns without launching it: a host-only check that
  * needs no GPU (used by the CPU tests and to pre-warm the code cache). */

@@ -25,7 +25,7 @@ EXPORTED = (
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
-    "pm_linear_jit_compile", "pm_scan_nfa_errs",
+    "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async",
 )
 
 
@@ -61,6 +61,7 @@ def _declare(lib):
     lib.pm_db_info.argtypes = [P, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
     lib.pm_db_decode.argtypes = [P, u64, ctypes.c_uint32, ctypes.c_char_p]
     lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, PP]
+    lib.pm_scan_linear_async.argtypes = lib.pm_scan_linear.argtypes
     lib.pm_scan_nfa.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, PP]
     lib.pm_scan_nfa_errs.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,

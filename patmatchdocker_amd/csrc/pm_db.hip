@@ -309,14 +309,28 @@ void init_stream(pm_db* db, void* stream) {
     if (stream) {
         db->stream = (hipStream_t)stream;
     } else {
-        HIPCHK(hipStreamCreate(&db->stream));   // blocking: ordered with the null stream
+        // non-blocking: work a caller queues on the null stream (e.g. copying
+        // out the previous query's hits) must not wait for -- or stall the
+        // host behind -- the scan in flight; consumers order on events
+        HIPCHK(hipStreamCreateWithFlags(&db->stream, hipStreamNonBlocking));
         db->own_stream = true;
     }
 }
 
 void free_db(pm_db* db) {
     if (!db) return;
+    // pipelined scans still pending resolve now (a re-run needs the database)
+    while (!db->pending.empty()) {
+        pm_hits* h = *db->pending.begin();
+        try {
+            hits_finalize(h);
+        } catch (...) {
+            db->pending.erase(h);   // the list stays unresolved (count 0)
+        }
+    }
     if (db->stream) (void)hipStreamSynchronize(db->stream);
+    if (db->up_fence) (void)hipEventDestroy(db->up_fence);
+    if (db->slots_fence) (void)hipEventDestroy(db->slots_fence);
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->bytes, db->ws_tab.p, db->ws_sink.p, db->ws_post.p, db->ws_rec.p};
     for (void* p : ptrs)
@@ -366,9 +380,17 @@ void* reserve_host(pm_db* db, pm_hostbuf& b, size_t bytes) {
 
 uint8_t* Upload::commit(pm_db* db) {
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_tab, std::max<size_t>(blob.size(), 256)));
+    if (db->up_cache_p == (void*)d && db->up_cache == blob) return d;   // a repeated query: tables in place
+    // the pinned staging buffer is rewritten only after its last copy ran
+    // (a pipelined scan may still have it queued)
+    if (db->up_fence) HIPCHK(hipEventSynchronize(db->up_fence));
     uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_up, std::max<size_t>(blob.size(), 256)));
     memcpy(h, blob.data(), blob.size());
     HIPCHK(hipMemcpyAsync(d, h, blob.size(), hipMemcpyHostToDevice, db->stream));
+    if (!db->up_fence) HIPCHK(hipEventCreateWithFlags(&db->up_fence, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(db->up_fence, db->stream));
+    db->up_cache = blob;
+    db->up_cache_p = d;
     return d;
 }
 

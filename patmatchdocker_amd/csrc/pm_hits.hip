@@ -120,13 +120,82 @@ __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* 
 
 std::mutex g_pool_mu;
 std::map<std::pair<int, size_t>, std::vector<void*>> g_pool;   // (device, capacity) -> free buffers
+std::map<size_t, std::vector<void*>> g_pinned;                 // capacity -> free pinned host buffers
+// destroyed hit lists whose buffers some queued work may still touch (a
+// copy out on the caller's stream, a pipelined scan): recycled once their
+// events have completed, so pm_hits_destroy never blocks the host
+std::vector<pm_hits*> g_deferred;
+
+bool event_done(hipEvent_t e) { return !e || hipEventQuery(e) == hipSuccess; }
+
+bool hits_idle(const pm_hits* h) {
+    return event_done(h->ready) && event_done(h->last_use) && (!h->pending || event_done(h->pending->counted));
+}
+
+void release_hits(pm_hits* h) {   // every event of h has completed
+    if (h->ready) (void)hipEventDestroy(h->ready);
+    if (h->last_use) (void)hipEventDestroy(h->last_use);
+    delete h->pending;
+    pool_put(h->device, h->keys, h->keys_cap);
+    pool_put(h->device, h->lens, h->lens_cap);
+    delete h;
+}
+
+// caller holds g_pool_mu; recycles every deferred list that is idle
+void sweep_deferred_locked(std::vector<pm_hits*>& idle) {
+    for (size_t i = 0; i < g_deferred.size();) {
+        if (hits_idle(g_deferred[i])) {
+            idle.push_back(g_deferred[i]);
+            g_deferred[i] = g_deferred.back();
+            g_deferred.pop_back();
+        } else {
+            ++i;
+        }
+    }
+}
+
+void sweep_deferred() {
+    std::vector<pm_hits*> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        sweep_deferred_locked(idle);
+    }
+    for (pm_hits* h : idle) release_hits(h);   // pool_put takes the lock itself
+}
 
 }  // namespace
+
+void* pinned_get(size_t bytes, size_t* cap) {
+    size_t c = 4096;
+    while (c < bytes) c <<= 1;
+    *cap = c;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto& v = g_pinned[c];
+        if (!v.empty()) {
+            void* p = v.back();
+            v.pop_back();
+            return p;
+        }
+    }
+    void* p = nullptr;
+    HIPCHK(hipHostMalloc(&p, c, hipHostMallocDefault));
+    return p;
+}
+
+void pinned_put(void* p, size_t cap) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto& v = g_pinned[cap];
+    if (v.size() < 8) v.push_back(p);
+    else (void)hipHostFree(p);
+}
 
 void* pool_get(int device, size_t bytes, size_t* cap) {
     size_t c = 256;
     while (c < bytes) c <<= 1;
     *cap = c;
+    sweep_deferred();
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         auto it = g_pool.find({device, c});
@@ -185,12 +254,15 @@ static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const s
     // repeat finds them in place
     if (db->slot_cache_p != (void*)d || db->slot_cache_per != per_slot || db->slot_cache_caps != caps) {
         static_assert(sizeof(uint64_t) == 8, "");
+        if (db->slots_fence) HIPCHK(hipEventSynchronize(db->slots_fence));   // last copy out of pin_slots ran
         uint8_t* h = static_cast<uint8_t*>(reserve_host(db, db->pin_slots, (size_t)n_slots * 12 + 16));
         memcpy(h, base.data(), n_slots * 8);
         memcpy(h + (size_t)n_slots * 8, caps.data(), n_slots * 4);
         // o_base and o_cap are adjacent (8-byte entries then 4-byte ones, 256-aligned carve)
         HIPCHK(hipMemcpyAsync(sb.slot_base, h, n_slots * 8, hipMemcpyHostToDevice, db->stream));
         HIPCHK(hipMemcpyAsync(sb.slot_cap, h + (size_t)n_slots * 8, n_slots * 4, hipMemcpyHostToDevice, db->stream));
+        if (!db->slots_fence) HIPCHK(hipEventCreateWithFlags(&db->slots_fence, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(db->slots_fence, db->stream));
         db->slot_cache_p = d;
         db->slot_cache_per = per_slot;
         db->slot_cache_caps = caps;
@@ -317,6 +389,11 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
 
 }  // namespace pm
 
+pm_pending::~pm_pending() {
+    if (counted) (void)hipEventDestroy(counted);
+    pm::pinned_put(counts_h, counts_cap);
+}
+
 using namespace pm;
 
 extern "C" {
@@ -324,6 +401,7 @@ extern "C" {
 int pm_hits_count(const pm_hits* h, uint64_t* count) {
     return guarded([&] {
         require(h != nullptr && count != nullptr, "null argument");
+        hits_finalize(const_cast<pm_hits*>(h));
         *count = h->count;
     });
 }
@@ -331,6 +409,7 @@ int pm_hits_count(const pm_hits* h, uint64_t* count) {
 int pm_hits_copy(const pm_hits* h, int32_t* pattern, int64_t* beg, int64_t* end, uint64_t max_count) {
     return guarded([&] {
         require(h != nullptr, "hits is NULL");
+        hits_finalize(const_cast<pm_hits*>(h));
         const uint64_t n = std::min<uint64_t>(h->count, max_count);
         if (n == 0) return;
         DeviceGuard g(h->device);
@@ -352,6 +431,7 @@ int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst
                         void* stream) {
     return guarded([&] {
         require(h != nullptr, "hits is NULL");
+        hits_finalize(const_cast<pm_hits*>(h));
         const uint64_t n = std::min<uint64_t>(h->count, max_count);
         if (n == 0) return;
         DeviceGuard g(h->device);
@@ -373,6 +453,7 @@ int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst
 int pm_hits_kernel_ms(const pm_hits* h, double* ms) {
     return guarded([&] {
         require(h != nullptr && ms != nullptr, "null argument");
+        hits_finalize(const_cast<pm_hits*>(h));
         *ms = h->kernel_ms;
     });
 }
@@ -380,6 +461,7 @@ int pm_hits_kernel_ms(const pm_hits* h, double* ms) {
 int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count) {
     return guarded([&] {
         require(h != nullptr, "hits is NULL");
+        hits_finalize(const_cast<pm_hits*>(h));
         DeviceGuard g(h->device);
         if (h->ready) HIPCHK(hipEventSynchronize(h->ready));   // the pointers are read by foreign streams
         if (keys) *keys = h->keys;
@@ -393,18 +475,16 @@ int pm_hits_destroy(pm_hits* h) {
         if (!h) return;
         DeviceGuard g(h->device);
         // the producing stream's work and any async copy out must be done
-        // before the buffers go back to the pool
-        if (h->ready) {
-            HIPCHK(hipEventSynchronize(h->ready));
-            (void)hipEventDestroy(h->ready);
+        // before the buffers go back to the pool: recycled now if they are,
+        // else by a later pool_get / pm_hits_destroy (the host never waits)
+        if (h->pending) h->pending->db->pending.erase(h);   // never resolved: no re-run
+        if (hits_idle(h)) {
+            release_hits(h);
+        } else {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            g_deferred.push_back(h);
         }
-        if (h->last_use) {
-            HIPCHK(hipEventSynchronize(h->last_use));
-            (void)hipEventDestroy(h->last_use);
-        }
-        pool_put(h->device, h->keys, h->keys_cap);
-        pool_put(h->device, h->lens, h->lens_cap);
-        delete h;
+        sweep_deferred();
     });
 }
 

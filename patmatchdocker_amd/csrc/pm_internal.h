@@ -40,6 +40,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -184,6 +186,23 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    EventPair() {
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+    }
+    ~EventPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+    double ms() {
+        float v = 0.f;
+        HIPCHK(hipEventElapsedTime(&v, a, b));
+        return v;
+    }
+};
+
 }  // namespace pm
 
 // ---------------------------------------------------------------------------
@@ -224,7 +243,37 @@ struct pm_db {
     void* slot_cache_p = nullptr;
     uint32_t slot_cache_per = 0;
     std::vector<uint32_t> slot_cache_caps;
+    // pinned staging buffers are rewritten by the host only after the copy
+    // that last read them has run (pipelined scans keep work in flight)
+    hipEvent_t up_fence = nullptr, slots_fence = nullptr;
+    std::vector<uint8_t> up_cache;    // tables last uploaded into ws_tab
+    void* up_cache_p = nullptr;
+    std::set<pm_hits*> pending;       // pipelined scans not yet resolved
     uint64_t device_bytes = 0;
+};
+
+// A pipelined scan (pm_scan_linear_async) between launch and resolution: the
+// hit list was sorted speculatively into segment-sized capacity; its bin
+// counts travel to pinned memory behind `counted`.  Resolution validates
+// them (no overflow, no record overflow, every bin LDS-sortable) or re-runs
+// the query synchronously.
+struct pm_pending {
+    pm_db* db = nullptr;
+    hipEvent_t counted = nullptr;
+    uint32_t* counts_h = nullptr;     // nbins counts + the record-overflow counter
+    size_t counts_cap = 0;
+    uint32_t nbins = 0, bins_per_pattern = 0;
+    std::vector<uint32_t> slot_cap_h;
+    std::vector<std::unique_ptr<pm::EventPair>> jev;   // per specialized launch
+    std::string hint_key;
+    std::vector<uint32_t> slot_caps;
+    uint32_t rcap = 0;
+    // the query itself, for the synchronous re-run
+    int n_patterns = 0, n_classes = 0, k = 0;
+    std::vector<int32_t> lengths;
+    std::vector<uint8_t> pos_class, class_acgt, class_is_any;
+    std::vector<uint32_t> class_bytes;
+    ~pm_pending();
 };
 
 struct pm_hits {
@@ -236,6 +285,7 @@ struct pm_hits {
     double kernel_ms = 0.0;
     hipEvent_t ready = nullptr;     // recorded after the last kernel writing keys/lens
     hipEvent_t last_use = nullptr;  // recorded by pm_hits_copy_device on the caller's stream
+    pm_pending* pending = nullptr;  // pipelined scan not yet resolved (count unknown)
 };
 
 namespace pm {
@@ -285,22 +335,6 @@ struct Upload {
     uint8_t* commit(pm_db* db);   // uploads into db->ws_tab; returns its device base
 };
 
-struct EventPair {
-    hipEvent_t a = nullptr, b = nullptr;
-    EventPair() {
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
-    }
-    ~EventPair() {
-        if (a) (void)hipEventDestroy(a);
-        if (b) (void)hipEventDestroy(b);
-    }
-    double ms() {
-        float v = 0.f;
-        HIPCHK(hipEventElapsedTime(&v, a, b));
-        return v;
-    }
-};
 
 // ---------------------------------------------------------------------------
 // hit collection (pm_hits.hip)
@@ -345,5 +379,12 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                       const int32_t* slot_len = nullptr, bool* lens_done = nullptr);
 // records h->ready on the db stream: call after the last kernel filling h
 void hits_ready(pm_db* db, pm_hits* h);
+// Resolves a pipelined scan's hit list (no-op for a resolved one): waits for
+// its counts, keeps the speculative list or replaces it by a synchronous
+// re-run of the query (pm_linear.hip).
+void hits_finalize(pm_hits* h);
+// pinned host buffers for count readbacks (pooled, no hipHostMalloc per scan)
+void* pinned_get(size_t bytes, size_t* cap);
+void pinned_put(void* p, size_t cap);
 
 }  // namespace pm

@@ -808,12 +808,20 @@ bool use_jit(const pm_db* db) {
 
 using namespace pm;
 
-extern "C" {
+namespace {
 
-int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
-                   const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                   pm_hits** out) {
-    return guarded([&] {
+// (database, batch) whose hit bins outgrew the LDS sort: pipelined scans of
+// it run synchronously (the speculative list would be re-done every time)
+std::mutex g_nospec_mu;
+std::set<std::pair<const pm_db*, std::string>> g_nospec;
+
+// pm_scan_linear (async = false) and pm_scan_linear_async: the specialized
+// path launches the scan, record expansion, the speculative sort and the
+// count readback, and returns a pending hit list without a host sync.
+void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
+                      const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
+                      pm_hits** out, bool async) {
+    {
         require(db != nullptr && out != nullptr && lengths && pos_class && class_acgt && class_bytes && class_is_any,
                 "null argument");
         require(db->alphabet == PM_ALPHA_NUC, "pm_scan_linear needs a nucleotide database", PM_E_UNSUPPORTED);
@@ -946,6 +954,41 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                 }
                 if (sb.nbins <= 4096)   // sort before the host sees the counts (one sync per scan)
                     spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len));
+                bool nospec = false;
+                if (async && spec) {
+                    std::lock_guard<std::mutex> lk(g_nospec_mu);
+                    nospec = g_nospec.count({db, cap_key}) != 0;
+                }
+                if (async && spec && attempt == 0 && !nospec) {
+                    // pipelined: counts to pinned memory behind an event; the
+                    // list resolves on first use (hits_finalize)
+                    std::unique_ptr<pm_pending> pd(new pm_pending());
+                    pd->db = db;
+                    pd->nbins = sb.nbins;
+                    pd->bins_per_pattern = sb.bins_per_pattern;
+                    pd->slot_cap_h = sb.slot_cap_h;
+                    pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
+                    HIPCHK(hipMemcpyAsync(pd->counts_h, sb.cnt, (sb.nbins + 1) * 4, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
+                    HIPCHK(hipEventRecord(pd->counted, s));
+                    pd->jev = std::move(jev);
+                    pd->hint_key = cap_key;
+                    pd->slot_caps = slot_caps;
+                    pd->rcap = rcap;
+                    pd->n_patterns = n_patterns;
+                    pd->n_classes = n_classes;
+                    pd->k = k;
+                    pd->lengths.assign(lengths, lengths + n_patterns);
+                    pd->pos_class.assign(pos_class, pos_class + (size_t)64 * n_patterns);
+                    pd->class_acgt.assign(class_acgt, class_acgt + n_classes);
+                    pd->class_is_any.assign(class_is_any, class_is_any + n_classes);
+                    pd->class_bytes.assign(class_bytes, class_bytes + (size_t)8 * n_classes);
+                    hits_ready(db, spec);
+                    spec->pending = pd.release();
+                    db->pending.insert(spec);
+                    *out = spec;
+                    return;
+                }
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t rec_need = sb.aux;
@@ -1028,6 +1071,83 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
         // pm_hits_device, pm_hits_destroy)
         hits_ready(db, h);
         *out = h;
+    }
+}
+
+}  // namespace
+
+namespace pm {
+
+void hits_finalize(pm_hits* h) {
+    if (!h || !h->pending) return;
+    std::unique_ptr<pm_pending> pd(h->pending);
+    h->pending = nullptr;
+    pm_db* db = pd->db;
+    db->pending.erase(h);
+    DeviceGuard g(h->device);
+    HIPCHK(hipEventSynchronize(pd->counted));
+    uint64_t total = 0;
+    uint32_t maxc = 0;
+    bool overflow = false;
+    for (uint32_t b = 0; b < pd->nbins; ++b) {
+        const uint32_t c = pd->counts_h[b];
+        total += c;
+        maxc = std::max(maxc, c);
+        overflow |= c > pd->slot_cap_h[b / pd->bins_per_pattern];
+    }
+    const bool rec_over = pd->counts_h[pd->nbins] != 0;
+    if (!overflow && !rec_over && maxc <= LDS_SORT_CAP) {   // the speculative list is the answer
+        h->count = total;
+        double kms = 0.0;
+        for (auto& e : pd->jev) kms += e->ms();
+        h->kernel_ms = kms;
+        std::lock_guard<std::mutex> lk(g_cap_mu);
+        if (g_cap_hint.size() > 256) g_cap_hint.clear();
+        g_cap_hint[{db, pd->hint_key}] = {pd->slot_caps, pd->rcap};
+        return;
+    }
+    if (!overflow && !rec_over) {   // bins too large for the LDS sort: this batch stays synchronous
+        std::lock_guard<std::mutex> lk(g_nospec_mu);
+        if (g_nospec.size() > 256) g_nospec.clear();
+        g_nospec.insert({db, pd->hint_key});
+    }
+    // re-run synchronously (grows the capacities, remembers them) and adopt
+    // the result's buffers
+    pm_hits* r = nullptr;
+    scan_linear_impl(db, pd->n_patterns, pd->lengths.data(), pd->pos_class.data(), pd->n_classes,
+                     pd->class_acgt.data(), pd->class_bytes.data(), pd->class_is_any.data(), pd->k, &r, false);
+    pool_put(h->device, h->keys, h->keys_cap);
+    pool_put(h->device, h->lens, h->lens_cap);
+    h->keys = r->keys;
+    h->lens = r->lens;
+    h->keys_cap = r->keys_cap;
+    h->lens_cap = r->lens_cap;
+    h->count = r->count;
+    h->kernel_ms = r->kernel_ms;
+    if (h->ready) (void)hipEventDestroy(h->ready);
+    h->ready = r->ready;
+    delete r;
+}
+
+}  // namespace pm
+
+extern "C" {
+
+int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
+                   const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
+                   pm_hits** out) {
+    return guarded([&] {
+        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k, out,
+                         false);
+    });
+}
+
+int pm_scan_linear_async(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
+                         const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
+                         pm_hits** out) {
+    return guarded([&] {
+        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k, out,
+                         true);
     });
 }
 

@@ -212,13 +212,17 @@ class LinearBatch:
         self.lengths, self.pos_class, self.nc, self.acgt, self.bits, self.is_any = _linear_tables(progs)
         self.n = len(progs)
 
-    def launch(self, db: SequenceDatabase, k: int):
-        """Run pm_scan_linear; returns the raw pm_hits handle (caller destroys)."""
+    def launch(self, db: SequenceDatabase, k: int, pipelined: bool = False):
+        """Run pm_scan_linear; returns the raw pm_hits handle (caller destroys).
+
+        ``pipelined``: pm_scan_linear_async -- returns before the scan ends
+        (the handle resolves on first use), so a caller can launch the next
+        query before collecting this one."""
         out = ctypes.c_void_p()
-        check(_lib.load().pm_scan_linear(db.handle, self.n, self.lengths.ctypes.data,
-                                         self.pos_class.ctypes.data, self.nc, self.acgt.ctypes.data,
-                                         self.bits.ctypes.data, self.is_any.ctypes.data, k,
-                                         ctypes.byref(out)))
+        lib = _lib.load()
+        fn = lib.pm_scan_linear_async if pipelined else lib.pm_scan_linear
+        check(fn(db.handle, self.n, self.lengths.ctypes.data, self.pos_class.ctypes.data, self.nc,
+                 self.acgt.ctypes.data, self.bits.ctypes.data, self.is_any.ctypes.data, k, ctypes.byref(out)))
         return out
 
 

@@ -347,3 +347,42 @@ def test_unbounded_repeats(engine, oracle_mod, k, types):
             assert _gpu_pairs(res[0]) == oracle_mod.scan(text, prog, k, types or "s", skip_headers=True), (pat, k)
     finally:
         db.close()
+
+
+def _hits_pairs(h, n_pat):
+    return [list(zip(*[a.tolist() for a in h.for_pattern(i)])) for i in range(n_pat)]
+
+
+def test_pipelined_scans_match_synchronous(engine, oracle_mod, monkeypatch):
+    """pm_scan_linear_async: three different batches launched back to back
+    before any is collected, collected out of order, one destroyed
+    unresolved, and a dense batch whose speculative layout overflows (the
+    resolution re-runs it synchronously); every list equals the oracle's."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = dna_fasta(301, n_records=4, min_len=50000, max_len=90000, width=None)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    batches = []
+    for pats in (["TGCTGASTCAGCANW"], ["GAATTC", "TATAWAWR"], ["NNNNNANN", "RRYY", "CCAAT"]):
+        progs = []
+        for p in pats:
+            fwd = convert("-n", p)
+            progs += [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+        batches.append((progs, engine.LinearBatch(progs)))
+    try:
+        for k in (1, 2):
+            handles = [b.launch(db, k, pipelined=True) for _, b in batches]
+            extra = batches[0][1].launch(db, k, pipelined=True)
+            engine.destroy_hits(extra)   # never resolved
+            for i in (2, 0, 1):
+                progs = batches[i][0]
+                got = _hits_pairs(engine._collect(handles[i]), len(progs))
+                for prog, g in zip(progs, got):
+                    assert g == _oracle_hits(oracle_mod, text, prog, k), (prog.source, k)
+        # pending lists resolve before their database goes away
+        handles = [b.launch(db, 2, pipelined=True) for _, b in batches]
+    finally:
+        db.close()
+    for (progs, _), h in zip(batches, handles):
+        got = _hits_pairs(engine._collect(h), len(progs))
+        for prog, g in zip(progs, got):
+            assert g == _oracle_hits(oracle_mod, text, prog, 2), prog.source

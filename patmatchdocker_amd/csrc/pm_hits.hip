@@ -59,9 +59,15 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict
 __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
                                                    const uint64_t* __restrict__ off, BinShape sh,
                                                    uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
-                                                   uint32_t* __restrict__ lens) {
+                                                   uint32_t* __restrict__ lens, uint32_t* counts_host = nullptr,
+                                                   uint32_t nbins = 0) {
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
+    if (counts_host && bin == nbins) {   // one extra block: the pipelined scan's count readback (mapped host memory)
+        for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
+        __threadfence_system();
+        return;
+    }
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0 || c > LDS_SORT_CAP) return;   // (a speculative sort's caller redoes such lists)
     uint64_t base;
@@ -179,7 +185,8 @@ void* pinned_get(size_t bytes, size_t* cap) {
         }
     }
     void* p = nullptr;
-    HIPCHK(hipHostMalloc(&p, c, hipHostMallocDefault));
+    // mapped + coherent: kernels store into it, the host reads after an event
+    HIPCHK(hipHostMalloc(&p, c, hipHostMallocMapped | hipHostMallocCoherent));
     return p;
 }
 
@@ -225,7 +232,8 @@ void pool_put(int device, void* p, size_t cap) {
 
 // Allocates out/cnt/slot arrays for n_slots slots of `per_slot` bins with
 // per-slot capacities; counters zeroed, slot tables uploaded.
-static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& caps) {
+static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& caps,
+                              bool zero_counts = true) {
     SinkBuffers sb;
     require(n_slots >= 1 && per_slot >= 1 && caps.size() == (size_t)n_slots, "internal: bad sink shape");
     sb.bins_per_pattern = per_slot;
@@ -267,7 +275,7 @@ static SinkBuffers alloc_sink(pm_db* db, int n_slots, uint32_t per_slot, const s
         db->slot_cache_per = per_slot;
         db->slot_cache_caps = caps;
     }
-    HIPCHK(hipMemsetAsync(sb.cnt, 0, (sb.nbins + 1) * sizeof(uint32_t), db->stream));
+    if (zero_counts) HIPCHK(hipMemsetAsync(sb.cnt, 0, (sb.nbins + 1) * sizeof(uint32_t), db->stream));
     return sb;
 }
 
@@ -285,8 +293,9 @@ SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t exp
     return sb;
 }
 
-SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps) {
-    SinkBuffers sb = alloc_sink(db, n_slots, per_slot, slot_caps);
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps,
+                               bool zero_counts) {
+    SinkBuffers sb = alloc_sink(db, n_slots, per_slot, slot_caps, zero_counts);
     sb.pos_shift = 0;
     return sb;
 }
@@ -306,7 +315,7 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
     return total;
 }
 
-pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len) {
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host) {
     require(sb.nbins <= 4096, "internal: speculative sort needs <= 4096 bins");
     uint64_t cap_total = 0;
     for (uint32_t c : sb.slot_cap_h) cap_total += (uint64_t)c * sb.bins_per_pattern;
@@ -316,8 +325,8 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, db->stream, sb.out, sb.cnt, nullptr, sh,
-                           h->keys, slot_len, h->lens);
+        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins + (counts_host ? 1 : 0)), dim3(256), 0, db->stream, sb.out,
+                           sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
         HIPCHK(hipGetLastError());
     } catch (...) {
         discard_hits(h);

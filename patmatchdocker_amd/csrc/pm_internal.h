@@ -362,7 +362,8 @@ struct SinkBuffers {
 SinkBuffers make_sink(pm_db* db, int n_slots, uint64_t n_positions, uint64_t expected);
 // Bins filled by the producer itself: n_slots x per_slot segments of `cap`
 // keys, each a position range in increasing order (pm_linear_jit).
-SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps);
+SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const std::vector<uint32_t>& slot_caps,
+                               bool zero_counts = true);
 // Reads bin counters; returns total, sets `overflow` if a bin exceeded cap.
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
 // bins -> one sorted key list (pattern << 48 | pos) owned by the returned
@@ -371,7 +372,9 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
 // sized for all capacities BEFORE the counts reach the host, so a scan needs
 // one host sync; count unset -- the caller validates the counts it reads
 // afterwards and keeps the result (count = total) or discards it.
-pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len);
+// counts_host (mapped pinned, optional): the sort also stores the raw bin
+// counts and the aux counter there (the pipelined scan's readback).
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host);
 void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // slot_len (device, per slot, optional): fixed match length of every key of
 // a slot -- the LDS sort writes h->lens with the keys.
@@ -383,7 +386,8 @@ void hits_ready(pm_db* db, pm_hits* h);
 // its counts, keeps the speculative list or replaces it by a synchronous
 // re-run of the query (pm_linear.hip).
 void hits_finalize(pm_hits* h);
-// pinned host buffers for count readbacks (pooled, no hipHostMalloc per scan)
+// mapped pinned host buffers for count readbacks (pooled, no hipHostMalloc
+// per scan; kernels write them directly)
 void* pinned_get(size_t bytes, size_t* cap);
 void pinned_put(void* p, size_t cap);
 

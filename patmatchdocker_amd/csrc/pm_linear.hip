@@ -305,6 +305,7 @@ struct JArgs {
     const uint2* hl;
     uint2* rec;             // [nwg * 4][rcap]
     u32* rec_cnt;           // [nwg * 4]
+    u32* aux_zero;          // the sink's record-overflow counter, zeroed by the first launch of a scan (or null)
     u64 ntiles;
     u32 rcap, tiles_per_wg;
 };
@@ -331,6 +332,7 @@ struct JArgsHost {           // must match JArgs in kJitCommon
     const uint2* hl;
     uint2* rec;
     uint32_t* rec_cnt;
+    uint32_t* aux_zero;
     uint64_t ntiles;
     uint32_t rcap, tiles_per_wg;
 };
@@ -650,6 +652,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * 4 + wid) * a.rcap);\n"
          "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
          "  u32 scnt = 0, gcnt = 0;   // staged / flushed records (wave-uniform)\n"
+         "  if (a.aux_zero && blockIdx.x == 0 && threadIdx.x == 0) *a.aux_zero = 0u;   // read by k_linear_expand (after)\n"
          "  stage(a, lds_base, t0, tend, wid, lane);\n"
          "  stage(a, lds_base + LDS_TILE, t0 + 1, tend, wid, lane);\n"
          "  u32 slot = 0;\n"
@@ -668,14 +671,15 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
          "#endif\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
-         "    u32 dd[STEPS][P];   // dead windows per step and pattern\n"
-         "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) dd[s][p] = ~0u;\n";
+         "    u32 dd[STEPS][P];   // dead windows per step and pattern (every path writes all of them)\n";
     if (nocompute) {
-        o << "    if (sw[lane].x == 0x12345u && lane == 99) dd[0][0] = 0u;   // keeps the tile reads\n";
+        o << "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) dd[s][p] = ~0u;\n"
+             "    if (sw[lane].x == 0x12345u && lane == 99) dd[0][0] = 0u;   // keeps the tile reads\n";
     } else {
+        // wid < 4: the last part is the plain else (no ~0 initialization of dd)
         for (int part = 0; part < PARTS; ++part)
-            o << "    " << (part ? "else " : "") << "if (wid == " << part << ") tile_body" << part
-              << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
+            o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
+              << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
     }
     o << "    u32 all = ~0u;\n"
          "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
@@ -924,13 +928,15 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 uint2* d_rec = reinterpret_cast<uint2*>(rbase + o_rec);
                 uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
                 (void)o_over;
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps);
+                // no counter memset: k_linear_expand stores every (pattern,
+                // segment) count, the first launch zeroes the aux counter
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
                 uint32_t* d_over = sb.cnt + sb.nbins;   // the sink's aux counter
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
                 jev.clear();
                 for (const Chunk& ch : chunks) {
-                    JArgsHost ja{db->hl, d_rec, d_rcnt, db->ntiles, rcap, (uint32_t)tpw};
+                    JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
                     jev.emplace_back(new EventPair());
                     HIPCHK(hipEventRecord(jev.back()->a, s));
@@ -952,23 +958,22 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                         HIPCHK(hipGetLastError());
                     }
                 }
-                if (sb.nbins <= 4096)   // sort before the host sees the counts (one sync per scan)
-                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len));
                 bool nospec = false;
-                if (async && spec) {
+                if (async && sb.nbins <= 4096 && attempt == 0) {
                     std::lock_guard<std::mutex> lk(g_nospec_mu);
                     nospec = g_nospec.count({db, cap_key}) != 0;
                 }
-                if (async && spec && attempt == 0 && !nospec) {
-                    // pipelined: counts to pinned memory behind an event; the
-                    // list resolves on first use (hits_finalize)
+                if (async && sb.nbins <= 4096 && attempt == 0 && !nospec) {
+                    // pipelined: the speculative sort also writes the bin
+                    // counts into mapped pinned memory (no copy), an event
+                    // follows; the list resolves on first use (hits_finalize)
                     std::unique_ptr<pm_pending> pd(new pm_pending());
                     pd->db = db;
                     pd->nbins = sb.nbins;
                     pd->bins_per_pattern = sb.bins_per_pattern;
                     pd->slot_cap_h = sb.slot_cap_h;
                     pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
-                    HIPCHK(hipMemcpyAsync(pd->counts_h, sb.cnt, (sb.nbins + 1) * 4, hipMemcpyDeviceToHost, s));
+                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h);
                     HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
                     HIPCHK(hipEventRecord(pd->counted, s));
                     pd->jev = std::move(jev);
@@ -989,6 +994,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     *out = spec;
                     return;
                 }
+                if (sb.nbins <= 4096)   // sort before the host sees the counts (one sync per scan)
+                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), nullptr);
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t rec_need = sb.aux;

@@ -329,15 +329,23 @@ void free_db(pm_db* db) {
         }
     }
     if (db->stream) (void)hipStreamSynchronize(db->stream);
-    if (db->up_fence) (void)hipEventDestroy(db->up_fence);
-    if (db->slots_fence) (void)hipEventDestroy(db->slots_fence);
+    if (db->post) {
+        (void)hipStreamSynchronize(db->post);
+        (void)hipStreamDestroy(db->post);
+    }
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->bytes, db->ws_tab.p, db->ws_sink.p, db->ws_post.p, db->ws_rec.p};
+                    db->lflag, db->bytes, db->ws_post.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    if (db->pin_up.p) (void)hipHostFree(db->pin_up.p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
-    if (db->pin_slots.p) (void)hipHostFree(db->pin_slots.p);
+    for (pm_lane* l : {static_cast<pm_lane*>(db), &db->alt}) {
+        for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p})
+            if (p) (void)hipFree(p);
+        for (void* p : {l->pin_up.p, l->pin_slots.p})
+            if (p) (void)hipHostFree(p);
+        for (hipEvent_t e : {l->up_fence, l->slots_fence, l->free_ev})
+            if (e) (void)hipEventDestroy(e);
+    }
     if (db->own_stream && db->stream) (void)hipStreamDestroy(db->stream);
     delete db;
 }
@@ -352,9 +360,26 @@ void check_device(int device) {
 
 // Grow a workspace.  Growing waits for the stream first, so no queued work
 // can still reference the old allocation.
+void lane_begin(pm_db* db) {
+    if (db->free_ev) HIPCHK(hipStreamWaitEvent(db->stream, db->free_ev, 0));
+}
+
+void lane_end(pm_db* db, hipStream_t s) {
+    if (!db->free_ev) HIPCHK(hipEventCreateWithFlags(&db->free_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(db->free_ev, s));
+}
+
+void switch_lane(pm_db* db) { std::swap(static_cast<pm_lane&>(*db), db->alt); }
+
+hipStream_t post_stream(pm_db* db) {
+    if (!db->post) HIPCHK(hipStreamCreateWithFlags(&db->post, hipStreamNonBlocking));
+    return db->post;
+}
+
 void* reserve(pm_db* db, pm_devbuf& b, size_t bytes) {
     if (b.cap < bytes) {
         HIPCHK(hipStreamSynchronize(db->stream));
+        if (db->post) HIPCHK(hipStreamSynchronize(db->post));
         if (b.p) HIPCHK(hipFree(b.p));
         b.p = nullptr;
         b.cap = 0;

@@ -220,6 +220,7 @@ void* pool_get(int device, size_t bytes, size_t* cap) {
 void hits_ready(pm_db* db, pm_hits* h) {
     if (!h->ready) HIPCHK(hipEventCreateWithFlags(&h->ready, hipEventDisableTiming));
     HIPCHK(hipEventRecord(h->ready, db->stream));
+    lane_end(db, db->stream);
 }
 
 void pool_put(int device, void* p, size_t cap) {
@@ -315,7 +316,8 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
     return total;
 }
 
-pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host) {
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host,
+                               hipStream_t stream) {
     require(sb.nbins <= 4096, "internal: speculative sort needs <= 4096 bins");
     uint64_t cap_total = 0;
     for (uint32_t c : sb.slot_cap_h) cap_total += (uint64_t)c * sb.bins_per_pattern;
@@ -325,7 +327,7 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins + (counts_host ? 1 : 0)), dim3(256), 0, db->stream, sb.out,
+        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins + (counts_host ? 1 : 0)), dim3(256), 0, stream, sb.out,
                            sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
         HIPCHK(hipGetLastError());
     } catch (...) {

@@ -217,7 +217,26 @@ struct pm_hostbuf {      // pinned host staging buffer
     size_t cap = 0;
 };
 
-struct pm_db {
+// Per-scan workspaces ("lane"): device buffers the kernels of one scan
+// write, the pinned staging they are uploaded from, and `free_ev`, recorded
+// after the last work that reads them (a scan waits for it on the GPU before
+// reusing the lane).  Never stream-ordered allocations.
+struct pm_lane {
+    pm_devbuf ws_tab, ws_sink, ws_rec;
+    pm_hostbuf pin_up, pin_slots;
+    // slot tables last uploaded into ws_sink (skip the copy when unchanged)
+    void* slot_cache_p = nullptr;
+    uint32_t slot_cache_per = 0;
+    std::vector<uint32_t> slot_cache_caps;
+    // pinned staging buffers are rewritten by the host only after the copy
+    // that last read them has run (pipelined scans keep work in flight)
+    hipEvent_t up_fence = nullptr, slots_fence = nullptr;
+    std::vector<uint8_t> up_cache;    // tables last uploaded into ws_tab
+    void* up_cache_p = nullptr;
+    hipEvent_t free_ev = nullptr;
+};
+
+struct pm_db : pm_lane {
     int device = 0;
     int alphabet = PM_ALPHA_NUC;
     uint64_t n = 0;          // positions (file bytes)
@@ -236,18 +255,14 @@ struct pm_db {
     uint8_t* bytes = nullptr;    // BYTE alphabet
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    // per-call workspaces (never stream-ordered allocations)
-    pm_devbuf ws_tab, ws_sink, ws_post, ws_rec;
-    pm_hostbuf pin_up, pin_down, pin_slots;
-    // slot tables last uploaded into ws_sink (skip the copy when unchanged)
-    void* slot_cache_p = nullptr;
-    uint32_t slot_cache_per = 0;
-    std::vector<uint32_t> slot_cache_caps;
-    // pinned staging buffers are rewritten by the host only after the copy
-    // that last read them has run (pipelined scans keep work in flight)
-    hipEvent_t up_fence = nullptr, slots_fence = nullptr;
-    std::vector<uint8_t> up_cache;    // tables last uploaded into ws_tab
-    void* up_cache_p = nullptr;
+    // synchronous-path workspaces
+    pm_devbuf ws_post;
+    pm_hostbuf pin_down;
+    // pipelined scans: record expansion + sort of scan i run on `post` while
+    // scan i+1's kernel runs on `stream`, each on its own workspace lane (the
+    // inherited pm_lane is the active one, `alt` the other; switch_lane swaps)
+    hipStream_t post = nullptr;
+    pm_lane alt;
     std::set<pm_hits*> pending;       // pipelined scans not yet resolved
     uint64_t device_bytes = 0;
 };
@@ -304,6 +319,13 @@ struct DeviceGuard {
     }
 };
 
+// workspace lanes (pm_lane): a scan waits on the GPU for its lane's last
+// reader (lane_begin) and marks its own last reader (lane_end, also done by
+// hits_ready on db->stream); switch_lane alternates lanes (pipelined scans)
+void lane_begin(pm_db* db);
+void lane_end(pm_db* db, hipStream_t s);
+void switch_lane(pm_db* db);
+hipStream_t post_stream(pm_db* db);
 void* reserve(pm_db* db, pm_devbuf& b, size_t bytes);
 // Per-device pool of hit-list buffers (sizes rounded to powers of two):
 // scans allocate their result from it and pm_hits_destroy returns it, so a
@@ -374,7 +396,8 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
 // afterwards and keeps the result (count = total) or discards it.
 // counts_host (mapped pinned, optional): the sort also stores the raw bin
 // counts and the aux counter there (the pipelined scan's readback).
-pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host);
+pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host,
+                               hipStream_t stream);
 void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // slot_len (device, per slot, optional): fixed match length of every key of
 // a slot -- the LDS sort writes h->lens with the keys.

@@ -868,6 +868,17 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             chunks.push_back({base, P, fn});
             base += P;
         }
+        // pipelined single-launch scans alternate workspace lanes, so that
+        // this scan's record expansion + sort (on the post stream) overlap
+        // the next scan's kernel; every scan first waits (on the GPU) for the
+        // last reader of its lane
+        // Off by default: measured no faster per step (the chip is at its
+        // power limit either way) and the overlapped expansion slows the
+        // kernel it overlaps.  PM_OFFLOAD=1 turns it on (experiment knob).
+        static const bool want_offload = getenv("PM_OFFLOAD") && getenv("PM_OFFLOAD")[0] == '1';
+        const bool offload = async && jit && chunks.size() == 1 && want_offload;
+        if (offload) switch_lane(db);
+        lane_begin(db);
         uint8_t* d_up = up.commit(db);
 
         SinkBuffers sb;
@@ -935,6 +946,15 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
                 jev.clear();
+                bool nospec = false;
+                if (async && sb.nbins <= 4096 && attempt == 0) {
+                    std::lock_guard<std::mutex> lk(g_nospec_mu);
+                    nospec = g_nospec.count({db, cap_key}) != 0;
+                }
+                const bool spec_async = async && sb.nbins <= 4096 && attempt == 0 && !nospec;
+                // expansion, others and the sort: on the post stream after the
+                // kernel's event when this scan returns pipelined in one launch
+                const hipStream_t xs = spec_async && offload ? post_stream(db) : s;
                 for (const Chunk& ch : chunks) {
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
@@ -942,11 +962,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     HIPCHK(hipEventRecord(jev.back()->a, s));
                     HIPCHK(hipModuleLaunchKernel(ch.jit, (uint32_t)nwg, 1, 1, 256, 1, 1, 0, s, params, nullptr));
                     HIPCHK(hipEventRecord(jev.back()->b, s));
+                    if (xs != s) HIPCHK(hipStreamWaitEvent(xs, jev.back()->b, 0));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
                                   (uint32_t)tpw};
-                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, s, xa);
+                    hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
                     if (db->nflag && db->n_oth_words) {
                         OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
@@ -954,16 +975,11 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
                                       sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout,
                                       (uint32_t)(tpw * group)};
-                        hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, s, oa);
+                        hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, xs, oa);
                         HIPCHK(hipGetLastError());
                     }
                 }
-                bool nospec = false;
-                if (async && sb.nbins <= 4096 && attempt == 0) {
-                    std::lock_guard<std::mutex> lk(g_nospec_mu);
-                    nospec = g_nospec.count({db, cap_key}) != 0;
-                }
-                if (async && sb.nbins <= 4096 && attempt == 0 && !nospec) {
+                if (spec_async) {
                     // pipelined: the speculative sort also writes the bin
                     // counts into mapped pinned memory (no copy), an event
                     // follows; the list resolves on first use (hits_finalize)
@@ -973,9 +989,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->bins_per_pattern = sb.bins_per_pattern;
                     pd->slot_cap_h = sb.slot_cap_h;
                     pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
-                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h);
+                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h,
+                                                 xs);
                     HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
-                    HIPCHK(hipEventRecord(pd->counted, s));
+                    HIPCHK(hipEventRecord(pd->counted, xs));
                     pd->jev = std::move(jev);
                     pd->hint_key = cap_key;
                     pd->slot_caps = slot_caps;
@@ -988,14 +1005,20 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->class_acgt.assign(class_acgt, class_acgt + n_classes);
                     pd->class_is_any.assign(class_is_any, class_is_any + n_classes);
                     pd->class_bytes.assign(class_bytes, class_bytes + (size_t)8 * n_classes);
-                    hits_ready(db, spec);
+                    if (xs == s) {
+                        hits_ready(db, spec);
+                    } else {   // the list and the lane's last reader are on the post stream
+                        HIPCHK(hipEventCreateWithFlags(&spec->ready, hipEventDisableTiming));
+                        HIPCHK(hipEventRecord(spec->ready, xs));
+                        lane_end(db, xs);
+                    }
                     spec->pending = pd.release();
                     db->pending.insert(spec);
                     *out = spec;
                     return;
                 }
                 if (sb.nbins <= 4096)   // sort before the host sees the counts (one sync per scan)
-                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), nullptr);
+                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), nullptr, s);
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t rec_need = sb.aux;

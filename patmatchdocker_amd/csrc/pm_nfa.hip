@@ -313,6 +313,7 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
         require(max_len + ins_extra <= 1024 + PM_MAX_K, "max_len above 1024", PM_E_UNSUPPORTED);
         DeviceGuard g(db->device);
+        lane_begin(db);
         hipStream_t s = db->stream;
         const int nt = (m + 7) / 8;
         // Glushkov transition tables per 8-position slice: follow / precede

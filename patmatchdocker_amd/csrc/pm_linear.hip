@@ -343,8 +343,27 @@ int jit_wg_per_cu() {
     return e ? std::max(1, atoi(e)) : 4;
 }
 
-// mismatch of an ACGT subset as an expression of the plane words h, l
+// mismatch of an ACGT subset as an expression of the plane words h, l.
+// Forms with an inverted plane are one explicit v_bitop3 (truth table over
+// (h, l, l)): written as C, the compiler splits them into a NOT (shared or
+// not) plus an OR/AND -- measured 16 extra ops per wave-tile.
 std::string subset_expr(int subset, const std::string& h, const std::string& l) {
+    auto b3 = [&](int (*f)(int, int)) {
+        int tt = 0;
+        for (int idx = 0; idx < 8; ++idx) tt |= f((idx >> 2) & 1, (idx >> 1) & 1) << idx;   // idx = 4h + 2l + l
+        char buf[8];
+        snprintf(buf, sizeof buf, "0x%02X", tt);
+        return "B3(" + h + ", " + l + ", " + l + ", " + buf + ")";
+    };
+    switch (subset & 15) {
+        case 0x2: return b3([](int a, int b) { return a | (b ^ 1); });
+        case 0x4: return b3([](int a, int b) { return (a ^ 1) | b; });
+        case 0x8: return b3([](int a, int b) { return (a ^ 1) | (b ^ 1); });
+        case 0xB: return b3([](int a, int b) { return a & (b ^ 1); });
+        case 0xD: return b3([](int a, int b) { return (a ^ 1) & b; });
+        case 0xE: return b3([](int a, int b) { return (a ^ 1) & (b ^ 1); });
+        default: break;
+    }
     switch (subset & 15) {
         case 0x0: return "~0u";
         case 0x1: return "(" + h + " | " + l + ")";

@@ -16,8 +16,8 @@ Reported beside the throughput:
                 words) / its HIP-event duration vs the 8 TB/s HBM peak;
                 traffic = PMC HBM bytes per launch from profiles/ when a
                 counter run of this workload is committed there, else null;
-  cpu_baseline  the CPU oracle (oracle/pm_oracle.c, single thread) timed on a
-                bounded sample of the same database (decoded from HBM), which
+  cpu_baseline  the CPU oracle (oracle/pm_oracle.c, one thread per host core
+                of the box's CPU share, at most 16) timed on a bounded sample of the same database (decoded from HBM), which
                 is also a bit-exact parity spot check of the GPU hits.
 """
 
@@ -44,7 +44,10 @@ def parse_args():
     ap.add_argument("--rec-len", type=int, default=1_000_000)
     ap.add_argument("--motif", default=MOTIF)
     ap.add_argument("--k", type=int, default=2)
-    ap.add_argument("--sample-mbp", type=float, default=160.0, help="CPU-baseline sample (Mbp)")
+    ap.add_argument("--sample-mbp", type=float, default=None,
+                    help="CPU-baseline sample (Mbp; default 20 per CPU thread)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU-baseline threads (default: the box's CPU share, at most 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="collect each query before launching the next (default: query i+1 is launched "
@@ -87,12 +90,21 @@ def load_traffic(workload):
     return None
 
 
-def cpu_baseline(db, progs, k, sample_bp, gpu_hits):
-    """Oracle on the first `sample_bp` positions; returns (dict, parity_ok)."""
+def cpu_threads_default():
+    """The box's CPU share: OMP_NUM_THREADS (16 on the GPU box), else the
+    affinity mask, capped at 16."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    n = int(n) if n and n.isdigit() else len(os.sched_getaffinity(0))
+    return max(1, min(16, n))
+
+
+def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads):
+    """Oracle on the first `sample_bp` positions over `threads` host threads
+    (the sample is cut at record starts); returns (dict, parity_ok)."""
     from oracle import oracle
     text = db.decode(0, int(sample_bp))
     t0 = time.perf_counter()
-    want = [oracle.scan(text, p, k, "s", skip_headers=True) for p in progs]
+    want = [oracle.scan_threads(text, p, k, "s", skip_headers=True, threads=threads) for p in progs]
     dt = time.perf_counter() - t0
     bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
     ok = True
@@ -103,9 +115,10 @@ def cpu_baseline(db, progs, k, sample_bp, gpu_hits):
         got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
                if (kk >> 48) == pid and (kk & ((1 << 48) - 1)) + ln <= len(text)]
         ok &= got == w
-    return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "port",
+    return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
             "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, "
-                      "oracle/pm_oracle.c single thread, %.1f s" % (sample_bp / 1e6, dt)}, ok
+                      "oracle/pm_oracle.c on %d host threads (records split across threads), "
+                      "%.1f s wall" % (sample_bp / 1e6, threads, dt)}, ok
 
 
 def main():
@@ -260,7 +273,9 @@ def main():
             line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
             line["roofline"]["traffic"] = None
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
-            cb, ok = cpu_baseline(db, progs, args.k, args.sample_mbp * 1e6, result)
+            thr = args.cpu_threads or cpu_threads_default()
+            mbp = args.sample_mbp if args.sample_mbp is not None else 20.0 * thr
+            cb, ok = cpu_baseline(db, progs, args.k, mbp * 1e6, result, thr)
             line["cpu_baseline"] = cb
             line["parity_sample_bit_exact"] = ok
         else:

@@ -103,6 +103,35 @@ def scan(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool =
         cap = int(n)
 
 
+def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
+                 threads: int = 1):
+    """``scan`` over ``threads`` host threads: the text is cut at record starts
+    (a hit never spans a record), each piece is scanned by
+    ``pmo_scan`` (ctypes releases the GIL) and the hits are shifted back to
+    file offsets.  Same output as ``scan``; used for the bench's CPU baseline."""
+    if threads <= 1 or len(text) < (1 << 20):
+        return scan(text, prog, k, types, skip_headers)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [0]
+    step = len(text) // threads
+    for t in range(1, threads):
+        c = text.find(b"\n>", max(cuts[-1], t * step))
+        if c < 0:
+            break
+        if c + 1 > cuts[-1]:
+            cuts.append(c + 1)
+    cuts.append(len(text))
+    pieces = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+
+    def one(span):
+        a, b = span
+        return [(x + a, y + a) for x, y in scan(text[a:b], prog, k, types, skip_headers)]
+
+    with ThreadPoolExecutor(max_workers=len(pieces)) as ex:
+        parts = list(ex.map(one, pieces))
+    return [h for part in parts for h in part]
+
+
 def record_index(text: bytes):
     """generate_sequence_index.pl restated: [(offset, name)] in file order."""
     L = lib()

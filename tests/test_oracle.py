@@ -66,3 +66,16 @@ def test_reverse_complement_strand(oracle_mod):
     rev = compile_pattern(convert("-c", convert("-n", "TATAWAWR")))
     assert oracle_mod.scan(text, fwd) == []
     assert oracle_mod.scan(text, rev) == [(14, 22)]     # CTTTTATA = revcomp of TATAAAAG
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_oracle_threaded_scan_matches_serial(oracle_mod, threads):
+    """The bench's multi-threaded CPU baseline (records split across host
+    threads) returns exactly the serial scan's hits, header filter included."""
+    text = dna_fasta(77, n_records=400, min_len=2000, max_len=6000)
+    assert len(text) >= (1 << 20)
+    for p, k in [("(GAATTC)", 0), ("(TATA[AT]A[AT][AG])", 1), ("(AC|GT.)", 0)]:
+        prog = compile_pattern(p)
+        want = oracle_mod.scan(text, prog, k, "s", skip_headers=True)
+        got = oracle_mod.scan_threads(text, prog, k, "s", skip_headers=True, threads=threads)
+        assert got == want, (p, k, threads)

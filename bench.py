@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
-ROUND = "r01c"
+ROUND = "r01c"   # committed PMC traffic run (profiles/r01c_traffic.json)
 
 
 def parse_args():
@@ -100,12 +100,13 @@ def cpu_threads_default():
 
 def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads):
     """Oracle on the first `sample_bp` positions over `threads` host threads
-    (the sample is cut at record starts); returns (dict, parity_ok)."""
+    (the sample is cut at line breaks); returns (dict, parity_ok)."""
     from oracle import oracle
     text = db.decode(0, int(sample_bp))
-    t0 = time.perf_counter()
+    t0, c0 = time.perf_counter(), time.process_time()
     want = [oracle.scan_threads(text, p, k, "s", skip_headers=True, threads=threads) for p in progs]
     dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0
     bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
     ok = True
     keys, lens = gpu_hits
@@ -117,8 +118,9 @@ def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads):
         ok &= got == w
     return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
             "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, "
-                      "oracle/pm_oracle.c on %d host threads (records split across threads), "
-                      "%.1f s wall" % (sample_bp / 1e6, threads, dt)}, ok
+                      "oracle/pm_oracle.c on %d host threads (text cut at line breaks), "
+                      "%.1f s wall, %.1f s CPU, %d CPUs in the affinity mask"
+                      % (sample_bp / 1e6, threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok
 
 
 def main():

@@ -105,8 +105,10 @@ def scan(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool =
 
 def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
                  threads: int = 1):
-    """``scan`` over ``threads`` host threads: the text is cut at record starts
-    (a hit never spans a record), each piece is scanned by
+    """``scan`` over ``threads`` host threads: the text is cut after line
+    breaks (no hit spans a '\\n'; header lines stay whole, so
+    the header filter is unchanged -- and a database decoded from HBM renders
+    headers as '\\n' bytes, so it has no '>' to cut at), each piece is scanned by
     ``pmo_scan`` (ctypes releases the GIL) and the hits are shifted back to
     file offsets.  Same output as ``scan``; used for the bench's CPU baseline."""
     if threads <= 1 or len(text) < (1 << 20):
@@ -115,7 +117,7 @@ def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers
     cuts = [0]
     step = len(text) // threads
     for t in range(1, threads):
-        c = text.find(b"\n>", max(cuts[-1], t * step))
+        c = text.find(b"\n", max(cuts[-1], t * step))
         if c < 0:
             break
         if c + 1 > cuts[-1]:

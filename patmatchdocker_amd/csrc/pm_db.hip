@@ -365,6 +365,10 @@ void lane_begin(pm_db* db) {
 }
 
 void lane_end(pm_db* db, hipStream_t s) {
+    // while every scan of this database ran on its own stream (no post
+    // stream yet), stream order already serializes the lane's users: no
+    // marker packet between one scan's sort and the next scan's kernel
+    if (!db->post && s == db->stream) return;
     if (!db->free_ev) HIPCHK(hipEventCreateWithFlags(&db->free_ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(db->free_ev, s));
 }

@@ -63,10 +63,9 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
                                                    uint32_t nbins = 0) {
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
-    if (counts_host && bin == nbins) {   // one extra block: the pipelined scan's count readback (mapped host memory)
+    if (counts_host && bin == 0) {   // the pipelined scan's count readback (mapped host memory)
         for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
         __threadfence_system();
-        return;
     }
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0 || c > LDS_SORT_CAP) return;   // (a speculative sort's caller redoes such lists)
@@ -76,13 +75,11 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
     } else {   // few bins: the block sums the counts before it (no offsets pass)
         uint64_t acc = 0;
         for (uint32_t b = threadIdx.x; b < bin; b += blockDim.x) acc += min(cnt[b], sh.cap(b));
-        s[threadIdx.x] = acc;
+        for (int d2 = 32; d2 > 0; d2 >>= 1) acc += __shfl_xor(acc, d2, 64);   // wave sum
+        if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
         __syncthreads();
-        for (uint32_t d2 = blockDim.x / 2; d2 > 0; d2 >>= 1) {
-            if (threadIdx.x < d2) s[threadIdx.x] += s[threadIdx.x + d2];
-            __syncthreads();
-        }
-        base = s[0];
+        base = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; ++w) base += s[w];
         __syncthreads();
     }
     const uint64_t* src = sh.src(out, bin);
@@ -93,6 +90,25 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
     }
     if (c == 1) {
         if (threadIdx.x == 0) d[0] = src[0];
+        return;
+    }
+    if (c <= blockDim.x) {
+        // small bin (the common case: ~100 keys): rank sort -- every thread
+        // counts the keys before its own (LDS broadcast reads, ties broken by
+        // index) and stores its key at that rank; one barrier instead of the
+        // bitonic network's log^2 rounds
+        const uint32_t i = threadIdx.x;
+        uint64_t mine = 0;
+        if (i < c) s[i] = mine = src[i];
+        __syncthreads();
+        if (i < c) {
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < c; ++j) {
+                const uint64_t v = s[j];
+                r += (v < mine) | ((v == mine) & (j < i));
+            }
+            d[r] = mine;
+        }
         return;
     }
     uint32_t n2 = 2;
@@ -327,7 +343,7 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins + (counts_host ? 1 : 0)), dim3(256), 0, stream, sb.out,
+        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
                            sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
         HIPCHK(hipGetLastError());
     } catch (...) {

@@ -98,7 +98,7 @@ constexpr int MAX_WINDOW = HALO;                     // longest linear pattern (
 constexpr uint32_t NBINS = 1024;                     // hit bins (at least)
 constexpr uint32_t MAX_BINS = 8192;
 constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_nfa_rev
-constexpr uint32_t LDS_SORT_CAP = 4096;              // keys per bin sorted in LDS (32 KB)
+constexpr uint32_t LDS_SORT_CAP = 2048;              // keys per bin sorted in LDS (16 KB: 8 sort blocks per CU)
 constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
 
 __host__ __device__ inline uint8_t fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }

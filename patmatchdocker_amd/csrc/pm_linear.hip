@@ -234,15 +234,21 @@ struct ExpandArgs {
     uint32_t nwg, nout, group, tiles_per_wg;
 };
 
-constexpr int EXPAND_THREADS = 1024;
+// One block per output segment (`group` workgroups x 4 wave segments); each
+// wave segment is expanded by SEG_LANES lanes (a segment holds a few records:
+// ~7 at the bench's density), so all 32 segments of a block are in flight at
+// once and 4 blocks fit a CU -- the whole grid is resident in one round and a
+// block's latency is one chain of loads (count, records, lane flags).
+constexpr int EXPAND_THREADS = 512;
+constexpr uint32_t SEG_LANES = 16;
 
 __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) {
     __shared__ uint32_t cnt_p[JIT_MAX_P];
-    const uint32_t og = blockIdx.x, wave = threadIdx.x >> 6, lane_t = threadIdx.x & 63;
+    const uint32_t og = blockIdx.x, sub = threadIdx.x / SEG_LANES, lane_t = threadIdx.x % SEG_LANES;
     if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * 4;
-    for (uint32_t q = wave; q < pairs; q += EXPAND_THREADS / 64) {
+    for (uint32_t q = sub; q < pairs; q += EXPAND_THREADS / SEG_LANES) {
         const uint32_t wg = wg0 + q / 4, part = q % 4;
         const uint32_t seg = wg * 4 + part;
         uint32_t cnt = a.rec_cnt[seg];
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
             if (lane_t == 0) atomicMax(a.rec_over, cnt);
             cnt = a.rcap;
         }
-        for (uint32_t i = lane_t; i < cnt; i += 64) {
+        for (uint32_t i = lane_t; i < cnt; i += SEG_LANES) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
             const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 12);
             const uint32_t lane = (r.x >> 6) & 63, s = (r.x >> 3) & 7, p = r.x & 7;
@@ -1010,8 +1016,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
                     spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h,
                                                  xs);
-                    HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
-                    HIPCHK(hipEventRecord(pd->counted, xs));
+                    // on the db stream the list's own ready event (hits_ready,
+                    // below) marks the same point: no second marker packet
+                    if (xs != s) {
+                        HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
+                        HIPCHK(hipEventRecord(pd->counted, xs));
+                    }
                     pd->jev = std::move(jev);
                     pd->hint_key = cap_key;
                     pd->slot_caps = slot_caps;
@@ -1134,7 +1144,7 @@ void hits_finalize(pm_hits* h) {
     pm_db* db = pd->db;
     db->pending.erase(h);
     DeviceGuard g(h->device);
-    HIPCHK(hipEventSynchronize(pd->counted));
+    HIPCHK(hipEventSynchronize(pd->counted ? pd->counted : h->ready));
     uint64_t total = 0;
     uint32_t maxc = 0;
     bool overflow = false;

@@ -79,3 +79,12 @@ def test_oracle_threaded_scan_matches_serial(oracle_mod, threads):
         want = oracle_mod.scan(text, prog, k, "s", skip_headers=True)
         got = oracle_mod.scan_threads(text, prog, k, "s", skip_headers=True, threads=threads)
         assert got == want, (p, k, threads)
+
+
+def test_oracle_threaded_scan_on_decoded_layout(oracle_mod):
+    """Cuts at line breaks also split a text without '>' (a database decoded
+    from HBM renders header bytes as '\\n'), and hits stay identical."""
+    text = dna_fasta(78, n_records=300, min_len=3000, max_len=8000).replace(b">", b"\n")
+    prog = compile_pattern("(TATA[AT]A[AT][AG])")
+    want = oracle_mod.scan(text, prog, 1, "s")
+    assert oracle_mod.scan_threads(text, prog, 1, "s", threads=8) == want

@@ -9,6 +9,7 @@
 // workgroup and written at its exclusive offset, which yields the same
 // order as the reference's concatenated runs without a global sort.  Bins
 // too large for LDS fall back to a device radix sort of everything.
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <map>
@@ -343,8 +344,17 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
-                           sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
+        if (counts_host) {
+            // pipelined scan: the list's ready event is bound to the sort's
+            // own dispatch (no marker packet before the next scan's kernel)
+            HIPCHK(hipEventCreate(&h->ready));
+            hipExtLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, nullptr, h->ready, 0u, sb.out,
+                                  sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
+                                  sb.nbins);
+        } else {
+            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
+                               sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
+        }
         HIPCHK(hipGetLastError());
     } catch (...) {
         discard_hits(h);

@@ -33,6 +33,8 @@
 #include <mutex>
 #include <sstream>
 
+#include <hip/hip_ext.h>
+
 #include "pm_internal.h"
 
 namespace pm {
@@ -984,9 +986,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
                     jev.emplace_back(new EventPair());
-                    HIPCHK(hipEventRecord(jev.back()->a, s));
-                    HIPCHK(hipModuleLaunchKernel(ch.jit, (uint32_t)nwg, 1, 1, 256, 1, 1, 0, s, params, nullptr));
-                    HIPCHK(hipEventRecord(jev.back()->b, s));
+                    // the events take the dispatch's own start/end timestamps
+                    // (no marker packets around the launch; sizes in threads)
+                    HIPCHK(hipExtModuleLaunchKernel(ch.jit, (uint32_t)nwg * 256u, 1, 1, 256, 1, 1, 0, s, params,
+                                                    nullptr, jev.back()->a, jev.back()->b, 0));
                     if (xs != s) HIPCHK(hipStreamWaitEvent(xs, jev.back()->b, 0));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
@@ -1016,8 +1019,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
                     spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h,
                                                  xs);
-                    // on the db stream the list's own ready event (hits_ready,
-                    // below) marks the same point: no second marker packet
+                    // on the db stream the list's own ready event (bound to
+                    // the sort's dispatch) marks the same point
                     if (xs != s) {
                         HIPCHK(hipEventCreateWithFlags(&pd->counted, hipEventDisableTiming));
                         HIPCHK(hipEventRecord(pd->counted, xs));
@@ -1034,13 +1037,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->class_acgt.assign(class_acgt, class_acgt + n_classes);
                     pd->class_is_any.assign(class_is_any, class_is_any + n_classes);
                     pd->class_bytes.assign(class_bytes, class_bytes + (size_t)8 * n_classes);
-                    if (xs == s) {
-                        hits_ready(db, spec);
-                    } else {   // the list and the lane's last reader are on the post stream
-                        HIPCHK(hipEventCreateWithFlags(&spec->ready, hipEventDisableTiming));
-                        HIPCHK(hipEventRecord(spec->ready, xs));
-                        lane_end(db, xs);
-                    }
+                    // spec->ready is bound to the sort's dispatch on xs (the
+                    // lane's last reader too)
+                    lane_end(db, xs);
                     spec->pending = pd.release();
                     db->pending.insert(spec);
                     *out = spec;

@@ -386,3 +386,23 @@ def test_pipelined_scans_match_synchronous(engine, oracle_mod, monkeypatch):
         got = _hits_pairs(engine._collect(h), len(progs))
         for prog, g in zip(progs, got):
             assert g == _oracle_hits(oracle_mod, text, prog, 2), prog.source
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_sort_regimes_around_thresholds(engine, oracle_mod, monkeypatch, pipelined):
+    """Hit bins of every size class of the collection path, vs the oracle:
+    ~128 keys (rank sort), ~256 (the rank/bitonic boundary), ~512 (bitonic),
+    ~2,048 (the LDS capacity boundary) and ~8,192 (radix sort) per bin, on
+    a database whose bins cover ~8 stream tiles, synchronous and pipelined."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = dna_fasta(907, n_records=4, min_len=250000, max_len=300000, width=None)
+    progs = [compile_pattern(convert("-n", p)) for p in ["ACGTAC", "ACGTAS", "ACGTA", "ACGT", "ACG"]]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for k in (0, 1):
+            batch = engine.LinearBatch(progs)
+            got = _hits_pairs(engine._collect(batch.launch(db, k, pipelined=pipelined)), len(progs))
+            for prog, g in zip(progs, got):
+                assert g == _oracle_hits(oracle_mod, text, prog, k), (prog.source, k)
+    finally:
+        db.close()

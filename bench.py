@@ -104,7 +104,7 @@ def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads):
     from oracle import oracle
     text = db.decode(0, int(sample_bp))
     t0, c0 = time.perf_counter(), time.process_time()
-    want = [oracle.scan_threads(text, p, k, "s", skip_headers=True, threads=threads) for p in progs]
+    want = [oracle.scan_threads(text, p, k, "s", skip_headers=True, threads=threads, report="nrgrep") for p in progs]
     dt = time.perf_counter() - t0
     cpu_s = time.process_time() - c0
     bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")

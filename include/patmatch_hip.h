@@ -63,20 +63,40 @@ int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet,
 /* Decode positions [beg, beg+len) back to folded text (bench/debug). */
 int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
 
+/* --- what a scan reports (the `flags` argument) ---------------------------
+ * The kernels find candidates: every start with a match.  nrgrep_coords
+ * prints a subset (from the binary's own code): the scan of a
+ * region [R, end of text) returns the first match it finds, prints it and
+ * resumes at the match's end (record.c recSearchFile), so reported matches
+ * never overlap.  PM_REPORT_NRGREP applies that selection (the drop-in
+ * behaviour); PM_REPORT_ALL keeps every candidate.  A pattern whose first
+ * character was '^' / last was '$' is searched with the anchor stripped
+ * and PM_ANCHOR_START / PM_ANCHOR_END set (nrgrep main(): OptStartLine /
+ * OptEndLine): the match must start at a line start or where the previous
+ * report ended / end at a line end.  Hits starting on a header line are
+ * never returned (process_output discards them, patmatch.py:548).      */
+#define PM_REPORT_ALL 0
+#define PM_REPORT_NRGREP 1
+#define PM_ANCHOR_START 2
+#define PM_ANCHOR_END 4
+
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched
  * with at most k substitutions.  The classes are numbered 0..n_classes-1:
  *   class_acgt[c]     4-bit subset of {A,C,G,T} (bit0=A .. bit3=T)
  *   class_bytes[8*c]  256-bit membership over folded bytes (for non-ACGT
  *                     text bytes such as N)
- *   class_is_any[c]   1 if the class is '.' (matches every non-break byte)
+ *   class_is_any[c]   1 if the class is '.' (accepts every byte)
  * pos_class[64*p + j] is the class of position j of pattern p, lengths[p]
  * its length (1..64).  Hits are (pattern, beg) with end = beg + lengths[p].
+ * k = 0 is nrgrep's "simple" engine: a window is checked against the whole
+ * text, so with a class that accepts '\n' ('.', '[^..]', '#') a match may
+ * span a line break; k > 0 ("esimple") matches stay inside one line.
  * Replaces one nrgrep_coords run per pattern (per strand).              */
 int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths,
                    const uint8_t* pos_class, int n_classes, const uint8_t* class_acgt,
                    const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                   pm_hits** out);
+                   int flags, pm_hits** out);
 
 /* pm_scan_linear without a host synchronization: launches the scan and
  * returns a hit list that resolves on first use (pm_hits_count, _copy*,
@@ -89,7 +109,7 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths,
 int pm_scan_linear_async(pm_db* db, int n_patterns, const int32_t* lengths,
                          const uint8_t* pos_class, int n_classes, const uint8_t* class_acgt,
                          const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                         pm_hits** out);
+                         int flags, pm_hits** out);
 
 /* Generates and compiles (hipRTC, gfx950) the pattern-specialized linear
  * kernel for up to 8 patterns without launching it: a host-only check that
@@ -102,8 +122,9 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
  * m positions (1..64); byte_mask[256] = positions accepting each folded
  * byte; follow[m] / first / last as produced by regex.py; max_len = the
  * longest match, 0 = unbounded (`*`, `+`: a match may run to the end of
- * its record).  Reports, for every start with a match of <= k
- * substitutions, the shortest end.  Hits carry pattern id `pattern_id`. */
+ * its record).  Candidates: for every start with a match of <= k
+ * substitutions, the shortest end; reported as PM_REPORT_NRGREP selects.
+ * Hits carry pattern id `pattern_id`. */
 int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
                 uint64_t first, uint64_t last, int max_len, int k, int pattern_id,
                 pm_hits** out);
@@ -122,7 +143,7 @@ int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* fol
  * PM_ERR_SUB, ...). */
 int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
                      uint64_t first, uint64_t last, int max_len, int min_len, int k, int errs,
-                     int pattern_id, pm_hits** out);
+                     int pattern_id, int flags, pm_hits** out);
 
 /* --- hits --------------------------------------------------------------- */
 int pm_hits_count(const pm_hits* h, uint64_t* count);

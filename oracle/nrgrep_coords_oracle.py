@@ -2,7 +2,10 @@
 """CPU oracle behind an nrgrep_coords-style command line.  TEST INFRASTRUCTURE
 ONLY: used by tests/golden/make_e2e.py to run the reference's own Python
 pipeline (www/FlaskApp/FlaskApp/patmatch.py run_test) with this oracle in
-place of the prebuilt binary.  Prints "[beg, end]: match" lines."""
+place of the prebuilt binary.  Prints what the binary prints:
+the engine banner searchPreproc puts() ("SIMPLE search", ...), then one
+"[beg, end]: match" line per reported match (record.c 0x402327-0x402383;
+the output separator OptRecSep defaults to "" at 0x41cdd5)."""
 import argparse
 import os
 import sys
@@ -10,7 +13,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from oracle import oracle  # noqa: E402
-from patmatchdocker_amd.regex import RegexSyntaxError, compile_pattern  # noqa: E402
+from patmatchdocker_amd.regex import RegexSyntaxError, compile_pattern, engine_banner  # noqa: E402
 
 
 def main():
@@ -28,9 +31,10 @@ def main():
     except RegexSyntaxError:
         print("Syntax error in pattern %s" % a.pattern, file=sys.stderr)
         return 1
+    print(engine_banner(prog, k))
     for path in a.files:
         text = open(path, "rb").read()
-        for b, e in oracle.scan(text, prog, k, types):
+        for b, e in oracle.scan_reported(text, prog, k, types):
             sys.stdout.write("[%d, %d]: %s\n" % (b, e, text[b:e].decode("latin-1")))
     return 0
 

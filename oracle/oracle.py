@@ -41,6 +41,10 @@ def lib():
         _LIB.pmo_scan.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_uint64,
                                   ctypes.c_uint64, pu64, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmo_scan2.restype = ctypes.c_int64
+        _LIB.pmo_scan2.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_uint64,
+                                   ctypes.c_uint64, pu64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -63,8 +67,9 @@ def header_spans(text: bytes):
 
 
 def drop_header_hits(text: bytes, hits):
-    """Remove hits starting inside a header line: process_output discards them
-    (patmatch.py:548-550, records whose name starts with '>')."""
+    """Remove hits starting on a header line, its terminating '\n' included:
+    process_output maps such a start to the '>name' record offset
+    (get_name_offset, patmatch.py:214-238) and discards it (:548-550)."""
     spans = header_spans(text)
     if not spans:
         return hits
@@ -73,10 +78,56 @@ def drop_header_hits(text: bytes, hits):
     out = []
     for beg, end in hits:
         i = bisect.bisect_right(starts, beg) - 1
-        if i >= 0 and spans[i][0] <= beg < spans[i][1]:
+        if i >= 0 and spans[i][0] <= beg <= spans[i][1]:
             continue
         out.append((beg, end))
     return out
+
+
+PMO_NRGREP, PMO_START, PMO_END, PMO_SIMPLE = 1, 2, 4, 8
+
+
+def mode_of(prog, k: int, report: str = "nrgrep", simple=None) -> int:
+    """pmo_scan2 mode bits for a compiled program: nrgrep's engine choice
+    (simple = k 0 + class sequence, searchPreproc 0x402660), the anchors and
+    the report rule."""
+    m = PMO_NRGREP if report == "nrgrep" else 0
+    if prog.anchor_start:
+        m |= PMO_START
+    if prog.anchor_end:
+        m |= PMO_END
+    if (k == 0 and prog.linear) if simple is None else simple:
+        m |= PMO_SIMPLE
+    return m
+
+
+def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
+                  report: str = "nrgrep", simple=None):
+    """What ``nrgrep_coords`` prints for ``prog`` (pmo_scan2): the candidates
+    of ``scan`` (or the simple engine's whole-text windows at k = 0) reduced
+    by the binary's report rule -- first found wins, the scan resumes at the
+    match end -- and its '^'/'$' checks; ``skip_headers`` then drops the
+    header-line hits process_output throws away.  ``simple`` overrides the
+    engine choice (False: line-bounded windows even at k = 0)."""
+    L = lib()
+    B = np.array(prog.byte_masks(), dtype=np.uint64)
+    F = np.array(prog.follow + [0], dtype=np.uint64)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = L.pmo_scan2(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                        prog.first, prog.last, F.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                        prog.m, k, err_flags(types) if k else 0, 1 if prog.ignore_case else 0,
+                        mode_of(prog, k, report, simple),
+                        beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                        end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("oracle rejected k=%d" % k)
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
 
 
 def scan(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False):
@@ -104,15 +155,21 @@ def scan(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool =
 
 
 def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
-                 threads: int = 1):
+                 threads: int = 1, report: str = None):
     """``scan`` over ``threads`` host threads: the text is cut after line
     breaks (no hit spans a '\\n'; header lines stay whole, so
     the header filter is unchanged -- and a database decoded from HBM renders
     headers as '\\n' bytes, so it has no '>' to cut at), each piece is scanned by
     ``pmo_scan`` (ctypes releases the GIL) and the hits are shifted back to
     file offsets.  Same output as ``scan``; used for the bench's CPU baseline."""
-    if threads <= 1 or len(text) < (1 << 20):
-        return scan(text, prog, k, types, skip_headers)
+    def one_piece(t):
+        if report is None:
+            return scan(t, prog, k, types, skip_headers)
+        return scan_reported(t, prog, k, types, skip_headers, report)
+    # the simple engine's windows may span a line break: no cut is safe
+    cross = report is not None and k == 0 and prog.linear and any(10 in c for c in prog.classes)
+    if threads <= 1 or len(text) < (1 << 20) or cross or prog.anchor_start:
+        return one_piece(text)
     from concurrent.futures import ThreadPoolExecutor
     cuts = [0]
     step = len(text) // threads
@@ -127,7 +184,7 @@ def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers
 
     def one(span):
         a, b = span
-        return [(x + a, y + a) for x, y in scan(text[a:b], prog, k, types, skip_headers)]
+        return [(x + a, y + a) for x, y in one_piece(text[a:b])]
 
     with ThreadPoolExecutor(max_workers=len(pieces)) as ex:
         parts = list(ex.map(one, pieces))

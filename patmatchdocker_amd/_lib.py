@@ -18,6 +18,7 @@ PM_ALPHA_BYTE = 1
 PM_E_UNSUPPORTED = -4
 PM_MAX_K = 3
 PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
+PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END = 0, 1, 2, 4
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -60,12 +61,12 @@ def _declare(lib):
     lib.pm_db_destroy.argtypes = [P]
     lib.pm_db_info.argtypes = [P, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
     lib.pm_db_decode.argtypes = [P, u64, ctypes.c_uint32, ctypes.c_char_p]
-    lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, PP]
+    lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_scan_linear_async.argtypes = lib.pm_scan_linear.argtypes
     lib.pm_scan_nfa.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, PP]
     lib.pm_scan_nfa_errs.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                     ctypes.c_int, ctypes.c_int, PP]
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_hits_count.argtypes = [P, pu64]
     lib.pm_hits_copy.argtypes = [P, P, P, P, u64]
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]

@@ -138,12 +138,33 @@ __global__ void k_sb_flags(const uint2* __restrict__ bo, uint64_t nsb, uint32_t*
     sbcnt[s] = __popc(f);
 }
 
+// byte p of the synthetic FASTA text (k_pack_synth): ">r%08u\n" header
+// lines (record index, 0-based), rec_len bases, "\n"; folded like every
+// stored byte.  Only header and '\n' positions are asked for.
+__device__ inline uint8_t synth_byte(uint64_t p, uint64_t rec_len) {
+    const uint64_t stride = SYN_HDR + 1 + rec_len + 1;
+    const uint64_t r = p / stride, q = p % stride;
+    if (q == 0) return (uint8_t)'>';
+    if (q == 1) return (uint8_t)'R';
+    if (q < SYN_HDR) {
+        uint64_t v = r % 100000000ull;
+        for (uint64_t d = q; d < SYN_HDR - 1; ++d) v /= 10;
+        return (uint8_t)('0' + v % 10);
+    }
+    return (uint8_t)'\n';
+}
+
+// Side tables of every flagged word: the break / other masks, the physical
+// word, and the raw (folded) byte of each of its exception positions --
+// header-line bytes and '\n' included, so the simple engine's windows that
+// span a line break (k_linear_others) and the '^'/'$' checks see the file's
+// own bytes.  Positions past the end of the file store 0.
 __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, uint64_t nwords,
                                   const uint2* __restrict__ bo,
                                   const uint32_t* __restrict__ sbflag, const uint32_t* __restrict__ sbbase,
                                   uint32_t* __restrict__ xbrk, uint32_t* __restrict__ xoth,
                                   uint64_t* __restrict__ xword, uint8_t* __restrict__ xbytes,
-                                  uint32_t* __restrict__ n_oth_words) {
+                                  uint32_t* __restrict__ n_oth_words, uint64_t syn_rec_len) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (w >= nwords) return;
     const uint32_t f = sbflag[w >> 5];
@@ -160,8 +181,8 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
     const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
     for (uint32_t i = 0; i < 32; ++i) {
         const uint64_t p = pos_of(t, lw, i);
-        uint8_t c = '\n';
-        if (((ot >> i) & 1) && raw != nullptr && p < n) c = fold(raw[p]);
+        uint8_t c = 0;
+        if ((((br | ot) >> i) & 1) && p < n) c = raw != nullptr ? fold(raw[p]) : synth_byte(p, syn_rec_len);
         xbytes[idx * 32 + i] = c;
     }
 }
@@ -205,7 +226,7 @@ __global__ void k_mark_ranges_bytes(const uint64_t* __restrict__ ranges, uint64_
 
 __global__ void k_decode(NucView v, uint64_t beg, uint32_t len, uint8_t* out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < len) out[i] = nuc_char_at(v, beg + i);
+    if (i < len) out[i] = nuc_raw_at(v, beg + i);
 }
 
 // ---------------------------------------------------------------------------
@@ -265,7 +286,7 @@ void alloc_planes(pm_db* db) {
 }
 
 // halo words, flags, compacted exception side tables, lane flags
-void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw) {
+void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint64_t syn_rec_len = 0) {
     hipStream_t s = db->stream;
     hipLaunchKernelGGL(k_clean_oth, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, db->nwords, db->bo);
     HIPCHK(hipGetLastError());
@@ -295,7 +316,7 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw) {
     HIPCHK(hipMemsetAsync(d_noth, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_fill_exceptions, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, d_raw, db->n,
                        db->nwords, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword,
-                       db->xbytes, d_noth);
+                       db->xbytes, d_noth, syn_rec_len);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h, d_noth, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -334,12 +355,12 @@ void free_db(pm_db* db) {
         (void)hipStreamDestroy(db->post);
     }
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->bytes, db->ws_post.p};
+                    db->lflag, db->bytes, db->bytes_raw, db->ws_post.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
     for (pm_lane* l : {static_cast<pm_lane*>(db), &db->alt}) {
-        for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p})
+        for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p, l->ws_rep.p})
             if (p) (void)hipFree(p);
         for (void* p : {l->pin_up.p, l->pin_slots.p})
             if (p) (void)hipHostFree(p);
@@ -482,6 +503,10 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
             hipLaunchKernelGGL(k_pack_bytes, dim3(blocks_for(db->nbytes_alloc, 256)), dim3(256), 0, s, d_raw, n,
                                db->nbytes_alloc, db->bytes);
             HIPCHK(hipGetLastError());
+            // the file's own bytes (headers kept): nrgrep's simple engine may
+            // match across a line break, and '^'/'$' look at real bytes
+            db->bytes_raw = dalloc<uint8_t>(db, db->nbytes_alloc);
+            HIPCHK(hipMemcpyAsync(db->bytes_raw, db->bytes, db->nbytes_alloc, hipMemcpyDeviceToDevice, s));
             if (nr) {
                 hipLaunchKernelGGL(k_mark_ranges_bytes, dim3((uint32_t)nr), dim3(256), 0, s, d_ranges, nr, db->bytes);
                 HIPCHK(hipGetLastError());
@@ -516,7 +541,7 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         hipLaunchKernelGGL(k_pack_synth, dim3(blocks_for(db->ntiles * STREAM, 256)), dim3(256), 0, db->stream,
                            db->n, db->ntiles, rec_len, seed, db->hl, db->bo);
         HIPCHK(hipGetLastError());
-        finish_nuc(db, owned, nullptr);
+        finish_nuc(db, owned, nullptr, rec_len);
         free_all(db, owned);
         *out = db;
     });

@@ -61,12 +61,21 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
                                                    const uint64_t* __restrict__ off, BinShape sh,
                                                    uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
                                                    uint32_t* __restrict__ lens, uint32_t* counts_host = nullptr,
-                                                   uint32_t nbins = 0) {
+                                                   uint32_t nbins = 0, uint64_t* total_out = nullptr) {
     __shared__ uint64_t s[LDS_SORT_CAP];
     const uint32_t bin = blockIdx.x;
     if (counts_host && bin == 0) {   // the pipelined scan's count readback (mapped host memory)
         for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
         __threadfence_system();
+    }
+    if (total_out && bin == 0) {     // list length for the report pass (device-side count)
+        uint64_t acc = 0;
+        for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) acc += min(cnt[b], sh.cap(b));
+        for (int d2 = 32; d2 > 0; d2 >>= 1) acc += __shfl_xor(acc, d2, 64);
+        __shared__ uint64_t wsum[4];
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) *total_out = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0 || c > LDS_SORT_CAP) return;   // (a speculative sort's caller redoes such lists)
@@ -334,7 +343,7 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
 }
 
 pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host,
-                               hipStream_t stream) {
+                               hipStream_t stream, uint64_t* total_out, bool bind_ready) {
     require(sb.nbins <= 4096, "internal: speculative sort needs <= 4096 bins");
     uint64_t cap_total = 0;
     for (uint32_t c : sb.slot_cap_h) cap_total += (uint64_t)c * sb.bins_per_pattern;
@@ -344,16 +353,17 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        if (counts_host) {
+        if (counts_host && bind_ready) {
             // pipelined scan: the list's ready event is bound to the sort's
             // own dispatch (no marker packet before the next scan's kernel)
             HIPCHK(hipEventCreate(&h->ready));
             hipExtLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, nullptr, h->ready, 0u, sb.out,
                                   sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
-                                  sb.nbins);
+                                  sb.nbins, total_out);
         } else {
             hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
-                               sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host, sb.nbins);
+                               sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host,
+                               (counts_host || total_out) ? sb.nbins : 0u, total_out);
         }
         HIPCHK(hipGetLastError());
     } catch (...) {
@@ -422,6 +432,319 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         throw;
     }
     return h;
+}
+
+// ---------------------------------------------------------------------------
+// nrgrep report selection (see pm_internal.h and DESIGN.md §1)
+// ---------------------------------------------------------------------------
+// Input: a (pattern, beg)-sorted candidate list with match lengths.  Output:
+// what nrgrep_coords prints, per pattern: scanning from R = 0, the first
+// candidate with beg >= R is reported and R becomes its end.  Parallel form:
+// candidate i is a "head" when its key is >= the running maximum of
+// (pattern, end) over every earlier candidate -- whatever was reported
+// before it ended at or before its start, so it is reported; the head's
+// thread then walks its cluster (the candidates up to the next head)
+// sequentially.  Clusters are short (overlapping matches), so the walk is
+// cheap; the running maximum comes from per-chunk maxima (k_rep_max) and an
+// in-block scan.  With '^' the acceptance of a candidate depends on where
+// the previous report ended (a start equal to R passes the check, 0x402182)
+// so one thread walks each list sequentially (anchored queries only).
+namespace {
+
+constexpr uint32_t REP_G = 512;           // chunks (blocks) of the list
+constexpr uint32_t REP_T = 256;           // threads per block
+constexpr uint64_t POS_MASK = (1ull << 48) - 1;
+
+__device__ inline uint8_t tv_raw(const TextView& tv, uint64_t p) {
+    return tv.nuc_layout ? nuc_raw_at(tv.nuc, p) : tv.raw[p];
+}
+__device__ inline bool tv_header(const TextView& tv, uint64_t p) {
+    return tv.nuc_layout ? nuc_is_header(tv.nuc, p) : (tv.bytes[p] == (uint8_t)'\n' && tv.raw[p] != (uint8_t)'\n');
+}
+
+struct RepArgs {
+    const uint64_t* keys;
+    const uint32_t* lens;
+    uint64_t* okeys;
+    uint32_t* olens;
+    uint8_t* acc;
+    uint64_t* bmax;
+    uint32_t* bcnt;
+    const uint64_t* total_d;
+    uint64_t total_h;
+    uint32_t* count;
+    uint32_t* host_count;
+    TextView tv;
+    uint32_t flags;
+};
+
+__device__ inline uint64_t rep_total(const RepArgs& a) { return a.total_d ? *a.total_d : a.total_h; }
+__device__ inline uint64_t rep_chunk(uint64_t total) { return (total + REP_G - 1) / REP_G; }
+
+// '$': the match must end at a line end or at the end of the text (the
+// region end, recCheckRightContext 0x4021e0)
+__device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
+    if (len == 0) return false;   // a start whose verify found no (anchored) end
+    if (!(a.flags & PM_ANCHOR_END)) return true;
+    const uint64_t e = (key & POS_MASK) + len;
+    return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n';
+}
+__device__ inline uint64_t rep_val(uint64_t key, uint32_t len) { return key + len; }   // (pattern, end)
+
+__device__ inline uint64_t block_max(uint64_t v, uint64_t* red) {
+    for (int d = 32; d > 0; d >>= 1) v = max(v, (uint64_t)__shfl_xor(v, d, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t r = 0;
+    for (uint32_t w = 0; w < REP_T / 64; ++w) r = max(r, red[w]);
+    __syncthreads();
+    return r;
+}
+__device__ inline uint64_t block_sum(uint64_t v, uint64_t* red) {
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t r = 0;
+    for (uint32_t w = 0; w < REP_T / 64; ++w) r += red[w];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
+    __shared__ uint64_t red[REP_T / 64];
+    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    uint64_t m = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
+        const uint64_t key = a.keys[i];
+        const uint32_t len = a.lens[i];
+        if (rep_valid(a, key, len)) m = max(m, rep_val(key, len));
+    }
+    m = block_max(m, red);
+    if (threadIdx.x == 0) a.bmax[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
+    __shared__ uint64_t red[REP_T / 64];
+    __shared__ uint64_t scan[REP_T];
+    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    if (!(a.flags & PM_REPORT_NRGREP)) {   // every candidate: only the anchors filter
+        for (uint64_t i = blockIdx.x * (uint64_t)REP_T + threadIdx.x; i < total; i += (uint64_t)REP_G * REP_T) {
+            const uint64_t key = a.keys[i];
+            const uint64_t s = key & POS_MASK;
+            bool ok = rep_valid(a, key, a.lens[i]);
+            if (ok && (a.flags & PM_ANCHOR_START)) ok = s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n';
+            if (ok) a.acc[i] = 1;
+        }
+        return;
+    }
+    if (a.flags & PM_ANCHOR_START) {
+        if (blockIdx.x != 0 || threadIdx.x != 0) return;
+        uint64_t R = 0, pat = ~0ull;
+        for (uint64_t i = 0; i < total; ++i) {
+            const uint64_t key = a.keys[i];
+            const uint32_t len = a.lens[i];
+            if (!rep_valid(a, key, len)) continue;
+            if ((key >> 48) != pat) { pat = key >> 48; R = 0; }
+            const uint64_t s = key & POS_MASK;
+            if (s < R) continue;
+            if (s == R || s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n') {
+                a.acc[i] = 1;
+                R = s + len;
+            }
+        }
+        return;
+    }
+    // running maximum of every chunk before this one
+    uint64_t carry = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = max(carry, a.bmax[b]);
+    carry = block_max(carry, red);
+    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    for (uint64_t base = b0; base < b1; base += REP_T) {
+        const uint64_t i = base + threadIdx.x;
+        uint64_t key = 0, val = 0;
+        uint32_t len = 0;
+        bool valid = false;
+        if (i < b1) {
+            key = a.keys[i];
+            len = a.lens[i];
+            valid = rep_valid(a, key, len);
+            if (valid) val = rep_val(key, len);
+        }
+        scan[threadIdx.x] = val;
+        __syncthreads();
+        for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive max-scan
+            const uint64_t o = threadIdx.x >= d ? scan[threadIdx.x - d] : 0;
+            __syncthreads();
+            scan[threadIdx.x] = max(scan[threadIdx.x], o);
+            __syncthreads();
+        }
+        const uint64_t excl = max(carry, threadIdx.x ? scan[threadIdx.x - 1] : 0ull);
+        const uint64_t tile_max = scan[REP_T - 1];
+        __syncthreads();
+        carry = max(carry, tile_max);
+        if (!valid || key < excl) continue;   // not a head
+        // head: reported; walk its cluster
+        a.acc[i] = 1;
+        uint64_t R = (key & POS_MASK) + len, run = val;
+        for (uint64_t j = i + 1; j < total; ++j) {
+            const uint64_t kj = a.keys[j];
+            if (kj >= run) break;                    // the next head
+            const uint32_t lj = a.lens[j];
+            if (!rep_valid(a, kj, lj)) continue;
+            if ((kj & POS_MASK) >= R) {
+                a.acc[j] = 1;
+                R = (kj & POS_MASK) + lj;
+            }
+            run = max(run, rep_val(kj, lj));
+        }
+    }
+}
+
+// a start on a header line or on the '\n' that ends it maps to the '>name'
+// record in process_output (get_name_offset) and is discarded
+__device__ inline bool rep_keep(const RepArgs& a, uint64_t i) {
+    if (!a.acc[i]) return false;
+    const uint64_t s = a.keys[i] & POS_MASK;
+    if (tv_header(a.tv, s)) return false;
+    return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
+}
+
+__global__ __launch_bounds__(REP_T) void k_rep_count(RepArgs a) {
+    __shared__ uint64_t red[REP_T / 64];
+    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    uint64_t c = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) c += rep_keep(a, i) ? 1 : 0;
+    c = block_sum(c, red);
+    if (threadIdx.x == 0) a.bcnt[blockIdx.x] = (uint32_t)c;
+}
+
+__global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
+    __shared__ uint64_t red[REP_T / 64];
+    __shared__ uint32_t scan[REP_T];
+    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    uint64_t base_out = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) base_out += a.bcnt[b];
+    base_out = block_sum(base_out, red);
+    if (blockIdx.x == REP_G - 1 && threadIdx.x == 0) {
+        const uint32_t cnt = (uint32_t)(base_out + a.bcnt[blockIdx.x]);
+        *a.count = cnt;
+        if (a.host_count) {
+            *a.host_count = cnt;
+            __threadfence_system();
+        }
+    }
+    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    for (uint64_t base = b0; base < b1; base += REP_T) {
+        const uint64_t i = base + threadIdx.x;
+        const uint32_t keep = (i < b1 && rep_keep(a, i)) ? 1u : 0u;
+        scan[threadIdx.x] = keep;
+        __syncthreads();
+        for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive sum-scan
+            const uint32_t o = threadIdx.x >= d ? scan[threadIdx.x - d] : 0u;
+            __syncthreads();
+            scan[threadIdx.x] += o;
+            __syncthreads();
+        }
+        if (keep) {
+            const uint64_t o = base_out + scan[threadIdx.x] - 1;
+            a.okeys[o] = a.keys[i];
+            a.olens[o] = a.lens[i];
+        }
+        const uint32_t tile = scan[REP_T - 1];
+        __syncthreads();
+        base_out += tile;
+    }
+}
+
+// old key/len buffers of a hit list: recycled once the pass that reads them
+// has run (an event-tracked shell on the deferred list)
+void retire_buffers(pm_hits* h, hipStream_t s) {
+    pm_hits* old = new pm_hits();
+    old->device = h->device;
+    old->keys = h->keys;
+    old->lens = h->lens;
+    old->keys_cap = h->keys_cap;
+    old->lens_cap = h->lens_cap;
+    HIPCHK(hipEventCreateWithFlags(&old->ready, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(old->ready, s));
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_deferred.push_back(old);
+}
+
+}  // namespace
+
+TextView text_view(const pm_db* db) {
+    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0};
+}
+
+bool report_needed(uint32_t flags, bool cross) {
+    return (flags & (PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) || cross;
+}
+
+ReportWs report_ws(pm_db* db, uint64_t cap_items) {
+    Carve c;
+    const size_t o_t = c.take(8), o_c = c.take(8), o_m = c.take(REP_G * 8), o_b = c.take(REP_G * 4),
+                 o_a = c.take(std::max<uint64_t>(cap_items, 1));
+    uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_rep, c.off));
+    ReportWs ws;
+    ws.total = reinterpret_cast<uint64_t*>(d + o_t);
+    ws.count = reinterpret_cast<uint32_t*>(d + o_c);
+    ws.bmax = reinterpret_cast<uint64_t*>(d + o_m);
+    ws.bcnt = reinterpret_cast<uint32_t*>(d + o_b);
+    ws.acc = d + o_a;
+    ws.cap = std::max<uint64_t>(cap_items, 1);
+    return ws;
+}
+
+void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done) {
+    // acc is indexed below the list length, which never exceeds the
+    // capacity the workspace was sized for (the sort's slot capacities)
+    const uint64_t cap_items = std::min<uint64_t>(h->keys_cap / 8, ws.cap);
+    RepArgs a{};
+    a.keys = h->keys;
+    a.lens = h->lens;
+    size_t kc = 0, lc = 0;
+    a.okeys = static_cast<uint64_t*>(pool_get(h->device, h->keys_cap, &kc));
+    a.olens = static_cast<uint32_t*>(pool_get(h->device, h->lens_cap, &lc));
+    a.acc = ws.acc;
+    a.bmax = ws.bmax;
+    a.bcnt = ws.bcnt;
+    a.total_d = total_on_device ? ws.total : nullptr;
+    a.total_h = total_h;
+    a.count = ws.count;
+    a.host_count = host_count;
+    a.tv = text_view(db);
+    a.flags = flags;
+    HIPCHK(hipMemsetAsync(ws.acc, 0, cap_items, s));
+    hipLaunchKernelGGL(k_rep_max, dim3(REP_G), dim3(REP_T), 0, s, a);
+    hipLaunchKernelGGL(k_rep_walk, dim3(REP_G), dim3(REP_T), 0, s, a);
+    hipLaunchKernelGGL(k_rep_count, dim3(REP_G), dim3(REP_T), 0, s, a);
+    if (done)
+        hipExtLaunchKernelGGL(k_rep_scatter, dim3(REP_G), dim3(REP_T), 0, s, nullptr, done, 0u, a);
+    else
+        hipLaunchKernelGGL(k_rep_scatter, dim3(REP_G), dim3(REP_T), 0, s, a);
+    HIPCHK(hipGetLastError());
+    retire_buffers(h, s);
+    h->keys = a.okeys;
+    h->lens = a.olens;
+    h->keys_cap = kc;
+    h->lens_cap = lc;
+}
+
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total) {
+    if (total == 0) {
+        h->count = 0;
+        return;
+    }
+    const ReportWs ws = report_ws(db, h->keys_cap / 8);
+    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr);
+    uint32_t* hc = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
+    HIPCHK(hipMemcpyAsync(hc, ws.count, 4, hipMemcpyDeviceToHost, db->stream));
+    HIPCHK(hipStreamSynchronize(db->stream));
+    h->count = *hc;
 }
 
 }  // namespace pm

@@ -146,7 +146,32 @@ __device__ inline uint32_t exception_index(const uint32_t* sbflag, const uint32_
     return sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
 }
 
-// folded byte at file position p ('\n' for breaks and the tail padding)
+// the exact (folded) file byte at position p < n: breaks and "other" bytes
+// come from the side table (xbytes holds the raw byte of every flagged
+// position: header-line bytes, '\n', N, IUPAC letters, ...)
+__device__ inline uint8_t nuc_raw_at(const NucView& v, uint64_t p) {
+    const Loc l = loc_of(p);
+    const uint2 e = v.bo[l.word];
+    if (((e.x | e.y) >> l.bit) & 1) {
+        const uint32_t idx = exception_index(v.sbflag, v.sbbase, l.word);
+        return v.xbytes[(uint64_t)idx * 32 + l.bit];
+    }
+    const uint2 d = v.hl[l.word];
+    const uint32_t code = (((d.x >> l.bit) & 1) << 1) | ((d.y >> l.bit) & 1);
+    return (uint8_t)((0x54474341u >> (8 * code)) & 0xff);   // "ACGT"
+}
+
+// a header-line byte (/^>\S/ lines, generate_sequence_index.pl:33) -- a break
+// whose raw byte is not the delimiter
+__device__ inline bool nuc_is_header(const NucView& v, uint64_t p) {
+    const Loc l = loc_of(p);
+    if (!((v.bo[l.word].x >> l.bit) & 1)) return false;
+    const uint32_t idx = exception_index(v.sbflag, v.sbbase, l.word);
+    return v.xbytes[(uint64_t)idx * 32 + l.bit] != (uint8_t)'\n';
+}
+
+// folded byte at file position p as the line-bounded scans see it: '\n' for
+// every break (header bytes included) and the tail padding
 __device__ inline uint8_t nuc_char_at(const NucView& v, uint64_t p) {
     const Loc l = loc_of(p);
     const uint2 e = v.bo[l.word];
@@ -222,7 +247,7 @@ struct pm_hostbuf {      // pinned host staging buffer
 // after the last work that reads them (a scan waits for it on the GPU before
 // reusing the lane).  Never stream-ordered allocations.
 struct pm_lane {
-    pm_devbuf ws_tab, ws_sink, ws_rec;
+    pm_devbuf ws_tab, ws_sink, ws_rec, ws_rep;
     pm_hostbuf pin_up, pin_slots;
     // slot tables last uploaded into ws_sink (skip the copy when unchanged)
     void* slot_cache_p = nullptr;
@@ -252,7 +277,8 @@ struct pm_db : pm_lane {
     uint8_t* xbytes = nullptr;
     uint64_t* xword = nullptr;   // NUC: physical word of each flagged word
     uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
-    uint8_t* bytes = nullptr;    // BYTE alphabet
+    uint8_t* bytes = nullptr;    // BYTE alphabet: folded bytes, header lines stored as '\n'
+    uint8_t* bytes_raw = nullptr;   // BYTE alphabet: folded bytes as in the file (headers kept)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // synchronous-path workspaces
@@ -285,6 +311,8 @@ struct pm_pending {
     uint32_t rcap = 0;
     // the query itself, for the synchronous re-run
     int n_patterns = 0, n_classes = 0, k = 0;
+    uint32_t flags = 0;               // PM_REPORT_* / PM_ANCHOR_*
+    bool reported = false;            // counts_h[nbins + 1] holds the reported count
     std::vector<int32_t> lengths;
     std::vector<uint8_t> pos_class, class_acgt, class_is_any;
     std::vector<uint32_t> class_bytes;
@@ -396,8 +424,9 @@ uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& cou
 // afterwards and keeps the result (count = total) or discards it.
 // counts_host (mapped pinned, optional): the sort also stores the raw bin
 // counts and the aux counter there (the pipelined scan's readback).
+// total_out (device, optional): the list length (sum of the clamped counts).
 pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* slot_len, uint32_t* counts_host,
-                               hipStream_t stream);
+                               hipStream_t stream, uint64_t* total_out = nullptr, bool bind_ready = true);
 void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // slot_len (device, per slot, optional): fixed match length of every key of
 // a slot -- the LDS sort writes h->lens with the keys.
@@ -413,5 +442,50 @@ void hits_finalize(pm_hits* h);
 // per scan; kernels write them directly)
 void* pinned_get(size_t bytes, size_t* cap);
 void pinned_put(void* p, size_t cap);
+
+// ---------------------------------------------------------------------------
+// nrgrep report selection (pm_hits.hip)
+// ---------------------------------------------------------------------------
+// The scan kernels produce candidates: every start with a match (and its
+// end).  nrgrep_coords prints a subset: recSearchFile (0x402250) calls the
+// scanner on [R, buffer end), prints the match it returns and resumes at its
+// end (R = end, 0x4022de-0x4022f4), so reported matches never overlap and the
+// first one found wins; '^' / '$' (main 0x40164d / 0x40162a) are checked by
+// recCheckLeftContext / recCheckRightContext (0x402170 / 0x4021e0) against
+// the region start R and the line ends.  Hits whose start lies on a header
+// line (incl. its '\n') are dropped afterwards (process_output discards them,
+// patmatch.py:548).
+struct TextView {
+    NucView nuc;
+    const uint8_t* bytes;   // BYTE layout (header bytes stored as '\n')
+    const uint8_t* raw;     // BYTE layout, the file's own bytes
+    uint64_t n;
+    int nuc_layout;
+};
+TextView text_view(const pm_db* db);
+// true when the pass changes anything for `flags` (cross: candidates may
+// start on header lines)
+bool report_needed(uint32_t flags, bool cross);
+// report_enqueue_ws (below) enqueues the pass on s: h's keys/lens are
+// replaced by the reported subset (the old buffers are recycled once the pass
+// has read them).  The input count is *ws.total (device; the speculative
+// sort's sum) or total_h.  The selected count is stored in ws.count and at
+// host_count (mapped pinned, optional).  `done` (optional) is bound to the
+// last kernel's dispatch.
+// Synchronous form: enqueue on db->stream, read the count back, set h->count.
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total);
+// Workspace of one pass (db's current lane), sized for `cap_items` keys;
+// reserve it BEFORE enqueueing the producer of *total (reserve() may move it).
+struct ReportWs {
+    uint64_t* total = nullptr;   // input count written by the producer (speculative sort)
+    uint32_t* count = nullptr;   // selected count
+    uint64_t* bmax = nullptr;
+    uint32_t* bcnt = nullptr;
+    uint8_t* acc = nullptr;
+    uint64_t cap = 0;
+};
+ReportWs report_ws(pm_db* db, uint64_t cap_items);
+void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done);
 
 }  // namespace pm

@@ -54,6 +54,7 @@ struct LinearArgs {
     const uint32_t* class_bytes;  // [nc][8] membership over folded bytes
     int k;
     int pattern_base;
+    int cross;                    // k = 0 simple engine: windows may span breaks (k_linear_others)
     Sink sink;
 };
 
@@ -89,14 +90,15 @@ __global__ __launch_bounds__(256) void k_linear_generic(LinearArgs a) {
                     uint2 e = make_uint2(0u, 0u);
                     if (flagged) {
                         e = a.nuc.bo[pw];
-                        kill |= e.x;
+                        if (!a.cross) kill |= e.x;   // line-bounded: a break kills (see k_linear_others)
                     }
                     if (a.class_any[cls]) continue;
                     const uint2 v = a.nuc.hl[pw];
                     uint32_t x = subset_mismatch(a.class_acgt[cls], v.x, v.y);
-                    if (e.y) {
+                    const uint32_t exc = e.y | (a.cross ? e.x : 0u);
+                    if (exc) {
                         const uint32_t idx = exception_index(a.nuc.sbflag, a.nuc.sbbase, pw);
-                        uint32_t o = e.y;
+                        uint32_t o = exc;
                         while (o) {
                             const int b = __builtin_ctz(o);
                             o &= o - 1;
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(256) void k_linear_generic(LinearArgs a) {
                     const uint32_t b = __builtin_ctz(live);
                     live &= live - 1;
                     const uint64_t pos = pos_of(tile, w0, b);
-                    if (pos < a.n) {
+                    if (pos + (uint64_t)len <= a.n) {
                         const uint32_t slot = (uint32_t)(a.pattern_base + p);
                         a.sink.push(a.sink.bin_of(slot, pos), ((uint64_t)slot << 48) | pos);
                     }
@@ -144,21 +146,29 @@ void launch_generic(int P, const LinearArgs& a, hipStream_t s) {
     }
 }
 
-// Windows of a specialized scan that overlap an "other" byte (N, IUPAC
-// letter, ...) and no break, evaluated exactly.  One thread per flagged word;
-// a window is owned by the first "other" position it contains, so each is
-// evaluated once.  (The fast path drops every window that overlaps any
-// exception; windows with a break are dead.)
+// Windows of a specialized scan that overlap an exception, evaluated exactly.
+// One thread per flagged word; a window is owned by the first position it
+// contains that this pass evaluates, so each is evaluated once.  The fast
+// path drops every window that overlaps any exception.
+//  * line-bounded (k > 0: nrgrep's esimple verifies inside the record found
+//    by recGetRecord, 0x41522d; or no class accepts '\n'): windows with a
+//    break are dead, the pass owns windows by their first "other" byte;
+//  * cross (k = 0 and some class accepts '\n'): nrgrep's simple engine
+//    checks a window against the region, not the record (simplePreproc sets
+//    the flag at 0x417f73, checkMatch 0x4167c7 then skips recGetRecord), so a
+//    match may span '\n' and header bytes; every exception byte is compared
+//    with its raw value and windows past the end of the file are dead.
 struct OthersArgs {
     NucView nuc;
     const uint32_t* xoth;
+    const uint32_t* xbrk;
     const uint64_t* xword;
     uint64_t nflag, n;
     const uint8_t* pos_class;
     const int32_t* lengths;
     const uint8_t* class_any;
     const uint32_t* class_bytes;
-    int P, k, pattern_base;
+    int P, k, pattern_base, cross;
     uint64_t* out;       // the specialized kernel's (pattern, segment) hit lists
     uint32_t* seg_cnt;
     const uint64_t* slot_base;
@@ -169,7 +179,7 @@ struct OthersArgs {
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (idx >= a.nflag) return;
-    uint32_t ot = a.xoth[idx];
+    uint32_t ot = a.xoth[idx] | (a.cross ? a.xbrk[idx] : 0u);
     if (!ot) return;
     const uint64_t w = a.xword[idx];
     const uint64_t tile = w / TILE_WORDS;
@@ -184,15 +194,19 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
             const int len = a.lengths[p];
             for (int d = 0; d < len && (uint64_t)d <= e; ++d) {
                 const uint64_t s = e - d;
+                if (s + len > a.n) continue;
                 int mm = 0;
                 bool ok = true;
                 for (int j = 0; j < len && ok; ++j) {
-                    const uint8_t ch = nuc_char_at(a.nuc, s + j);
-                    if (ch == '\n') { ok = false; break; }
-                    const bool other = !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
-                    if (other && s + j < e) { ok = false; break; }   // owned by an earlier other
+                    const Loc l = loc_of(s + j);
+                    const uint2 ex = a.nuc.bo[l.word];
+                    const bool brk = (ex.x >> l.bit) & 1;
+                    if (brk && !a.cross) { ok = false; break; }
+                    const bool owned_type = (((ex.x | ex.y) >> l.bit) & 1) != 0;   // brk or other
+                    if (owned_type && s + j < e) { ok = false; break; }   // owned by an earlier exception
                     const int c = a.pos_class[p * 64 + j];
                     if (a.class_any[c]) continue;
+                    const uint8_t ch = nuc_raw_at(a.nuc, s + j);
                     if (!((a.class_bytes[c * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
                 }
                 if (ok) {
@@ -202,6 +216,45 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
                     if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
                 }
             }
+        }
+    }
+}
+
+// Fixed-length patterns on the byte layout (peptides): one thread per window
+// start, every pattern of the batch; the file is small next to a genome
+// (a proteome is a few MB), so a plain exact check per window suffices.
+// Line-bounded (k > 0, or no class accepts '\n'): the folded bytes with
+// header lines stored as '\n' -- a window holding one is dead.  Cross (k = 0
+// and a class accepts '\n', nrgrep's simple engine): the file's own bytes.
+struct ByteLinArgs {
+    const uint8_t* bytes;
+    const uint8_t* raw;
+    uint64_t n;
+    const uint8_t* pos_class;
+    const int32_t* lengths;
+    const uint8_t* class_any;
+    const uint32_t* class_bytes;
+    int P, k, cross;
+    Sink sink;
+};
+
+__global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint8_t* text = a.cross ? a.raw : a.bytes;
+    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < a.n; s += stride) {
+        for (int p = 0; p < a.P; ++p) {
+            const int len = a.lengths[p];
+            if (s + (uint64_t)len > a.n) continue;
+            int mm = 0;
+            bool ok = true;
+            for (int j = 0; j < len && ok; ++j) {
+                const uint8_t ch = text[s + j];
+                if (!a.cross && ch == (uint8_t)'\n') { ok = false; break; }
+                const int c = a.pos_class[p * 64 + j];
+                if (a.class_any[c]) continue;
+                if (!((a.class_bytes[c * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
+            }
+            if (ok) a.sink.push(a.sink.bin_of((uint32_t)p, s), ((uint64_t)p << 48) | s);
         }
     }
 }
@@ -846,16 +899,63 @@ namespace {
 std::mutex g_nospec_mu;
 std::set<std::pair<const pm_db*, std::string>> g_nospec;
 
+// pm_scan_linear on the byte layout (synchronous; the pipelined entry point
+// runs it too)
+void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
+                       const uint32_t* class_bytes, const uint8_t* class_is_any, int k, uint32_t flags, bool cross,
+                       pm_hits** out) {
+    require(n_patterns <= (int)MAX_BINS, "too many patterns for one byte-layout scan", PM_E_UNSUPPORTED);
+    hipStream_t s = db->stream;
+    lane_begin(db);
+    Upload up;
+    const size_t o_cb = up.add(class_bytes, (size_t)n_classes * 32);
+    const size_t o_len = up.add(lengths, (size_t)n_patterns * 4);
+    const size_t o_pc = up.add(pos_class, (size_t)n_patterns * 64);
+    const size_t o_any = up.add(class_is_any, (size_t)n_classes);
+    uint8_t* d_up = up.commit(db);
+    ByteLinArgs a{db->bytes, db->bytes_raw, db->n, d_up + o_pc, reinterpret_cast<const int32_t*>(d_up + o_len),
+                  d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), n_patterns, k, cross ? 1 : 0, Sink{}};
+    uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
+    SinkBuffers sb;
+    std::vector<uint32_t> counts;
+    uint64_t total = 0;
+    EventPair ev;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(blocks_for(db->n, 256), 256 * 64);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        sb = make_sink(db, n_patterns, db->n, expected);
+        a.sink = sb.sink();
+        HIPCHK(hipEventRecord(ev.a, s));
+        hipLaunchKernelGGL(k_bytes_linear, dim3(blocks), dim3(256), 0, s, a);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev.b, s));
+        bool overflow = false;
+        total = sink_total(db, sb, counts, overflow);
+        if (!overflow) break;
+        require(attempt == 0, "internal: hit bins overflowed twice");
+        expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
+    }
+    bool lens_done = false;
+    pm_hits* h = sink_to_hits(db, sb, counts, total, reinterpret_cast<const int32_t*>(d_up + o_len), &lens_done);
+    h->kernel_ms = ev.ms();
+    if (total && !lens_done) {
+        hipLaunchKernelGGL(k_linear_lens, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
+                           reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
+        HIPCHK(hipGetLastError());
+    }
+    if (report_needed(flags, cross)) report_sync(db, h, flags, total);
+    hits_ready(db, h);
+    *out = h;
+}
+
 // pm_scan_linear (async = false) and pm_scan_linear_async: the specialized
 // path launches the scan, record expansion, the speculative sort and the
 // count readback, and returns a pending hit list without a host sync.
 void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
                       const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                      pm_hits** out, bool async) {
+                      uint32_t flags, pm_hits** out, bool async) {
     {
         require(db != nullptr && out != nullptr && lengths && pos_class && class_acgt && class_bytes && class_is_any,
                 "null argument");
-        require(db->alphabet == PM_ALPHA_NUC, "pm_scan_linear needs a nucleotide database", PM_E_UNSUPPORTED);
         require(n_patterns >= 1 && n_patterns <= 4096, "n_patterns out of range");
         require(n_classes >= 1 && n_classes <= 256, "n_classes out of range");
         require(k >= 0 && k <= PM_MAX_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
@@ -863,9 +963,21 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
             for (int j = 0; j < lengths[p]; ++j) require(pos_class[64 * p + j] < n_classes, "class id out of range");
         }
+        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) == 0, "bad flags");
         DeviceGuard g(db->device);
         hipStream_t s = db->stream;
         const bool jit = use_jit(db);
+        // k = 0: nrgrep's simple engine, whose windows may span lines when a
+        // class accepts the delimiter (k_linear_others)
+        bool cross = false;
+        if (k == 0)
+            for (int c = 0; c < n_classes; ++c) cross |= ((class_bytes[8 * c] >> '\n') & 1) != 0;
+        const bool report = report_needed(flags, cross);
+        if (db->alphabet == PM_ALPHA_BYTE) {
+            scan_linear_bytes(db, n_patterns, lengths, pos_class, n_classes, class_bytes, class_is_any, k, flags,
+                              cross, out);
+            return;
+        }
 
         Upload up;
         const size_t o_cb = up.add(class_bytes, (size_t)n_classes * 32);
@@ -997,11 +1109,11 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                   (uint32_t)tpw};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
-                    if (db->nflag && db->n_oth_words) {
-                        OthersArgs oa{nuc_view(db), db->xoth, db->xword, db->nflag, db->n,
+                    if (db->nflag && (db->n_oth_words || cross)) {
+                        OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                      sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout,
+                                      cross ? 1 : 0, sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout,
                                       (uint32_t)(tpw * group)};
                         hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, xs, oa);
                         HIPCHK(hipGetLastError());
@@ -1016,9 +1128,24 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     pd->nbins = sb.nbins;
                     pd->bins_per_pattern = sb.bins_per_pattern;
                     pd->slot_cap_h = sb.slot_cap_h;
-                    pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 1) * 4, &pd->counts_cap));
-                    spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), pd->counts_h,
-                                                 xs);
+                    pd->counts_h = static_cast<uint32_t*>(pinned_get((sb.nbins + 2) * 4, &pd->counts_cap));
+                    pd->flags = flags;
+                    if (report) {
+                        // the report pass runs behind the sort, driven by the
+                        // sort's device-side list length; the list's ready
+                        // event is bound to the pass's last dispatch
+                        uint64_t cap_total = 0;
+                        for (uint32_t c : sb.slot_cap_h) cap_total += (uint64_t)c * sb.bins_per_pattern;
+                        const ReportWs ws = report_ws(db, cap_total);
+                        spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len),
+                                                     pd->counts_h, xs, ws.total, /*bind_ready=*/false);
+                        HIPCHK(hipEventCreate(&spec->ready));
+                        report_enqueue_ws(db, spec, flags, ws, true, 0, pd->counts_h + sb.nbins + 1, xs, spec->ready);
+                        pd->reported = true;
+                    } else {
+                        spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len),
+                                                     pd->counts_h, xs);
+                    }
                     // on the db stream the list's own ready event (bound to
                     // the sort's dispatch) marks the same point
                     if (xs != s) {
@@ -1098,6 +1225,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     a.class_bytes = reinterpret_cast<const uint32_t*>(d_up + o_cb);
                     a.k = k;
                     a.pattern_base = ch.base;
+                    a.cross = cross ? 1 : 0;
                     a.sink = sb.sink();
                     launch_generic(ch.P, a, s);
                     HIPCHK(hipGetLastError());
@@ -1125,6 +1253,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
             HIPCHK(hipGetLastError());
         }
+        if (report) report_sync(db, h, flags, total);
         // no host sync here: consumers wait on h->ready (pm_hits_copy*,
         // pm_hits_device, pm_hits_destroy)
         hits_ready(db, h);
@@ -1155,7 +1284,7 @@ void hits_finalize(pm_hits* h) {
     }
     const bool rec_over = pd->counts_h[pd->nbins] != 0;
     if (!overflow && !rec_over && maxc <= LDS_SORT_CAP) {   // the speculative list is the answer
-        h->count = total;
+        h->count = pd->reported ? pd->counts_h[pd->nbins + 1] : total;
         double kms = 0.0;
         for (auto& e : pd->jev) kms += e->ms();
         h->kernel_ms = kms;
@@ -1173,7 +1302,8 @@ void hits_finalize(pm_hits* h) {
     // the result's buffers
     pm_hits* r = nullptr;
     scan_linear_impl(db, pd->n_patterns, pd->lengths.data(), pd->pos_class.data(), pd->n_classes,
-                     pd->class_acgt.data(), pd->class_bytes.data(), pd->class_is_any.data(), pd->k, &r, false);
+                     pd->class_acgt.data(), pd->class_bytes.data(), pd->class_is_any.data(), pd->k, pd->flags, &r,
+                     false);
     pool_put(h->device, h->keys, h->keys_cap);
     pool_put(h->device, h->lens, h->lens_cap);
     h->keys = r->keys;
@@ -1193,19 +1323,19 @@ extern "C" {
 
 int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
                    const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                   pm_hits** out) {
+                   int flags, pm_hits** out) {
     return guarded([&] {
-        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k, out,
-                         false);
+        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k,
+                         (uint32_t)flags, out, false);
     });
 }
 
 int pm_scan_linear_async(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
                          const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
-                         pm_hits** out) {
+                         int flags, pm_hits** out) {
     return guarded([&] {
-        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k, out,
-                         true);
+        scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k,
+                         (uint32_t)flags, out, true);
     });
 }
 

@@ -38,6 +38,7 @@ struct NfaArgs {
     uint64_t n;
     uint64_t nchunks;
     int pattern_id;
+    int end_anchor;           // '$': the verify's end must be a line end
     Sink sink;
     int errs;                 // PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB
     uint64_t rev_pre[4];      // reverse: prec(S[j]) | (I[j] ? last : 0) for the injected start config
@@ -244,7 +245,12 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
             any |= R[j];
             alive |= init[j];
         }
-        if (any & a.last) { len = (uint32_t)(d + 1); break; }
+        if (any & a.last) {
+            // '$': nrgrep's forward verification keeps extending while the
+            // right context fails (extended checkMatch 0x411eb0), i.e. the
+            // match must end at the line end
+            if (!a.end_anchor || char_at<NUC>(a, s + d + 1) == (uint8_t)'\n') { len = (uint32_t)(d + 1); break; }
+        }
         if (!any && !alive) break;
     }
     a.lens[i] = len;   // 0 = no match (cannot happen for a start found by k_nfa_rev)
@@ -288,13 +294,15 @@ using namespace pm;
 
 extern "C" int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow, uint64_t first,
                            uint64_t last, int max_len, int k, int pattern_id, pm_hits** out) {
-    return pm_scan_nfa_errs(db, m, byte_mask, follow, first, last, max_len, 0, k, PM_ERR_SUB, pattern_id, out);
+    return pm_scan_nfa_errs(db, m, byte_mask, follow, first, last, max_len, 0, k, PM_ERR_SUB, pattern_id,
+                            PM_REPORT_NRGREP, out);
 }
 
 extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow, uint64_t first,
                                 uint64_t last, int max_len, int min_len, int k, int errs, int pattern_id,
-                                pm_hits** out) {
+                                int flags, pm_hits** out) {
     return guarded([&] {
+        require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) == 0, "bad flags");
         require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");
         require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range");
         require(max_len >= 0, "max_len < 0");
@@ -380,6 +388,7 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         }
         a.n = db->n;
         a.pattern_id = pattern_id;
+        a.end_anchor = (flags & PM_ANCHOR_END) ? 1 : 0;
         // chunk per lane: a power of two (so that on the nucleotide layout
         // the lanes of a wave walk the streams of one tile in lock step and
         // their loads coincide), enough lanes to fill the chip
@@ -464,6 +473,10 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
             kms += ev2.ms();
         }
         h->kernel_ms = kms;
+        // line-bounded engines (nrgrep's extended/regular/e* verify inside the
+        // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
+        // header line, the pass only selects what nrgrep reports
+        if (report_needed((uint32_t)flags, false)) report_sync(db, h, (uint32_t)flags, total);
         HIPCHK(hipStreamSynchronize(s));
         hits_ready(db, h);
         *out = h;

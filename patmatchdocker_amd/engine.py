@@ -6,11 +6,18 @@ This is the host half of the replacement for one or more
 :class:`SequenceDatabase` uploads a FASTA file into HBM once; :func:`scan`
 routes every compiled :class:`~patmatchdocker_amd.regex.Program` to a kernel:
 
-* ``linear`` -- fixed-length class sequences on a nucleotide database go to
-  the bit-sliced Hamming kernel (``pm_scan_linear``), all strands/patterns of
-  a query in ONE pass over the data;
-* ``nfa``    -- everything else with a bounded match length goes to the
-  Glushkov reverse-scan + verify kernels (``pm_scan_nfa``).
+* ``linear`` -- fixed-length class sequences with substitutions only go to
+  ``pm_scan_linear``: the bit-sliced Hamming kernel on a nucleotide database
+  (all strands/patterns of a query in ONE pass over the data), a per-window
+  byte kernel on a peptide database; at k = 0 this is nrgrep's "simple"
+  engine, whose windows may span a line break;
+* ``nfa``    -- everything else goes to the Glushkov reverse-scan + verify
+  kernels (``pm_scan_nfa_errs``), which stay inside one line.
+
+Every scan returns what nrgrep_coords PRINTS (``report="nrgrep"``): the
+kernels' candidates reduced on the GPU by the binary's report rule (first
+match found wins, the scan resumes at its end) and its '^'/'$' checks --
+DESIGN.md §1.
 
 Queries with insertions/deletions (``-k <k>ids``, the web form's default
 when mismatches > 0) go to the Glushkov kernels with the error-type mask.
@@ -33,7 +40,22 @@ from . import _lib
 from ._lib import UnsupportedOnGPU, check
 from .regex import ALL_BYTES, Program, fold_byte
 
-ANY_FOLDED = frozenset(fold_byte(b) for b in ALL_BYTES)
+ANY_FOLDED = frozenset(fold_byte(b) for b in ALL_BYTES)   # '.': every byte value a folded text can hold
+
+REPORT_NRGREP = "nrgrep"   # what nrgrep_coords prints (non-overlapping, first found wins)
+REPORT_ALL = "all"         # every candidate start (shortest end)
+
+
+def report_flags(prog: Program, report: str = REPORT_NRGREP) -> int:
+    """PM_REPORT_* / PM_ANCHOR_* flags of one program (include/patmatch_hip.h)."""
+    if report not in (REPORT_NRGREP, REPORT_ALL):
+        raise ValueError("report must be %r or %r" % (REPORT_NRGREP, REPORT_ALL))
+    f = _lib.PM_REPORT_NRGREP if report == REPORT_NRGREP else _lib.PM_REPORT_ALL
+    if prog.anchor_start:
+        f |= _lib.PM_ANCHOR_START
+    if prog.anchor_end:
+        f |= _lib.PM_ANCHOR_END
+    return f
 _ACGT = tuple(ord(c) for c in "ACGT")
 
 NUC = "nuc"
@@ -172,8 +194,8 @@ def route(prog: Program, alphabet: str, k: int, types: str) -> str:
     if indel and "d" in types and prog.min_len <= k:
         raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
                                % (k, prog.min_len))
-    if prog.linear and alphabet == NUC and not indel:
-        return "linear"
+    if prog.linear and not indel:
+        return "linear"   # nucleotide planes (bit-sliced) or the byte layout (k_bytes_linear)
     if prog.max_len is not None and prog.max_len > 1024:
         raise UnsupportedOnGPU("match length bound above 1024")
     return "nfa"
@@ -196,7 +218,7 @@ def _linear_tables(progs: Sequence[Program]):
     bits = np.zeros((nc, 8), dtype=np.uint32)
     for c, cls in enumerate(classes):
         acgt[c] = sum(1 << i for i, b in enumerate(_ACGT) if b in cls)
-        is_any[c] = 1 if ANY_FOLDED <= cls else 0
+        is_any[c] = 1 if ANY_FOLDED <= cls else 0   # accepts every byte, '\n' included
         for b in cls:
             bits[c, b >> 5] |= np.uint32(1 << (b & 31))
     return lengths, pos_class, nc, acgt, bits, is_any
@@ -212,17 +234,20 @@ class LinearBatch:
         self.lengths, self.pos_class, self.nc, self.acgt, self.bits, self.is_any = _linear_tables(progs)
         self.n = len(progs)
 
-    def launch(self, db: SequenceDatabase, k: int, pipelined: bool = False):
+    def launch(self, db: SequenceDatabase, k: int, pipelined: bool = False, flags: int = None):
         """Run pm_scan_linear; returns the raw pm_hits handle (caller destroys).
 
         ``pipelined``: pm_scan_linear_async -- returns before the scan ends
         (the handle resolves on first use), so a caller can launch the next
-        query before collecting this one."""
+        query before collecting this one.  ``flags``: PM_REPORT_* /
+        PM_ANCHOR_* (default: what nrgrep_coords reports)."""
         out = ctypes.c_void_p()
         lib = _lib.load()
         fn = lib.pm_scan_linear_async if pipelined else lib.pm_scan_linear
+        flags = _lib.PM_REPORT_NRGREP if flags is None else flags
         check(fn(db.handle, self.n, self.lengths.ctypes.data, self.pos_class.ctypes.data, self.nc,
-                 self.acgt.ctypes.data, self.bits.ctypes.data, self.is_any.ctypes.data, k, ctypes.byref(out)))
+                 self.acgt.ctypes.data, self.bits.ctypes.data, self.is_any.ctypes.data, k, flags,
+                 ctypes.byref(out)))
         return out
 
 
@@ -246,8 +271,8 @@ def destroy_hits(handle):
     check(_lib.load().pm_hits_destroy(handle))
 
 
-def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int) -> Hits:
-    return _collect(LinearBatch(progs).launch(db, k))
+def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int, flags: int = None) -> Hits:
+    return _collect(LinearBatch(progs).launch(db, k, flags=flags))
 
 
 def error_mask(types: str) -> int:
@@ -256,23 +281,30 @@ def error_mask(types: str) -> int:
             | (_lib.PM_ERR_SUB if "s" in types else 0))
 
 
-def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s") -> Hits:
+def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
+             flags: int = None) -> Hits:
     bm = np.array(prog.byte_masks(), dtype=np.uint64)
     fol = np.array(prog.follow, dtype=np.uint64)
     errs = error_mask(types) if k else _lib.PM_ERR_SUB
+    flags = report_flags(prog) if flags is None else flags
     out = ctypes.c_void_p()
     check(_lib.load().pm_scan_nfa_errs(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
-                                       prog.max_len or 0, prog.min_len, k, errs, pattern_id, ctypes.byref(out)))
+                                       prog.max_len or 0, prog.min_len, k, errs, pattern_id, flags,
+                                       ctypes.byref(out)))
     return _collect(out)
 
 
 def _same_automaton(a: Program, b: Program) -> bool:
-    return a.classes == b.classes and a.follow == b.follow and a.first == b.first and a.last == b.last
+    return (a.classes == b.classes and a.follow == b.follow and a.first == b.first and a.last == b.last
+            and a.anchor_start == b.anchor_start and a.anchor_end == b.anchor_end)
 
 
-def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str = "ids"):
+def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str = "ids",
+         report: str = REPORT_NRGREP):
     """Scan all programs; returns ([(beg, end) arrays per program], kernel_ms).
 
+    ``report``: "nrgrep" (default) = exactly the matches nrgrep_coords prints
+    (one run per program), "all" = every candidate start.
     Programs equal as automata (a palindromic site and its reverse
     complement, e.g. GAATTC) are scanned once and their hits reported for
     each of them, as the reference's two nrgrep runs would.
@@ -285,15 +317,19 @@ def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str 
         canonical.append(i if twin is None else twin)
     results: List[Optional[tuple]] = [None] * len(progs)
     total_ms = 0.0
-    linear_ids = [i for i in range(len(progs)) if routes[i] == "linear" and canonical[i] == i]
-    if linear_ids:
-        hits = scan_linear(db, [progs[i] for i in linear_ids], k)
+    # one linear batch per distinct flag set (anchors are per program)
+    groups = {}
+    for i in range(len(progs)):
+        if routes[i] == "linear" and canonical[i] == i:
+            groups.setdefault(report_flags(progs[i], report), []).append(i)
+    for flags, linear_ids in groups.items():
+        hits = scan_linear(db, [progs[i] for i in linear_ids], k, flags)
         total_ms += hits.kernel_ms
         for slot, i in enumerate(linear_ids):
             results[i] = hits.for_pattern(slot)
     for i in range(len(progs)):
         if routes[i] == "nfa" and canonical[i] == i:
-            hits = scan_nfa(db, progs[i], k, 0, types)
+            hits = scan_nfa(db, progs[i], k, 0, types, report_flags(progs[i], report))
             total_ms += hits.kernel_ms
             results[i] = (hits.beg, hits.end)
     for i in range(len(progs)):

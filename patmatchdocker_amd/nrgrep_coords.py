@@ -5,8 +5,9 @@ Drop-in for the prebuilt binary the reference shells out to
 
     nrgrep_coords -i -b <bufsize> -k <err>[idst] '<nrgrep pattern>' <file>...
 
-prints one "[beg, end]: <match>" line per hit (the binary's own format
-string "[%d, %d]: "), in increasing `beg`.  Supported options are the ones
+prints the engine banner line ("SIMPLE search", ...) and one
+"[beg, end]: <match>" line per reported match (the binary's own format
+string "[%d, %d]: "), in increasing `beg` -- DESIGN.md §1.  Supported options are the ones
 the reference passes: -i (required: the database is case-folded), -b
 (accepted, ignored: records are never split here), -k.  An invalid pattern
 prints nrgrep's "Syntax error in pattern" to stderr and exits 1 with no
@@ -19,7 +20,7 @@ import argparse
 import sys
 
 from . import engine
-from .regex import RegexSyntaxError, compile_pattern
+from .regex import RegexSyntaxError, compile_pattern, engine_banner
 from .service import _format_hits, parse_error_option
 
 
@@ -41,6 +42,7 @@ def main(argv=None) -> int:
         return 1
     k, types = parse_error_option(args.k)
     out = sys.stdout
+    out.write(engine_banner(prog, k) + "\n")   # searchPreproc's puts(), before any hit
     for path in args.files:
         db = engine.SequenceDatabase.from_file(path)
         try:

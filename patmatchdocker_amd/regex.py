@@ -6,9 +6,20 @@ the converted pattern to the prebuilt ``nrgrep_coords`` binary
 its own ``-H`` help text (nrgrep 1.1, G. Navarro, GPL): ``.`` any character,
 ``#`` any separator, ``[..]`` classes with ``^`` complement and ``a-z`` ranges,
 postfix ``?`` ``*`` ``+``, union ``|``, grouping ``( )`` and the escapes
-``\\t`` ``\\n`` ``\\xdd`` ``\\c``.  ``^``/``$``/``{``/``}``/``<``/``>`` are
-ordinary characters there, so a PatMatch pattern anchored at both ends (which
-``patmatch_to_nrgrep.pl`` turns into ``(...)$``) searches for a literal ``$``.
+``\\t`` ``\\n`` ``\\xdd`` ``\\c``.  Details read from the binary's code
+(``www/bin/nrgrep_coords``, disassembled, never run):
+
+* ``.`` sets all 256 bytes, the delimiter ``'\\n'`` included (getAclass
+  0x4198c0); ``[^..]`` starts from all 256 and clears the listed bytes
+  (0x419988); ``#`` is every non-``isalnum`` byte (0x419780); with ``-i`` a
+  class gains the other case of each letter it holds (0x4196b8), a negated
+  class loses the other case of each letter it lacks (0x4197fb) -- i.e.
+  membership of the case-folded byte;
+* a reversed range ``[z-a]`` adds nothing (0x419aac), it is no error;
+* a ``^`` as the FIRST character of the pattern and a ``$`` as its LAST are
+  anchors, stripped before parsing (main 0x4012a1 / 0x4012bd, OptStartLine /
+  OptEndLine); anywhere else they are ordinary characters, as are
+  ``{`` ``}`` ``<`` ``>``.
 
 The compiled :class:`Program` is what the HIP library consumes: every
 position of the regular expression gets a 256-bit membership set over the
@@ -27,7 +38,7 @@ __all__ = ["RegexSyntaxError", "Program", "compile_pattern", "fold_byte",
 
 MAX_POSITIONS = 64          # one 64-bit NFA state word per lane
 DELIMITER = 0x0A            # record delimiter (nrgrep default '\n')
-ALL_BYTES = frozenset(range(256)) - {DELIMITER}
+ALL_BYTES = frozenset(range(256))   # '.' (the delimiter included)
 
 
 class RegexSyntaxError(ValueError):
@@ -47,7 +58,7 @@ def _isalnum(b: int) -> bool:
     return 48 <= b <= 57 or 65 <= b <= 90 or 97 <= b <= 122
 
 
-SEPARATORS = frozenset(b for b in range(256) if not _isalnum(b)) - {DELIMITER}
+SEPARATORS = frozenset(b for b in range(256) if not _isalnum(b))
 
 
 # --------------------------------------------------------------------------
@@ -109,9 +120,7 @@ class _Parser:
                 self.i += 1
                 hb = self.take()
                 hi = self.escape() if hb == ord("\\") else hb
-                if hi < lo:
-                    raise RegexSyntaxError("reversed class range")
-                members.update(range(lo, hi + 1))
+                members.update(range(lo, hi + 1))   # reversed: empty (0x419aac)
             else:
                 members.add(lo)
         if self.icase:
@@ -177,7 +186,9 @@ class Program:
     ``nullable``     the empty string matches (never reported)
     ``min_len``/``max_len``   match length bounds (``max_len`` None = unbounded)
     ``linear``       True when the pattern is a plain sequence of classes
-                     (fixed length, no ``? * + |``) -- the bit-sliced fast path
+                     (fixed length, no ``? * + |``) -- the bit-sliced fast path;
+                     nrgrep's "simple" engine at k = 0 (detClass() == 1)
+    ``anchor_start``/``anchor_end``  the stripped leading ``^`` / trailing ``$``
     """
 
     source: str
@@ -191,6 +202,9 @@ class Program:
     linear: bool
     ignore_case: bool = True
     precede: List[int] = field(default_factory=list)
+    anchor_start: bool = False   # leading '^' (OptStartLine)
+    anchor_end: bool = False     # trailing '$' (OptEndLine)
+    kind: str = "simple"         # nrgrep engine class: simple / extended / regular
 
     @property
     def m(self) -> int:
@@ -260,6 +274,24 @@ def _length_bounds(node) -> Tuple[int, Optional[int]]:
     return a, (0 if b == 0 else None)
 
 
+def _kind(node) -> str:
+    """nrgrep's engine class (detClass, called by searchPreproc 0x4025b5):
+    "simple" = a sequence of classes, "extended" = a sequence of classes
+    each optionally followed by ``? * +``, "regular" = anything else."""
+    items = node[1] if node[0] == "cat" else [node]
+    if all(c[0] == "sym" for c in items):
+        return "simple"
+    if all(c[0] == "sym" or (c[0] in ("opt", "star", "plus") and c[1][0] == "sym") for c in items):
+        return "extended"
+    return "regular"
+
+
+# the line searchPreproc puts() before scanning (0x402654 .. 0x40275d):
+# "SIMPLE search" .. "EREGULAR search"; 'E' = with errors (-k > 0)
+def engine_banner(prog: "Program", k: int) -> str:
+    return ("E" if k else "") + prog.kind.upper() + " search"
+
+
 def _is_linear(node) -> bool:
     if node[0] == "sym":
         return True
@@ -268,9 +300,23 @@ def _is_linear(node) -> bool:
     return False
 
 
+def split_anchors(text: bytes):
+    """nrgrep main(): a leading ``^`` sets OptStartLine and is skipped
+    (0x4012a1 / 0x40164d), then a trailing ``$`` sets OptEndLine and is cut
+    (0x4012bd / 0x40162a).  Returns (core, anchor_start, anchor_end)."""
+    start = text[:1] == b"^"
+    if start:
+        text = text[1:]
+    end = text[-1:] == b"$"
+    if end:
+        text = text[:-1]
+    return text, start, end
+
+
 def compile_pattern(pattern, ignore_case: bool = True) -> Program:
     """Compile an nrgrep-syntax pattern (e.g. ``(GAA[CT]TC)``)."""
-    text = pattern.encode("latin-1") if isinstance(pattern, str) else bytes(pattern)
+    source = pattern.encode("latin-1") if isinstance(pattern, str) else bytes(pattern)
+    text, a_start, a_end = split_anchors(source)
     parser = _Parser(text, ignore_case)
     if not text:
         raise RegexSyntaxError("empty pattern")
@@ -290,7 +336,7 @@ def compile_pattern(pattern, ignore_case: bool = True) -> Program:
             if f >> j & 1:
                 precede[j] |= 1 << i
     lo, hi = _length_bounds(ast)
-    return Program(source=text.decode("latin-1"), classes=classes, first=first,
+    return Program(source=source.decode("latin-1"), classes=classes, first=first,
                    last=last, follow=follow, nullable=nullable, min_len=lo,
                    max_len=hi, linear=_is_linear(ast), ignore_case=ignore_case,
-                   precede=precede)
+                   precede=precede, anchor_start=a_start, anchor_end=a_end, kind=_kind(ast))

@@ -34,7 +34,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import engine
 from .convert import convert
-from .regex import RegexSyntaxError, compile_pattern
+from .regex import RegexSyntaxError, compile_pattern, engine_banner
 
 MAX_BUFFER_SIZE = 1600000
 MIN_TOKEN = 3
@@ -130,8 +130,9 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
         return outputs
     db = DATABASES.get(datafile)
     results, _ = engine.scan(db, progs, k=k, types=types)
-    for slot, (beg, end) in zip(slots, results):
-        outputs[slot] = _format_hits(db, beg, end)
+    for slot, prog, (beg, end) in zip(slots, progs, results):
+        # the binary's stdout: searchPreproc's engine banner, then the hits
+        outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(db, beg, end)
     return outputs
 
 

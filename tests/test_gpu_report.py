@@ -1,0 +1,169 @@
+"""GPU parity of what nrgrep_coords REPORTS: the report pass
+(pm_hits.hip k_rep_*) and the simple engine's cross-line windows
+(k_linear_others / k_linear_generic with `cross`), through the C ABI, vs
+the CPU oracle's pmo_scan2 -- on texts rich in overlapping matches
+(AT-repeats, homopolymer runs), multi-line records, headers that match
+the pattern, and '^'/'$' anchors; both linear kernels (run-time tables,
+PM_JIT=0; hipRTC-specialized, PM_JIT=1), synchronous and pipelined, and
+the Glushkov kernels."""
+import random
+
+import pytest
+
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from patmatchdocker_amd import engine as eng
+    from patmatchdocker_amd import _lib
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+    return eng
+
+
+def repeat_fasta(seed, n_records=6, min_len=2000, max_len=9000, width=None):
+    """FASTA with dense self-overlapping matches: AT repeats, A/T runs, TATA
+    boxes, GAATTC sites, N runs and lower case; headers that contain the
+    motifs themselves."""
+    rng = random.Random(seed)
+    pieces = [b"TATATATATATA", b"AAAAAAAAAA", b"TTTTTTT", b"TATAAAAG", b"GAATTCGAATTC", b"NNNNN",
+              b"tatatata", b"CAACAACAA", b"ACACACAC"]
+    out = bytearray()
+    for r in range(n_records):
+        out += b">rec%d TATATA GAATTC AAAA %d\n" % (r, rng.randint(0, 9))
+        n = rng.randint(min_len, max_len)
+        s = bytearray()
+        while len(s) < n:
+            s += rng.choice(pieces) if rng.random() < 0.3 else bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 12)))
+        s = s[:n]
+        if width:
+            for i in range(0, len(s), width):
+                out += s[i:i + width] + b"\n"
+        else:
+            out += s + b"\n"
+    return bytes(out)
+
+
+DNA = ["TATA", "AAA", "TATAWAWR", "AWA", "GAATTC", "TANN", "NNT", "ACA", "RRRR", "TGCTGASTCAGCANW"]
+
+
+def _pairs(res):
+    beg, end = res
+    return list(zip(beg.tolist(), end.tolist()))
+
+
+@pytest.mark.parametrize("jit", ["0", "1"])
+@pytest.mark.parametrize("width", [None, 60])
+def test_linear_reported_vs_oracle(engine, oracle_mod, monkeypatch, jit, width):
+    monkeypatch.setenv("PM_JIT", jit)
+    text = repeat_fasta(11 if width else 12, width=width)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in DNA:
+            fwd = convert("-n", pat)
+            progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+            for k in (0, 1, 2):
+                if k >= len(pat):
+                    continue
+                for report in ("nrgrep", "all"):
+                    res, _ = engine.scan(db, progs, k=k, types="s", report=report)
+                    for prog, r in zip(progs, res):
+                        want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True, report=report)
+                        assert _pairs(r) == want, (pat, prog.source, k, report, jit)
+    finally:
+        db.close()
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_linear_reported_large_pipelined(engine, oracle_mod, monkeypatch, pipelined):
+    """Multi-tile database through the specialized kernel, speculative sort
+    + report pass driven by the device-side list length (pipelined)."""
+    monkeypatch.setenv("PM_JIT", "1")
+    text = repeat_fasta(13, n_records=5, min_len=150000, max_len=260000)
+    progs = []
+    for p in ("TATA", "AWA", "TGCTGASTCAGCANW", "GAATTC"):
+        fwd = convert("-n", p)
+        progs += [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for k in (0, 1):
+            batch = engine.LinearBatch(progs)
+            h = engine._collect(batch.launch(db, k, pipelined=pipelined))
+            for i, prog in enumerate(progs):
+                got = list(zip(*[a.tolist() for a in h.for_pattern(i)]))
+                want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+                assert got == want, (prog.source, k)
+    finally:
+        db.close()
+
+
+def test_cross_line_windows_and_headers(engine, oracle_mod, monkeypatch):
+    """k = 0 simple engine: '.' / negated classes take '\\n' and header
+    bytes; a match starting on a header line hides an overlapping sequence
+    match (then dropped itself)."""
+    text = (b">hX AXA\nXAXA\nTCAA\n>TCA.q\nACCA\nAC\nC\n>x\nGAATTCA\n" * 3) + b"TCAG"
+    for jit in ("0", "1"):
+        monkeypatch.setenv("PM_JIT", jit)
+        db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+        try:
+            for pat in ("([AX].[AX])", "(TCA.)", "(.C)", "(C[^G])", "(A.)", "(..)", "(.)", "(#)", "(C.A.C)"):
+                prog = compile_pattern(pat)
+                for report in ("nrgrep", "all"):
+                    res, _ = engine.scan(db, [prog], k=0, types="", report=report)
+                    want = oracle_mod.scan_reported(text, prog, 0, "", skip_headers=True, report=report)
+                    assert _pairs(res[0]) == want, (pat, report, jit)
+        finally:
+            db.close()
+
+
+def test_anchors_on_gpu(engine, oracle_mod):
+    text = repeat_fasta(17, n_records=4, min_len=100, max_len=600, width=40)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat in ("^(TA)", "(TA)$", "^(TATA)$", "^(A.)", "(.A)$", "^(TA.?A)", "(A(TA)*)$"):
+            prog = compile_pattern(pat)
+            for k in (0, 1):
+                res, _ = engine.scan(db, [prog], k=k, types="s")
+                want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+                assert _pairs(res[0]) == want, (pat, k)
+    finally:
+        db.close()
+
+
+@pytest.mark.parametrize("alpha", ["nuc", "byte"])
+def test_nfa_reported_vs_oracle(engine, oracle_mod, alpha):
+    """Variable-length patterns and indels: candidates (leftmost start,
+    shortest end) reduced by the report rule, vs pmo_scan2."""
+    text = repeat_fasta(19, n_records=4, min_len=1000, max_len=5000, width=70)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=alpha)
+    try:
+        for pat, k, t in [("(TA(TA)?A)", 0, ""), ("(A+T)", 0, ""), ("(GA...?TC)", 1, "s"), ("(TATA)", 1, "ids"),
+                          ("(AAA)", 1, "id"), ("(T.?A.?T)", 2, "s"), ("(CAA|ACA)", 0, "")]:
+            prog = compile_pattern(pat)
+            for report in ("nrgrep", "all"):
+                r = engine.scan_nfa(db, prog, k, 0, t or "s", engine.report_flags(prog, report))
+                want = oracle_mod.scan_reported(text, prog, k, t or "s", skip_headers=True, report=report) \
+                    if not (k == 0 and prog.linear) else None
+                if want is None:
+                    continue
+                assert list(zip(r.beg.tolist(), r.end.tolist())) == want, (pat, k, t, report)
+    finally:
+        db.close()
+
+
+def test_synthetic_db_headers_are_reported_like_a_file(engine, oracle_mod):
+    """The synthetic database's header bytes (">r%08u") live on the device:
+    a cross-line pattern over the decoded text equals the GPU."""
+    db = engine.SequenceDatabase.synthetic(n_records=5, rec_len=20011, seed=3)
+    try:
+        text = db.decode(0, db.info()["positions"])
+        for pat in ("(.R0)", "(..)", "(A.)", "(TCA.)"):
+            prog = compile_pattern(pat)
+            res, _ = engine.scan(db, [prog], k=0, types="")
+            assert _pairs(res[0]) == oracle_mod.scan_reported(text, prog, 0, "", skip_headers=True), pat
+    finally:
+        db.close()

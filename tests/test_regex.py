@@ -28,7 +28,8 @@ def test_case_folding_and_classes():
     p = compile_pattern("(a[^c].)")
     assert ord("A") in p.classes[0] and ord("a") not in p.classes[0]
     assert ord("C") not in p.classes[1] and ord("G") in p.classes[1]
-    assert 10 not in p.classes[2]          # '.' never matches the delimiter
+    assert 10 in p.classes[2]              # '.' sets all 256 bytes (getAclass 0x4198c0)
+    assert 10 in p.classes[1]              # so does a negated class (0x419988)
 
 
 def test_escapes_and_ranges():
@@ -38,9 +39,13 @@ def test_escapes_and_ranges():
     assert p.classes[2] == frozenset([9]) and p.classes[3] == frozenset(b"(")
 
 
-def test_literal_anchor_characters():
+def test_anchor_characters():
+    # a trailing '$' / leading '^' are anchors (nrgrep main 0x4012a1/0x4012bd),
+    # elsewhere ordinary characters
     p = compile_pattern("(ACG)$")
-    assert p.m == 4 and p.classes[3] == frozenset(b"$")
+    assert p.m == 3 and p.anchor_end and not p.anchor_start
+    q = compile_pattern("(A$C^G)")
+    assert q.m == 5 and q.classes[1] == frozenset(b"$") and q.classes[3] == frozenset(b"^")
 
 
 @pytest.mark.parametrize("bad", ["", "()", "(?A)", "(A", "A)", "(*)", "[AC", "(A|)"])

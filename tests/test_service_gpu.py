@@ -43,6 +43,6 @@ def test_nrgrep_coords_cli(service, tmp_path, capsys):
     assert nrgrep_coords.main(["-i", "-b", "1600000", "-k", "1s", "(GAA[CT]TC)", path]) == 0
     got = capsys.readouterr().out
     text = open(path, "rb").read()
-    want = "".join("[%d, %d]: %s\n" % (b, e, text[b:e].decode("latin-1"))
-                   for b, e in oracle.scan(text, compile_pattern("(GAA[CT]TC)"), 1, "s", skip_headers=True))
+    want = "ESIMPLE search\n" + "".join("[%d, %d]: %s\n" % (b, e, text[b:e].decode("latin-1"))
+                   for b, e in oracle.scan_reported(text, compile_pattern("(GAA[CT]TC)"), 1, "s", skip_headers=True))
     assert got == want

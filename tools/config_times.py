@@ -29,7 +29,7 @@ def run(text, alphabet, progs, k, types, reps=10):
     finally:
         db.close()
     t0 = time.perf_counter()
-    want = [oracle.scan(text, p, k, types, skip_headers=True) for p in progs]
+    want = [oracle.scan_reported(text, p, k, types, skip_headers=True) for p in progs]
     cpu = (time.perf_counter() - t0) * 1e3
     ok = all(list(zip(b.tolist(), e.tolist())) == w for (b, e), w in zip(res, want))
     return {"kernel_ms": round(statistics.median(ms), 4), "query_ms": round(statistics.median(wall), 3),

@@ -467,19 +467,21 @@ struct RepArgs {
     const uint32_t* lens;
     uint64_t* okeys;
     uint32_t* olens;
-    uint8_t* acc;
+    uint8_t* acc;           // per candidate: 1 = reported and kept (written exactly once, or twice with 0)
     uint64_t* bmax;
-    uint32_t* bcnt;
+    uint32_t* bcnt;         // kept candidates per chunk
     const uint64_t* total_d;
     uint64_t total_h;
     uint32_t* count;
     uint32_t* host_count;
     TextView tv;
     uint32_t flags;
+    int hdr;                // candidates may start on a header line (simple engine, cross windows)
+    int debug;
 };
 
 __device__ inline uint64_t rep_total(const RepArgs& a) { return a.total_d ? *a.total_d : a.total_h; }
-__device__ inline uint64_t rep_chunk(uint64_t total) { return (total + REP_G - 1) / REP_G; }
+__device__ inline uint64_t rep_chunk(uint64_t total, uint32_t G) { return (total + G - 1) / G; }
 
 // '$': the match must end at a line end or at the end of the text (the
 // region end, recCheckRightContext 0x4021e0)
@@ -491,17 +493,32 @@ __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
 }
 __device__ inline uint64_t rep_val(uint64_t key, uint32_t len) { return key + len; }   // (pattern, end)
 
+// a start on a header line or on the '\n' that ends it maps to the '>name'
+// record in process_output (get_name_offset) and is discarded
+__device__ inline bool rep_keep(const RepArgs& a, uint64_t key) {
+    if (!a.hdr) return true;
+    const uint64_t s = key & POS_MASK;
+    if (tv_header(a.tv, s)) return false;
+    return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
+}
+
+// 64-bit wave shuffle as two 32-bit halves (a (pattern, end) key does not
+// fit the 32-bit shuffle)
+__device__ inline uint64_t shfl_xor64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, d, 64), hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline uint64_t block_max(uint64_t v, uint64_t* red) {
-    for (int d = 32; d > 0; d >>= 1) v = max(v, (uint64_t)__shfl_xor(v, d, 64));
+    for (int d = 32; d > 0; d >>= 1) v = umax64(v, shfl_xor64(v, d));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     uint64_t r = 0;
-    for (uint32_t w = 0; w < REP_T / 64; ++w) r = max(r, red[w]);
+    for (uint32_t w = 0; w < REP_T / 64; ++w) r = umax64(r, red[w]);
     __syncthreads();
     return r;
 }
 __device__ inline uint64_t block_sum(uint64_t v, uint64_t* red) {
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    for (int d = 32; d > 0; d >>= 1) v += shfl_xor64(v, d);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     uint64_t r = 0;
@@ -510,56 +527,89 @@ __device__ inline uint64_t block_sum(uint64_t v, uint64_t* red) {
     return r;
 }
 
+// per chunk: the largest (pattern, end) of a valid candidate; the kept
+// counters start at 0
 __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
     __shared__ uint64_t red[REP_T / 64];
-    const uint64_t total = rep_total(a), C = rep_chunk(total);
-    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
+    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     uint64_t m = 0;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
-        const uint64_t key = a.keys[i];
-        const uint32_t len = a.lens[i];
-        if (rep_valid(a, key, len)) m = max(m, rep_val(key, len));
+    if (a.flags & PM_REPORT_NRGREP) {
+        for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
+            const uint64_t key = a.keys[i];
+            const uint32_t len = a.lens[i];
+            if (rep_valid(a, key, len)) m = umax64(m, rep_val(key, len));
+        }
+        m = block_max(m, red);
     }
-    m = block_max(m, red);
-    if (threadIdx.x == 0) a.bmax[blockIdx.x] = m;
+    if (threadIdx.x == 0) {
+        a.bmax[blockIdx.x] = m;
+        a.bcnt[blockIdx.x] = 0u;
+    }
 }
 
+// acc[] and the kept count of every chunk
 __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     __shared__ uint64_t red[REP_T / 64];
     __shared__ uint64_t scan[REP_T];
-    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
+    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     if (!(a.flags & PM_REPORT_NRGREP)) {   // every candidate: only the anchors filter
-        for (uint64_t i = blockIdx.x * (uint64_t)REP_T + threadIdx.x; i < total; i += (uint64_t)REP_G * REP_T) {
+        uint64_t own = 0;
+        for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint64_t s = key & POS_MASK;
             bool ok = rep_valid(a, key, a.lens[i]);
             if (ok && (a.flags & PM_ANCHOR_START)) ok = s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n';
-            if (ok) a.acc[i] = 1;
+            ok = ok && rep_keep(a, key);
+            a.acc[i] = ok ? 1 : 0;
+            own += ok;
         }
+        own = block_sum(own, red);
+        if (threadIdx.x == 0) a.bcnt[blockIdx.x] = (uint32_t)own;
         return;
     }
     if (a.flags & PM_ANCHOR_START) {
         if (blockIdx.x != 0 || threadIdx.x != 0) return;
         uint64_t R = 0, pat = ~0ull;
-        for (uint64_t i = 0; i < total; ++i) {
-            const uint64_t key = a.keys[i];
-            const uint32_t len = a.lens[i];
-            if (!rep_valid(a, key, len)) continue;
-            if ((key >> 48) != pat) { pat = key >> 48; R = 0; }
-            const uint64_t s = key & POS_MASK;
-            if (s < R) continue;
-            if (s == R || s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n') {
-                a.acc[i] = 1;
-                R = s + len;
+        for (uint32_t c = 0; c < gridDim.x; ++c) {
+            uint32_t cnt = 0;
+            for (uint64_t i = c * C; i < umin64(total, (uint64_t)(c + 1) * C); ++i) {
+                const uint64_t key = a.keys[i];
+                const uint32_t len = a.lens[i];
+                uint8_t kept = 0;
+                if (rep_valid(a, key, len)) {
+                    if ((key >> 48) != pat) { pat = key >> 48; R = 0; }
+                    const uint64_t s = key & POS_MASK;
+                    if (s >= R && (s == R || s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n')) {
+                        R = s + len;
+                        kept = rep_keep(a, key) ? 1 : 0;
+                    }
+                }
+                a.acc[i] = kept;
+                cnt += kept;
             }
+            a.bcnt[c] = cnt;
         }
         return;
     }
     // running maximum of every chunk before this one
     uint64_t carry = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = max(carry, a.bmax[b]);
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
     carry = block_max(carry, red);
-    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    if (a.debug) {   // PM_REPORT_DEBUG=1: brute-force check of the chunk carry
+        uint64_t c2 = 0;
+        for (uint64_t i = threadIdx.x; i < b0; i += REP_T) {
+            const uint64_t key = a.keys[i];
+            const uint32_t len = a.lens[i];
+            if (rep_valid(a, key, len)) c2 = umax64(c2, rep_val(key, len));
+        }
+        c2 = block_max(c2, red);
+        if (threadIdx.x == 0 && c2 != carry)
+            printf("rep carry mismatch block %u: bmax-carry %llx brute %llx\n", blockIdx.x, (unsigned long long)carry,
+                   (unsigned long long)c2);
+    }
+    uint64_t own = 0;   // kept candidates of this chunk found by this thread's walks
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
         uint64_t key = 0, val = 0;
@@ -570,64 +620,73 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             len = a.lens[i];
             valid = rep_valid(a, key, len);
             if (valid) val = rep_val(key, len);
+            else a.acc[i] = 0;
         }
         scan[threadIdx.x] = val;
         __syncthreads();
         for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive max-scan
             const uint64_t o = threadIdx.x >= d ? scan[threadIdx.x - d] : 0;
             __syncthreads();
-            scan[threadIdx.x] = max(scan[threadIdx.x], o);
+            scan[threadIdx.x] = umax64(scan[threadIdx.x], o);
             __syncthreads();
         }
-        const uint64_t excl = max(carry, threadIdx.x ? scan[threadIdx.x - 1] : 0ull);
+        const uint64_t excl = umax64(carry, threadIdx.x ? scan[threadIdx.x - 1] : 0ull);
         const uint64_t tile_max = scan[REP_T - 1];
         __syncthreads();
-        carry = max(carry, tile_max);
-        if (!valid || key < excl) continue;   // not a head
+        carry = umax64(carry, tile_max);
+        if (!valid || key < excl) continue;   // not a head: its head's walk writes it
         // head: reported; walk its cluster
-        a.acc[i] = 1;
+        uint8_t kept = rep_keep(a, key) ? 1 : 0;
+        a.acc[i] = kept;
+        own += kept;
         uint64_t R = (key & POS_MASK) + len, run = val;
         for (uint64_t j = i + 1; j < total; ++j) {
             const uint64_t kj = a.keys[j];
             if (kj >= run) break;                    // the next head
             const uint32_t lj = a.lens[j];
-            if (!rep_valid(a, kj, lj)) continue;
-            if ((kj & POS_MASK) >= R) {
-                a.acc[j] = 1;
-                R = (kj & POS_MASK) + lj;
+            kept = 0;
+            if (rep_valid(a, kj, lj)) {
+                if ((kj & POS_MASK) >= R) {
+                    R = (kj & POS_MASK) + lj;
+                    kept = rep_keep(a, kj) ? 1 : 0;
+                }
+                run = umax64(run, rep_val(kj, lj));
             }
-            run = max(run, rep_val(kj, lj));
+            a.acc[j] = kept;
+            if (kept) {
+                if (j < b1) ++own;
+                else atomicAdd(&a.bcnt[j / C], 1u);   // a cluster running into a later chunk (rare)
+            }
         }
     }
+    own = block_sum(own, red);
+    if (threadIdx.x == 0 && own) atomicAdd(&a.bcnt[blockIdx.x], (uint32_t)own);
 }
 
-// a start on a header line or on the '\n' that ends it maps to the '>name'
-// record in process_output (get_name_offset) and is discarded
-__device__ inline bool rep_keep(const RepArgs& a, uint64_t i) {
-    if (!a.acc[i]) return false;
-    const uint64_t s = a.keys[i] & POS_MASK;
-    if (tv_header(a.tv, s)) return false;
-    return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
-}
-
-__global__ __launch_bounds__(REP_T) void k_rep_count(RepArgs a) {
+__global__ __launch_bounds__(REP_T) void k_rep_check(RepArgs a) {   // PM_REPORT_DEBUG: acc sums vs counts
     __shared__ uint64_t red[REP_T / 64];
-    const uint64_t total = rep_total(a), C = rep_chunk(total);
-    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
-    uint64_t c = 0;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) c += rep_keep(a, i) ? 1 : 0;
+    const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
+    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
+    uint64_t c = 0, bad = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
+        c += a.acc[i] == 1;
+        bad += a.acc[i] > 1;
+    }
     c = block_sum(c, red);
-    if (threadIdx.x == 0) a.bcnt[blockIdx.x] = (uint32_t)c;
+    bad = block_sum(bad, red);
+    if (threadIdx.x == 0 && (c != a.bcnt[blockIdx.x] || bad))
+        printf("rep check block %u: acc sum %llu bcnt %u bad %llu (C %llu)\n", blockIdx.x, (unsigned long long)c,
+               a.bcnt[blockIdx.x], (unsigned long long)bad, (unsigned long long)C);
 }
 
 __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
     __shared__ uint64_t red[REP_T / 64];
     __shared__ uint32_t scan[REP_T];
-    const uint64_t total = rep_total(a), C = rep_chunk(total);
+    const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
     uint64_t base_out = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) base_out += a.bcnt[b];
     base_out = block_sum(base_out, red);
-    if (blockIdx.x == REP_G - 1 && threadIdx.x == 0) {
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
         const uint32_t cnt = (uint32_t)(base_out + a.bcnt[blockIdx.x]);
         *a.count = cnt;
         if (a.host_count) {
@@ -635,10 +694,10 @@ __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
             __threadfence_system();
         }
     }
-    const uint64_t b0 = blockIdx.x * C, b1 = min(total, b0 + C);
+    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
-        const uint32_t keep = (i < b1 && rep_keep(a, i)) ? 1u : 0u;
+        const uint32_t keep = (i < b1 && a.acc[i]) ? 1u : 0u;
         scan[threadIdx.x] = keep;
         __syncthreads();
         for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive sum-scan
@@ -699,7 +758,7 @@ ReportWs report_ws(pm_db* db, uint64_t cap_items) {
 }
 
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
-                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done) {
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr) {
     // acc is indexed below the list length, which never exceeds the
     // capacity the workspace was sized for (the sort's slot capacities)
     const uint64_t cap_items = std::min<uint64_t>(h->keys_cap / 8, ws.cap);
@@ -718,14 +777,19 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     a.host_count = host_count;
     a.tv = text_view(db);
     a.flags = flags;
-    HIPCHK(hipMemsetAsync(ws.acc, 0, cap_items, s));
-    hipLaunchKernelGGL(k_rep_max, dim3(REP_G), dim3(REP_T), 0, s, a);
-    hipLaunchKernelGGL(k_rep_walk, dim3(REP_G), dim3(REP_T), 0, s, a);
-    hipLaunchKernelGGL(k_rep_count, dim3(REP_G), dim3(REP_T), 0, s, a);
+    // PM_REPORT_KEEP_HEADERS=1 (debugging): keep header-line starts
+    static const bool keep_hdr = getenv("PM_REPORT_KEEP_HEADERS") && getenv("PM_REPORT_KEEP_HEADERS")[0] == '1';
+    a.hdr = hdr && !keep_hdr ? 1 : 0;
+    a.debug = getenv("PM_REPORT_DEBUG") ? 1 : 0;
+    (void)cap_items;   // every acc entry below the list length is written by k_rep_walk (no memset)
+    static const uint32_t G = getenv("PM_REPORT_G") ? std::min<uint32_t>(REP_G, std::max(1, atoi(getenv("PM_REPORT_G")))) : REP_G;
+    hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
+    hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
+    if (a.debug) hipLaunchKernelGGL(k_rep_check, dim3(G), dim3(REP_T), 0, s, a);
     if (done)
-        hipExtLaunchKernelGGL(k_rep_scatter, dim3(REP_G), dim3(REP_T), 0, s, nullptr, done, 0u, a);
+        hipExtLaunchKernelGGL(k_rep_scatter, dim3(G), dim3(REP_T), 0, s, nullptr, done, 0u, a);
     else
-        hipLaunchKernelGGL(k_rep_scatter, dim3(REP_G), dim3(REP_T), 0, s, a);
+        hipLaunchKernelGGL(k_rep_scatter, dim3(G), dim3(REP_T), 0, s, a);
     HIPCHK(hipGetLastError());
     retire_buffers(h, s);
     h->keys = a.okeys;
@@ -734,13 +798,13 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     h->lens_cap = lc;
 }
 
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total) {
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr) {
     if (total == 0) {
         h->count = 0;
         return;
     }
     const ReportWs ws = report_ws(db, h->keys_cap / 8);
-    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr);
+    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr, hdr);
     uint32_t* hc = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
     HIPCHK(hipMemcpyAsync(hc, ws.count, 4, hipMemcpyDeviceToHost, db->stream));
     HIPCHK(hipStreamSynchronize(db->stream));

@@ -103,6 +103,12 @@ constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
 
 __host__ __device__ inline uint8_t fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 
+// exact 64-bit min / max: device max()/min() on uint64_t can resolve to the
+// floating-point overloads (53-bit mantissa), which corrupts (pattern, pos)
+// keys above 2^53
+__host__ __device__ inline uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__host__ __device__ inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
 // physical word index of logical word w (0 <= w < TILE_WORDS) of tile t
 __host__ __device__ inline uint64_t phys_word(uint64_t tile, uint32_t w) {
     return tile * TILE_WORDS + (w < STREAM ? (uint64_t)((w & 31u) * 64u + (w >> 5)) : (uint64_t)w);
@@ -473,7 +479,9 @@ bool report_needed(uint32_t flags, bool cross);
 // host_count (mapped pinned, optional).  `done` (optional) is bound to the
 // last kernel's dispatch.
 // Synchronous form: enqueue on db->stream, read the count back, set h->count.
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total);
+// hdr: candidates may start on a header line (the simple engine's cross
+// windows) -- only then is every start checked against the header bytes.
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr);
 // Workspace of one pass (db's current lane), sized for `cap_items` keys;
 // reserve it BEFORE enqueueing the producer of *total (reserve() may move it).
 struct ReportWs {
@@ -486,6 +494,6 @@ struct ReportWs {
 };
 ReportWs report_ws(pm_db* db, uint64_t cap_items);
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
-                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done);
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr);
 
 }  // namespace pm

@@ -942,7 +942,7 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
                            reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
         HIPCHK(hipGetLastError());
     }
-    if (report_needed(flags, cross)) report_sync(db, h, flags, total);
+    if (report_needed(flags, cross)) report_sync(db, h, flags, total, cross);
     hits_ready(db, h);
     *out = h;
 }
@@ -1140,7 +1140,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                         spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len),
                                                      pd->counts_h, xs, ws.total, /*bind_ready=*/false);
                         HIPCHK(hipEventCreate(&spec->ready));
-                        report_enqueue_ws(db, spec, flags, ws, true, 0, pd->counts_h + sb.nbins + 1, xs, spec->ready);
+                        report_enqueue_ws(db, spec, flags, ws, true, 0, pd->counts_h + sb.nbins + 1, xs, spec->ready,
+                                          cross);
                         pd->reported = true;
                     } else {
                         spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len),
@@ -1253,7 +1254,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
             HIPCHK(hipGetLastError());
         }
-        if (report) report_sync(db, h, flags, total);
+        if (report) report_sync(db, h, flags, total, cross);
         // no host sync here: consumers wait on h->ready (pm_hits_copy*,
         // pm_hits_device, pm_hits_destroy)
         hits_ready(db, h);

@@ -476,7 +476,7 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         // line-bounded engines (nrgrep's extended/regular/e* verify inside the
         // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
         // header line, the pass only selects what nrgrep reports
-        if (report_needed((uint32_t)flags, false)) report_sync(db, h, (uint32_t)flags, total);
+        if (report_needed((uint32_t)flags, false)) report_sync(db, h, (uint32_t)flags, total, false);
         HIPCHK(hipStreamSynchronize(s));
         hits_ready(db, h);
         *out = h;

@@ -167,3 +167,32 @@ def test_synthetic_db_headers_are_reported_like_a_file(engine, oracle_mod):
             assert _pairs(res[0]) == oracle_mod.scan_reported(text, prog, 0, "", skip_headers=True), pat
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("k,mbp", [(0, 6.0), (1, 1.5)])
+def test_config4_batch_of_256_patterns(engine, oracle_mod, monkeypatch, k, mbp):
+    """BASELINE configs[4]'s batch (bench.batch_patterns(256): degenerate
+    12-nt IUPAC motifs) in ONE query through the specialized kernel on a
+    multi-tile database, every pattern's report list vs the oracle."""
+    import bench
+    monkeypatch.setenv("PM_JIT", "1")
+    rng = random.Random(404)
+    text = bytearray()
+    r = 0
+    while len(text) < mbp * 1e6:
+        text += b">chr%d batch test\n" % r
+        text += bytes(rng.choice(b"ACGT") for _ in range(rng.randint(200000, 700000))) + b"\n"
+        r += 1
+    text = bytes(text)
+    progs = [compile_pattern(convert("-n", m)) for m in bench.batch_patterns(256)]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=k, types="s")
+    finally:
+        db.close()
+    total = 0
+    for prog, r in zip(progs, res):
+        want = oracle_mod.scan_threads(text, prog, k, "s", skip_headers=True, threads=16, report="nrgrep")
+        assert _pairs(r) == want, (prog.source, k)
+        total += len(want)
+    assert total > 1000

@@ -54,7 +54,9 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device,
                  void* stream, pm_db** out);
 /* Synthetic nucleotide database generated on the device: n_records records
  * laid out like a FASTA file (">r%08u\n" header line, rec_len random bases,
- * "\n"), bases from a counter-based hash of (seed, position).           */
+ * "\n"), bases from a counter-based hash of (seed, position); every record
+ * holds one run of 50..499 N and IUPAC letters at ~1e-5 of its bases, so
+ * scans exercise the exception path as on a real genome.               */
 int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed,
                            int device, void* stream, pm_db** out);
 int pm_db_destroy(pm_db* db);

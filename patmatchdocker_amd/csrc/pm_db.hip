@@ -68,8 +68,24 @@ __device__ inline uint64_t mix64(uint64_t x) {
 
 constexpr uint64_t SYN_HDR = 10;  // ">r%08u" then '\n'
 
+// Exceptions of the synthetic text, at genome-like density: every record has
+// one run of N (length 50..499 at a hashed offset) and IUPAC ambiguity
+// letters at ~1e-5 of the bases (hashed per position).  Returns the byte of
+// sequence offset `b` (0-based inside the record) of record `r`, or 0 for
+// an A/C/G/T base (drawn from the per-word hash by k_pack_synth).
+__device__ inline uint8_t synth_other(uint64_t r, uint64_t b, uint64_t p, uint64_t rec_len, uint64_t seed) {
+    const uint64_t h = mix64(seed ^ (r * 0xd6e8feb86659fd93ull + 0x5bd1e995ull));
+    const uint64_t run_len = 50 + (h >> 40) % 450;
+    const uint64_t run_beg = (h % rec_len);
+    if (b >= run_beg && b < run_beg + run_len) return (uint8_t)'N';
+    const uint64_t x = mix64(p * 0x9e3779b97f4a7c15ull ^ seed ^ 0x2545f4914f6cdd1dull);
+    if (x < 184467440737096ull) return (uint8_t)"RYKMSWBDHV"[(x >> 8) % 10];   // ~1e-5
+    return 0;
+}
+
 // Synthetic FASTA-shaped text: records of SYN_HDR header bytes + '\n' +
-// rec_len bases + '\n'; bases from a counter-based hash of (seed, word).
+// rec_len bases + '\n'; bases from a counter-based hash of (seed, word),
+// exceptions from synth_other.
 __global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint64_t seed,
                              uint2* __restrict__ hl, uint2* __restrict__ bo) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -78,7 +94,7 @@ __global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint
     const uint32_t w = (uint32_t)(g % STREAM);
     const uint64_t stride = SYN_HDR + 1 + rec_len + 1;
     const uint64_t r = mix64(seed * 0x9e3779b97f4a7c15ull + g);
-    uint32_t br = 0;
+    uint32_t br = 0, ot = 0;
     const uint64_t p0 = pos_of(t, w, 0);
     uint64_t q = p0 % stride;
     const uint64_t d = STREAM % stride;
@@ -86,12 +102,13 @@ __global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint
         const uint64_t p = p0 + (uint64_t)b * STREAM;
         const bool is_base = p < n && q >= SYN_HDR + 1 && q < SYN_HDR + 1 + rec_len;
         if (!is_base) br |= 1u << b;
+        else if (synth_other(p / stride, q - (SYN_HDR + 1), p, rec_len, seed)) ot |= 1u << b;
         q += d;
         if (q >= stride) q -= stride;
     }
     const uint64_t pw = phys_word(t, w);
-    hl[pw] = make_uint2((uint32_t)(r >> 32) & ~br, (uint32_t)r & ~br);
-    bo[pw] = make_uint2(br, 0u);
+    hl[pw] = make_uint2((uint32_t)(r >> 32) & ~(br | ot), (uint32_t)r & ~(br | ot));
+    bo[pw] = make_uint2(br, ot);
 }
 
 // Header lines become breaks: one thread per [beg, end) range.
@@ -140,10 +157,12 @@ __global__ void k_sb_flags(const uint2* __restrict__ bo, uint64_t nsb, uint32_t*
 
 // byte p of the synthetic FASTA text (k_pack_synth): ">r%08u\n" header
 // lines (record index, 0-based), rec_len bases, "\n"; folded like every
-// stored byte.  Only header and '\n' positions are asked for.
-__device__ inline uint8_t synth_byte(uint64_t p, uint64_t rec_len) {
+// stored byte.  Only exception positions (header bytes, '\n', N, IUPAC
+// letters) are asked for.
+__device__ inline uint8_t synth_byte(uint64_t p, uint64_t rec_len, uint64_t seed) {
     const uint64_t stride = SYN_HDR + 1 + rec_len + 1;
     const uint64_t r = p / stride, q = p % stride;
+    if (q >= SYN_HDR + 1 && q < SYN_HDR + 1 + rec_len) return synth_other(r, q - (SYN_HDR + 1), p, rec_len, seed);
     if (q == 0) return (uint8_t)'>';
     if (q == 1) return (uint8_t)'R';
     if (q < SYN_HDR) {
@@ -164,7 +183,7 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
                                   const uint32_t* __restrict__ sbflag, const uint32_t* __restrict__ sbbase,
                                   uint32_t* __restrict__ xbrk, uint32_t* __restrict__ xoth,
                                   uint64_t* __restrict__ xword, uint8_t* __restrict__ xbytes,
-                                  uint32_t* __restrict__ n_oth_words, uint64_t syn_rec_len) {
+                                  uint32_t* __restrict__ n_oth_words, uint64_t syn_rec_len, uint64_t syn_seed) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (w >= nwords) return;
     const uint32_t f = sbflag[w >> 5];
@@ -182,7 +201,7 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
     for (uint32_t i = 0; i < 32; ++i) {
         const uint64_t p = pos_of(t, lw, i);
         uint8_t c = 0;
-        if ((((br | ot) >> i) & 1) && p < n) c = raw != nullptr ? fold(raw[p]) : synth_byte(p, syn_rec_len);
+        if ((((br | ot) >> i) & 1) && p < n) c = raw != nullptr ? fold(raw[p]) : synth_byte(p, syn_rec_len, syn_seed);
         xbytes[idx * 32 + i] = c;
     }
 }
@@ -286,7 +305,8 @@ void alloc_planes(pm_db* db) {
 }
 
 // halo words, flags, compacted exception side tables, lane flags
-void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint64_t syn_rec_len = 0) {
+void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint64_t syn_rec_len = 0,
+                uint64_t syn_seed = 0) {
     hipStream_t s = db->stream;
     hipLaunchKernelGGL(k_clean_oth, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, db->nwords, db->bo);
     HIPCHK(hipGetLastError());
@@ -316,7 +336,7 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipMemsetAsync(d_noth, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_fill_exceptions, dim3(blocks_for(db->nwords, 256)), dim3(256), 0, s, d_raw, db->n,
                        db->nwords, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword,
-                       db->xbytes, d_noth, syn_rec_len);
+                       db->xbytes, d_noth, syn_rec_len, syn_seed);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h, d_noth, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -541,7 +561,7 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         hipLaunchKernelGGL(k_pack_synth, dim3(blocks_for(db->ntiles * STREAM, 256)), dim3(256), 0, db->stream,
                            db->n, db->ntiles, rec_len, seed, db->hl, db->bo);
         HIPCHK(hipGetLastError());
-        finish_nuc(db, owned, nullptr, rec_len);
+        finish_nuc(db, owned, nullptr, rec_len, seed);
         free_all(db, owned);
         *out = db;
     });
@@ -557,6 +577,17 @@ int pm_db_destroy(pm_db* db) {
     return guarded([&] {
         if (!db) return;
         DeviceGuard g(db->device);
+        {   // wait for a scan in flight on another thread; its pending lists resolve here
+            std::lock_guard<std::recursive_mutex> lk(db->mu);
+            while (!db->pending.empty()) {
+                pm_hits* h = *db->pending.begin();
+                try {
+                    hits_finalize(h);
+                } catch (...) {
+                    db->pending.erase(h);   // the list stays unresolved (count 0)
+                }
+            }
+        }
         free_db(db);
     });
 }
@@ -575,6 +606,7 @@ int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet, uint64_t* 
 int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out) {
     return guarded([&] {
         require(db != nullptr && out != nullptr, "null argument");
+        std::lock_guard<std::recursive_mutex> lk(db->mu);
         require(beg + len <= db->n, "decode range outside the database");
         if (len == 0) return;
         DeviceGuard g(db->device);

@@ -901,7 +901,10 @@ int pm_hits_destroy(pm_hits* h) {
         // the producing stream's work and any async copy out must be done
         // before the buffers go back to the pool: recycled now if they are,
         // else by a later pool_get / pm_hits_destroy (the host never waits)
-        if (h->pending) h->pending->db->pending.erase(h);   // never resolved: no re-run
+        if (h->pending) {   // never resolved: no re-run
+            std::lock_guard<std::recursive_mutex> lk(h->pending->db->mu);
+            h->pending->db->pending.erase(h);
+        }
         if (hits_idle(h)) {
             release_hits(h);
         } else {

@@ -41,6 +41,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -268,6 +269,13 @@ struct pm_lane {
 };
 
 struct pm_db : pm_lane {
+    // every entry point that uses the database (scans, decode, destroy, the
+    // resolution of a pending list) holds this lock: ctypes releases the GIL
+    // around a call, so a multi-threaded server (mod_wsgi's 15 threads) may
+    // enter from several threads at once; the workspaces, slot caches and
+    // the pending set are per database.  Recursive: resolving a pending list
+    // can re-run its scan.
+    std::recursive_mutex mu;
     int device = 0;
     int alphabet = PM_ALPHA_NUC;
     uint64_t n = 0;          // positions (file bytes)

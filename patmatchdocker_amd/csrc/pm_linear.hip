@@ -190,9 +190,19 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
         ot &= ot - 1;
         const uint64_t e = pos_of(tile, lw, b);
         if (e >= a.n) continue;
+        // a window that also holds position e - 1 is owned by an earlier
+        // exception (or killed by a break) when e - 1 is one: inside a run
+        // of N only the window starting at e is left to this position
+        bool prev_exc = false;
+        if (e > 0) {
+            const Loc lp = loc_of(e - 1);
+            const uint2 ep = a.nuc.bo[lp.word];
+            prev_exc = (((ep.x | ep.y) >> lp.bit) & 1) != 0;
+        }
         for (int p = 0; p < a.P; ++p) {
             const int len = a.lengths[p];
-            for (int d = 0; d < len && (uint64_t)d <= e; ++d) {
+            const int dmax = prev_exc ? 1 : len;
+            for (int d = 0; d < dmax && (uint64_t)d <= e; ++d) {
                 const uint64_t s = e - d;
                 if (s + len > a.n) continue;
                 int mm = 0;
@@ -1268,9 +1278,11 @@ namespace pm {
 
 void hits_finalize(pm_hits* h) {
     if (!h || !h->pending) return;
+    pm_db* db = h->pending->db;
+    std::lock_guard<std::recursive_mutex> lk(db->mu);
+    if (!h->pending) return;   // resolved meanwhile (by pm_db_destroy)
     std::unique_ptr<pm_pending> pd(h->pending);
     h->pending = nullptr;
-    pm_db* db = pd->db;
     db->pending.erase(h);
     DeviceGuard g(h->device);
     HIPCHK(hipEventSynchronize(pd->counted ? pd->counted : h->ready));
@@ -1326,6 +1338,8 @@ int pm_scan_linear(pm_db* db, int n_patterns, const int32_t* lengths, const uint
                    const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
                    int flags, pm_hits** out) {
     return guarded([&] {
+        require(db != nullptr, "db is NULL");
+        std::lock_guard<std::recursive_mutex> lk(db->mu);
         scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k,
                          (uint32_t)flags, out, false);
     });
@@ -1335,6 +1349,8 @@ int pm_scan_linear_async(pm_db* db, int n_patterns, const int32_t* lengths, cons
                          const uint8_t* class_acgt, const uint32_t* class_bytes, const uint8_t* class_is_any, int k,
                          int flags, pm_hits** out) {
     return guarded([&] {
+        require(db != nullptr, "db is NULL");
+        std::lock_guard<std::recursive_mutex> lk(db->mu);
         scan_linear_impl(db, n_patterns, lengths, pos_class, n_classes, class_acgt, class_bytes, class_is_any, k,
                          (uint32_t)flags, out, true);
     });

@@ -303,6 +303,8 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
                                 int flags, pm_hits** out) {
     return guarded([&] {
         require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) == 0, "bad flags");
+        require(db != nullptr, "db is NULL");
+        std::lock_guard<std::recursive_mutex> lk(db->mu);
         require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");
         require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range");
         require(max_len >= 0, "max_len < 0");

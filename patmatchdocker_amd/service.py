@@ -63,28 +63,76 @@ def _set_dirs_for_test(root_dir, root_data_dir):
 # database residency: one SequenceDatabase per data file, kept in HBM
 # ---------------------------------------------------------------------------
 
+class _Entry:
+    """A resident database with the number of requests using it; a replaced
+    entry (the file changed) is closed when its last user leaves."""
+
+    def __init__(self, stamp, db):
+        self.stamp, self.db, self.users, self.retired = stamp, db, 0, False
+
+
 class _DatabaseCache:
+    """One SequenceDatabase per data file, shared by the request threads
+    (mod_wsgi runs 15, FlaskApp.conf).  The library serializes calls on one
+    database (pm_db's lock); this cache reference-counts the entries so a
+    database is never closed under a request that is scanning it."""
+
     def __init__(self):
         self._lock = threading.Lock()
-        self._dbs: Dict[Tuple[str, int], tuple] = {}
+        self._dbs: Dict[Tuple[str, int], _Entry] = {}
 
-    def get(self, path: str, device: int = 0):
+    def _acquire(self, path: str, device: int) -> _Entry:
         st = os.stat(path)
+        stamp = (st.st_mtime_ns, st.st_size)
         key = (os.path.realpath(path), device)
         with self._lock:
-            hit = self._dbs.get(key)
-            if hit and hit[0] == (st.st_mtime_ns, st.st_size):
-                return hit[1]
-            if hit:
-                hit[1].close()
-            db = engine.SequenceDatabase.from_file(path, device=device)
-            self._dbs[key] = ((st.st_mtime_ns, st.st_size), db)
-            return db
+            ent = self._dbs.get(key)
+            if ent is None or ent.stamp != stamp:
+                if ent is not None:
+                    self._retire(ent)
+                ent = _Entry(stamp, engine.SequenceDatabase.from_file(path, device=device))
+                self._dbs[key] = ent
+            ent.users += 1
+            return ent
+
+    def _retire(self, ent: _Entry):   # caller holds the lock
+        ent.retired = True
+        if ent.users == 0:
+            ent.db.close()
+
+    def _release(self, ent: _Entry):
+        with self._lock:
+            ent.users -= 1
+            if ent.retired and ent.users == 0:
+                ent.db.close()
+
+    class _Lease:
+        def __init__(self, cache, path, device):
+            self.cache, self.path, self.device, self.ent = cache, path, device, None
+
+        def __enter__(self):
+            self.ent = self.cache._acquire(self.path, self.device)
+            return self.ent.db
+
+        def __exit__(self, *exc):
+            self.cache._release(self.ent)
+            return False
+
+    def lease(self, path: str, device: int = 0):
+        """``with DATABASES.lease(path) as db:`` -- the database stays open
+        until the block ends, even if the file is replaced meanwhile."""
+        return self._Lease(self, path, device)
+
+    def get(self, path: str, device: int = 0):
+        """The resident database (no lease: for single-threaded callers)."""
+        ent = self._acquire(path, device)
+        self._release(ent)
+        return ent.db
 
     def clear(self):
         with self._lock:
-            for _, db in self._dbs.values():
-                db.close()
+            for ent in self._dbs.values():
+                self._retire(ent)
             self._dbs.clear()
 
 
@@ -128,11 +176,11 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
     outputs = [""] * len(patterns)
     if not progs:
         return outputs
-    db = DATABASES.get(datafile)
-    results, _ = engine.scan(db, progs, k=k, types=types)
-    for slot, prog, (beg, end) in zip(slots, progs, results):
-        # the binary's stdout: searchPreproc's engine banner, then the hits
-        outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(db, beg, end)
+    with DATABASES.lease(datafile) as db:
+        results, _ = engine.scan(db, progs, k=k, types=types)
+        for slot, prog, (beg, end) in zip(slots, progs, results):
+            # the binary's stdout: searchPreproc's engine banner, then the hits
+            outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(db, beg, end)
     return outputs
 
 

@@ -46,3 +46,30 @@ def test_nrgrep_coords_cli(service, tmp_path, capsys):
     want = "ESIMPLE search\n" + "".join("[%d, %d]: %s\n" % (b, e, text[b:e].decode("latin-1"))
                    for b, e in oracle.scan_reported(text, compile_pattern("(GAA[CT]TC)"), 1, "s", skip_headers=True))
     assert got == want
+
+
+def test_concurrent_requests_share_one_database(service, tmp_path):
+    """Request threads (mod_wsgi runs 15) scanning the same resident
+    database at once -- linear and Glushkov scans, both alphabets -- each get
+    exactly the single-threaded answer (the library serializes calls per
+    database; the cache never closes a database under a scan)."""
+    from concurrent.futures import ThreadPoolExecutor
+    queries = [(["(GAA[CT]TC)", "(GA[AG]TTC)"], "1s", "orf_dna.seq"), (["(TATA[AT]A[AT][AG])"], "0ids", "orf_dna.seq"),
+               (["(C..?.?C...[LIVMFYWC])"], "0ids", "orf_pep.seq"), (["(GA...?TC)"], "1ids", "orf_dna.seq"),
+               (["(RGD)"], "1s", "orf_pep.seq")]
+    want = [service.search_output(p, o, str(tmp_path / f)) for p, o, f in queries]
+    jobs = [queries[i % len(queries)] for i in range(40)]
+    with ThreadPoolExecutor(max_workers=12) as ex:
+        got = list(ex.map(lambda q: service.search_output(q[0], q[1], str(tmp_path / q[2])), jobs))
+    for i, g in enumerate(got):
+        assert g == want[i % len(queries)], jobs[i]
+
+
+def test_replaced_file_is_rescanned_without_closing_a_busy_database(service, tmp_path):
+    path = tmp_path / "orf_dna.seq"
+    before = service.search_output(["(GAATTC)"], "0ids", str(path))
+    with service.DATABASES.lease(str(path)) as db_old:
+        path.write_bytes(path.read_bytes() + b">new rec\nGAATTCGAATTC\n")
+        after = service.search_output(["(GAATTC)"], "0ids", str(path))
+        assert db_old.info()["positions"] > 0   # still open under the lease
+    assert after.count("\n") == before.count("\n") + 2

@@ -25,8 +25,8 @@ ERR_INS, ERR_DEL, ERR_SUB = 1, 2, 4
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    src = os.path.join(_HERE, "pm_oracle.c")
-    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "Makefile")]
+    if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return path
 
@@ -45,6 +45,9 @@ def lib():
         _LIB.pmo_scan2.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_uint64,
                                    ctypes.c_uint64, pu64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmc_shiftadd.restype = ctypes.c_int64
+        _LIB.pmc_shiftadd.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, p64, ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -259,3 +262,54 @@ def scan_py(text: bytes, prog, k: int = 0, types: str = "ids"):
                     break
         pos += len(line) + 1
     return hits
+
+
+# ---------------------------------------------------------------------------
+# bit-parallel CPU scan (pm_cpuscan.c): the bench's CPU baseline
+# ---------------------------------------------------------------------------
+
+def shiftadd_scan(text: bytes, prog, k: int, skip_headers: bool = False):
+    """Reported windows of a fixed-length class sequence with <= k
+    substitutions, by the Shift-Add bit-parallel automaton (pm_cpuscan.c);
+    same output as ``scan_reported(text, prog, k, "s")``."""
+    if not prog.linear:
+        raise ValueError("shiftadd_scan needs a class sequence")
+    L = lib()
+    B = np.array(prog.byte_masks(), dtype=np.uint64)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        n = L.pmc_shiftadd(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), prog.m, k,
+                           1 if prog.ignore_case else 0, beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pattern too long for one Shift-Add word (m=%d, k=%d)" % (prog.m, k))
+        if n <= cap:
+            hits = [(b, b + prog.m) for b in beg[:n].tolist()]
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+def shiftadd_threads(text: bytes, prog, k: int, skip_headers: bool = False, threads: int = 1):
+    """``shiftadd_scan`` over host threads, the text cut after line breaks
+    (k > 0: windows never span one, so the pieces are independent)."""
+    if threads <= 1 or k == 0 or len(text) < (1 << 20):
+        return shiftadd_scan(text, prog, k, skip_headers)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [0]
+    step = len(text) // threads
+    for t in range(1, threads):
+        c = text.find(b"\n", max(cuts[-1], t * step))
+        if c < 0:
+            break
+        if c + 1 > cuts[-1]:
+            cuts.append(c + 1)
+    cuts.append(len(text))
+    pieces = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+
+    def one(span):
+        a, b = span
+        return [(x + a, y + a) for x, y in shiftadd_scan(text[a:b], prog, k, skip_headers)]
+
+    with ThreadPoolExecutor(max_workers=len(pieces)) as ex:
+        parts = list(ex.map(one, pieces))
+    return [h for part in parts for h in part]

@@ -206,6 +206,31 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
     }
 }
 
+// Run interiors (one thread per flagged word): bit b of xint = position e
+// (bit b of logical word lw) has an exception at e - 1 (bit b of word lw - 1)
+// and "other" bytes at e .. e + RUN_SKIP (words lw .. lw + RUN_SKIP, halo
+// included).  Flagged words with a break or "other" bit outside xint are
+// appended to xedge: only they can own a live window for patterns whose
+// first k+1 A/C/G/T-only classes lie within RUN_SKIP (k_linear_others).
+__global__ void k_run_interior(uint64_t nflag, const uint64_t* __restrict__ xword, const uint32_t* __restrict__ xbrk,
+                               const uint32_t* __restrict__ xoth, const uint2* __restrict__ bo,
+                               uint32_t* __restrict__ xint, uint32_t* __restrict__ xedge,
+                               unsigned long long* __restrict__ nedge) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= nflag) return;
+    const uint64_t w = xword[idx];
+    const uint64_t tile = w / TILE_WORDS;
+    const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
+    uint32_t m = 0;
+    if (lw >= 1 && lw < STREAM) {
+        const uint2 pv = bo[phys_word(tile, lw - 1)];
+        m = (pv.x | pv.y) & xoth[idx];
+        for (uint32_t j = 1; j <= (uint32_t)RUN_SKIP && m; ++j) m &= bo[phys_word(tile, lw + j)].y;
+    }
+    xint[idx] = m;
+    if (lw < STREAM && ((xoth[idx] | xbrk[idx]) & ~m)) xedge[atomicAdd(nedge, 1ull)] = (uint32_t)idx;
+}
+
 // oth = oth & ~brk everywhere (a header byte is a break, not an "other")
 __global__ void k_clean_oth(uint64_t nwords, uint2* __restrict__ bo) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -344,6 +369,19 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     hipLaunchKernelGGL(k_lane_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
                        db->lflag);
     HIPCHK(hipGetLastError());
+    require(db->nflag < (1ull << 32), "too many exception words for the run index", PM_E_UNSUPPORTED);
+    db->xint = dalloc<uint32_t>(db, db->nflag);
+    db->xedge = dalloc<uint32_t>(db, db->nflag);
+    unsigned long long* d_nedge = static_cast<unsigned long long*>(reserve(db, db->ws_post, sizeof(uint64_t)));
+    HIPCHK(hipMemsetAsync(d_nedge, 0, sizeof(uint64_t), s));
+    if (db->nflag) {
+        hipLaunchKernelGGL(k_run_interior, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, s, db->nflag, db->xword,
+                           db->xbrk, db->xoth, db->bo, db->xint, db->xedge, d_nedge);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(h, d_nedge, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    db->nedge = *reinterpret_cast<uint64_t*>(h);
 }
 
 void init_stream(pm_db* db, void* stream) {
@@ -375,7 +413,7 @@ void free_db(pm_db* db) {
         (void)hipStreamDestroy(db->post);
     }
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->bytes, db->bytes_raw, db->ws_post.p};
+                    db->lflag, db->xint, db->xedge, db->bytes, db->bytes_raw, db->ws_post.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);

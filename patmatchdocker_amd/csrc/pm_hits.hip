@@ -487,8 +487,12 @@ __device__ inline uint64_t rep_chunk(uint64_t total, uint32_t G) { return (total
 // region end, recCheckRightContext 0x4021e0)
 __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
     if (len == 0) return false;   // a start whose verify found no (anchored) end
+    // a speculative list that will be discarded (a bin the LDS sort skipped)
+    // holds stale keys: never read the text at a position outside it
+    const uint64_t s = key & POS_MASK;
+    if (s >= a.tv.n || len > a.tv.n - s) return false;
     if (!(a.flags & PM_ANCHOR_END)) return true;
-    const uint64_t e = (key & POS_MASK) + len;
+    const uint64_t e = s + len;
     return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n';
 }
 __device__ inline uint64_t rep_val(uint64_t key, uint32_t len) { return key + len; }   // (pattern, end)

@@ -101,6 +101,7 @@ constexpr uint32_t MAX_BINS = 8192;
 constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_nfa_rev
 constexpr uint32_t LDS_SORT_CAP = 2048;              // keys per bin sorted in LDS (16 KB: 8 sort blocks per CU)
 constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
+constexpr int RUN_SKIP = 8;                          // run-interior lookahead (xint)
 
 __host__ __device__ inline uint8_t fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 
@@ -291,6 +292,12 @@ struct pm_db : pm_lane {
     uint8_t* xbytes = nullptr;
     uint64_t* xword = nullptr;   // NUC: physical word of each flagged word
     uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
+    // NUC, runs of N: per flagged word, the bits whose position is preceded
+    // by an exception and followed by RUN_SKIP more "other" bytes (xint);
+    // the flagged words with a bit outside that mask (xedge, nedge of them)
+    uint32_t* xint = nullptr;
+    uint32_t* xedge = nullptr;
+    uint64_t nedge = 0;
     uint8_t* bytes = nullptr;    // BYTE alphabet: folded bytes, header lines stored as '\n'
     uint8_t* bytes_raw = nullptr;   // BYTE alphabet: folded bytes as in the file (headers kept)
     hipStream_t stream = nullptr;

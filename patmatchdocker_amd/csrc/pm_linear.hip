@@ -169,6 +169,13 @@ struct OthersArgs {
     const uint8_t* class_any;
     const uint32_t* class_bytes;
     int P, k, pattern_base, cross;
+    int skip_ok;         // every pattern has k+1 positions whose class accepts only A/C/G/T
+    const uint8_t* jsel; // [P][4]: the first k+1 such positions of each pattern
+    int maxlen;          // longest pattern of the chunk
+    int use_edge;        // skip_ok and every jsel <= RUN_SKIP: iterate the edge words only
+    const uint32_t* xint;
+    const uint32_t* xedge;
+    uint64_t nedge;
     uint64_t* out;       // the specialized kernel's (pattern, segment) hit lists
     uint32_t* seg_cnt;
     const uint64_t* slot_base;
@@ -177,55 +184,102 @@ struct OthersArgs {
 };
 
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
-    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (idx >= a.nflag) return;
+    // one wave per flagged word; its lanes share the word's windows
+    // (exception bit x pattern x start offset), so a word's work is one
+    // short dependent chain per lane instead of ~30 windows in a row
+    const uint64_t widx = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    uint64_t idx = widx;
+    if (a.use_edge) {   // run interiors removed at build time (k_run_interior)
+        if (widx >= a.nedge) return;
+        idx = a.xedge[widx];
+    } else if (idx >= a.nflag) {
+        return;
+    }
     uint32_t ot = a.xoth[idx] | (a.cross ? a.xbrk[idx] : 0u);
+    if (a.use_edge) ot &= ~a.xint[idx];
     if (!ot) return;
     const uint64_t w = a.xword[idx];
     const uint64_t tile = w / TILE_WORDS;
     const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
     if (lw >= STREAM) return;   // halo copy of a main word
-    while (ot) {
-        const uint32_t b = __builtin_ctz(ot);
-        ot &= ot - 1;
-        const uint64_t e = pos_of(tile, lw, b);
-        if (e >= a.n) continue;
-        // a window that also holds position e - 1 is owned by an earlier
-        // exception (or killed by a break) when e - 1 is one: inside a run
-        // of N only the window starting at e is left to this position
-        bool prev_exc = false;
-        if (e > 0) {
-            const Loc lp = loc_of(e - 1);
-            const uint2 ep = a.nuc.bo[lp.word];
-            prev_exc = (((ep.x | ep.y) >> lp.bit) & 1) != 0;
-        }
-        for (int p = 0; p < a.P; ++p) {
-            const int len = a.lengths[p];
-            const int dmax = prev_exc ? 1 : len;
-            for (int d = 0; d < dmax && (uint64_t)d <= e; ++d) {
-                const uint64_t s = e - d;
-                if (s + len > a.n) continue;
-                int mm = 0;
-                bool ok = true;
-                for (int j = 0; j < len && ok; ++j) {
-                    const Loc l = loc_of(s + j);
-                    const uint2 ex = a.nuc.bo[l.word];
-                    const bool brk = (ex.x >> l.bit) & 1;
-                    if (brk && !a.cross) { ok = false; break; }
-                    const bool owned_type = (((ex.x | ex.y) >> l.bit) & 1) != 0;   // brk or other
-                    if (owned_type && s + j < e) { ok = false; break; }   // owned by an earlier exception
-                    const int c = a.pos_class[p * 64 + j];
-                    if (a.class_any[c]) continue;
-                    const uint8_t ch = nuc_raw_at(a.nuc, s + j);
-                    if (!((a.class_bytes[c * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
+    // exceptions right before each bit's position (lw >= 1: bit b of word
+    // lw - 1 is position e - 1; lw == 0: per lane below)
+    uint32_t prev = 0;
+    if (lw >= 1) {
+        const uint2 pv = a.nuc.bo[phys_word(tile, lw - 1)];
+        prev = pv.x | pv.y;
+        // Runs of N, all 32 streams at once: a position e whose predecessor
+        // is an exception owns only the window starting at e; that window is
+        // dead when, for every pattern, the bytes at e + j are "other" for
+        // the first k+1 positions j whose class accepts only A/C/G/T (jsel:
+        // k+1 mismatches).  Bit b of logical word lw + j is position e + j.
+        if (a.skip_ok && !a.use_edge) {
+            const uint32_t m0 = prev & a.xoth[idx];
+            uint32_t m = m0;
+            for (int p = 0; p < a.P && m; ++p) {   // dead for every pattern of the chunk
+                uint32_t mp = m0;
+                for (int t = 0; t <= a.k && mp; ++t) {
+                    const uint32_t j = a.jsel[p * 4 + t];
+                    if (j) mp &= a.nuc.bo[phys_word(tile, lw + j)].y;
                 }
-                if (ok) {
-                    const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                    const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
-                    const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
-                    if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
-                }
+                m &= mp;
             }
+            ot &= ~m;
+        }
+    }
+    const int nbits = __popc(ot);
+    const int per_bit = a.P * a.maxlen;
+    for (int c = lane; c < nbits * per_bit; c += 64) {
+        const int bi = c / per_bit, p = (c / a.maxlen) % a.P, d = c % a.maxlen;
+        const int len = a.lengths[p];
+        if (d >= len) continue;
+        uint32_t rest = ot;
+        for (int q = 0; q < bi; ++q) rest &= rest - 1;
+        const uint32_t b = __builtin_ctz(rest);
+        const uint64_t e = pos_of(tile, lw, b);
+        if (e >= a.n || (uint64_t)d > e) continue;
+        // a window that also holds position e - 1 is owned by an earlier
+        // exception (or killed by a break) when e - 1 is one
+        bool prev_exc;
+        if (lw >= 1) {
+            prev_exc = (prev >> b) & 1;
+        } else {
+            prev_exc = false;
+            if (e > 0) {
+                const Loc lp = loc_of(e - 1);
+                const uint2 ep = a.nuc.bo[lp.word];
+                prev_exc = (((ep.x | ep.y) >> lp.bit) & 1) != 0;
+            }
+        }
+        if (prev_exc && d > 0) continue;
+        const uint64_t s = e - d;
+        if (s + len > a.n) continue;
+        int mm = 0;
+        bool ok = true;
+        for (int j = 0; j < len && ok; ++j) {
+            const Loc l = loc_of(s + j);
+            const uint2 ex = a.nuc.bo[l.word];
+            const bool brk = (ex.x >> l.bit) & 1;
+            if (brk && !a.cross) { ok = false; break; }
+            const bool owned_type = (((ex.x | ex.y) >> l.bit) & 1) != 0;   // brk or other
+            if (owned_type && s + j < e) { ok = false; break; }   // owned by an earlier exception
+            const int cl = a.pos_class[p * 64 + j];
+            if (a.class_any[cl]) continue;
+            uint8_t ch;
+            if (owned_type) {
+                ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
+            } else {
+                const uint2 hv = a.nuc.hl[l.word];
+                ch = (uint8_t)((0x54474341u >> (8 * ((((hv.x >> l.bit) & 1) << 1) | ((hv.y >> l.bit) & 1)))) & 0xff);
+            }
+            if (!((a.class_bytes[cl * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
+        }
+        if (ok) {
+            const uint32_t slot = (uint32_t)(a.pattern_base + p);
+            const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
+            const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
+            if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
         }
     }
 }
@@ -983,6 +1037,36 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         if (k == 0)
             for (int c = 0; c < n_classes; ++c) cross |= ((class_bytes[8 * c] >> '\n') & 1) != 0;
         const bool report = report_needed(flags, cross);
+        // k_linear_others' run skip: per pattern, the first k+1 positions
+        // whose class accepts only A/C/G/T (an "other" byte there is a
+        // mismatch); jsel_ok[p]: the pattern has k+1 of them
+        std::vector<uint8_t> jsel((size_t)n_patterns * 4, 0), jsel_ok(n_patterns, 0);
+        for (int p = 0; p < n_patterns; ++p) {
+            int t = 0;
+            for (int j = 0; j < lengths[p] && t <= k; ++j) {
+                const uint32_t* cb = class_bytes + 8 * pos_class[64 * p + j];
+                bool acgt_only = true;
+                for (int w = 0; w < 8 && acgt_only; ++w) {
+                    uint32_t bits = cb[w];
+                    if (w == 2) bits &= ~((1u << ('A' - 64)) | (1u << ('C' - 64)) | (1u << ('G' - 64)) | (1u << ('T' - 64)));
+                    acgt_only = bits == 0;
+                }
+                if (acgt_only) jsel[(size_t)p * 4 + t++] = (uint8_t)j;
+            }
+            jsel_ok[p] = t == k + 1;
+        }
+        auto skip_ok = [&](int base, int P) {
+            for (int p = base; p < base + P; ++p)
+                if (!jsel_ok[p]) return false;
+            return true;
+        };
+        auto edge_ok = [&](int base, int P) {   // every jsel within the build-time lookahead
+            if (!skip_ok(base, P)) return false;
+            for (int p = base; p < base + P; ++p)
+                for (int t = 0; t <= k; ++t)
+                    if (jsel[(size_t)p * 4 + t] > RUN_SKIP) return false;
+            return true;
+        };
         if (db->alphabet == PM_ALPHA_BYTE) {
             scan_linear_bytes(db, n_patterns, lengths, pos_class, n_classes, class_bytes, class_is_any, k, flags,
                               cross, out);
@@ -995,6 +1079,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         const size_t o_pc = up.add(pos_class, (size_t)n_patterns * 64);
         const size_t o_acgt = up.add(class_acgt, (size_t)n_classes);
         const size_t o_any = up.add(class_is_any, (size_t)n_classes);
+        const size_t o_jsel = up.add(jsel.data(), jsel.size());
         struct Chunk { int base, P; hipFunction_t jit; };
         std::vector<Chunk> chunks;
         for (int base = 0; base < n_patterns;) {
@@ -1123,9 +1208,14 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                         OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
                                       d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
                                       d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                      cross ? 1 : 0, sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout,
-                                      (uint32_t)(tpw * group)};
-                        hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, xs, oa);
+                                      cross ? 1 : 0, skip_ok(ch.base, ch.P) ? 1 : 0, d_up + o_jsel + 4 * ch.base,
+                                      *std::max_element(lengths + ch.base, lengths + ch.base + ch.P),
+                                      edge_ok(ch.base, ch.P) ? 1 : 0, db->xint, db->xedge, db->nedge,
+                                      sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tpw * group)};
+                        // one wave per flagged word (per edge word: runs of N skipped)
+                        const uint64_t words = oa.use_edge ? db->nedge : db->nflag;
+                        if (words)
+                            hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(words * 64, 256)), dim3(256), 0, xs, oa);
                         HIPCHK(hipGetLastError());
                     }
                 }

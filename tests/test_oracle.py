@@ -88,3 +88,20 @@ def test_oracle_threaded_scan_on_decoded_layout(oracle_mod):
     prog = compile_pattern("(TATA[AT]A[AT][AG])")
     want = oracle_mod.scan(text, prog, 1, "s")
     assert oracle_mod.scan_threads(text, prog, 1, "s", threads=8) == want
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_shiftadd_cpu_scan_equals_reported_oracle(oracle_mod, seed):
+    """The bench's bit-parallel CPU baseline (pm_cpuscan.c, Shift-Add) reports
+    exactly what pmo_scan2 reports for class sequences with substitutions."""
+    text = dna_fasta(seed + 60, n_records=5, max_len=4000, width=(70 if seed == 1 else None))
+    for pat in ["TGCTGASTCAGCANW", "TATAWAWR", "GAATTC", "NNGCNN", "AAAA", "TANNNNTA"]:
+        for strand in ("-n", "-c"):
+            fwd = convert("-n", pat)
+            prog = compile_pattern(fwd if strand == "-n" else convert("-c", fwd))
+            for k in (0, 1, 2, 3):
+                if k >= prog.m:
+                    continue
+                want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+                assert oracle_mod.shiftadd_scan(text, prog, k, skip_headers=True) == want, (pat, k)
+                assert oracle_mod.shiftadd_threads(text, prog, k, skip_headers=True, threads=3) == want, (pat, k)

@@ -72,4 +72,4 @@ def test_replaced_file_is_rescanned_without_closing_a_busy_database(service, tmp
         path.write_bytes(path.read_bytes() + b">new rec\nGAATTCGAATTC\n")
         after = service.search_output(["(GAATTC)"], "0ids", str(path))
         assert db_old.info()["positions"] > 0   # still open under the lease
-    assert after.count("\n") == before.count("\n") + 2
+    assert after[0].count("\n") == before[0].count("\n") + 2

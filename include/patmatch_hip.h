@@ -76,11 +76,15 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
  * and PM_ANCHOR_START / PM_ANCHOR_END set (nrgrep main(): OptStartLine /
  * OptEndLine): the match must start at a line start or where the previous
  * report ended / end at a line end.  Hits starting on a header line are
- * never returned (process_output discards them, patmatch.py:548).      */
+ * not returned (process_output discards them, patmatch.py:548) unless
+ * PM_KEEP_HEADERS is set: a caller that joins the scans of consecutive
+ * pieces of one file needs them, since they take part in the report rule
+ * (patmatchdocker_amd/shards.py).                                         */
 #define PM_REPORT_ALL 0
 #define PM_REPORT_NRGREP 1
 #define PM_ANCHOR_START 2
 #define PM_ANCHOR_END 4
+#define PM_KEEP_HEADERS 8
 
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched

@@ -104,8 +104,16 @@ def mode_of(prog, k: int, report: str = "nrgrep", simple=None) -> int:
     return m
 
 
+def scan_candidates(text: bytes, prog, k: int = 0, types: str = "ids"):
+    """Every start with a match under nrgrep's engine choice (shortest end;
+    '$' applied, '^' not, header-line starts kept): what the sharded scan
+    re-chains when a report crosses into the next piece."""
+    m = mode_of(prog, k, "all") & ~PMO_START
+    return scan_reported(text, prog, k, types, mode=m)
+
+
 def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
-                  report: str = "nrgrep", simple=None):
+                  report: str = "nrgrep", simple=None, mode=None):
     """What ``nrgrep_coords`` prints for ``prog`` (pmo_scan2): the candidates
     of ``scan`` (or the simple engine's whole-text windows at k = 0) reduced
     by the binary's report rule -- first found wins, the scan resumes at the
@@ -122,7 +130,7 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
         n = L.pmo_scan2(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                         prog.first, prog.last, F.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                         prog.m, k, err_flags(types) if k else 0, 1 if prog.ignore_case else 0,
-                        mode_of(prog, k, report, simple),
+                        mode_of(prog, k, report, simple) if mode is None else mode,
                         beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                         end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
         if n < 0:

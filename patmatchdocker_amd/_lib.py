@@ -18,7 +18,7 @@ PM_ALPHA_BYTE = 1
 PM_E_UNSUPPORTED = -4
 PM_MAX_K = 3
 PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
-PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END = 0, 1, 2, 4
+PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END, PM_KEEP_HEADERS = 0, 1, 2, 4, 8
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (

@@ -215,7 +215,7 @@ __global__ void k_fill_exceptions(const uint8_t* __restrict__ raw, uint64_t n, u
 __global__ void k_run_interior(uint64_t nflag, const uint64_t* __restrict__ xword, const uint32_t* __restrict__ xbrk,
                                const uint32_t* __restrict__ xoth, const uint2* __restrict__ bo,
                                uint32_t* __restrict__ xint, uint32_t* __restrict__ xedge,
-                               unsigned long long* __restrict__ nedge) {
+                               uint32_t* __restrict__ xedge_oth, unsigned long long* __restrict__ nedge) {
     const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (idx >= nflag) return;
     const uint64_t w = xword[idx];
@@ -228,7 +228,9 @@ __global__ void k_run_interior(uint64_t nflag, const uint64_t* __restrict__ xwor
         for (uint32_t j = 1; j <= (uint32_t)RUN_SKIP && m; ++j) m &= bo[phys_word(tile, lw + j)].y;
     }
     xint[idx] = m;
-    if (lw < STREAM && ((xoth[idx] | xbrk[idx]) & ~m)) xedge[atomicAdd(nedge, 1ull)] = (uint32_t)idx;
+    if (lw >= STREAM) return;
+    if ((xoth[idx] | xbrk[idx]) & ~m) xedge[atomicAdd(&nedge[0], 1ull)] = (uint32_t)idx;
+    if (xoth[idx] & ~m) xedge_oth[atomicAdd(&nedge[1], 1ull)] = (uint32_t)idx;
 }
 
 // oth = oth & ~brk everywhere (a header byte is a break, not an "other")
@@ -348,7 +350,7 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
     void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
-    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
+    uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 16));
     HIPCHK(hipMemcpyAsync(h, db->sbbase + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h + 1, sbcnt + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -372,16 +374,23 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     require(db->nflag < (1ull << 32), "too many exception words for the run index", PM_E_UNSUPPORTED);
     db->xint = dalloc<uint32_t>(db, db->nflag);
     db->xedge = dalloc<uint32_t>(db, db->nflag);
-    unsigned long long* d_nedge = static_cast<unsigned long long*>(reserve(db, db->ws_post, sizeof(uint64_t)));
-    HIPCHK(hipMemsetAsync(d_nedge, 0, sizeof(uint64_t), s));
+    db->xedge_oth = dalloc<uint32_t>(db, db->nflag);
+    unsigned long long* d_nedge = static_cast<unsigned long long*>(reserve(db, db->ws_post, 2 * sizeof(uint64_t)));
+    HIPCHK(hipMemsetAsync(d_nedge, 0, 2 * sizeof(uint64_t), s));
     if (db->nflag) {
         hipLaunchKernelGGL(k_run_interior, dim3(blocks_for(db->nflag, 256)), dim3(256), 0, s, db->nflag, db->xword,
-                           db->xbrk, db->xoth, db->bo, db->xint, db->xedge, d_nedge);
+                           db->xbrk, db->xoth, db->bo, db->xint, db->xedge, db->xedge_oth, d_nedge);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipMemcpyAsync(h, d_nedge, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h, d_nedge, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    db->nedge = *reinterpret_cast<uint64_t*>(h);
+    db->nedge = reinterpret_cast<uint64_t*>(h)[0];
+    db->nedge_oth = reinterpret_cast<uint64_t*>(h)[1];
+    if (env_flag("PM_DEBUG_DB", false))
+        fprintf(stderr, "pm_db: n=%llu tiles=%llu flagged words=%llu other words=%llu edge words=%llu (other %llu)\n",
+                (unsigned long long)db->n, (unsigned long long)db->ntiles, (unsigned long long)db->nflag,
+                (unsigned long long)db->n_oth_words, (unsigned long long)db->nedge,
+                (unsigned long long)db->nedge_oth);
 }
 
 void init_stream(pm_db* db, void* stream) {
@@ -412,13 +421,19 @@ void free_db(pm_db* db) {
         (void)hipStreamSynchronize(db->post);
         (void)hipStreamDestroy(db->post);
     }
+    if (db->exc) {
+        (void)hipStreamSynchronize(db->exc);
+        (void)hipStreamDestroy(db->exc);
+    }
+    for (hipEvent_t e : {db->exc_fork, db->exc_join})
+        if (e) (void)hipEventDestroy(e);
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->bytes, db->bytes_raw, db->ws_post.p};
+                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->bytes, db->bytes_raw, db->ws_post.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
     for (pm_lane* l : {static_cast<pm_lane*>(db), &db->alt}) {
-        for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p, l->ws_rep.p})
+        for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p, l->ws_rep.p, l->ws_oth.p})
             if (p) (void)hipFree(p);
         for (void* p : {l->pin_up.p, l->pin_slots.p})
             if (p) (void)hipHostFree(p);
@@ -459,10 +474,20 @@ hipStream_t post_stream(pm_db* db) {
     return db->post;
 }
 
+hipStream_t exc_stream(pm_db* db) {
+    if (!db->exc) {
+        HIPCHK(hipStreamCreateWithFlags(&db->exc, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&db->exc_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&db->exc_join, hipEventDisableTiming));
+    }
+    return db->exc;
+}
+
 void* reserve(pm_db* db, pm_devbuf& b, size_t bytes) {
     if (b.cap < bytes) {
         HIPCHK(hipStreamSynchronize(db->stream));
         if (db->post) HIPCHK(hipStreamSynchronize(db->post));
+        if (db->exc) HIPCHK(hipStreamSynchronize(db->exc));
         if (b.p) HIPCHK(hipFree(b.p));
         b.p = nullptr;
         b.cap = 0;

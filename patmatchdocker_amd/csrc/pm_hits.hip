@@ -783,7 +783,7 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     a.flags = flags;
     // PM_REPORT_KEEP_HEADERS=1 (debugging): keep header-line starts
     static const bool keep_hdr = getenv("PM_REPORT_KEEP_HEADERS") && getenv("PM_REPORT_KEEP_HEADERS")[0] == '1';
-    a.hdr = hdr && !keep_hdr ? 1 : 0;
+    a.hdr = hdr && !keep_hdr && !(flags & PM_KEEP_HEADERS) ? 1 : 0;
     a.debug = getenv("PM_REPORT_DEBUG") ? 1 : 0;
     (void)cap_items;   // every acc entry below the list length is written by k_rep_walk (no memset)
     static const uint32_t G = getenv("PM_REPORT_G") ? std::min<uint32_t>(REP_G, std::max(1, atoi(getenv("PM_REPORT_G")))) : REP_G;

@@ -133,6 +133,11 @@ __host__ __device__ inline Loc loc_of(uint64_t p) {
     return Loc{phys_word(t, q % (uint32_t)STREAM), q / (uint32_t)STREAM};
 }
 
+// an on/off knob from the environment ("0" off, anything else on)
+inline bool env_flag(const char* name, bool dflt) {
+    const char* e = getenv(name);
+    return e ? e[0] != '0' : dflt;
+}
 inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 inline uint32_t blocks_for(uint64_t n, uint32_t threads) {
     return (uint32_t)std::max<uint64_t>(1, (n + threads - 1) / threads);
@@ -152,6 +157,15 @@ __device__ inline uint32_t exception_index(const uint32_t* sbflag, const uint32_
     const uint32_t f = sbflag[w >> 5];
     const uint32_t wb = (uint32_t)(w & 31);
     return sbbase[w >> 5] + __popc(f & ((1u << wb) - 1));
+}
+
+// orders one wave's LDS stores before its later LDS loads (and loads before
+// later stores) across lanes, without a block barrier: a wave's DS
+// operations execute in issue order, so only the compiler must not move them
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // the exact (folded) file byte at position p < n: breaks and "other" bytes
@@ -255,7 +269,7 @@ struct pm_hostbuf {      // pinned host staging buffer
 // after the last work that reads them (a scan waits for it on the GPU before
 // reusing the lane).  Never stream-ordered allocations.
 struct pm_lane {
-    pm_devbuf ws_tab, ws_sink, ws_rec, ws_rep;
+    pm_devbuf ws_tab, ws_sink, ws_rec, ws_rep, ws_oth;
     pm_hostbuf pin_up, pin_slots;
     // slot tables last uploaded into ws_sink (skip the copy when unchanged)
     void* slot_cache_p = nullptr;
@@ -294,10 +308,13 @@ struct pm_db : pm_lane {
     uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
     // NUC, runs of N: per flagged word, the bits whose position is preceded
     // by an exception and followed by RUN_SKIP more "other" bytes (xint);
-    // the flagged words with a bit outside that mask (xedge, nedge of them)
+    // the flagged words with a bit outside that mask (xedge, nedge of them;
+    // xedge_oth / nedge_oth: those with an "other" bit outside it)
     uint32_t* xint = nullptr;
     uint32_t* xedge = nullptr;
     uint64_t nedge = 0;
+    uint32_t* xedge_oth = nullptr;
+    uint64_t nedge_oth = 0;
     uint8_t* bytes = nullptr;    // BYTE alphabet: folded bytes, header lines stored as '\n'
     uint8_t* bytes_raw = nullptr;   // BYTE alphabet: folded bytes as in the file (headers kept)
     hipStream_t stream = nullptr;
@@ -310,6 +327,11 @@ struct pm_db : pm_lane {
     // inherited pm_lane is the active one, `alt` the other; switch_lane swaps)
     hipStream_t post = nullptr;
     pm_lane alt;
+    // the exception pass (k_linear_others) runs on `exc`, concurrently with
+    // the specialized scan: forked from the scan stream after the counters
+    // are zeroed, joined before the sort
+    hipStream_t exc = nullptr;
+    hipEvent_t exc_fork = nullptr, exc_join = nullptr;
     std::set<pm_hits*> pending;       // pipelined scans not yet resolved
     uint64_t device_bytes = 0;
 };
@@ -375,6 +397,7 @@ void lane_begin(pm_db* db);
 void lane_end(pm_db* db, hipStream_t s);
 void switch_lane(pm_db* db);
 hipStream_t post_stream(pm_db* db);
+hipStream_t exc_stream(pm_db* db);   // creates exc, exc_fork and exc_join on first use
 void* reserve(pm_db* db, pm_devbuf& b, size_t bytes);
 // Per-device pool of hit-list buffers (sizes rounded to powers of two):
 // scans allocate their result from it and pm_hits_destroy returns it, so a

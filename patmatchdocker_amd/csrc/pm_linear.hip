@@ -147,7 +147,7 @@ void launch_generic(int P, const LinearArgs& a, hipStream_t s) {
 }
 
 // Windows of a specialized scan that overlap an exception, evaluated exactly.
-// One thread per flagged word; a window is owned by the first position it
+// One wave per flagged word; a window is owned by the first position it
 // contains that this pass evaluates, so each is evaluated once.  The fast
 // path drops every window that overlaps any exception.
 //  * line-bounded (k > 0: nrgrep's esimple verifies inside the record found
@@ -158,6 +158,12 @@ void launch_generic(int P, const LinearArgs& a, hipStream_t s) {
 //    the flag at 0x417f73, checkMatch 0x4167c7 then skips recGetRecord), so a
 //    match may span '\n' and header bytes; every exception byte is compared
 //    with its raw value and windows past the end of the file are dead.
+struct OtherSel {
+    uint64_t word;   // physical word
+    uint32_t bits;   // its exception bits that can own a live window
+    uint32_t pad;
+};
+
 struct OthersArgs {
     NucView nuc;
     const uint32_t* xoth;
@@ -174,28 +180,24 @@ struct OthersArgs {
     int maxlen;          // longest pattern of the chunk
     int use_edge;        // skip_ok and every jsel <= RUN_SKIP: iterate the edge words only
     const uint32_t* xint;
-    const uint32_t* xedge;
+    const uint32_t* xedge;   // the edge words (cross: any exception; else: "other" bytes)
     uint64_t nedge;
+    OtherSel* sel;       // k_others_select -> k_linear_others
+    uint32_t* nsel;
     uint64_t* out;       // the specialized kernel's (pattern, segment) hit lists
     uint32_t* seg_cnt;
     const uint64_t* slot_base;
     const uint32_t* slot_cap;
     uint32_t nwg, tiles_per_wg;
+    int items_per_wave;  // k_linear_others: 1, 2 or 4 (2 * maxlen - 1 <= 64 / items_per_wave)
 };
 
-__global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
-    // one wave per flagged word; its lanes share the word's windows
-    // (exception bit x pattern x start offset), so a word's work is one
-    // short dependent chain per lane instead of ~30 windows in a row
-    const uint64_t widx = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    uint64_t idx = widx;
-    if (a.use_edge) {   // run interiors removed at build time (k_run_interior)
-        if (widx >= a.nedge) return;
-        idx = a.xedge[widx];
-    } else if (idx >= a.nflag) {
-        return;
-    }
+// Phase 1, one thread per candidate word: the exception bits that can own a
+// live window, compacted into `sel`.
+__global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= (a.use_edge ? a.nedge : a.nflag)) return;
+    const uint64_t idx = a.use_edge ? a.xedge[t] : t;   // run interiors removed at build (k_run_interior)
     uint32_t ot = a.xoth[idx] | (a.cross ? a.xbrk[idx] : 0u);
     if (a.use_edge) ot &= ~a.xint[idx];
     if (!ot) return;
@@ -203,84 +205,137 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     const uint64_t tile = w / TILE_WORDS;
     const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
     if (lw >= STREAM) return;   // halo copy of a main word
-    // exceptions right before each bit's position (lw >= 1: bit b of word
-    // lw - 1 is position e - 1; lw == 0: per lane below)
-    uint32_t prev = 0;
-    if (lw >= 1) {
+    if (lw >= 1 && a.skip_ok) {
+        // exceptions right before each bit's position (bit b of word lw - 1
+        // is position e - 1)
         const uint2 pv = a.nuc.bo[phys_word(tile, lw - 1)];
-        prev = pv.x | pv.y;
+        const uint32_t prev = pv.x | pv.y;
         // Runs of N, all 32 streams at once: a position e whose predecessor
         // is an exception owns only the window starting at e; that window is
         // dead when, for every pattern, the bytes at e + j are "other" for
         // the first k+1 positions j whose class accepts only A/C/G/T (jsel:
         // k+1 mismatches).  Bit b of logical word lw + j is position e + j.
-        if (a.skip_ok && !a.use_edge) {
-            const uint32_t m0 = prev & a.xoth[idx];
+        // The build-time index (xint/xedge) drops the run interiors for
+        // any jsel <= RUN_SKIP; this query's jsel also drops most of the
+        // RUN_SKIP edge words at a run's end.
+        // (no early exits: the loads of all (pattern, jsel) words are issued
+        // together instead of as a dependent chain)
+        const uint32_t m0 = prev & a.xoth[idx];
+        if (m0) {
             uint32_t m = m0;
-            for (int p = 0; p < a.P && m; ++p) {   // dead for every pattern of the chunk
+            for (int p = 0; p < a.P; ++p) {   // dead for every pattern of the chunk
                 uint32_t mp = m0;
-                for (int t = 0; t <= a.k && mp; ++t) {
-                    const uint32_t j = a.jsel[p * 4 + t];
-                    if (j) mp &= a.nuc.bo[phys_word(tile, lw + j)].y;
+                for (int t2 = 0; t2 <= a.k; ++t2) {
+                    const uint32_t j = a.jsel[p * 4 + t2];
+                    mp &= j ? a.nuc.bo[phys_word(tile, lw + j)].y : ~0u;
                 }
                 m &= mp;
             }
             ot &= ~m;
         }
     }
-    const int nbits = __popc(ot);
+    if (ot) a.sel[atomicAdd(a.nsel, 1u)] = OtherSel{w, ot, 0u};
+}
+
+constexpr int OTH_MAX_POS = 8 * 64;   // (pattern, position) entries of a chunk (JIT_MAX_P x 64)
+constexpr uint32_t OTH_BLOCKS = 2048;   // phase 2: persistent blocks (8 per CU)
+
+// The windows owned by the exception bits `ot` of logical word lw of a tile
+// (one wave; a window is owned by the first exception it holds).
+__device__ inline void other_windows(const OthersArgs& a, const uint32_t (*s_memb)[8], uint64_t tile, uint32_t lw,
+                                     uint32_t ot, int lane, int lanes, int slice) {
+    // per exception bit e: the bytes of every window holding e --
+    // positions e - maxlen + 1 .. e + maxlen - 1 -- are gathered once, one
+    // position per lane (a few independent loads instead of one dependent
+    // chain per window), into this wave's LDS slice; the lanes then test
+    // (pattern, start offset) windows from LDS
+    __shared__ uint8_t s_ch[4][128];
+    __shared__ uint8_t s_fl[4][128];   // bit 0: break or other, bit 1: break
+    uint8_t* const wch = &s_ch[threadIdx.x >> 6][slice * lanes];   // this item's part of the wave's slice
+    uint8_t* const wfl = &s_fl[threadIdx.x >> 6][slice * lanes];
+    const int span = 2 * a.maxlen - 1;
     const int per_bit = a.P * a.maxlen;
-    for (int c = lane; c < nbits * per_bit; c += 64) {
-        const int bi = c / per_bit, p = (c / a.maxlen) % a.P, d = c % a.maxlen;
-        const int len = a.lengths[p];
-        if (d >= len) continue;
-        uint32_t rest = ot;
-        for (int q = 0; q < bi; ++q) rest &= rest - 1;
+    uint32_t rest = ot;
+    while (rest) {
         const uint32_t b = __builtin_ctz(rest);
+        rest &= rest - 1;
         const uint64_t e = pos_of(tile, lw, b);
-        if (e >= a.n || (uint64_t)d > e) continue;
+        if (e >= a.n) continue;
+        const int64_t q0 = (int64_t)e - (a.maxlen - 1);
+        wave_lds_sync();   // the previous bit's reads are done
+        for (int i = lane; i < span; i += lanes) {
+            const int64_t q = q0 + i;
+            uint8_t c = 0, f = 0;
+            if (q >= 0 && (uint64_t)q < a.n) {
+                const Loc l = loc_of((uint64_t)q);
+                const uint2 ex = a.nuc.bo[l.word];
+                const uint2 hv = a.nuc.hl[l.word];   // issued with bo: one round trip for a base
+                const uint32_t brk = (ex.x >> l.bit) & 1, oth = (ex.y >> l.bit) & 1;
+                f = (uint8_t)((brk | oth) | (brk << 1));
+                if (brk | oth)
+                    c = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
+                else
+                    c = (uint8_t)((0x54474341u >> (8 * ((((hv.x >> l.bit) & 1) << 1) | ((hv.y >> l.bit) & 1)))) & 0xff);
+            }
+            wch[i] = c;
+            wfl[i] = f;
+        }
+        wave_lds_sync();
         // a window that also holds position e - 1 is owned by an earlier
         // exception (or killed by a break) when e - 1 is one
-        bool prev_exc;
-        if (lw >= 1) {
-            prev_exc = (prev >> b) & 1;
-        } else {
-            prev_exc = false;
-            if (e > 0) {
-                const Loc lp = loc_of(e - 1);
-                const uint2 ep = a.nuc.bo[lp.word];
-                prev_exc = (((ep.x | ep.y) >> lp.bit) & 1) != 0;
+        const bool prev_exc = a.maxlen >= 2 && (wfl[a.maxlen - 2] & 1);
+        for (int c = lane; c < per_bit; c += lanes) {
+            const int p = c / a.maxlen, d = c % a.maxlen;
+            const int len = a.lengths[p];
+            if (d >= len || (uint64_t)d > e || (prev_exc && d > 0)) continue;
+            const uint64_t s = e - d;
+            if (s + len > a.n) continue;
+            const int i0 = a.maxlen - 1 - d;   // LDS index of position s
+            int mm = 0;
+            bool ok = true;
+            for (int j = 0; j < len; ++j) {
+                const uint8_t f = wfl[i0 + j];
+                if ((f & 2) && !a.cross) { ok = false; break; }
+                if ((f & 1) && j < d) { ok = false; break; }   // owned by an earlier exception
+                const uint8_t ch = wch[i0 + j];
+                if (!((s_memb[p * a.maxlen + j][ch >> 5] >> (ch & 31)) & 1) && ++mm > a.k) { ok = false; break; }
+            }
+            if (ok) {
+                const uint32_t slot = (uint32_t)(a.pattern_base + p);
+                const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
+                const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
+                if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
             }
         }
-        if (prev_exc && d > 0) continue;
-        const uint64_t s = e - d;
-        if (s + len > a.n) continue;
-        int mm = 0;
-        bool ok = true;
-        for (int j = 0; j < len && ok; ++j) {
-            const Loc l = loc_of(s + j);
-            const uint2 ex = a.nuc.bo[l.word];
-            const bool brk = (ex.x >> l.bit) & 1;
-            if (brk && !a.cross) { ok = false; break; }
-            const bool owned_type = (((ex.x | ex.y) >> l.bit) & 1) != 0;   // brk or other
-            if (owned_type && s + j < e) { ok = false; break; }   // owned by an earlier exception
+    }
+}
+
+// Phase 2: one wave per selected word, waves loop over the list (its length
+// is on the device), so every wave reaches the end of the list and exits.
+__global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
+    // membership of every byte in the class of (pattern p, position j), at
+    // p * maxlen + j ('.' all ones), staged in LDS once per block: the window
+    // tests below then touch no global table
+    __shared__ uint32_t s_memb[OTH_MAX_POS][8];
+    for (int i = threadIdx.x; i < a.P * a.maxlen * 8; i += blockDim.x) {
+        const int e = i >> 3, p = e / a.maxlen, j = e % a.maxlen;
+        uint32_t m = 0;
+        if (j < a.lengths[p]) {
             const int cl = a.pos_class[p * 64 + j];
-            if (a.class_any[cl]) continue;
-            uint8_t ch;
-            if (owned_type) {
-                ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
-            } else {
-                const uint2 hv = a.nuc.hl[l.word];
-                ch = (uint8_t)((0x54474341u >> (8 * ((((hv.x >> l.bit) & 1) << 1) | ((hv.y >> l.bit) & 1)))) & 0xff);
-            }
-            if (!((a.class_bytes[cl * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
+            m = a.class_any[cl] ? ~0u : a.class_bytes[cl * 8 + (i & 7)];
         }
-        if (ok) {
-            const uint32_t slot = (uint32_t)(a.pattern_base + p);
-            const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
-            const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
-            if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
-        }
+        s_memb[e][i & 7] = m;
+    }
+    __syncthreads();
+    // items_per_wave (1, 2 or 4) items share a wave, 64 / items_per_wave
+    // lanes each (an item's window span fits them): more gathers in flight
+    const int G = a.items_per_wave, lanes = 64 / G;
+    const int lane = (threadIdx.x & 63) % lanes, slice = (threadIdx.x & 63) / lanes;
+    const uint32_t nsel = *a.nsel, nitems = gridDim.x * (blockDim.x >> 6) * G;
+    for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * G + slice; it < nsel; it += nitems) {
+        const OtherSel sv = a.sel[it];
+        other_windows(a, s_memb, sv.word / TILE_WORDS, logical_word((uint32_t)(sv.word % TILE_WORDS)), sv.bits, lane,
+                      lanes, slice);
     }
 }
 
@@ -325,6 +380,7 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
 
 constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
+static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
 
 // Hit records of pm_linear_jit -> hit keys.  A record is (tile, lane, step,
 // pattern) and the live mask of that window word, exact for the ACGT fast
@@ -351,6 +407,8 @@ struct ExpandArgs {
     const uint64_t* slot_base;
     const uint32_t* slot_cap;
     uint32_t nwg, nout, group, tiles_per_wg;
+    int accumulate;   // counters zeroed before the scan, k_linear_others appending concurrently:
+                      // slots reserved on the global counters
 };
 
 // One block per output segment (`group` workgroups x 4 wave segments); each
@@ -394,6 +452,18 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
             const uint32_t slot = (uint32_t)a.pattern_base + p;
             const uint32_t cap = a.slot_cap[slot];
             uint64_t* dst = a.out + a.slot_base[slot] + (uint64_t)og * cap;
+            if (a.accumulate) {
+                // k_linear_others appends to the same lists concurrently:
+                // reserve each record's slots on the global counter
+                uint32_t v = 0;
+                for (uint32_t t = live; t; t &= t - 1)
+                    if (pos_of(tile, w0, __builtin_ctz(t)) < a.n) v |= t & (0u - t);
+                if (!v) continue;
+                uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nout + og], (uint32_t)__popc(v));
+                for (; v; v &= v - 1, ++o)
+                    if (o < cap) dst[o] = ((uint64_t)slot << 48) | pos_of(tile, w0, __builtin_ctz(v));
+                continue;
+            }
             for (; live; live &= live - 1) {
                 const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
                 if (pos >= a.n) continue;
@@ -404,7 +474,8 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
     }
     __syncthreads();
     // k_linear_others (launched after) appends to the same counters
-    if ((int)threadIdx.x < a.P) a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nout + og] = cnt_p[threadIdx.x];
+    if (!a.accumulate && (int)threadIdx.x < a.P)
+        a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nout + og] = cnt_p[threadIdx.x];
 }
 
 __global__ void k_linear_lens(const uint64_t* __restrict__ keys, uint64_t n, const int32_t* __restrict__ lengths,
@@ -1027,7 +1098,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
             for (int j = 0; j < lengths[p]; ++j) require(pos_class[64 * p + j] < n_classes, "class id out of range");
         }
-        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) == 0, "bad flags");
+        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS)) == 0, "bad flags");
         DeviceGuard g(db->device);
         hipStream_t s = db->stream;
         const bool jit = use_jit(db);
@@ -1175,7 +1246,16 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 (void)o_over;
                 // no counter memset: k_linear_expand stores every (pattern,
                 // segment) count, the first launch zeroes the aux counter
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
+                // the exception pass runs after the expansion on the same
+                // stream; PM_EXC_CONCURRENT=1 runs it on its own stream,
+                // concurrently with the specialized scan (its windows are
+                // independent of the scan, only the hit-list counters are
+                // shared) -- measured no faster: the two contend for the CUs
+                const bool exc = db->nflag && (db->n_oth_words || cross);
+                const bool exc_conc = exc && env_flag("PM_EXC_CONCURRENT", false);
+                // without the concurrent pass no counter memset: the expansion
+                // stores every (pattern, segment) count
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/exc_conc);
                 uint32_t* d_over = sb.cnt + sb.nbins;   // the sink's aux counter
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
@@ -1189,6 +1269,43 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 // expansion, others and the sort: on the post stream after the
                 // kernel's event when this scan returns pipelined in one launch
                 const hipStream_t xs = spec_async && offload ? post_stream(db) : s;
+                auto launch_others = [&](const Chunk& ch, hipStream_t os) {
+                    const bool use_edge = edge_ok(ch.base, ch.P);
+                    // line-bounded: only words with an "other" byte can own a window
+                    const uint32_t* edge = cross ? db->xedge : db->xedge_oth;
+                    const uint64_t nedge = cross ? db->nedge : db->nedge_oth;
+                    const uint64_t words = use_edge ? nedge : db->nflag;
+                    if (!words) return;
+                    uint8_t* ws = static_cast<uint8_t*>(reserve(db, db->ws_oth, 256 + words * sizeof(OtherSel)));
+                    OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
+                                  d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
+                                  d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
+                                  cross ? 1 : 0, skip_ok(ch.base, ch.P) ? 1 : 0, d_up + o_jsel + 4 * ch.base,
+                                  *std::max_element(lengths + ch.base, lengths + ch.base + ch.P),
+                                  use_edge ? 1 : 0, db->xint, edge, nedge,
+                                  reinterpret_cast<OtherSel*>(ws + 256), reinterpret_cast<uint32_t*>(ws),
+                                  sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tpw * group), 1};
+                    const int span = 2 * oa.maxlen - 1;
+                    oa.items_per_wave = span <= 16 ? 4 : span <= 32 ? 2 : 1;
+                    // phase 1: one thread per candidate word selects the
+                    // exception bits that can own a live window; phase 2:
+                    // persistent waves evaluate them
+                    HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
+                    hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
+                    HIPCHK(hipGetLastError());
+                    hipLaunchKernelGGL(k_linear_others, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
+                                       dim3(256), 0, os, oa);
+                    HIPCHK(hipGetLastError());
+                };
+                if (exc_conc) {
+                    // forked after the counter memset and the table uploads
+                    // (both on s, behind lane_begin's wait for the lane)
+                    const hipStream_t es = exc_stream(db);
+                    HIPCHK(hipEventRecord(db->exc_fork, s));
+                    HIPCHK(hipStreamWaitEvent(es, db->exc_fork, 0));
+                    for (const Chunk& ch : chunks) launch_others(ch, es);
+                    HIPCHK(hipEventRecord(db->exc_join, es));
+                }
                 for (const Chunk& ch : chunks) {
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
@@ -1201,24 +1318,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
-                                  (uint32_t)tpw};
+                                  (uint32_t)tpw, exc_conc ? 1 : 0};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
-                    if (db->nflag && (db->n_oth_words || cross)) {
-                        OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
-                                      d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
-                                      d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                      cross ? 1 : 0, skip_ok(ch.base, ch.P) ? 1 : 0, d_up + o_jsel + 4 * ch.base,
-                                      *std::max_element(lengths + ch.base, lengths + ch.base + ch.P),
-                                      edge_ok(ch.base, ch.P) ? 1 : 0, db->xint, db->xedge, db->nedge,
-                                      sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tpw * group)};
-                        // one wave per flagged word (per edge word: runs of N skipped)
-                        const uint64_t words = oa.use_edge ? db->nedge : db->nflag;
-                        if (words)
-                            hipLaunchKernelGGL(k_linear_others, dim3(blocks_for(words * 64, 256)), dim3(256), 0, xs, oa);
-                        HIPCHK(hipGetLastError());
-                    }
+                    if (exc && !exc_conc) launch_others(ch, xs);
                 }
+                if (exc_conc) HIPCHK(hipStreamWaitEvent(xs, db->exc_join, 0));
                 if (spec_async) {
                     // pipelined: the speculative sort also writes the bin
                     // counts into mapped pinned memory (no copy), an event

@@ -302,7 +302,7 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
                                 uint64_t last, int max_len, int min_len, int k, int errs, int pattern_id,
                                 int flags, pm_hits** out) {
     return guarded([&] {
-        require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) == 0, "bad flags");
+        require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS)) == 0, "bad flags");
         require(db != nullptr, "db is NULL");
         std::lock_guard<std::recursive_mutex> lk(db->mu);
         require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");

@@ -46,12 +46,17 @@ REPORT_NRGREP = "nrgrep"   # what nrgrep_coords prints (non-overlapping, first f
 REPORT_ALL = "all"         # every candidate start (shortest end)
 
 
-def report_flags(prog: Program, report: str = REPORT_NRGREP) -> int:
-    """PM_REPORT_* / PM_ANCHOR_* flags of one program (include/patmatch_hip.h)."""
+def report_flags(prog: Program, report: str = REPORT_NRGREP, keep_headers: bool = False,
+                 start_anchor: bool = True) -> int:
+    """PM_REPORT_* / PM_ANCHOR_* / PM_KEEP_HEADERS flags of one program
+    (include/patmatch_hip.h).  ``start_anchor=False`` leaves the '^' check to
+    the caller (shards.py re-chains candidates across pieces of a file)."""
     if report not in (REPORT_NRGREP, REPORT_ALL):
         raise ValueError("report must be %r or %r" % (REPORT_NRGREP, REPORT_ALL))
     f = _lib.PM_REPORT_NRGREP if report == REPORT_NRGREP else _lib.PM_REPORT_ALL
-    if prog.anchor_start:
+    if keep_headers:
+        f |= _lib.PM_KEEP_HEADERS
+    if prog.anchor_start and start_anchor:
         f |= _lib.PM_ANCHOR_START
     if prog.anchor_end:
         f |= _lib.PM_ANCHOR_END
@@ -300,11 +305,14 @@ def _same_automaton(a: Program, b: Program) -> bool:
 
 
 def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str = "ids",
-         report: str = REPORT_NRGREP):
+         report: str = REPORT_NRGREP, keep_headers: bool = False, start_anchor: bool = True):
     """Scan all programs; returns ([(beg, end) arrays per program], kernel_ms).
 
     ``report``: "nrgrep" (default) = exactly the matches nrgrep_coords prints
     (one run per program), "all" = every candidate start.
+    ``keep_headers``: also return hits starting on a header line (they take
+    part in the report rule; process_output drops them).  ``start_anchor``:
+    False = no '^' check (the caller applies it).
     Programs equal as automata (a palindromic site and its reverse
     complement, e.g. GAATTC) are scanned once and their hits reported for
     each of them, as the reference's two nrgrep runs would.
@@ -321,7 +329,7 @@ def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str 
     groups = {}
     for i in range(len(progs)):
         if routes[i] == "linear" and canonical[i] == i:
-            groups.setdefault(report_flags(progs[i], report), []).append(i)
+            groups.setdefault(report_flags(progs[i], report, keep_headers, start_anchor), []).append(i)
     for flags, linear_ids in groups.items():
         hits = scan_linear(db, [progs[i] for i in linear_ids], k, flags)
         total_ms += hits.kernel_ms
@@ -329,7 +337,7 @@ def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str 
             results[i] = hits.for_pattern(slot)
     for i in range(len(progs)):
         if routes[i] == "nfa" and canonical[i] == i:
-            hits = scan_nfa(db, progs[i], k, 0, types, report_flags(progs[i], report))
+            hits = scan_nfa(db, progs[i], k, 0, types, report_flags(progs[i], report, keep_headers, start_anchor))
             total_ms += hits.kernel_ms
             results[i] = (hits.beg, hits.end)
     for i in range(len(progs)):

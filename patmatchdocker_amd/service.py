@@ -81,16 +81,21 @@ class _DatabaseCache:
         self._lock = threading.Lock()
         self._dbs: Dict[Tuple[str, int], _Entry] = {}
 
-    def _acquire(self, path: str, device: int) -> _Entry:
+    def _acquire(self, path: str, device: int, shard: Optional[Tuple[int, int]] = None) -> _Entry:
         st = os.stat(path)
         stamp = (st.st_mtime_ns, st.st_size)
-        key = (os.path.realpath(path), device)
+        key = (os.path.realpath(path), device, shard)
         with self._lock:
             ent = self._dbs.get(key)
             if ent is None or ent.stamp != stamp:
                 if ent is not None:
                     self._retire(ent)
-                ent = _Entry(stamp, engine.SequenceDatabase.from_file(path, device=device))
+                if shard is None:
+                    db = engine.SequenceDatabase.from_file(path, device=device)
+                else:   # this rank's record-aligned piece (shards.py)
+                    from . import shards
+                    db = shards.ShardedDatabase.from_file(path, shard[0], shard[1], device=device)
+                ent = _Entry(stamp, db)
                 self._dbs[key] = ent
             ent.users += 1
             return ent
@@ -107,21 +112,23 @@ class _DatabaseCache:
                 ent.db.close()
 
     class _Lease:
-        def __init__(self, cache, path, device):
-            self.cache, self.path, self.device, self.ent = cache, path, device, None
+        def __init__(self, cache, path, device, shard=None):
+            self.cache, self.path, self.device, self.shard, self.ent = cache, path, device, shard, None
 
         def __enter__(self):
-            self.ent = self.cache._acquire(self.path, self.device)
+            self.ent = self.cache._acquire(self.path, self.device, self.shard)
             return self.ent.db
 
         def __exit__(self, *exc):
             self.cache._release(self.ent)
             return False
 
-    def lease(self, path: str, device: int = 0):
+    def lease(self, path: str, device: int = 0, shard: Optional[Tuple[int, int]] = None):
         """``with DATABASES.lease(path) as db:`` -- the database stays open
-        until the block ends, even if the file is replaced meanwhile."""
-        return self._Lease(self, path, device)
+        until the block ends, even if the file is replaced meanwhile.
+        ``shard=(world, rank)``: this rank's piece of the file
+        (:class:`~patmatchdocker_amd.shards.ShardedDatabase`)."""
+        return self._Lease(self, path, device, shard)
 
     def get(self, path: str, device: int = 0):
         """The resident database (no lease: for single-threaded callers)."""
@@ -176,12 +183,34 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
     outputs = [""] * len(patterns)
     if not progs:
         return outputs
+    world, rank = _world()
+    if world > 1:
+        # one process per GPU (torchrun): every rank scans its record-aligned
+        # piece of the file, the reports are joined across the cuts and
+        # gathered, every rank returns the whole output
+        from . import shards
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+        with DATABASES.lease(datafile, device, shard=(world, rank)) as piece:
+            results = shards.scan_sharded(piece, progs, k=k, types=types)
+            for slot, prog, (beg, end) in zip(slots, progs, results):
+                outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(piece, beg, end)
+        return outputs
     with DATABASES.lease(datafile) as db:
         results, _ = engine.scan(db, progs, k=k, types=types)
         for slot, prog, (beg, end) in zip(slots, progs, results):
             # the binary's stdout: searchPreproc's engine banner, then the hits
             outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(db, beg, end)
     return outputs
+
+
+def _world() -> Tuple[int, int]:
+    """(world size, rank) of the torch.distributed job this process is in;
+    (1, 0) outside one."""
+    import sys
+    dist = getattr(sys.modules.get("torch"), "distributed", None)   # no torch import for a 1-process server
+    if dist is not None and dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
 
 
 # ---------------------------------------------------------------------------

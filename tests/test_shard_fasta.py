@@ -1,0 +1,177 @@
+"""Real-FASTA sharding (shards.split_fasta / scan_sharded): a file cut at
+header lines over world_size 2 and 3 gloo ranks gives exactly the
+single-process report, including reports that cross a cut (the simple
+engine's windows run over '\\n' into the next record, patmatch.py:733-743
+scans the whole file in one process).
+
+The per-piece scans are the oracle here (CPU, no GPU); the same protocol on
+the GPU engine is tests/test_gpu_shards.py.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from patmatchdocker_amd import shards
+
+# nrgrep patterns (compiled directly): cross-line windows ('.' takes '\n'),
+# a dense all-'.' window whose chain phase differs across a cut, anchors,
+# and line-bounded ones (k > 0 / no '\n' class) that never cross
+CASES = [("....", 0), ("AC..", 0), ("A.C", 0), ("^A..", 0), ("G..$", 0), ("GAATTC", 0),
+         ("TATA", 1), ("ACGTAC", 2), ("A..T", 1)]
+
+
+def make_fasta(seed=5, n_records=9):
+    rnd = random.Random(seed)
+    out = []
+    for r in range(n_records):
+        out.append(">r%d %s\n" % (r, "x" * rnd.randint(0, 3)))
+        n = rnd.randint(20, 300)
+        seq = "".join(rnd.choice("ACGT" if rnd.random() < 0.97 else "NR") for _ in range(n))
+        for i in range(0, n, 60):
+            out.append(seq[i:i + 60] + "\n")
+        if r % 3 == 1:
+            out.append("AC\n")   # a record ending in "AC": 'AC..' runs over the next header
+    return "".join(out).encode()
+
+
+class OracleScanner:
+    """scan_sharded's two scans, restated on the CPU oracle over the piece
+    (its bytes + halo, local offsets)."""
+
+    def __init__(self, piece):
+        self.text = piece.raw[piece.beg:piece.stop]
+
+    def reported(self, progs, k, types):
+        from oracle import oracle
+        out = []
+        for p in progs:
+            hits = oracle.scan_reported(self.text, p, k, types)
+            out.append((np.array([b for b, _ in hits], dtype=np.int64), np.array([e for _, e in hits], dtype=np.int64)))
+        return out
+
+    def candidates(self, prog, k, types):
+        from oracle import oracle
+        hits = oracle.scan_candidates(self.text, prog, k, types)
+        return (np.array([b for b, _ in hits], dtype=np.int64), np.array([e for _, e in hits], dtype=np.int64))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, data, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from patmatchdocker_amd.regex import compile_pattern
+        piece = shards.ShardedDatabase(data, world, rank, open_db=False)
+        res = []
+        for pat, k in CASES:
+            prog = compile_pattern(pat, ignore_case=True)
+            (b, e), = shards.scan_sharded(piece, [prog], k, "s", scanner=OracleScanner(piece))
+            res.append(list(zip(b.tolist(), e.tolist())))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_fasta_cuts_at_headers():
+    data = make_fasta()
+    starts, _ = shards.header_lines(data)
+    for world in (1, 2, 3, 8, 40):
+        rs = shards.split_fasta(data, world)
+        assert rs[0][0] == 0 and rs[-1][1] == len(data)
+        assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+        for b, e in rs[1:]:
+            assert b == len(data) or b in starts.tolist()
+
+
+def test_header_lines_follow_the_index_script():
+    data = b">a\nAC\n> notname\nGG\n>b\tx\n>\n>c"
+    hs, he = shards.header_lines(data)
+    assert hs.tolist() == [0, 19, 26]
+    assert he.tolist() == [2, 23, 28]
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_scan_equals_whole_file(world):
+    from oracle import oracle
+    from patmatchdocker_amd.regex import compile_pattern
+    data = make_fasta()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    crossed = 0
+    for i, (pat, k) in enumerate(CASES):
+        want = oracle.scan_reported(data, compile_pattern(pat, ignore_case=True), k, "s", skip_headers=True)
+        for r in range(world):
+            assert got[r][i] == want, (pat, k, r)
+        cuts = [b for b, _ in shards.split_fasta(data, world)[1:]]
+        crossed += any(b < c < e for b, e in want for c in cuts)
+    assert crossed   # the cross-cut re-chaining was exercised
+
+
+SERVICE_PATTERNS = ["AC..", "....", "TATA", "GAATTC", "A..T"]
+
+
+def _service_worker(rank, world, port, path, option, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from patmatchdocker_amd import service
+        # the pieces are scanned by the oracle (no GPU here)
+        shards.ShardedDatabase.from_file = classmethod(
+            lambda cls, p, w, r, device=0: cls(open(p, "rb").read(), w, r, device, open_db=False))
+        shards.ShardedDatabase.scanner = lambda self: OracleScanner(self)
+        q.put((rank, service.search_output(SERVICE_PATTERNS, option, path)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("option", ["0", "1s"])
+def test_service_search_output_multi_rank(tmp_path, option):
+    """service.search_output inside a world_size-2 job: both ranks return the
+    single-process output (engine banner + reported hits, header starts
+    dropped) for the whole file."""
+    from oracle import oracle
+    from patmatchdocker_amd.regex import compile_pattern, engine_banner
+    data = make_fasta(seed=11, n_records=12)
+    path = str(tmp_path / "db.fasta")
+    open(path, "wb").write(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_service_worker, args=(r, 2, port, path, option, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    k = int(option[0])
+    for i, pat in enumerate(SERVICE_PATTERNS):
+        prog = compile_pattern(pat, ignore_case=True)
+        hits = oracle.scan_reported(data, prog, k, option[1:] or "idst", skip_headers=True)
+        want = engine_banner(prog, k) + "\n" + "".join(
+            "[%d, %d]: %s\n" % (b, e, data[b:e].decode("latin-1")) for b, e in hits)
+        assert got[0][i] == want and got[1][i] == want, pat

@@ -35,8 +35,10 @@ extern "C" {
 #define PM_ALPHA_NUC 0     /* 2-bit A/C/G/T planes + sparse exceptions    */
 #define PM_ALPHA_BYTE 1    /* one folded byte per residue (peptides)      */
 
-#define PM_MAX_POSITIONS 64
-#define PM_MAX_K 3         /* errors handled by the GPU kernels           */
+#define PM_MAX_POSITIONS 256        /* automaton positions (pm_scan_nfa_wide)   */
+#define PM_MAX_K 15                 /* errors (pm_scan_nfa_wide; <= 7 above 128 positions) */
+#define PM_MAX_LINEAR_POSITIONS 64  /* pattern length of pm_scan_linear          */
+#define PM_MAX_LINEAR_K 3           /* substitutions of pm_scan_linear           */
 
 typedef struct pm_db pm_db;        /* device-resident sequence database   */
 typedef struct pm_hits pm_hits;    /* device/host hit list of one scan    */
@@ -85,6 +87,10 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
 #define PM_ANCHOR_START 2
 #define PM_ANCHOR_END 4
 #define PM_KEEP_HEADERS 8
+/* pm_scan_nfa_wide only: nrgrep's simple engine (k = 0, a class sequence):
+ * windows are checked against the file's own bytes and may span a line
+ * break (pm_scan_linear decides this by itself).                          */
+#define PM_CROSS_LINES 16
 
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched
@@ -150,6 +156,16 @@ int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* fol
 int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,
                      uint64_t first, uint64_t last, int max_len, int min_len, int k, int errs,
                      int pattern_id, int flags, pm_hits** out);
+
+/* pm_scan_nfa_errs for automata of up to PM_MAX_POSITIONS positions and up
+ * to PM_MAX_K errors (a long oligo, an unrolled x(m,n), `-k 5`): position
+ * sets are `words` 64-bit words (position i = bit i % 64 of word i / 64):
+ * byte_mask[256 * words], follow[m * words], first[words], last[words].
+ * words = ceil(m / 64) <= 4; k <= 7 when words == 4.  max_len is not
+ * bounded.  flags may add PM_CROSS_LINES. */
+int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
+                     const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
+                     int errs, int pattern_id, int flags, pm_hits** out);
 
 /* --- hits --------------------------------------------------------------- */
 int pm_hits_count(const pm_hits* h, uint64_t* count);

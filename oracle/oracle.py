@@ -221,7 +221,9 @@ def record_index(text: bytes):
 # pure-Python restatement (explicit (position, errors) state sets), small n
 # ---------------------------------------------------------------------------
 
-def scan_py(text: bytes, prog, k: int = 0, types: str = "ids"):
+def scan_py(text: bytes, prog, k: int = 0, types: str = "ids", to_line_end: bool = False):
+    """Every start of a line-bounded match and its shortest end (any number
+    of positions); ``to_line_end``: the end must be the line end ('$')."""
     types = types if k else ""
     fold = (lambda c: c - 32 if 97 <= c <= 122 else c) if prog.ignore_case else (lambda c: c)
     START = -1
@@ -263,13 +265,30 @@ def scan_py(text: bytes, prog, k: int = 0, types: str = "ids"):
                     if "i" in types:
                         put(st, e + 1)
                 cur = closure(nxt)
-                if any(st != START and prog.last >> st & 1 for st in cur):
+                if any(st != START and prog.last >> st & 1 for st in cur) and (not to_line_end or p + 1 == len(line)):
                     hits.append((pos + s, pos + p + 1))
                     break
                 if not cur:
                     break
         pos += len(line) + 1
     return hits
+
+
+def scan_py_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False):
+    """What nrgrep_coords prints for a line-bounded engine (k > 0, or k = 0
+    with no class accepting '\n'), restated in pure Python for automata of
+    any size (pm_oracle.c holds 64 positions): the candidates of scan_py,
+    the report rule (first found wins, resume at its end) and the '^'
+    check (a line start or the resume point, pmo_scan2)."""
+    out, R = [], 0
+    for b, e in scan_py(text, prog, k, types, to_line_end=prog.anchor_end):
+        if b < R:
+            continue
+        if prog.anchor_start and not (b == R or b == 0 or text[b - 1] == 10):
+            continue
+        out.append((b, e))
+        R = e
+    return drop_header_hits(text, out) if skip_headers else out
 
 
 # ---------------------------------------------------------------------------

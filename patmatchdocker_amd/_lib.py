@@ -16,9 +16,13 @@ LIB_PATH = os.path.join(_HERE, "libpatmatch_hip.so")
 PM_ALPHA_NUC = 0
 PM_ALPHA_BYTE = 1
 PM_E_UNSUPPORTED = -4
-PM_MAX_K = 3
+PM_MAX_K = 15                 # errors, general patterns (<= 7 above 128 positions)
+PM_MAX_POSITIONS = 256        # automaton positions, general patterns
+PM_MAX_LINEAR_K = 3           # substitutions, fixed-length kernel
+PM_MAX_LINEAR_POSITIONS = 64  # pattern length, fixed-length kernel
 PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
 PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END, PM_KEEP_HEADERS = 0, 1, 2, 4, 8
+PM_CROSS_LINES = 16
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -26,7 +30,7 @@ EXPORTED = (
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
-    "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async",
+    "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
 )
 
 
@@ -67,6 +71,8 @@ def _declare(lib):
                                 ctypes.c_int, PP]
     lib.pm_scan_nfa_errs.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
+    lib.pm_scan_nfa_wide.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_hits_count.argtypes = [P, pu64]
     lib.pm_hits_copy.argtypes = [P, P, P, P, u64]
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]

@@ -1093,9 +1093,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 "null argument");
         require(n_patterns >= 1 && n_patterns <= 4096, "n_patterns out of range");
         require(n_classes >= 1 && n_classes <= 256, "n_classes out of range");
-        require(k >= 0 && k <= PM_MAX_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
+        require(k >= 0 && k <= PM_MAX_LINEAR_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p) {
-            require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
+            require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
             for (int j = 0; j < lengths[p]; ++j) require(pos_class[64 * p + j] < n_classes, "class id out of range");
         }
         require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS)) == 0, "bad flags");
@@ -1557,9 +1557,9 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
         require(lengths && pos_class && class_acgt && class_is_any, "null argument");
         require(n_patterns >= 1 && n_patterns <= JIT_MAX_P, "n_patterns out of range for one specialized kernel");
         require(n_classes >= 1 && n_classes <= 256, "n_classes out of range");
-        require(k >= 0 && k <= PM_MAX_K, "k out of range", PM_E_UNSUPPORTED);
+        require(k >= 0 && k <= PM_MAX_LINEAR_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)
-            require(lengths[p] >= 1 && lengths[p] <= PM_MAX_POSITIONS, "pattern length out of range");
+            require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
         const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4);
         const std::vector<char> code = jit_compile(src);
         if (code_bytes) *code_bytes = code.size();

@@ -25,32 +25,38 @@
 namespace pm {
 namespace {
 
+constexpr int NFA_MAXW = PM_MAX_POSITIONS / 64;   // state words
+constexpr int NFA_MAXR = PM_MAX_K + 1;             // error rows
+
 struct NfaArgs {
     NucView nuc;
-    const uint8_t* bytes;
-    const uint64_t* prec;     // [nt][256]   positions preceding the set
-    const uint64_t* follow;   // [nt][256]   positions following the set
-    const uint64_t* bmask;    // [256]
-    uint64_t first, last;
-    int nt;
+    const uint8_t* bytes;       // BYTE alphabet (headers stored as '\n')
+    const uint8_t* bytes_raw;   // BYTE alphabet, the file's own bytes (cross mode)
+    const uint64_t* prec;       // [nt][2^S][W] positions preceding a slice value
+    const uint64_t* follow;     // [nt][2^S][W] positions following it
+    const uint64_t* bmask;      // [256][W]
+    uint64_t first[NFA_MAXW], last[NFA_MAXW], mmask[NFA_MAXW];
+    int nt;                     // slices of S = 8 (W = 1) or 4 (W > 1) positions
     int halo;
-    int chunk;                // positions per lane
+    int chunk;                  // positions per lane
     uint64_t n;
     uint64_t nchunks;
     int pattern_id;
-    int end_anchor;           // '$': the verify's end must be a line end
+    int end_anchor;             // '$': the verify's end must be a line end
+    int cross;                  // nrgrep's simple engine (k = 0 class sequence): windows span lines
+    int k;                      // errors (<= the kernel's row count - 1)
     Sink sink;
-    int errs;                 // PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB
-    uint64_t rev_pre[4];      // reverse: prec(S[j]) | (I[j] ? last : 0) for the injected start config
-    uint64_t rev_ins[4];      // reverse: S[j] (insertion source rows of the injected config)
-    uint64_t fwd_del[4];      // forward: deletion closure of the start config (rows of R)
+    int errs;                   // PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB
+    uint64_t rev_pre[NFA_MAXR][NFA_MAXW];   // reverse: prec(S[j]) | (I[j] ? last : 0) for the injected start config
+    uint64_t rev_ins[NFA_MAXR][NFA_MAXW];   // reverse: S[j] (insertion source rows of the injected config)
+    uint64_t fwd_del[NFA_MAXR][NFA_MAXW];   // forward: deletion closure of the start config (rows of R)
     // unbounded patterns: reverse state entering each chunk from the right
-    // (rows at stride 4), found by k_nfa_carry; null = start from the halo
+    // ((k+1) * W words per chunk), found by k_nfa_carry; null = start from the halo
     const uint64_t* in_state;
+    int st_stride;
     // a plain class sequence (follow(i) = {i+1}): transitions are shifts
-    // instead of table lookups; mmask = the m position bits
+    // instead of table lookups
     int shift_only;
-    uint64_t mmask;
     // verify
     const uint64_t* starts;
     uint64_t nstarts;
@@ -58,83 +64,190 @@ struct NfaArgs {
     int max_len;
 };
 
-__device__ inline uint64_t table_or(const uint64_t* __restrict__ tab, uint64_t set, int nt) {
-    uint64_t acc = 0;
-    for (int t = 0; t < nt; ++t) acc |= tab[t * 256 + ((set >> (8 * t)) & 255)];
+// A set of automaton positions: W 64-bit words (position i = bit i % 64 of
+// word i / 64).
+template <int W>
+struct Bits {
+    uint64_t w[W];
+};
+template <int W>
+__device__ inline Bits<W> bits_zero() {
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = 0;
+    return r;
+}
+template <int W>
+__device__ inline Bits<W> bits_of(const uint64_t* p) {
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = p[i];
+    return r;
+}
+template <int W>
+__device__ inline Bits<W> operator|(const Bits<W>& a, const Bits<W>& b) {
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = a.w[i] | b.w[i];
+    return r;
+}
+template <int W>
+__device__ inline Bits<W> operator&(const Bits<W>& a, const Bits<W>& b) {
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = a.w[i] & b.w[i];
+    return r;
+}
+template <int W>
+__device__ inline Bits<W> mask_if(const Bits<W>& a, bool keep) {
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = keep ? a.w[i] : 0ull;
+    return r;
+}
+template <int W>
+__device__ inline bool any_of(const Bits<W>& a) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) x |= a.w[i];
+    return x != 0;
+}
+template <int W>
+__device__ inline bool meets(const Bits<W>& a, const uint64_t* m) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) x |= a.w[i] & m[i];
+    return x != 0;
+}
+
+// transitions of a set: OR of per-slice table rows
+template <int W>
+__device__ inline Bits<W> table_or(const uint64_t* __restrict__ tab, const Bits<W>& set, int nt) {
+    Bits<W> acc = bits_zero<W>();
+    if constexpr (W == 1) {
+        for (int t = 0; t < nt; ++t) acc.w[0] |= tab[t * 256 + ((set.w[0] >> (8 * t)) & 255)];
+    } else {
+        // 4-position slices, only the non-empty ones (states are sparse)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            uint64_t x = set.w[i];
+            while (x) {
+                const int t = i * 16 + (__builtin_ctzll(x) >> 2);
+                const uint64_t* row = tab + ((uint64_t)t * 16 + ((set.w[i] >> ((t & 15) * 4)) & 15)) * W;
+#pragma unroll
+                for (int q = 0; q < W; ++q) acc.w[q] |= row[q];
+                x &= ~(15ull << ((t & 15) * 4));
+            }
+        }
+    }
     return acc;
 }
 // positions preceding / following a set (reverse / forward transitions)
-__device__ inline uint64_t prec_of(const NfaArgs& a, const uint64_t* __restrict__ s_prec, uint64_t set) {
-    return a.shift_only ? set >> 1 : table_or(s_prec, set, a.nt);
+template <int W>
+__device__ inline Bits<W> prec_of(const NfaArgs& a, const uint64_t* __restrict__ s_prec, const Bits<W>& set) {
+    if (!a.shift_only) return table_or<W>(s_prec, set, a.nt);
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = (set.w[i] >> 1) | (i + 1 < W ? set.w[i + 1] << 63 : 0ull);
+    return r;
 }
-__device__ inline uint64_t fol_of(const NfaArgs& a, const uint64_t* __restrict__ s_fol, uint64_t set) {
-    return a.shift_only ? (set << 1) & a.mmask : table_or(s_fol, set, a.nt);
+template <int W>
+__device__ inline Bits<W> fol_of(const NfaArgs& a, const uint64_t* __restrict__ s_fol, const Bits<W>& set) {
+    if (!a.shift_only) return table_or<W>(s_fol, set, a.nt);
+    Bits<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = ((set.w[i] << 1) | (i > 0 ? set.w[i - 1] >> 63 : 0ull)) & a.mmask[i];
+    return r;
 }
 
 // One character of the reverse search (right to left).  Substitution-only
-// patterns (the common case) take the short form.
-template <int K>
-__device__ inline void nfa_rev_step(uint64_t (&R)[K + 1], uint64_t bc, uint64_t nb,
+// patterns (the common case) take the short form.  Rows above a.k stay empty.
+template <int K, int W>
+__device__ inline void nfa_rev_step(Bits<W> (&R)[K + 1], const Bits<W>& bc, bool nb,
                                     const uint64_t* __restrict__ s_prec, const NfaArgs& a) {
-    uint64_t A[K + 1];
+    Bits<W> A[K + 1];
 #pragma unroll
-    for (int j = 0; j <= K; ++j) A[j] = prec_of(a, s_prec, R[j]) | a.rev_pre[j];
+    for (int j = 0; j <= K; ++j) A[j] = prec_of<W>(a, s_prec, R[j]) | bits_of<W>(a.rev_pre[j]);
     if (a.errs == PM_ERR_SUB) {
 #pragma unroll
-        for (int j = K; j >= 0; --j) R[j] = (A[j] & bc) | (j > 0 ? (A[j - 1] & nb) : 0ull);
+        for (int j = K; j >= 0; --j)
+            R[j] = mask_if<W>((A[j] & bc) | (j > 0 ? mask_if<W>(A[j - 1], nb) : bits_zero<W>()), j <= a.k);
         return;
     }
-    uint64_t N[K + 1];
+    Bits<W> N[K + 1];
 #pragma unroll
     for (int j = 0; j <= K; ++j) {
         N[j] = A[j] & bc;
         if (j > 0) {
-            if (a.errs & PM_ERR_SUB) N[j] |= A[j - 1] & nb;
-            if (a.errs & PM_ERR_INS) N[j] |= (R[j - 1] | a.rev_ins[j - 1]) & nb;
+            if (a.errs & PM_ERR_SUB) N[j] = N[j] | mask_if<W>(A[j - 1], nb);
+            if (a.errs & PM_ERR_INS) N[j] = N[j] | mask_if<W>(R[j - 1] | bits_of<W>(a.rev_ins[j - 1]), nb);
         }
     }
     if (a.errs & PM_ERR_DEL) {
         // ninit[j] (j >= 1) = an insertion-kept start; row 0's init is consumed
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            N[j + 1] |= prec_of(a, s_prec, N[j]) | ((j >= 1 && (a.errs & PM_ERR_INS) && nb) ? a.last : 0ull);
+            N[j + 1] = N[j + 1] | prec_of<W>(a, s_prec, N[j]) |
+                       mask_if<W>(bits_of<W>(a.last), j >= 1 && (a.errs & PM_ERR_INS) && nb);
     }
 #pragma unroll
-    for (int j = 0; j <= K; ++j) R[j] = N[j];
+    for (int j = 0; j <= K; ++j) R[j] = mask_if<W>(N[j], j <= a.k);
 }
 
+// Text byte at p and whether it ends every partial match: past the end of
+// the file always; a line break unless nrgrep's simple engine runs (cross:
+// the file's own bytes, header lines included).
 template <bool NUC>
-__device__ inline uint8_t char_at(const NfaArgs& a, uint64_t p) {
-    if constexpr (NUC) return nuc_char_at(a.nuc, p);
-    else return a.bytes[p];
+__device__ inline uint8_t char_at(const NfaArgs& a, uint64_t p, bool& kill) {
+    if (p >= a.n) {
+        kill = true;
+        return (uint8_t)'\n';
+    }
+    uint8_t ch;
+    if constexpr (NUC) ch = a.cross ? nuc_raw_at(a.nuc, p) : nuc_char_at(a.nuc, p);
+    else ch = a.cross ? a.bytes_raw[p] : a.bytes[p];
+    kill = !a.cross && ch == (uint8_t)'\n';
+    return ch;
 }
 
-template <int K, bool NUC>
-__global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
-    __shared__ uint64_t s_prec[8 * 256];
-    __shared__ uint64_t s_b[256];
-    for (int i = threadIdx.x; i < a.nt * 256; i += blockDim.x) s_prec[i] = a.prec[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_b[i] = a.bmask[i];
+template <int W>
+__device__ inline void load_tables(uint64_t* s_tab, uint64_t* s_b, const uint64_t* tab, const uint64_t* bmask, int nt) {
+    const int rows = W == 1 ? 256 : 16;
+    for (int i = threadIdx.x; i < nt * rows * W; i += blockDim.x) s_tab[i] = tab[i];
+    for (int i = threadIdx.x; i < 256 * W; i += blockDim.x) s_b[i] = bmask[i];
     __syncthreads();
+}
+// LDS words of the transition tables: 8 slices x 256 (W = 1), 16 * W
+// slices x 16 x W words otherwise
+template <int W>
+constexpr int tab_words() { return W == 1 ? 8 * 256 : 16 * W * 16 * W; }
+
+template <int K, int W, bool NUC>
+__global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
+    __shared__ uint64_t s_prec[tab_words<W>()];
+    __shared__ uint64_t s_b[256 * W];
+    load_tables<W>(s_prec, s_b, a.prec, a.bmask, a.nt);
     const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = gid < a.nchunks;
     const uint64_t chunk_id = live ? gid : a.nchunks - 1;
     const uint64_t c0 = chunk_id * a.chunk;
     const uint64_t c1 = c0 + a.chunk;           // emit for [c0, c1) ∩ [0, n)
-    const uint64_t top = c1 + a.halo;           // process (top .. c0], padded storage
-    uint64_t R[K + 1];
+    const uint64_t top = c1 + a.halo;           // process (top .. c0]
+    Bits<W> R[K + 1];
 #pragma unroll
-    for (int j = 0; j <= K; ++j)
-        R[j] = (a.in_state && chunk_id + 1 < a.nchunks) ? a.in_state[(chunk_id + 1) * 4 + j] : 0ull;
+    for (int j = 0; j <= K; ++j) {
+        R[j] = bits_zero<W>();
+        if (a.in_state && chunk_id + 1 < a.nchunks && j <= a.k)
+            R[j] = bits_of<W>(a.in_state + (chunk_id + 1) * a.st_stride + j * W);
+    }
     for (uint64_t p = top; p-- > c0;) {
-        const uint8_t ch = char_at<NUC>(a, p);
-        const uint64_t bc = s_b[ch];
-        const uint64_t nb = ch == '\n' ? 0ull : ~0ull;
-        nfa_rev_step<K>(R, bc, nb, s_prec, a);
-        uint64_t any = 0;
+        bool kill;
+        const uint8_t ch = char_at<NUC>(a, p, kill);
+        nfa_rev_step<K, W>(R, bits_of<W>(s_b + ch * W), !kill, s_prec, a);
+        Bits<W> any = bits_zero<W>();
 #pragma unroll
-        for (int j = 0; j <= K; ++j) any |= R[j];
-        if (live && p < c1 && p < a.n && (any & a.first))
+        for (int j = 0; j <= K; ++j) any = any | R[j];
+        if (live && p < c1 && p < a.n && meets<W>(any, a.first))
             a.sink.push(a.sink.bin_of(0, p), ((uint64_t)a.pattern_id << 48) | p);
     }
 }
@@ -148,143 +261,389 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
 // (at most the chunks per record; a record break kills every state, so
 // patterns that die quickly converge in 1-2 rounds).  Chunks whose input did
 // not change since the previous round copy their old output.
-template <int K, bool NUC>
+template <int K, int W, bool NUC>
 __global__ __launch_bounds__(256) void k_nfa_carry(NfaArgs a, const uint64_t* __restrict__ st_old,
                                                    uint64_t* __restrict__ st_new, const uint64_t* __restrict__ in_seen,
                                                    uint64_t* __restrict__ in_now, uint32_t* changed) {
-    __shared__ uint64_t s_prec[8 * 256];
-    __shared__ uint64_t s_b[256];
-    for (int i = threadIdx.x; i < a.nt * 256; i += blockDim.x) s_prec[i] = a.prec[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_b[i] = a.bmask[i];
-    __syncthreads();
+    __shared__ uint64_t s_prec[tab_words<W>()];
+    __shared__ uint64_t s_b[256 * W];
+    load_tables<W>(s_prec, s_b, a.prec, a.bmask, a.nt);
     const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (gid >= a.nchunks) return;
     const uint64_t c0 = gid * a.chunk, c1 = c0 + a.chunk;
-    uint64_t R[K + 1];
+    const int words = (a.k + 1) * W;
+    Bits<W> R[K + 1];
     bool same = true;
 #pragma unroll
-    for (int j = 0; j <= K; ++j) {
-        R[j] = gid + 1 < a.nchunks ? st_old[(gid + 1) * 4 + j] : 0ull;
-        same &= R[j] == in_seen[gid * 4 + j];
-        in_now[gid * 4 + j] = R[j];
+    for (int j = 0; j <= K; ++j) R[j] = bits_zero<W>();
+    for (int i = 0; i < words; ++i) {
+        const uint64_t v = gid + 1 < a.nchunks ? st_old[(gid + 1) * a.st_stride + i] : 0ull;
+        same &= v == in_seen[gid * a.st_stride + i];
+        in_now[gid * a.st_stride + i] = v;
     }
-    if (same) {   // input unchanged: output unchanged
 #pragma unroll
-        for (int j = 0; j <= K; ++j) st_new[gid * 4 + j] = st_old[gid * 4 + j];
+    for (int j = 0; j <= K; ++j)
+        if (j <= a.k && gid + 1 < a.nchunks) R[j] = bits_of<W>(st_old + (gid + 1) * a.st_stride + j * W);
+    if (same) {   // input unchanged: output unchanged
+        for (int i = 0; i < words; ++i) st_new[gid * a.st_stride + i] = st_old[gid * a.st_stride + i];
         return;
     }
     for (uint64_t p = c1; p-- > c0;) {
-        const uint8_t ch = char_at<NUC>(a, p);
-        nfa_rev_step<K>(R, s_b[ch], ch == '\n' ? 0ull : ~0ull, s_prec, a);
+        bool kill;
+        const uint8_t ch = char_at<NUC>(a, p, kill);
+        nfa_rev_step<K, W>(R, bits_of<W>(s_b + ch * W), !kill, s_prec, a);
     }
     bool diff = false;
 #pragma unroll
     for (int j = 0; j <= K; ++j) {
-        diff |= R[j] != st_old[gid * 4 + j];
-        st_new[gid * 4 + j] = R[j];
+        if (j > a.k) continue;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            diff |= R[j].w[q] != st_old[gid * a.st_stride + j * W + q];
+            st_new[gid * a.st_stride + j * W + q] = R[j].w[q];
+        }
     }
     if (diff) atomicOr(changed, 1u);
 }
 
 // k_nfa_verify: one lane per start, forward automaton -> shortest end.
-template <int K, bool NUC>
+template <int K, int W, bool NUC>
 __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
-    __shared__ uint64_t s_fol[8 * 256];
-    __shared__ uint64_t s_b[256];
-    for (int i = threadIdx.x; i < a.nt * 256; i += blockDim.x) s_fol[i] = a.follow[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_b[i] = a.bmask[i];
-    __syncthreads();
+    __shared__ uint64_t s_fol[tab_words<W>()];
+    __shared__ uint64_t s_b[256 * W];
+    load_tables<W>(s_fol, s_b, a.follow, a.bmask, a.nt);
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= a.nstarts) return;
     const uint64_t s = a.starts[i] & ((1ull << 48) - 1);
     // pm_oracle.c match_from(): rows R[j] and the "before the first position"
     // state init[j] (kept alive by insertions), deletion closures after every
     // step; the first accepting step gives the shortest end
-    uint64_t R[K + 1];
+    Bits<W> R[K + 1];
     bool init[K + 1];
 #pragma unroll
     for (int j = 0; j <= K; ++j) {
-        R[j] = a.fwd_del[j];
+        R[j] = bits_of<W>(a.fwd_del[j]);
         init[j] = j == 0;
     }
+    const Bits<W> first = bits_of<W>(a.first);
     uint32_t len = 0;
     // max_len == 0: unbounded pattern; every start came with a match inside
-    // its record, and the record break ('\n', also the tail padding) kills
+    // its record, and the record break ('\n', also the end of the file) kills
     // every state, so the loop ends at the shortest end
     const uint64_t steps = a.max_len ? (uint64_t)a.max_len : a.n - s + 1;
     for (uint64_t d = 0; d < steps; ++d) {
-        const uint8_t ch = char_at<NUC>(a, s + d);
-        const uint64_t bc = s_b[ch];
-        const uint64_t nb = ch == '\n' ? 0ull : ~0ull;
-        uint64_t A[K + 1], N[K + 1];
+        bool kill;
+        const uint8_t ch = char_at<NUC>(a, s + d, kill);
+        const Bits<W> bc = bits_of<W>(s_b + ch * W);
+        const bool nb = !kill;
+        Bits<W> A[K + 1], N[K + 1];
         bool ninit[K + 1];
 #pragma unroll
-        for (int j = 0; j <= K; ++j) A[j] = fol_of(a, s_fol, R[j]) | (init[j] ? a.first : 0ull);
+        for (int j = 0; j <= K; ++j) A[j] = fol_of<W>(a, s_fol, R[j]) | mask_if<W>(first, init[j]);
 #pragma unroll
         for (int j = 0; j <= K; ++j) {
-            N[j] = A[j] & bc;
+            N[j] = mask_if<W>(A[j] & bc, !kill);
             ninit[j] = false;
             if (j > 0) {
-                if (a.errs & PM_ERR_SUB) N[j] |= A[j - 1] & nb;
+                if (a.errs & PM_ERR_SUB) N[j] = N[j] | mask_if<W>(A[j - 1], nb);
                 if (a.errs & PM_ERR_INS) {
-                    N[j] |= R[j - 1] & nb;
+                    N[j] = N[j] | mask_if<W>(R[j - 1], nb);
                     ninit[j] = init[j - 1] && nb;
                 }
             }
         }
         if (a.errs & PM_ERR_DEL) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) N[j + 1] |= fol_of(a, s_fol, N[j]) | (ninit[j] ? a.first : 0ull);
+            for (int j = 0; j < K; ++j) N[j + 1] = N[j + 1] | fol_of<W>(a, s_fol, N[j]) | mask_if<W>(first, ninit[j]);
         }
-        uint64_t any = 0;
+        Bits<W> any = bits_zero<W>();
         bool alive = false;
 #pragma unroll
         for (int j = 0; j <= K; ++j) {
-            R[j] = N[j];
-            init[j] = ninit[j];
-            any |= R[j];
+            R[j] = mask_if<W>(N[j], j <= a.k);
+            init[j] = ninit[j] && j <= a.k;
+            any = any | R[j];
             alive |= init[j];
         }
-        if (any & a.last) {
+        if (meets<W>(any, a.last)) {
             // '$': nrgrep's forward verification keeps extending while the
             // right context fails (extended checkMatch 0x411eb0), i.e. the
             // match must end at the line end
-            if (!a.end_anchor || char_at<NUC>(a, s + d + 1) == (uint8_t)'\n') { len = (uint32_t)(d + 1); break; }
+            bool k2;
+            if (!a.end_anchor || char_at<NUC>(a, s + d + 1, k2) == (uint8_t)'\n') { len = (uint32_t)(d + 1); break; }
         }
-        if (!any && !alive) break;
+        if (!any_of<W>(any) && !alive) break;
     }
     a.lens[i] = len;   // 0 = no match (cannot happen for a start found by k_nfa_rev)
 }
 
+// kernels instantiated per (error rows K + 1, state words W, layout); the
+// runtime k runs on the smallest K >= k
+#define PM_NFA_KW(X) X(0, 1) X(1, 1) X(2, 1) X(3, 1) X(7, 1) X(15, 1) \
+                     X(0, 2) X(1, 2) X(2, 2) X(3, 2) X(7, 2) X(15, 2) \
+                     X(0, 4) X(1, 4) X(2, 4) X(3, 4) X(7, 4)
+
+int kernel_rows(int k) { return k <= 3 ? k : k <= 7 ? 7 : 15; }
+int kernel_words(int m) { return m <= 64 ? 1 : m <= 128 ? 2 : 4; }
+bool nfa_supported(int k, int m) { return k <= PM_MAX_K && m <= PM_MAX_POSITIONS && !(kernel_words(m) == 4 && k > 7); }
+
 template <bool NUC>
-void launch_nfa_rev(int k, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
-    switch (k) {
-        case 0: hipLaunchKernelGGL((k_nfa_rev<0, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_nfa_rev<1, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_nfa_rev<2, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_nfa_rev<3, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-    }
+void launch_nfa_rev(int K, int W, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
+#define PM_X(KK, WW) \
+    if (K == KK && W == WW) { hipLaunchKernelGGL((k_nfa_rev<KK, WW, NUC>), dim3(blocks), dim3(256), 0, s, a); return; }
+    PM_NFA_KW(PM_X)
+#undef PM_X
+    throw failure(PM_E_UNSUPPORTED, "no NFA kernel for these rows/words");
 }
 
 template <bool NUC>
-void launch_nfa_carry(int k, const NfaArgs& a, uint32_t blocks, hipStream_t s, const uint64_t* o, uint64_t* n,
+void launch_nfa_carry(int K, int W, const NfaArgs& a, uint32_t blocks, hipStream_t s, const uint64_t* o, uint64_t* n,
                       const uint64_t* seen, uint64_t* now, uint32_t* changed) {
-    switch (k) {
-        case 0: hipLaunchKernelGGL((k_nfa_carry<0, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
-        case 1: hipLaunchKernelGGL((k_nfa_carry<1, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
-        case 2: hipLaunchKernelGGL((k_nfa_carry<2, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
-        default: hipLaunchKernelGGL((k_nfa_carry<3, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); break;
+#define PM_X(KK, WW)                                                                                          \
+    if (K == KK && W == WW) {                                                                                 \
+        hipLaunchKernelGGL((k_nfa_carry<KK, WW, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); \
+        return;                                                                                               \
     }
+    PM_NFA_KW(PM_X)
+#undef PM_X
+    throw failure(PM_E_UNSUPPORTED, "no NFA kernel for these rows/words");
 }
 
 template <bool NUC>
-void launch_nfa_verify(int k, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
-    switch (k) {
-        case 0: hipLaunchKernelGGL((k_nfa_verify<0, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_nfa_verify<1, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_nfa_verify<2, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_nfa_verify<3, NUC>), dim3(blocks), dim3(256), 0, s, a); break;
+void launch_nfa_verify(int K, int W, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
+#define PM_X(KK, WW) \
+    if (K == KK && W == WW) { hipLaunchKernelGGL((k_nfa_verify<KK, WW, NUC>), dim3(blocks), dim3(256), 0, s, a); return; }
+    PM_NFA_KW(PM_X)
+#undef PM_X
+    throw failure(PM_E_UNSUPPORTED, "no NFA kernel for these rows/words");
+}
+
+}  // namespace
+}  // namespace pm
+
+namespace pm {
+namespace {
+
+// The scan behind pm_scan_nfa_errs / pm_scan_nfa_wide: position sets of W
+// words (W = ceil(m / 64)).
+void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t* follow, const uint64_t* first,
+              const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
+              pm_hits** out) {
+    require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES)) == 0,
+            "bad flags");
+    require(db != nullptr, "db is NULL");
+    std::lock_guard<std::recursive_mutex> lk(db->mu);
+    require(out != nullptr && byte_mask && follow && first && last, "null argument");
+    require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range", PM_E_UNSUPPORTED);
+    require(W == kernel_words(m), "words must be ceil(m / 64), at most 4");
+    require(max_len >= 0, "max_len < 0");
+    const bool unbounded = max_len == 0;   // '*' / '+': matches may run to the record end
+    require(k >= 0 && nfa_supported(k, m), "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
+    require(pattern_id >= 0 && pattern_id < 65536, "pattern_id out of range");
+    bool nonempty_first = false, nonempty_last = false;
+    for (int q = 0; q < W; ++q) {
+        nonempty_first |= first[q] != 0;
+        nonempty_last |= last[q] != 0;
     }
+    require(nonempty_first && nonempty_last, "empty automaton");
+    require((errs & ~(PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB)) == 0, "bad error-type mask");
+    if (k == 0) errs = PM_ERR_SUB;   // no errors: the type letters are irrelevant
+    const bool cross = (flags & PM_CROSS_LINES) != 0;
+    require(!cross || (k == 0 && !unbounded), "PM_CROSS_LINES is nrgrep's simple engine: k = 0, bounded");
+    // a match must consume a pattern position (pm_oracle.c reports
+    // non-empty matches only): with deletions that needs min_len > k
+    require(!(errs & PM_ERR_DEL) || min_len > k,
+            "deletions with k >= the shortest match length are not supported by the GPU scan", PM_E_UNSUPPORTED);
+    const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
+    require((uint64_t)max_len + ins_extra < (1ull << 31), "max_len out of range");
+    DeviceGuard g(db->device);
+    lane_begin(db);
+    hipStream_t s = db->stream;
+    const int K = kernel_rows(k);
+    // Glushkov transition tables per slice of S positions (S = 8 for one
+    // word, 4 above: nt * 2^S * W words of LDS)
+    const int S = W == 1 ? 8 : 4, V = 1 << S;
+    const int nt = (m + S - 1) / S;
+    std::vector<uint64_t> prec((size_t)m * W, 0);
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j)
+            if ((follow[(size_t)i * W + j / 64] >> (j % 64)) & 1) prec[(size_t)j * W + i / 64] |= 1ull << (i % 64);
+    std::vector<uint64_t> tf((size_t)nt * V * W, 0), tp((size_t)nt * V * W, 0);
+    for (int t = 0; t < nt; ++t)
+        for (int v = 0; v < V; ++v)
+            for (int b = 0; b < S; ++b)
+                if (((v >> b) & 1) && t * S + b < m)
+                    for (int q = 0; q < W; ++q) {
+                        tf[((size_t)t * V + v) * W + q] |= follow[(size_t)(t * S + b) * W + q];
+                        tp[((size_t)t * V + v) * W + q] |= prec[(size_t)(t * S + b) * W + q];
+                    }
+    // start configurations (see the kernel comment): forward deletion
+    // closure of the start, and the reverse search's injected config
+    using Set = std::vector<uint64_t>;
+    auto set_or = [&](const std::vector<uint64_t>& per_pos, const Set& set) {
+        Set acc(W, 0);
+        for (int i = 0; i < m; ++i)
+            if ((set[i / 64] >> (i % 64)) & 1)
+                for (int q = 0; q < W; ++q) acc[q] |= per_pos[(size_t)i * W + q];
+        return acc;
+    };
+    auto set_union = [&](Set a2, const uint64_t* b2, bool on) {
+        if (on)
+            for (int q = 0; q < W; ++q) a2[q] |= b2[q];
+        return a2;
+    };
+    const std::vector<uint64_t> fol_v(follow, follow + (size_t)m * W);
+    std::vector<Set> fwd_del(k + 1, Set(W, 0)), rev_pre(k + 1, Set(W, 0)), rev_ins(k + 1, Set(W, 0)),
+        S_rows(k + 1, Set(W, 0));
+    {
+        const bool del = errs & PM_ERR_DEL, ins = errs & PM_ERR_INS;
+        for (int j = 0; j < k && del; ++j) {
+            fwd_del[j + 1] = set_union(set_or(fol_v, fwd_del[j]), first, j == 0);
+            S_rows[j + 1] = set_union(set_or(prec, S_rows[j]), last, j == 0 || ins);
+        }
+        for (int j = 0; j <= k; ++j) {
+            rev_ins[j] = S_rows[j];
+            rev_pre[j] = set_union(set_or(prec, S_rows[j]), last, j == 0 || ins);
+        }
+    }
+    std::vector<uint64_t> bm(byte_mask, byte_mask + 256 * W);
+    if (!cross)
+        for (int q = 0; q < W; ++q) bm['\n' * W + q] = 0;   // records never span the delimiter
+    Upload up;
+    const size_t o_f = up.add(tf.data(), tf.size() * 8);
+    const size_t o_p = up.add(tp.data(), tp.size() * 8);
+    const size_t o_b = up.add(bm.data(), bm.size() * 8);
+    uint8_t* d_up = up.commit(db);
+
+    NfaArgs a{};
+    a.nuc = nuc_view(db);
+    a.bytes = db->bytes;
+    a.bytes_raw = db->bytes_raw;
+    a.follow = reinterpret_cast<const uint64_t*>(d_up + o_f);
+    a.prec = reinterpret_cast<const uint64_t*>(d_up + o_p);
+    a.bmask = reinterpret_cast<const uint64_t*>(d_up + o_b);
+    for (int q = 0; q < W; ++q) {
+        a.first[q] = first[q];
+        a.last[q] = last[q];
+        const int bits = std::min(64, m - 64 * q);
+        a.mmask[q] = bits >= 64 ? ~0ull : bits <= 0 ? 0ull : ((1ull << bits) - 1);
+    }
+    a.nt = nt;
+    a.halo = unbounded ? 0 : max_len + ins_extra - 1;
+    // a plain class sequence: first = {0}, last = {m-1}, follow(i) = {i+1}
+    a.shift_only = true;
+    for (int q = 0; q < W; ++q) {
+        a.shift_only = a.shift_only && first[q] == (q == 0 ? 1ull : 0ull);
+        a.shift_only = a.shift_only && last[q] == (q == (m - 1) / 64 ? 1ull << ((m - 1) % 64) : 0ull);
+    }
+    for (int i = 0; i < m && a.shift_only; ++i)
+        for (int q = 0; q < W; ++q)
+            a.shift_only = a.shift_only && follow[(size_t)i * W + q] ==
+                                               ((i + 1 < m && (i + 1) / 64 == q) ? 1ull << ((i + 1) % 64) : 0ull);
+    a.errs = errs;
+    a.k = k;
+    for (int j = 0; j <= k; ++j)
+        for (int q = 0; q < W; ++q) {
+            a.rev_pre[j][q] = rev_pre[j][q];
+            a.rev_ins[j][q] = rev_ins[j][q];
+            a.fwd_del[j][q] = fwd_del[j][q];
+        }
+    a.n = db->n;
+    a.pattern_id = pattern_id;
+    a.end_anchor = (flags & PM_ANCHOR_END) ? 1 : 0;
+    a.cross = cross ? 1 : 0;
+    require(!cross || db->alphabet == PM_ALPHA_NUC || db->bytes_raw, "internal: no raw bytes for a cross-line scan");
+    // chunk per lane: a power of two (so that on the nucleotide layout
+    // the lanes of a wave walk the streams of one tile in lock step and
+    // their loads coincide), enough lanes to fill the chip; reads stop at
+    // the end of the file (char_at), so the halo needs no padding
+    uint64_t chunk = 64;
+    while (chunk < (uint64_t)MAX_NFA_CHUNK && db->n / (chunk * 2) >= 256ull * 4 * 64 * 2) chunk *= 2;
+    if (db->alphabet == PM_ALPHA_NUC) chunk = std::min<uint64_t>(chunk, STREAM);
+    a.chunk = (int)chunk;
+    a.nchunks = std::max<uint64_t>(1, (db->n + chunk - 1) / chunk);
+    a.st_stride = (k + 1) * W;
+    const bool nuc = db->alphabet == PM_ALPHA_NUC;
+
+    uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
+    SinkBuffers sb;
+    std::vector<uint32_t> counts;
+    uint64_t total = 0;
+    EventPair ev;
+    const uint32_t blocks = blocks_for(a.nchunks, 256);
+    double carry_ms = 0.0;
+    if (unbounded) {
+        // relaxation rounds (k_nfa_carry) until no chunk's state changes
+        Carve c;
+        const size_t st_bytes = a.nchunks * (size_t)a.st_stride * sizeof(uint64_t);
+        const size_t o_a = c.take(st_bytes), o_b2 = c.take(st_bytes), o_s = c.take(st_bytes),
+                     o_n = c.take(st_bytes), o_f2 = c.take(sizeof(uint32_t));
+        uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_rec, c.off));
+        uint64_t* st[2] = {reinterpret_cast<uint64_t*>(base + o_a), reinterpret_cast<uint64_t*>(base + o_b2)};
+        uint64_t* in_seen = reinterpret_cast<uint64_t*>(base + o_s);
+        uint64_t* in_now = reinterpret_cast<uint64_t*>(base + o_n);
+        uint32_t* changed = reinterpret_cast<uint32_t*>(base + o_f2);
+        HIPCHK(hipMemsetAsync(st[0], 0, st_bytes, s));
+        HIPCHK(hipMemsetAsync(in_seen, 0xff, st_bytes, s));   // no chunk has been scanned yet
+        uint32_t* h_changed = static_cast<uint32_t*>(reserve_host(db, db->pin_slots, 64));
+        int cur = 0;
+        EventPair cev;
+        HIPCHK(hipEventRecord(cev.a, s));
+        for (uint64_t round = 0; round <= a.nchunks; ++round) {
+            HIPCHK(hipMemsetAsync(changed, 0, sizeof(uint32_t), s));
+            if (nuc) launch_nfa_carry<true>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+            else launch_nfa_carry<false>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+            HIPCHK(hipGetLastError());
+            std::swap(in_seen, in_now);
+            cur ^= 1;
+            HIPCHK(hipMemcpyAsync(h_changed, changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (!*h_changed) break;
+        }
+        HIPCHK(hipEventRecord(cev.b, s));
+        HIPCHK(hipEventSynchronize(cev.b));
+        carry_ms = cev.ms();
+        a.in_state = st[cur];
+    }
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        sb = make_sink(db, 1, db->n, expected);
+        a.sink = sb.sink();
+        HIPCHK(hipEventRecord(ev.a, s));
+        if (nuc) launch_nfa_rev<true>(K, W, a, blocks, s);
+        else launch_nfa_rev<false>(K, W, a, blocks, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev.b, s));
+        bool overflow = false;
+        total = sink_total(db, sb, counts, overflow);
+        if (!overflow) break;
+        require(attempt == 0, "internal: hit bins overflowed twice");
+        expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
+    }
+    double kms = ev.ms() + carry_ms;
+    pm_hits* h = sink_to_hits(db, sb, counts, total);
+    if (total) {
+        a.starts = h->keys;
+        a.nstarts = total;
+        a.lens = h->lens;
+        a.max_len = unbounded ? 0 : max_len + ins_extra;
+        EventPair ev2;
+        HIPCHK(hipEventRecord(ev2.a, s));
+        if (nuc) launch_nfa_verify<true>(K, W, a, blocks_for(total, 256), s);
+        else launch_nfa_verify<false>(K, W, a, blocks_for(total, 256), s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev2.b, s));
+        HIPCHK(hipStreamSynchronize(s));
+        kms += ev2.ms();
+    }
+    h->kernel_ms = kms;
+    // line-bounded engines (nrgrep's extended/regular/e* verify inside the
+    // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
+    // header line, the pass only selects what nrgrep reports; the simple
+    // engine (cross) also drops the windows starting on a header line
+    if (report_needed((uint32_t)flags, cross)) report_sync(db, h, (uint32_t)flags, total, cross);
+    HIPCHK(hipStreamSynchronize(s));
+    hits_ready(db, h);
+    *out = h;
 }
 
 }  // namespace
@@ -302,185 +661,16 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
                                 uint64_t last, int max_len, int min_len, int k, int errs, int pattern_id,
                                 int flags, pm_hits** out) {
     return guarded([&] {
-        require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS)) == 0, "bad flags");
-        require(db != nullptr, "db is NULL");
-        std::lock_guard<std::recursive_mutex> lk(db->mu);
-        require(db != nullptr && out != nullptr && byte_mask && follow, "null argument");
-        require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range");
-        require(max_len >= 0, "max_len < 0");
-        const bool unbounded = max_len == 0;   // '*' / '+': matches may run to the record end
-        require(max_len <= 1024, "max_len above 1024", PM_E_UNSUPPORTED);
-        require(k >= 0 && k <= PM_MAX_K, "k out of range for the GPU kernels", PM_E_UNSUPPORTED);
-        require(pattern_id >= 0 && pattern_id < 65536, "pattern_id out of range");
-        require(first != 0 && last != 0, "empty automaton");
-        require((errs & ~(PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB)) == 0, "bad error-type mask");
-        if (k == 0) errs = PM_ERR_SUB;   // no errors: the type letters are irrelevant
-        // a match must consume a pattern position (pm_oracle.c reports
-        // non-empty matches only): with deletions that needs min_len > k
-        require(!(errs & PM_ERR_DEL) || min_len > k,
-                "deletions with k >= the shortest match length are not supported by the GPU scan",
-                PM_E_UNSUPPORTED);
-        const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
-        require(max_len + ins_extra <= 1024 + PM_MAX_K, "max_len above 1024", PM_E_UNSUPPORTED);
-        DeviceGuard g(db->device);
-        lane_begin(db);
-        hipStream_t s = db->stream;
-        const int nt = (m + 7) / 8;
-        // Glushkov transition tables per 8-position slice: follow / precede
-        std::vector<uint64_t> tf(nt * 256, 0), tp(nt * 256, 0), prec(m, 0);
-        for (int i = 0; i < m; ++i)
-            for (int j = 0; j < m; ++j)
-                if ((follow[i] >> j) & 1) prec[j] |= 1ull << i;
-        for (int t = 0; t < nt; ++t)
-            for (int v = 0; v < 256; ++v)
-                for (int b = 0; b < 8; ++b)
-                    if (((v >> b) & 1) && t * 8 + b < m) {
-                        tf[t * 256 + v] |= follow[t * 8 + b];
-                        tp[t * 256 + v] |= prec[t * 8 + b];
-                    }
-        // start configurations (see the kernel comment): forward deletion
-        // closure of the start, and the reverse search's injected config
-        auto set_or = [&](const std::vector<uint64_t>& per_pos, uint64_t set) {
-            uint64_t acc = 0;
-            for (int i = 0; i < m; ++i)
-                if ((set >> i) & 1) acc |= per_pos[i];
-            return acc;
-        };
-        const std::vector<uint64_t> fol_v(follow, follow + m);
-        uint64_t fwd_del[4] = {0, 0, 0, 0}, rev_pre[4] = {0, 0, 0, 0}, rev_ins[4] = {0, 0, 0, 0};
-        {
-            uint64_t S[4] = {0, 0, 0, 0};
-            const bool del = errs & PM_ERR_DEL, ins = errs & PM_ERR_INS;
-            for (int j = 0; j < k && del; ++j) {
-                fwd_del[j + 1] = set_or(fol_v, fwd_del[j]) | (j == 0 ? first : 0);
-                S[j + 1] = set_or(prec, S[j]) | ((j == 0 || ins) ? last : 0);
-            }
-            for (int j = 0; j <= k; ++j) {
-                rev_ins[j] = S[j];
-                rev_pre[j] = set_or(prec, S[j]) | ((j == 0 || ins) ? last : 0);
-            }
-        }
-        std::vector<uint64_t> bm(byte_mask, byte_mask + 256);
-        bm['\n'] = 0;   // records never span the delimiter
-        Upload up;
-        const size_t o_f = up.add(tf.data(), tf.size() * 8);
-        const size_t o_p = up.add(tp.data(), tp.size() * 8);
-        const size_t o_b = up.add(bm.data(), 256 * 8);
-        uint8_t* d_up = up.commit(db);
+        require(m >= 1 && m <= 64, "m out of range (pm_scan_nfa_wide takes longer automata)");
+        require(!(flags & PM_CROSS_LINES), "bad flags");
+        scan_nfa(db, m, 1, byte_mask, follow, &first, &last, max_len, min_len, k, errs, pattern_id, flags, out);
+    });
+}
 
-        NfaArgs a{};
-        a.nuc = nuc_view(db);
-        a.bytes = db->bytes;
-        a.follow = reinterpret_cast<const uint64_t*>(d_up + o_f);
-        a.prec = reinterpret_cast<const uint64_t*>(d_up + o_p);
-        a.bmask = reinterpret_cast<const uint64_t*>(d_up + o_b);
-        a.first = first;
-        a.last = last;
-        a.nt = nt;
-        a.halo = unbounded ? 0 : max_len + ins_extra - 1;
-        a.mmask = m == 64 ? ~0ull : ((1ull << m) - 1);
-        a.shift_only = first == 1 && last == (1ull << (m - 1));
-        for (int i = 0; i < m && a.shift_only; ++i)
-            a.shift_only = follow[i] == (i + 1 < m ? (1ull << (i + 1)) : 0ull);
-        a.errs = errs;
-        for (int j = 0; j < 4; ++j) {
-            a.rev_pre[j] = rev_pre[j];
-            a.rev_ins[j] = rev_ins[j];
-            a.fwd_del[j] = fwd_del[j];
-        }
-        a.n = db->n;
-        a.pattern_id = pattern_id;
-        a.end_anchor = (flags & PM_ANCHOR_END) ? 1 : 0;
-        // chunk per lane: a power of two (so that on the nucleotide layout
-        // the lanes of a wave walk the streams of one tile in lock step and
-        // their loads coincide), enough lanes to fill the chip
-        uint64_t chunk = 64;
-        while (chunk < (uint64_t)MAX_NFA_CHUNK && db->n / (chunk * 2) >= 256ull * 4 * 64 * 2) chunk *= 2;
-        if (db->alphabet == PM_ALPHA_NUC) chunk = std::min<uint64_t>(chunk, STREAM);
-        a.chunk = (int)chunk;
-        a.nchunks = std::max<uint64_t>(1, (db->n + chunk - 1) / chunk);
-        const bool nuc = db->alphabet == PM_ALPHA_NUC;
-        const uint64_t need = a.nchunks * chunk + a.halo + 64;   // storage must cover the last halo
-        if (nuc) require(need <= db->ntiles * TILE_POS, "internal: NUC padding too small");
-        else require(need <= db->nbytes_alloc, "internal: byte padding too small");
-
-        uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
-        SinkBuffers sb;
-        std::vector<uint32_t> counts;
-        uint64_t total = 0;
-        EventPair ev;
-        const uint32_t blocks = blocks_for(a.nchunks, 256);
-        double carry_ms = 0.0;
-        if (unbounded) {
-            // relaxation rounds (k_nfa_carry) until no chunk's state changes
-            Carve c;
-            const size_t st_bytes = a.nchunks * 4 * sizeof(uint64_t);
-            const size_t o_a = c.take(st_bytes), o_b = c.take(st_bytes), o_s = c.take(st_bytes),
-                         o_n = c.take(st_bytes), o_f = c.take(sizeof(uint32_t));
-            uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_rec, c.off));
-            uint64_t* st[2] = {reinterpret_cast<uint64_t*>(base + o_a), reinterpret_cast<uint64_t*>(base + o_b)};
-            uint64_t* in_seen = reinterpret_cast<uint64_t*>(base + o_s);
-            uint64_t* in_now = reinterpret_cast<uint64_t*>(base + o_n);
-            uint32_t* changed = reinterpret_cast<uint32_t*>(base + o_f);
-            HIPCHK(hipMemsetAsync(st[0], 0, st_bytes, s));
-            HIPCHK(hipMemsetAsync(in_seen, 0xff, st_bytes, s));   // no chunk has been scanned yet
-            uint32_t* h_changed = static_cast<uint32_t*>(reserve_host(db, db->pin_slots, 64));
-            int cur = 0;
-            EventPair cev;
-            HIPCHK(hipEventRecord(cev.a, s));
-            for (uint64_t round = 0; round <= a.nchunks; ++round) {
-                HIPCHK(hipMemsetAsync(changed, 0, sizeof(uint32_t), s));
-                if (nuc) launch_nfa_carry<true>(k, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
-                else launch_nfa_carry<false>(k, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
-                HIPCHK(hipGetLastError());
-                std::swap(in_seen, in_now);
-                cur ^= 1;
-                HIPCHK(hipMemcpyAsync(h_changed, changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-                HIPCHK(hipStreamSynchronize(s));
-                if (!*h_changed) break;
-            }
-            HIPCHK(hipEventRecord(cev.b, s));
-            HIPCHK(hipEventSynchronize(cev.b));
-            carry_ms = cev.ms();
-            a.in_state = st[cur];
-        }
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            sb = make_sink(db, 1, db->n, expected);
-            a.sink = sb.sink();
-            HIPCHK(hipEventRecord(ev.a, s));
-            if (nuc) launch_nfa_rev<true>(k, a, blocks, s);
-            else launch_nfa_rev<false>(k, a, blocks, s);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev.b, s));
-            bool overflow = false;
-            total = sink_total(db, sb, counts, overflow);
-            if (!overflow) break;
-            require(attempt == 0, "internal: hit bins overflowed twice");
-            expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
-        }
-        double kms = ev.ms() + carry_ms;
-        pm_hits* h = sink_to_hits(db, sb, counts, total);
-        if (total) {
-            a.starts = h->keys;
-            a.nstarts = total;
-            a.lens = h->lens;
-            a.max_len = unbounded ? 0 : max_len + ins_extra;
-            EventPair ev2;
-            HIPCHK(hipEventRecord(ev2.a, s));
-            if (nuc) launch_nfa_verify<true>(k, a, blocks_for(total, 256), s);
-            else launch_nfa_verify<false>(k, a, blocks_for(total, 256), s);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev2.b, s));
-            HIPCHK(hipStreamSynchronize(s));
-            kms += ev2.ms();
-        }
-        h->kernel_ms = kms;
-        // line-bounded engines (nrgrep's extended/regular/e* verify inside the
-        // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
-        // header line, the pass only selects what nrgrep reports
-        if (report_needed((uint32_t)flags, false)) report_sync(db, h, (uint32_t)flags, total, false);
-        HIPCHK(hipStreamSynchronize(s));
-        hits_ready(db, h);
-        *out = h;
+extern "C" int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
+                                const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
+                                int errs, int pattern_id, int flags, pm_hits** out) {
+    return guarded([&] {
+        scan_nfa(db, m, words, byte_mask, follow, first, last, max_len, min_len, k, errs, pattern_id, flags, out);
     });
 }

@@ -22,10 +22,11 @@ DESIGN.md §1.
 Queries with insertions/deletions (``-k <k>ids``, the web form's default
 when mismatches > 0) go to the Glushkov kernels with the error-type mask.
 Unbounded ``*``/``+`` (``{m,}``) also run there (chunk states relaxed
-across chunks, :func:`scan_nfa`).  Anything else (more than 64 positions,
-k > 3, deletions with k >= the shortest match, a bounded match longer
-than 1024) raises :class:`UnsupportedOnGPU`;
-there is no CPU fallback by design.
+across chunks, :func:`scan_nfa`), as do class sequences longer than 64
+positions or with more than 3 errors (up to 256 positions and 15 errors,
+7 above 128 positions).  Anything else (deletions with k >= the shortest
+match, longer automata) raises :class:`UnsupportedOnGPU`; there is no CPU
+fallback by design.
 """
 
 from __future__ import annotations
@@ -189,21 +190,24 @@ def parse_error_types(k: int, types: str) -> str:
     return (types or "ids") if k else ""
 
 
+def nfa_words(m: int) -> int:
+    """64-bit words of a position set in the automaton kernels."""
+    return 1 if m <= 64 else 2 if m <= 128 else 4
+
+
 def route(prog: Program, alphabet: str, k: int, types: str) -> str:
     """Which kernel handles ``prog``; raises UnsupportedOnGPU if none does."""
-    if k > _lib.PM_MAX_K:
-        raise UnsupportedOnGPU("k=%d > %d errors is not supported by the GPU kernels" % (k, _lib.PM_MAX_K))
-    if prog.m > 64:
-        raise UnsupportedOnGPU("patterns longer than 64 positions are not supported")
     indel = bool(k) and ("i" in types or "d" in types)
+    if prog.linear and not indel and prog.m <= _lib.PM_MAX_LINEAR_POSITIONS and k <= _lib.PM_MAX_LINEAR_K:
+        return "linear"   # nucleotide planes (bit-sliced) or the byte layout (k_bytes_linear)
+    if prog.m > _lib.PM_MAX_POSITIONS:
+        raise UnsupportedOnGPU("patterns longer than %d positions are not supported" % _lib.PM_MAX_POSITIONS)
+    if k > _lib.PM_MAX_K or (nfa_words(prog.m) == 4 and k > 7):
+        raise UnsupportedOnGPU("k=%d errors is not supported by the GPU kernels for %d positions" % (k, prog.m))
     if indel and "d" in types and prog.min_len <= k:
         raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
                                % (k, prog.min_len))
-    if prog.linear and not indel:
-        return "linear"   # nucleotide planes (bit-sliced) or the byte layout (k_bytes_linear)
-    if prog.max_len is not None and prog.max_len > 1024:
-        raise UnsupportedOnGPU("match length bound above 1024")
-    return "nfa"
+    return "nfa"   # automaton kernels: anything else, long oligos and k > 3 included
 
 
 def _linear_tables(progs: Sequence[Program]):
@@ -286,16 +290,28 @@ def error_mask(types: str) -> int:
             | (_lib.PM_ERR_SUB if "s" in types else 0))
 
 
+def _words(x: int, w: int) -> List[int]:
+    return [(x >> (64 * q)) & 0xFFFFFFFFFFFFFFFF for q in range(w)]
+
+
 def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
              flags: int = None) -> Hits:
-    bm = np.array(prog.byte_masks(), dtype=np.uint64)
-    fol = np.array(prog.follow, dtype=np.uint64)
+    """The automaton kernels (pm_scan_nfa_wide).  A class sequence at k = 0
+    runs as nrgrep's simple engine (PM_CROSS_LINES: windows may span a line
+    break when a class accepts '\n'), as in the fixed-length kernel."""
+    w = nfa_words(prog.m)
+    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
+    fol = np.array([_words(x, w) for x in prog.follow], dtype=np.uint64)
+    first = np.array(_words(prog.first, w), dtype=np.uint64)
+    last = np.array(_words(prog.last, w), dtype=np.uint64)
     errs = error_mask(types) if k else _lib.PM_ERR_SUB
     flags = report_flags(prog) if flags is None else flags
+    if k == 0 and prog.linear and any(10 in c for c in prog.classes):
+        flags |= _lib.PM_CROSS_LINES
     out = ctypes.c_void_p()
-    check(_lib.load().pm_scan_nfa_errs(db.handle, prog.m, bm.ctypes.data, fol.ctypes.data, prog.first, prog.last,
-                                       prog.max_len or 0, prog.min_len, k, errs, pattern_id, flags,
-                                       ctypes.byref(out)))
+    check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
+                                       last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,
+                                       flags, ctypes.byref(out)))
     return _collect(out)
 
 

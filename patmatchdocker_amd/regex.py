@@ -36,7 +36,7 @@ from typing import List, Optional, Tuple
 __all__ = ["RegexSyntaxError", "Program", "compile_pattern", "fold_byte",
            "MAX_POSITIONS"]
 
-MAX_POSITIONS = 64          # one 64-bit NFA state word per lane
+MAX_POSITIONS = 4096        # parser bound; the GPU kernels take up to 256 (engine.route)
 DELIMITER = 0x0A            # record delimiter (nrgrep default '\n')
 ALL_BYTES = frozenset(range(256))   # '.' (the delimiter included)
 

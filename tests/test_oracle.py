@@ -105,3 +105,15 @@ def test_shiftadd_cpu_scan_equals_reported_oracle(oracle_mod, seed):
                 want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
                 assert oracle_mod.shiftadd_scan(text, prog, k, skip_headers=True) == want, (pat, k)
                 assert oracle_mod.shiftadd_threads(text, prog, k, skip_headers=True, threads=3) == want, (pat, k)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_python_reported_oracle_equals_c_oracle(oracle_mod, seed):
+    """scan_py_reported (any number of positions; checks the >64-position
+    GPU scans) against pmo_scan2 on automata it holds, line-bounded engines."""
+    text = dna_fasta(seed + 30, n_records=3, max_len=150, width=40) if seed % 2 else pep_fasta(seed, 4, 60)
+    for p in PATTERNS + ["^(A.C)", "(G.T)$", "^(AC|GT.)$"]:
+        prog = compile_pattern(p)
+        for k, t in [(0, "s"), (1, "s"), (1, "ids"), (2, "id"), (2, "s")]:
+            want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True, simple=False)
+            assert oracle_mod.scan_py_reported(text, prog, k, t, skip_headers=True) == want, (p, k, t)

@@ -54,6 +54,10 @@ def test_syntax_errors(bad):
         compile_pattern(bad)
 
 
-def test_too_many_positions():
-    with pytest.raises(RegexSyntaxError):
-        compile_pattern("(" + "A" * 65 + ")")
+def test_long_patterns_compile():
+    # nrgrep takes long patterns (multi-word masks); the GPU route decides
+    # what runs (engine.route, tests/test_route.py)
+    p = compile_pattern("(" + "A" * 300 + ")")
+    assert p.m == 300 and p.linear
+    with pytest.raises(RegexSyntaxError):   # the parser's own bound
+        compile_pattern("A" * 5000)

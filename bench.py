@@ -46,6 +46,9 @@ def parse_args():
     ap.add_argument("--rec-len", type=int, default=1_000_000)
     ap.add_argument("--motif", default=MOTIF)
     ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--types", default="s",
+                    help="error types of '-k <k><types>': s = mismatches (default, the metric's workload); "
+                         "ids = the web form's default (insertions, deletions, substitutions)")
     ap.add_argument("--sample-mbp", type=float, default=None,
                     help="CPU-baseline sample (Mbp; default 200 per CPU thread)")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -136,6 +139,42 @@ def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads, parity_bp=320e6):
                       % (sample_bp / 1e6, threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok
 
 
+def cpu_baseline_ids(db, progs, k, types, sample_bp, gpu_hits, threads, parity_bp=40e6):
+    """`-k <k>ids` CPU baseline: the bit-parallel Wu-Manber scan
+    (oracle/pm_cpuscan.c pmc_ids_scan, nrgrep's e* engines' recurrence)
+    on `threads` host threads over the first `sample_bp` positions, timed;
+    its reported matches must equal the GPU's, and the first `parity_bp`
+    positions are also checked against pm_oracle.c."""
+    from oracle import oracle
+    text = db.decode(0, int(sample_bp))
+    cut = text.rfind(b"\n") + 1
+    text = text[:cut]
+    t0, c0 = time.perf_counter(), time.process_time()
+    base = [oracle.ids_threads(text, p, k, types, skip_headers=True, threads=threads) for p in progs]
+    dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0
+    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
+    ptext = text[:int(parity_bp)]
+    ptext = ptext[:ptext.rfind(b"\n") + 1]
+    want = [oracle.scan_threads(ptext, p, k, types, skip_headers=True, threads=threads, report="nrgrep")
+            for p in progs]
+    keys, lens = gpu_hits
+    keys = keys.cpu().tolist()
+    lens = lens.cpu().tolist()
+    ok = True
+    for pid, (b, w) in enumerate(zip(base, want)):
+        got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
+               if (kk >> 48) == pid]
+        ok &= [h for h in got if h[1] <= len(text)] == b
+        ok &= [h for h in got if h[1] <= len(ptext)] == w
+    return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
+            "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, -k %d%s: "
+                      "bit-parallel Wu-Manber scan (oracle/pm_cpuscan.c pmc_ids_scan, reverse pass for starts + "
+                      "forward pass for the shortest end + report rule, same reported matches) on %d host "
+                      "threads, text cut at line breaks; %.1f s wall, %.1f s CPU"
+                      % (sample_bp / 1e6, k, types, threads, dt, cpu_s)}, ok
+
+
 def main():
     args = parse_args()
     import torch
@@ -171,7 +210,10 @@ def main():
         fwd = convert("-n", args.motif)
         comp = convert("-c", fwd)
         progs = [compile_pattern(fwd), compile_pattern(comp)]
-    batch = engine.LinearBatch(progs)
+    # '-k <k>ids' (insertions / deletions): the automaton kernels, one scan
+    # per strand (bit-sliced start pass pm_ids_rev + verify + report)
+    indel = args.k > 0 and any(c in args.types for c in "id")
+    batch = None if indel else engine.LinearBatch(progs)
 
     # node-wide virtual FASTA: rank r owns records [first, first+count)
     per_rank_records = max(1, int(round(args.gbp * 1e9 / args.rec_len)))
@@ -195,14 +237,31 @@ def main():
         out = shards.gather_hits(keys, lens)
         return out, ms
 
+    def ids_step():
+        parts_k, parts_l, ms = [], [], 0.0
+        for pid, prog in enumerate(progs):
+            h = engine.nfa_launch(db, prog, args.k, pid, args.types)
+            try:   # keys pid << 48 | beg, copied on the device
+                keys, lens = shards.hits_to_tensors(h, device)
+                ms += engine.kernel_ms(h)
+            finally:
+                engine.destroy_hits(h)
+            parts_k.append(keys)
+            parts_l.append(lens)
+        keys = shards.to_global(torch.cat(parts_k), offset)
+        out = shards.gather_hits(keys, torch.cat(parts_l))
+        return out, ms / len(progs)   # per launch (one strand)
+
     # pipelined (default): a step launches query i+1 (pm_scan_linear_async,
     # no host sync) and then collects query i, so the host-side collection
     # and the next launch overlap the GPU scan.  The query launched before
     # the timed region finishes before t0 (synchronize below); the timed
     # region holds K launches whose GPU work all completes inside it.
-    pending = [batch.launch(db, args.k, pipelined=True)] if not args.serial else []
+    pending = [batch.launch(db, args.k, pipelined=True)] if not (args.serial or indel) else []
 
     def step():
+        if indel:
+            return ids_step()
         if args.serial:
             return collect(batch.launch(db, args.k))
         nxt = batch.launch(db, args.k, pipelined=True)
@@ -246,6 +305,9 @@ def main():
         if args.config == 4:
             workload = "configs[4]: batch of %d degenerate 12-nt DNA patterns k=%d vs %.1f Gbp synthetic DNA per GPU" % (
                 len(progs), args.k, args.gbp)
+        elif indel:
+            workload = "configs[2]: %s -k %d%s both strands vs %.0f Gbp synthetic DNA per GPU" % (
+                args.motif, args.k, args.types, args.gbp)
         else:
             workload = "configs[2]: %s k=%d both strands vs %.0f Gbp synthetic DNA per GPU" % (
                 args.motif, args.k, args.gbp)
@@ -268,7 +330,7 @@ def main():
                        "k_mismatches": args.k, "patterns": len(progs),
                        "strands": 2 if args.config == 2 else 1, "gbp_per_gpu": args.gbp, "record_len": args.rec_len,
                        "hits": n_hits, "parallelism": "shard-by-record x%d + RCCL hit gather" % world,
-                       "pipelined": not args.serial},
+                       "error_types": args.types if args.k else "", "pipelined": not (args.serial or indel)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": ("pm_linear_jit (hipRTC-specialized, stream tiles + LDS-DMA ring)" if jit
@@ -288,10 +350,20 @@ def main():
             line["roofline"]["note"] = ("one database read per query; kernel_ms = the sum of the query's "
                                         "specialized launches (<= 8 patterns each); VALU-bound, see DESIGN.md §4")
             line["roofline"]["traffic"] = None
+        if indel:
+            line["roofline"].update({
+                "kernel": "pm_ids_rev (hipRTC, bit-sliced over the 32 streams of a tile) + k_nfa_verify",
+                "note": "per strand launch: start pass + verify of its candidates; one read of the planes "
+                        "(0.25 B/base) per launch; VALU-bound (DESIGN.md §4)"})
+            line["roofline"]["traffic"] = None
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
             thr = args.cpu_threads or cpu_threads_default()
-            mbp = args.sample_mbp if args.sample_mbp is not None else 200.0 * thr
-            cb, ok = cpu_baseline(db, progs, args.k, mbp * 1e6, result, thr)
+            if indel:
+                mbp = args.sample_mbp if args.sample_mbp is not None else 40.0 * thr
+                cb, ok = cpu_baseline_ids(db, progs, args.k, args.types, mbp * 1e6, result, thr)
+            else:
+                mbp = args.sample_mbp if args.sample_mbp is not None else 200.0 * thr
+                cb, ok = cpu_baseline(db, progs, args.k, mbp * 1e6, result, thr)
             line["cpu_baseline"] = cb
             line["parity_sample_bit_exact"] = ok
         else:

@@ -167,6 +167,12 @@ int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, con
                      const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
                      int errs, int pattern_id, int flags, pm_hits** out);
 
+/* Generates and compiles (hipRTC, gfx950) the bit-sliced start pass that
+ * pm_scan_nfa_errs / _wide use for a class sequence with insertions /
+ * deletions on a nucleotide database (m * (k + 1) <= 64), without
+ * launching it: a host-only check that needs no GPU. */
+int pm_ids_jit_compile(int m, const uint64_t* byte_mask, int k, int errs, uint64_t* code_bytes);
+
 /* --- hits --------------------------------------------------------------- */
 int pm_hits_count(const pm_hits* h, uint64_t* count);
 /* Copies hits sorted by (pattern, beg).  Any pointer may be NULL. */

@@ -45,6 +45,10 @@ def lib():
         _LIB.pmo_scan2.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_uint64,
                                    ctypes.c_uint64, pu64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmc_ids_scan.restype = ctypes.c_int64
+        _LIB.pmc_ids_scan.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                      ctypes.c_int64]
         _LIB.pmc_shiftadd.restype = ctypes.c_int64
         _LIB.pmc_shiftadd.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, p64, ctypes.c_int64]
@@ -336,6 +340,58 @@ def shiftadd_threads(text: bytes, prog, k: int, skip_headers: bool = False, thre
     def one(span):
         a, b = span
         return [(x + a, y + a) for x, y in shiftadd_scan(text[a:b], prog, k, skip_headers)]
+
+    with ThreadPoolExecutor(max_workers=len(pieces)) as ex:
+        parts = list(ex.map(one, pieces))
+    return [h for part in parts for h in part]
+
+
+def ids_scan(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False):
+    """Reported matches of a class sequence with <= k insertions / deletions /
+    substitutions by the bit-parallel Wu-Manber recurrence (pm_cpuscan.c
+    pmc_ids_scan: reverse pass for starts, forward pass for the shortest
+    end, report rule); same output as ``scan_reported(text, prog, k, types)``
+    for k > 0."""
+    if not prog.linear or k < 1:
+        raise ValueError("ids_scan needs a class sequence and k > 0")
+    L = lib()
+    B = np.array(prog.byte_masks(), dtype=np.uint64)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = L.pmc_ids_scan(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), prog.m, k,
+                           err_flags(types), 1 if prog.ignore_case else 0,
+                           beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                           end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("shape not covered by pmc_ids_scan (m=%d, k=%d)" % (prog.m, k))
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+def ids_threads(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False, threads: int = 1):
+    """``ids_scan`` over host threads, the text cut after line breaks (the
+    e* engines' matches never span one, so the pieces are independent)."""
+    if threads <= 1 or len(text) < (1 << 20):
+        return ids_scan(text, prog, k, types, skip_headers)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [0]
+    step = len(text) // threads
+    for t in range(1, threads):
+        c = text.find(b"\n", max(cuts[-1], t * step))
+        if c < 0:
+            break
+        if c + 1 > cuts[-1]:
+            cuts.append(c + 1)
+    cuts.append(len(text))
+    pieces = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+
+    def one(span):
+        a, b = span
+        return [(x + a, y + a) for x, y in ids_scan(text[a:b], prog, k, types, skip_headers)]
 
     with ThreadPoolExecutor(max_workers=len(pieces)) as ex:
         parts = list(ex.map(one, pieces))

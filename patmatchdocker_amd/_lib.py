@@ -31,6 +31,7 @@ EXPORTED = (
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
+    "pm_ids_jit_compile",
 )
 
 
@@ -73,6 +74,7 @@ def _declare(lib):
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_scan_nfa_wide.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
+    lib.pm_ids_jit_compile.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, pu64]
     lib.pm_hits_count.argtypes = [P, pu64]
     lib.pm_hits_copy.argtypes = [P, P, P, P, u64]
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]

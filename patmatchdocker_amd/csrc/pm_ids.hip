@@ -1,0 +1,356 @@
+// pm_ids.hip -- the web default `-k <k>ids` (insertions, deletions,
+// substitutions; patmatch.py:299-314) for a class sequence on the nucleotide
+// planes: the start-finding pass of the Glushkov kernels (k_nfa_rev, one
+// text stream per lane, one character per step) restated bit-sliced over
+// the 32 streams of a stream tile.
+//
+// The reverse automaton of a class sequence has shift transitions (position
+// i + 1 -> i), so with one 32-bit register per (error row j, position i) --
+// bit b = stream b -- a transition is a register renaming and a step over
+// 32 characters (one logical word of every stream) is, per (j, i),
+//     N[j][i] = (R[j][i+1] & M[c_i]) | R[j-1][i+1] | R[j-1][i] | N[j-1][i+1]
+// (match, substitution, insertion, deletion), where M[c] = the class-match
+// word of the word's 32 bases (one v_bitop3 of the hi/lo planes).  A start
+// of a match is emitted where any row holds position 0 -- exactly the
+// candidates k_nfa_rev emits; k_nfa_verify then finds each one's shortest
+// end.  The kernel is generated per pattern (hipRTC): positions and rows are
+// register names, the injected start configuration is folded into
+// constants.  Line breaks (bo.x) zero every state, "other" bytes (N, IUPAC
+// letters: bo.y) take their class membership from the byte's mask; both are
+// handled in a second copy of the step taken only when a lane of the wave
+// sees one.
+//
+// Lanes: each lane owns LW consecutive logical words of one tile's streams
+// and scans them right to left after a warm-up of L - 1 words (L = the
+// longest match, m + k), read from the next lane's words or the tile's halo.
+#include <map>
+#include <sstream>
+
+#include <hip/hip_ext.h>
+
+#include "pm_internal.h"
+
+namespace pm {
+namespace {
+
+// logical words per lane (2 lane columns of the layout); PM_IDS_LW = 32,
+// 64 or 128 (experiment knob)
+int ids_lw() {
+    const char* e = getenv("PM_IDS_LW");
+    const int v = e ? atoi(e) : 64;
+    return v == 32 || v == 128 ? v : 64;
+}
+constexpr int IDS_MAX_REGS = 64;   // m * (k + 1) state registers at most
+// steps per loop iteration = words loaded ahead; PM_IDS_U = 1, 2, 4, 8
+int ids_u() {
+    const char* e = getenv("PM_IDS_U");
+    const int v = e ? atoi(e) : 4;
+    return v == 1 || v == 2 || v == 8 ? v : 4;
+}
+
+const char* kIdsCommon = R"IDS(
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef unsigned char u8;
+#define STREAM 2048u
+#define TILE_POS 65536ull
+#define TILE_WORDS 2112ull
+#define B3(a, b, c, t) ((u32)__builtin_amdgcn_bitop3_b32((a), (b), (c), (t)))
+struct IArgs {
+    const uint2* hl;
+    const uint2* bo;
+    const u32* sbflag;
+    const u32* sbbase;
+    const u8* xbytes;
+    const u64* lflag;
+    const u64* bmask;      // [256] positions accepting each folded byte
+    u64 ntiles, n;
+    u64* sink_out;
+    u32* sink_cnt;
+    u32 sink_cap, bins_per_pattern, pos_shift, pattern_id;
+};
+__device__ inline u64 phys(u64 tile, u32 w) {
+    return tile * TILE_WORDS + (w < STREAM ? (u64)((w & 31u) * 64u + (w >> 5)) : (u64)w);
+}
+__device__ inline void push(const IArgs& a, u64 pos) {
+    const u32 bin = (u32)(pos >> a.pos_shift);
+    const u32 o = atomicAdd(&a.sink_cnt[bin], 1u);
+    if (o < a.sink_cap) a.sink_out[(u64)bin * a.sink_cap + o] = ((u64)a.pattern_id << 48) | pos;
+}
+)IDS";
+
+struct IArgsHost {   // must match IArgs in kIdsCommon
+    const uint2* hl;
+    const uint2* bo;
+    const uint32_t* sbflag;
+    const uint32_t* sbbase;
+    const uint8_t* xbytes;
+    const uint64_t* lflag;
+    const uint64_t* bmask;
+    uint64_t ntiles, n;
+    uint64_t* sink_out;
+    uint32_t* sink_cnt;
+    uint32_t sink_cap, bins_per_pattern, pos_shift, pattern_id;
+};
+
+// ACGT subset of the class of position i (bit 0 = A .. bit 3 = T) and
+// whether it takes every byte but '\n' ('.')
+struct PosClass {
+    int acgt;
+    bool any;
+};
+
+PosClass pos_class_of(const uint64_t* bm, int i) {
+    PosClass c{0, true};
+    const char* acgt = "ACGT";
+    for (int x = 0; x < 4; ++x)
+        if ((bm[(uint8_t)acgt[x]] >> i) & 1) c.acgt |= 1 << x;
+    for (int b = 0; b < 256; ++b)
+        if (b != '\n' && !((bm[b] >> i) & 1)) c.any = false;
+    return c;
+}
+
+// v_bitop3 truth table of "the base coded (hi, lo) is in subset s"
+// (A=00 C=01 G=10 T=11), inputs (hi, lo, lo)
+int subset_table(int s) {
+    int t = 0;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int c = 0; c < 2; ++c)
+                if ((s >> (2 * a + b)) & 1) t |= 1 << (4 * a + 2 * b + c);
+    return t;
+}
+
+std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
+    const int m = sp.m, k = sp.k;
+    const bool SUB = sp.errs & PM_ERR_SUB, INS = sp.errs & PM_ERR_INS, DEL = sp.errs & PM_ERR_DEL;
+    const int L = m + (INS ? k : 0);   // the longest match
+    const int WU = L - 1;              // warm-up words
+    std::vector<PosClass> pc(m);
+    std::map<std::pair<int, bool>, int> cls;   // distinct classes -> register index
+    std::vector<int> rep;                       // a position of each class
+    std::vector<int> ci(m);
+    for (int i = 0; i < m; ++i) {
+        pc[i] = pos_class_of(sp.byte_mask, i);
+        auto key = std::make_pair(pc[i].any ? 15 : pc[i].acgt, pc[i].any);
+        auto it = cls.find(key);
+        if (it == cls.end()) {
+            it = cls.emplace(key, (int)rep.size()).first;
+            rep.push_back(i);
+        }
+        ci[i] = it->second;
+    }
+    std::ostringstream sg;
+    const int LWv = ids_lw(), U = ids_u();
+    sg << "ids:" << m << ":" << k << ":" << sp.errs << ":" << LWv << ":" << U << ":";
+    for (int i = 0; i < m; ++i) sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
+    for (int j = 0; j <= k; ++j) sg << ":" << sp.rev_pre[j] << "," << sp.rev_ins[j];
+    *sig = sg.str();
+
+    // two register banks, r and s: a step reads one and writes the other,
+    // and the loop body is two steps (r -> s, s -> r), so no state moves
+    auto V = [](char bank, int j, int i) { return std::string(1, bank) + std::to_string(j) + "_" + std::to_string(i); };
+    auto bit = [](uint64_t set, int i) { return (set >> i) & 1; };
+    // one step over word t (`tv`): new state (bank dst) from the old (bank
+    // src) and the class words; `kill` masks every register with nb (a
+    // line break zeroes all states)
+    auto update = [&](std::ostringstream& o, char src, char dst, bool kill, const std::string& ind) {
+        for (int j = 0; j <= k; ++j)
+            for (int i = 0; i < m; ++i) {
+                // A(j, i) = R(j, i+1) | injected constant
+                auto A = [&](int jj) -> std::string {
+                    if (bit(sp.rev_pre[jj], i)) return "0xffffffffu";
+                    return i + 1 < m ? V(src, jj, i + 1) : "0u";
+                };
+                std::string t;
+                const std::string a = A(j);
+                if (a == "0xffffffffu") t = pc[i].any ? "0xffffffffu" : "M" + std::to_string(ci[i]);
+                else if (a == "0u") t = "0u";
+                else t = pc[i].any ? a : "(" + a + " & M" + std::to_string(ci[i]) + ")";
+                std::vector<std::string> terms{t};
+                if (j > 0 && SUB) terms.push_back(A(j - 1));
+                if (j > 0 && INS) terms.push_back(bit(sp.rev_ins[j - 1], i) ? "0xffffffffu" : V(src, j - 1, i));
+                if (j > 0 && DEL) {
+                    if (i + 1 < m) terms.push_back(V(dst, j - 1, i + 1));
+                    if (j >= 2 && INS && i == m - 1) terms.push_back("0xffffffffu");
+                }
+                std::string e;
+                for (const std::string& x : terms) {
+                    if (x == "0u") continue;
+                    e += (e.empty() ? "" : " | ") + x;
+                }
+                if (e.empty()) e = "0u";
+                o << ind << V(dst, j, i) << " = " << (kill ? "(" + e + ") & nb" : e) << ";\n";
+            }
+    };
+    // one step over word t = `tv`, whose plane / exception words are the
+    // variables `vv` / `ev` (loaded ahead, see below)
+    auto step = [&](std::ostringstream& o, char src, char dst, const std::string& tv, const std::string& vv,
+                    const std::string& ev) {
+        const std::string in = "            ";
+        o << in << "{\n";
+        o << in << "    const int t = " << tv << ";\n";
+        o << in << "    const u32 w = col * LW + (u32)t;\n";
+        o << in << "    const u64 pw = phys(tile, w);\n";
+        o << in << "    const uint2 v = " << vv << ", e = " << ev << ";\n";
+        for (size_t c = 0; c < rep.size(); ++c) {
+            const PosClass& p = pc[rep[c]];
+            if (p.any) o << in << "    u32 M" << c << " = 0xffffffffu;\n";
+            else o << in << "    u32 M" << c << " = B3(v.x, v.y, v.y, " << subset_table(p.acgt) << ");\n";
+        }
+        o << in << "    if (__ballot((e.x | e.y) != 0)) {   // wave-uniform\n";
+        o << in << "        const u32 nb = ~e.x;\n";
+        // "other" bytes: the byte's own class membership
+        o << in << "        if (e.y) {\n";
+        o << in << "            const u32 f = a.sbflag[pw >> 5];\n";
+        o << in << "            const u32 xi = a.sbbase[pw >> 5] + __popc(f & ((1u << (u32)(pw & 31)) - 1u));\n";
+        o << in << "            for (u32 ob = e.y; ob; ob &= ob - 1) {\n";
+        o << in << "                const u32 b = __builtin_ctz(ob);\n";
+        o << in << "                const u64 mk = a.bmask[a.xbytes[(u64)xi * 32 + b]];\n";
+        for (size_t c = 0; c < rep.size(); ++c)
+            o << in << "                M" << c << " = ((mk >> " << rep[c] << ") & 1ull) ? (M" << c << " | (1u << b)) : (M"
+              << c << " & ~(1u << b));\n";
+        o << in << "            }\n";
+        o << in << "        }\n";
+        update(o, src, dst, true, in + "        ");
+        o << in << "    } else {\n";
+        update(o, src, dst, false, in + "        ");
+        o << in << "    }\n";
+        o << in << "    if (t < (int)LW && live) {\n";
+        o << in << "        u32 em = 0u";
+        for (int j = 0; j <= k; ++j) o << " | " << V(dst, j, 0);
+        o << ";\n";
+        o << in << "        for (; em; em &= em - 1) {\n";
+        o << in << "            const u64 pos = tile * TILE_POS + (u64)__builtin_ctz(em) * STREAM + w;\n";
+        o << in << "            if (pos < a.n) push(a, pos);\n";
+        o << in << "        }\n";
+        o << in << "    }\n";
+        o << in << "}\n";
+    };
+
+    std::ostringstream o;
+    o << kIdsCommon;
+    o << "#define LW " << LWv << "u\n#define WU " << WU << "\n";
+    o << R"IDS(
+extern "C" __global__ __launch_bounds__(256) void pm_ids_rev(IArgs a) {
+    constexpr u32 LANES = STREAM / LW;   // lanes per tile
+    constexpr u32 TPW = 64 / LANES;      // tiles per wave
+    const u32 lane = threadIdx.x & 63, sub = lane / LANES, col = lane % LANES;
+    const u64 wave = (blockIdx.x * 256ull + threadIdx.x) >> 6, nwaves = gridDim.x * 4ull;
+    for (u64 tg = wave; tg * TPW < a.ntiles; tg += nwaves) {
+        const u64 tile0 = tg * TPW + sub;
+        const bool live = tile0 < a.ntiles;
+        const u64 tile = live ? tile0 : a.ntiles - 1;
+        // lflag bit c: lane column c (32 words) and the 63 words after it
+        // hold an exception
+        const u64 cols = ((1ull << (LW / 32)) - 1) << (col * (LW / 32));
+        const bool flagged = (a.lflag[tile] & cols) != 0;
+)IDS";
+    for (int j = 0; j <= k; ++j)
+        for (int i = 0; i < m; ++i) o << "        u32 " << V('r', j, i) << " = 0, " << V('s', j, i) << " = 0;\n";
+    const int steps = LWv + WU;
+    // words are loaded IDS_U steps ahead: the body is IDS_U steps over the
+    // words loaded by the previous iteration while the next IDS_U load; the
+    // first steps % IDS_U steps run alone with their own loads
+    auto load = [&](const std::string& tv, const std::string& vv, const std::string& ev) {
+        o << "            " << vv << " = a.hl[phys(tile, col * LW + (u32)(" << tv << "))];\n";
+        o << "            " << ev << " = flagged ? a.bo[phys(tile, col * LW + (u32)(" << tv
+          << "))] : make_uint2(0u, 0u);\n";
+    };
+    const int peel = steps % U;
+    char b0 = 'r', b1 = 's';
+    int top = steps - 1;
+    o << "        uint2 pv, pe;\n";
+    for (int q = 0; q < peel; ++q) {
+        o << "        {\n";
+        load(std::to_string(top), "pv", "pe");
+        step(o, b0, b1, std::to_string(top), "pv", "pe");
+        o << "        }\n";
+        std::swap(b0, b1);
+        --top;
+    }
+    for (int u = 0; u < U; ++u) o << "        uint2 c" << u << ", ce" << u << ", q" << u << ", qe" << u << ";\n";
+    for (int u = 0; u < U; ++u) {
+        o << "        {\n";
+        load(std::to_string(top - u), "c" + std::to_string(u), "ce" + std::to_string(u));
+        o << "        }\n";
+    }
+    o << "        for (int tt = " << top << "; tt >= " << U - 1 << "; tt -= " << U << ") {\n";
+    o << "            if (tt >= " << 2 * U - 1 << ") {   // the next iteration's words\n";
+    for (int u = 0; u < U; ++u)
+        load("tt - " + std::to_string(U + u), "q" + std::to_string(u), "qe" + std::to_string(u));
+    o << "            }\n";
+    for (int u = 0; u < U; ++u) {
+        step(o, b0, b1, "tt - " + std::to_string(u), "c" + std::to_string(u), "ce" + std::to_string(u));
+        std::swap(b0, b1);
+    }
+    for (int u = 0; u < U; ++u) o << "            c" << u << " = q" << u << "; ce" << u << " = qe" << u << ";\n";
+    o << "        }\n";
+    o << "    }\n}\n";
+    return o.str();
+}
+
+struct IdsKernel {
+    hipModule_t module = nullptr;
+    hipFunction_t fn = nullptr;
+};
+std::mutex g_ids_mu;
+std::map<std::pair<int, std::string>, IdsKernel> g_ids_cache;
+
+}  // namespace
+
+bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
+    if (db->alphabet != PM_ALPHA_NUC || sp.m * (sp.k + 1) > IDS_MAX_REGS || sp.m > 64) return false;
+    const int WU = sp.m + ((sp.errs & PM_ERR_INS) ? sp.k : 0) - 1;
+    if (WU > HALO - 1) return false;   // the warm-up must fit the next lane column or the halo
+    std::string sig;
+    const std::string src = gen_ids_source(sp, &sig);
+    hipFunction_t fn;
+    {
+        std::lock_guard<std::mutex> lk(g_ids_mu);
+        auto key = std::make_pair(db->device, sig);
+        auto it = g_ids_cache.find(key);
+        if (it == g_ids_cache.end()) {
+            std::vector<char> code = hiprtc_compile(src);
+            IdsKernel kk;
+            HIPCHK(hipModuleLoadData(&kk.module, code.data()));
+            HIPCHK(hipModuleGetFunction(&kk.fn, kk.module, "pm_ids_rev"));
+            it = g_ids_cache.emplace(key, kk).first;
+        }
+        fn = it->second.fn;
+    }
+    const NucView nv = nuc_view(db);
+    IArgsHost a{nv.hl, nv.bo, nv.sbflag, nv.sbbase, nv.xbytes, db->lflag, sp.d_bmask, db->ntiles, db->n,
+                sink.out, sink.bin_cnt, sink.cap, sink.bins_per_pattern, sink.pos_shift, (uint32_t)sp.pattern_id};
+    void* params[] = {&a};
+    const uint64_t tpw = 64 / (STREAM / ids_lw());
+    const uint64_t groups = (db->ntiles + tpw - 1) / tpw;   // one wave per tile group
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((groups + 3) / 4, 256 * 8));
+    HIPCHK(hipExtModuleLaunchKernel(fn, blocks * 256u, 1, 1, 256, 1, 1, 0, s, params, nullptr, ev_a, ev_b, 0));
+    return true;
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" int pm_ids_jit_compile(int m, const uint64_t* byte_mask, int k, int errs, uint64_t* code_bytes) {
+    return guarded([&] {
+        require(byte_mask != nullptr && code_bytes != nullptr, "null argument");
+        require(m >= 1 && m <= 64 && k >= 0 && k <= PM_MAX_K && m * (k + 1) <= IDS_MAX_REGS,
+                "shape not covered by the bit-sliced kernel", PM_E_UNSUPPORTED);
+        require((errs & ~(PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB)) == 0, "bad error-type mask");
+        // the start configuration of a plain class sequence, as scan_nfa builds it
+        IdsSpec sp{m, k, errs, byte_mask, nullptr, {}, {}, 0};
+        const uint64_t last = 1ull << (m - 1);
+        uint64_t S = 0;
+        for (int j = 0; j <= k; ++j) {
+            sp.rev_ins[j] = S;
+            sp.rev_pre[j] = (S >> 1) | ((j == 0 || (errs & PM_ERR_INS)) ? last : 0);
+            if (errs & PM_ERR_DEL) S = (S >> 1) | ((j == 0 || (errs & PM_ERR_INS)) ? last : 0);
+            else S = 0;
+        }
+        std::string sig;
+        *code_bytes = hiprtc_compile(gen_ids_source(sp, &sig)).size();
+    });
+}

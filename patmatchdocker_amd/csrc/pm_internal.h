@@ -407,6 +407,23 @@ void pool_put(int device, void* p, size_t cap);
 void* reserve_host(pm_db* db, pm_hostbuf& b, size_t bytes);
 NucView nuc_view(const pm_db* db);
 
+// hipRTC: compiles generated kernel source for gfx950 (pm_linear.hip)
+std::vector<char> hiprtc_compile(const std::string& src);
+
+// The reverse (start-finding) pass of a class-sequence automaton with
+// insertions / deletions / substitutions, bit-sliced over the 32 streams of
+// the nucleotide planes (pm_ids.hip).  Emits every start into `sink` as
+// k_nfa_rev would.  Returns false (nothing launched) when the shape is not
+// covered (positions x rows too many for registers).
+struct IdsSpec {
+    int m, k, errs;
+    const uint64_t* byte_mask;   // [256] positions accepting each folded byte (host)
+    const uint64_t* d_bmask;     // the same table on the device ('\n' accepted by none)
+    uint64_t rev_pre[PM_MAX_K + 1], rev_ins[PM_MAX_K + 1];   // the injected start config (scan_nfa)
+    int pattern_id;
+};
+bool ids_rev_scan(pm_db* db, const IdsSpec& spec, const Sink& sink, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b);
+
 // Carves 256-byte aligned pieces out of one buffer.
 struct Carve {
     size_t off = 0;

@@ -1471,6 +1471,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
 
 namespace pm {
 
+std::vector<char> hiprtc_compile(const std::string& src) { return jit_compile(src); }
+
 void hits_finalize(pm_hits* h) {
     if (!h || !h->pending) return;
     pm_db* db = h->pending->db;

@@ -383,6 +383,14 @@ __global__ __launch_bounds__(256) void k_nfa_verify(NfaArgs a) {
                      X(0, 2) X(1, 2) X(2, 2) X(3, 2) X(7, 2) X(15, 2) \
                      X(0, 4) X(1, 4) X(2, 4) X(3, 4) X(7, 4)
 
+// PM_IDS_JIT: "0" never, "1" always, default: databases of >= 64 Mi
+// positions (below, the hipRTC compile would dominate the scan)
+bool use_ids_kernel(const pm_db* db) {
+    const char* e = getenv("PM_IDS_JIT");
+    if (e) return e[0] != '0';
+    return db->n >= (64ull << 20);
+}
+
 int kernel_rows(int k) { return k <= 3 ? k : k <= 7 ? 7 : 15; }
 int kernel_words(int m) { return m <= 64 ? 1 : m <= 128 ? 2 : 4; }
 bool nfa_supported(int k, int m) { return k <= PM_MAX_K && m <= PM_MAX_POSITIONS && !(kernel_words(m) == 4 && k > 7); }
@@ -605,14 +613,28 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         carry_ms = cev.ms();
         a.in_state = st[cur];
     }
+    // a class sequence on the nucleotide planes: the bit-sliced start pass
+    // (pm_ids.hip), 32 streams per lane instead of one
+    const bool ids = nuc && W == 1 && a.shift_only && !cross && !unbounded && use_ids_kernel(db);
     for (int attempt = 0; attempt < 2; ++attempt) {
         sb = make_sink(db, 1, db->n, expected);
         a.sink = sb.sink();
-        HIPCHK(hipEventRecord(ev.a, s));
-        if (nuc) launch_nfa_rev<true>(K, W, a, blocks, s);
-        else launch_nfa_rev<false>(K, W, a, blocks, s);
+        bool launched = false;
+        if (ids) {
+            IdsSpec sp{m, k, errs, bm.data(), a.bmask, {}, {}, pattern_id};
+            for (int j = 0; j <= k; ++j) {
+                sp.rev_pre[j] = rev_pre[j][0];
+                sp.rev_ins[j] = rev_ins[j][0];
+            }
+            launched = ids_rev_scan(db, sp, a.sink, s, ev.a, ev.b);
+        }
+        if (!launched) {
+            HIPCHK(hipEventRecord(ev.a, s));
+            if (nuc) launch_nfa_rev<true>(K, W, a, blocks, s);
+            else launch_nfa_rev<false>(K, W, a, blocks, s);
+            HIPCHK(hipEventRecord(ev.b, s));
+        }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(ev.b, s));
         bool overflow = false;
         total = sink_total(db, sb, counts, overflow);
         if (!overflow) break;

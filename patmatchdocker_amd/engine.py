@@ -270,6 +270,18 @@ def jit_compile(progs: Sequence[Program], k: int) -> int:
     return nbytes.value
 
 
+def ids_jit_compile(prog: Program, k: int, types: str = "ids") -> int:
+    """Generate + hipRTC-compile the bit-sliced start pass for a class
+    sequence with insertions/deletions (no GPU needed); returns the
+    code-object size in bytes."""
+    bm = np.array(prog.byte_masks(), dtype=np.uint64)
+    bm[10] = 0
+    nbytes = ctypes.c_uint64()
+    check(_lib.load().pm_ids_jit_compile(prog.m, bm.ctypes.data, k, error_mask(types) if k else _lib.PM_ERR_SUB,
+                                         ctypes.byref(nbytes)))
+    return nbytes.value
+
+
 def kernel_ms(handle) -> float:
     ms = ctypes.c_double()
     check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))
@@ -294,11 +306,10 @@ def _words(x: int, w: int) -> List[int]:
     return [(x >> (64 * q)) & 0xFFFFFFFFFFFFFFFF for q in range(w)]
 
 
-def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
-             flags: int = None) -> Hits:
-    """The automaton kernels (pm_scan_nfa_wide).  A class sequence at k = 0
-    runs as nrgrep's simple engine (PM_CROSS_LINES: windows may span a line
-    break when a class accepts '\n'), as in the fixed-length kernel."""
+def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
+               flags: int = None):
+    """pm_scan_nfa_wide; returns the raw pm_hits handle (caller destroys),
+    keys ``pattern_id << 48 | beg`` -- see :func:`scan_nfa`."""
     w = nfa_words(prog.m)
     bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
     fol = np.array([_words(x, w) for x in prog.follow], dtype=np.uint64)
@@ -312,7 +323,15 @@ def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, t
     check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                        last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,
                                        flags, ctypes.byref(out)))
-    return _collect(out)
+    return out
+
+
+def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
+             flags: int = None) -> Hits:
+    """The automaton kernels (pm_scan_nfa_wide).  A class sequence at k = 0
+    runs as nrgrep's simple engine (PM_CROSS_LINES: windows may span a line
+    break when a class accepts '\\n'), as in the fixed-length kernel."""
+    return _collect(nfa_launch(db, prog, k, pattern_id, types, flags))
 
 
 def _same_automaton(a: Program, b: Program) -> bool:

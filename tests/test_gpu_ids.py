@@ -1,0 +1,89 @@
+"""The bit-sliced start pass for class sequences with insertions /
+deletions (pm_ids.hip, PM_IDS_JIT=1 forces it on small databases): the
+candidates and the reported matches equal the oracle's (pmo_scan2) on
+multi-tile databases with N runs, IUPAC letters, lower case, wrapped lines
+and motif-laden headers."""
+import os
+import sys
+
+import pytest
+
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+from tests.fastagen import dna_fasta
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_gpu_report import repeat_fasta  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from patmatchdocker_amd import _lib
+    from patmatchdocker_amd import engine as eng
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+    return eng
+
+
+def _pairs(r):
+    return list(zip(r[0].tolist(), r[1].tolist()))
+
+
+TEXTS = {
+    "dna": lambda: dna_fasta(81, n_records=4, min_len=60000, max_len=140000),
+    "repeats": lambda: repeat_fasta(82, n_records=3, min_len=50000, max_len=90000),
+    "wrapped": lambda: dna_fasta(83, n_records=3, min_len=20000, max_len=50000, width=60),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_ids_pass_equals_oracle(engine, oracle_mod, monkeypatch, name):
+    monkeypatch.setenv("PM_IDS_JIT", "1")
+    text = TEXTS[name]()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat, k, types in [("TGCTGASTCAGCANW", 2, "ids"), ("TATAWAWR", 1, "ids"), ("GAATTC", 1, "id"),
+                              ("GAATTC", 2, "i"), ("TGCTGASTCAGCANW", 3, "ds"), ("AWA", 1, "is"),
+                              ("CAACAACAA", 2, "ids"), ("TANNA", 1, "ids")]:
+            fwd = convert("-n", pat)
+            progs = [compile_pattern(fwd, ignore_case=True), compile_pattern(convert("-c", fwd), ignore_case=True)]
+            for prog in progs:
+                for report in ("nrgrep", "all"):
+                    r = engine.scan_nfa(db, prog, k, 0, types, engine.report_flags(prog, report))
+                    want = oracle_mod.scan_reported(text, prog, k, types, skip_headers=True, report=report)
+                    assert list(zip(r.beg.tolist(), r.end.tolist())) == want, (name, prog.source, k, types, report)
+    finally:
+        db.close()
+
+
+def test_ids_pass_substitutions_only(engine, oracle_mod, monkeypatch):
+    """errs = s through the automaton path (the linear kernel's job normally)."""
+    monkeypatch.setenv("PM_IDS_JIT", "1")
+    text = dna_fasta(84, n_records=3, min_len=40000, max_len=90000)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for pat, k in [("TGCTGASTCAGCANW", 2), ("TATAWAWR", 1), ("GAATTC", 3)]:
+            prog = compile_pattern(convert("-n", pat), ignore_case=True)
+            r = engine.scan_nfa(db, prog, k, 0, "s")
+            want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+            assert _pairs((r.beg, r.end)) == want, (pat, k)
+    finally:
+        db.close()
+
+
+def test_ids_pass_through_engine_scan(engine, oracle_mod, monkeypatch):
+    """engine.scan routes '-k 2ids' to the automaton kernels, which take the
+    bit-sliced start pass: both strands, reported."""
+    monkeypatch.setenv("PM_IDS_JIT", "1")
+    text = dna_fasta(85, n_records=3, min_len=30000, max_len=70000)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        fwd = convert("-n", "TGCTGASTCAGCANW")
+        progs = [compile_pattern(fwd, ignore_case=True), compile_pattern(convert("-c", fwd), ignore_case=True)]
+        res, _ = engine.scan(db, progs, k=2, types="ids")
+        for prog, r in zip(progs, res):
+            assert _pairs(r) == oracle_mod.scan_reported(text, prog, 2, "ids", skip_headers=True)
+    finally:
+        db.close()

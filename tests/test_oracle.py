@@ -117,3 +117,19 @@ def test_python_reported_oracle_equals_c_oracle(oracle_mod, seed):
         for k, t in [(0, "s"), (1, "s"), (1, "ids"), (2, "id"), (2, "s")]:
             want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True, simple=False)
             assert oracle_mod.scan_py_reported(text, prog, k, t, skip_headers=True) == want, (p, k, t)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ids_cpu_scan_equals_reported_oracle(oracle_mod, seed):
+    """The bench's `-k <k>ids` CPU baseline (pmc_ids_scan, bit-parallel)
+    reports exactly what the oracle does."""
+    from tests.test_gpu_report import repeat_fasta
+    text = dna_fasta(seed + 40, n_records=4, max_len=4000) if seed % 2 else repeat_fasta(seed + 40, 3, 1000, 4000)
+    for pat in ["TGCTGASTCAGCANW", "TATAWAWR", "GAATTC", "AWA", "CAACAACAA", "TANNA"]:
+        prog = compile_pattern(convert("-n", pat), ignore_case=True)
+        for k, t in [(1, "ids"), (2, "ids"), (2, "i"), (1, "d"), (3, "ds"), (2, "is"), (1, "s")]:
+            if "d" in t and k >= prog.m:
+                continue
+            want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True)
+            assert oracle_mod.ids_scan(text, prog, k, t, skip_headers=True) == want, (pat, k, t)
+            assert oracle_mod.ids_threads(text, prog, k, t, skip_headers=True, threads=3) == want, (pat, k, t)

@@ -20,9 +20,9 @@
 // handled in a second copy of the step taken only when a lane of the wave
 // sees one.
 //
-// Lanes: each lane owns LW consecutive logical words of one tile's streams
-// and scans them right to left after a warm-up of L - 1 words (L = the
-// longest match, m + k), read from the next lane's words or the tile's halo.
+// Lanes: one wave per tile, lane c owns the tile's stream column c (32
+// logical words) and scans it right to left after a warm-up of L - 1 words
+// (L = the longest match, m + k) read from the next column or the halo.
 #include <map>
 #include <sstream>
 
@@ -33,20 +33,7 @@
 namespace pm {
 namespace {
 
-// logical words per lane (2 lane columns of the layout); PM_IDS_LW = 32,
-// 64 or 128 (experiment knob)
-int ids_lw() {
-    const char* e = getenv("PM_IDS_LW");
-    const int v = e ? atoi(e) : 64;
-    return v == 32 || v == 128 ? v : 64;
-}
 constexpr int IDS_MAX_REGS = 64;   // m * (k + 1) state registers at most
-// steps per loop iteration = words loaded ahead; PM_IDS_U = 1, 2, 4, 8
-int ids_u() {
-    const char* e = getenv("PM_IDS_U");
-    const int v = e ? atoi(e) : 4;
-    return v == 1 || v == 2 || v == 8 ? v : 4;
-}
 
 const char* kIdsCommon = R"IDS(
 typedef unsigned int u32;
@@ -141,8 +128,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    const int LWv = ids_lw(), U = ids_u();
-    sg << "ids:" << m << ":" << k << ":" << sp.errs << ":" << LWv << ":" << U << ":";
+    sg << "ids2:" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
     for (int j = 0; j <= k; ++j) sg << ":" << sp.rev_pre[j] << "," << sp.rev_ins[j];
     *sig = sg.str();
@@ -183,15 +169,13 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
                 o << ind << V(dst, j, i) << " = " << (kill ? "(" + e + ") & nb" : e) << ";\n";
             }
     };
-    // one step over word t = `tv`, whose plane / exception words are the
-    // variables `vv` / `ev` (loaded ahead, see below)
+    // one step over word t = `tv` of the lane's stream column, whose plane /
+    // exception words are `vv` / `ev` and whose plane word is at pointer `pv`;
+    // `emit`: t < 32 (the lane's own column) -- report starts
     auto step = [&](std::ostringstream& o, char src, char dst, const std::string& tv, const std::string& vv,
-                    const std::string& ev) {
+                    const std::string& ev, const std::string& pv, bool emit) {
         const std::string in = "            ";
         o << in << "{\n";
-        o << in << "    const int t = " << tv << ";\n";
-        o << in << "    const u32 w = col * LW + (u32)t;\n";
-        o << in << "    const u64 pw = phys(tile, w);\n";
         o << in << "    const uint2 v = " << vv << ", e = " << ev << ";\n";
         for (size_t c = 0; c < rep.size(); ++c) {
             const PosClass& p = pc[rep[c]];
@@ -202,6 +186,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         o << in << "        const u32 nb = ~e.x;\n";
         // "other" bytes: the byte's own class membership
         o << in << "        if (e.y) {\n";
+        o << in << "            const u64 pw = (u64)(" << pv << " - a.hl);\n";
         o << in << "            const u32 f = a.sbflag[pw >> 5];\n";
         o << in << "            const u32 xi = a.sbbase[pw >> 5] + __popc(f & ((1u << (u32)(pw & 31)) - 1u));\n";
         o << in << "            for (u32 ob = e.y; ob; ob &= ob - 1) {\n";
@@ -216,76 +201,84 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         o << in << "    } else {\n";
         update(o, src, dst, false, in + "        ");
         o << in << "    }\n";
-        o << in << "    if (t < (int)LW && live) {\n";
-        o << in << "        u32 em = 0u";
-        for (int j = 0; j <= k; ++j) o << " | " << V(dst, j, 0);
-        o << ";\n";
-        o << in << "        for (; em; em &= em - 1) {\n";
-        o << in << "            const u64 pos = tile * TILE_POS + (u64)__builtin_ctz(em) * STREAM + w;\n";
-        o << in << "            if (pos < a.n) push(a, pos);\n";
-        o << in << "        }\n";
-        o << in << "    }\n";
+        if (emit) {
+            o << in << "    u32 em = 0u";
+            for (int j = 0; j <= k; ++j) o << " | " << V(dst, j, 0);
+            o << ";\n";
+            o << in << "    for (; em; em &= em - 1) {\n";
+            o << in << "        const u64 pos = tile * TILE_POS + (u64)__builtin_ctz(em) * STREAM + col * 32u + (u32)("
+              << tv << ");\n";
+            o << in << "        if (pos < a.n) push(a, pos);\n";
+            o << in << "    }\n";
+        }
         o << in << "}\n";
     };
 
     std::ostringstream o;
     o << kIdsCommon;
-    o << "#define LW " << LWv << "u\n#define WU " << WU << "\n";
+    o << "#define WU " << WU << "\n";
     o << R"IDS(
+// One wave per tile; lane c owns stream column c (logical words 32c ..
+// 32c + 31, physical word t * 64 + c at step t): it scans the next column's
+// first WU words (or the tile's halo, lane 63) right to left as warm-up,
+// then its own 32 words, reporting starts.
 extern "C" __global__ __launch_bounds__(256) void pm_ids_rev(IArgs a) {
-    constexpr u32 LANES = STREAM / LW;   // lanes per tile
-    constexpr u32 TPW = 64 / LANES;      // tiles per wave
-    const u32 lane = threadIdx.x & 63, sub = lane / LANES, col = lane % LANES;
+    const u32 col = threadIdx.x & 63;
     const u64 wave = (blockIdx.x * 256ull + threadIdx.x) >> 6, nwaves = gridDim.x * 4ull;
-    for (u64 tg = wave; tg * TPW < a.ntiles; tg += nwaves) {
-        const u64 tile0 = tg * TPW + sub;
-        const bool live = tile0 < a.ntiles;
-        const u64 tile = live ? tile0 : a.ntiles - 1;
-        // lflag bit c: lane column c (32 words) and the 63 words after it
-        // hold an exception
-        const u64 cols = ((1ull << (LW / 32)) - 1) << (col * (LW / 32));
-        const bool flagged = (a.lflag[tile] & cols) != 0;
+    const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
+    for (u64 tile = wave; tile < a.ntiles; tile += nwaves) {
+        // lflag bit c: column c and the 63 words after it hold an exception
+        const bool flagged = (a.lflag[tile] >> col) & 1ull;
+        const uint2* tb = a.hl + tile * TILE_WORDS;
+        const uint2* pn = col < 63u ? tb + col + 1 : tb + STREAM;   // warm-up words: t - 32 ..
+        const long sn = col < 63u ? 64 : 1;
+        const uint2* pm = tb + col;                                  // own words: t * 64
 )IDS";
     for (int j = 0; j <= k; ++j)
         for (int i = 0; i < m; ++i) o << "        u32 " << V('r', j, i) << " = 0, " << V('s', j, i) << " = 0;\n";
-    const int steps = LWv + WU;
-    // words are loaded IDS_U steps ahead: the body is IDS_U steps over the
-    // words loaded by the previous iteration while the next IDS_U load; the
-    // first steps % IDS_U steps run alone with their own loads
-    auto load = [&](const std::string& tv, const std::string& vv, const std::string& ev) {
-        o << "            " << vv << " = a.hl[phys(tile, col * LW + (u32)(" << tv << "))];\n";
-        o << "            " << ev << " = flagged ? a.bo[phys(tile, col * LW + (u32)(" << tv
-          << "))] : make_uint2(0u, 0u);\n";
+    o << "        uint2 v0, e0, v1, e1;\n";
+    o << "        const uint2* p0;\n";
+    o << "        const uint2* p1;\n";
+    auto ptr = [](bool own, const std::string& tv) {
+        return own ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn";
     };
-    const int peel = steps % U;
+    auto load = [&](const std::string& pv, const std::string& vv, const std::string& ev, bool own,
+                    const std::string& tv, const std::string& ind) {
+        o << ind << pv << " = " << ptr(own, tv) << ";\n";
+        o << ind << vv << " = *" << pv << ";\n";
+        o << ind << ev << " = flagged ? " << pv << "[dbo] : make_uint2(0u, 0u);\n";
+    };
+    // a phase: `n` steps from t = `t0` down, pointer form `own`; pairs of
+    // steps alternate the register banks and the word buffers (each step's
+    // successor word is loaded before the step runs)
     char b0 = 'r', b1 = 's';
-    int top = steps - 1;
-    o << "        uint2 pv, pe;\n";
-    for (int q = 0; q < peel; ++q) {
+    auto phase = [&](int t0, int n, bool own) {
+        int t = t0;
+        if (n % 2) {   // a single step first
+            o << "        {\n";
+            load("p0", "v0", "e0", own, std::to_string(t), "            ");
+            step(o, b0, b1, std::to_string(t), "v0", "e0", "p0", own);
+            o << "        }\n";
+            std::swap(b0, b1);
+            --t;
+            --n;
+        }
+        if (!n) return;
+        const std::string ind = "            ";
         o << "        {\n";
-        load(std::to_string(top), "pv", "pe");
-        step(o, b0, b1, std::to_string(top), "pv", "pe");
+        load("p0", "v0", "e0", own, std::to_string(t), ind);
         o << "        }\n";
-        std::swap(b0, b1);
-        --top;
-    }
-    for (int u = 0; u < U; ++u) o << "        uint2 c" << u << ", ce" << u << ", q" << u << ", qe" << u << ";\n";
-    for (int u = 0; u < U; ++u) {
-        o << "        {\n";
-        load(std::to_string(top - u), "c" + std::to_string(u), "ce" + std::to_string(u));
+        o << "        for (int t = " << t << "; t >= " << t - n + 2 << "; t -= 2) {\n";
+        load("p1", "v1", "e1", own, "t - 1", ind);
+        step(o, b0, b1, "t", "v0", "e0", "p0", own);
+        o << ind << "if (t - 2 >= " << t - n + 1 << ") {\n";
+        load("p0", "v0", "e0", own, "t - 2", ind + "    ");
+        o << ind << "}\n";
+        step(o, b1, b0, "t - 1", "v1", "e1", "p1", own);
         o << "        }\n";
-    }
-    o << "        for (int tt = " << top << "; tt >= " << U - 1 << "; tt -= " << U << ") {\n";
-    o << "            if (tt >= " << 2 * U - 1 << ") {   // the next iteration's words\n";
-    for (int u = 0; u < U; ++u)
-        load("tt - " + std::to_string(U + u), "q" + std::to_string(u), "qe" + std::to_string(u));
-    o << "            }\n";
-    for (int u = 0; u < U; ++u) {
-        step(o, b0, b1, "tt - " + std::to_string(u), "c" + std::to_string(u), "ce" + std::to_string(u));
-        std::swap(b0, b1);
-    }
-    for (int u = 0; u < U; ++u) o << "            c" << u << " = q" << u << "; ce" << u << " = qe" << u << ";\n";
-    o << "        }\n";
+    };
+    phase(31 + WU, WU, false);   // warm-up: t = 32 + WU - 1 .. 32
+    phase(31, 32, true);         // own column: t = 31 .. 0
     o << "    }\n}\n";
     return o.str();
 }
@@ -323,9 +316,8 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     IArgsHost a{nv.hl, nv.bo, nv.sbflag, nv.sbbase, nv.xbytes, db->lflag, sp.d_bmask, db->ntiles, db->n,
                 sink.out, sink.bin_cnt, sink.cap, sink.bins_per_pattern, sink.pos_shift, (uint32_t)sp.pattern_id};
     void* params[] = {&a};
-    const uint64_t tpw = 64 / (STREAM / ids_lw());
-    const uint64_t groups = (db->ntiles + tpw - 1) / tpw;   // one wave per tile group
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((groups + 3) / 4, 256 * 8));
+    // one wave per tile, waves loop over tiles (every wave reaches the end)
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((db->ntiles + 3) / 4, 256 * 8));
     HIPCHK(hipExtModuleLaunchKernel(fn, blocks * 256u, 1, 1, 256, 1, 1, 0, s, params, nullptr, ev_a, ev_b, 0));
     return true;
 }

@@ -57,12 +57,15 @@ __global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict
 }
 
 // One workgroup per bin: bitonic sort in LDS, write at the bin's offset.
+// CAP keys per bin at most (2048: 16 KB of LDS; 4096 when a bin may hold
+// more, 32 KB); larger bins are left to the caller.
+template <uint32_t CAP>
 __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
                                                    const uint64_t* __restrict__ off, BinShape sh,
                                                    uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
                                                    uint32_t* __restrict__ lens, uint32_t* counts_host = nullptr,
                                                    uint32_t nbins = 0, uint64_t* total_out = nullptr) {
-    __shared__ uint64_t s[LDS_SORT_CAP];
+    __shared__ uint64_t s[CAP];
     const uint32_t bin = blockIdx.x;
     if (counts_host && bin == 0) {   // the pipelined scan's count readback (mapped host memory)
         for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
         if (threadIdx.x == 0) *total_out = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
     const uint32_t c = min(cnt[bin], sh.cap(bin));
-    if (c == 0 || c > LDS_SORT_CAP) return;   // (a speculative sort's caller redoes such lists)
+    if (c == 0 || c > CAP) return;   // (a speculative sort's caller redoes such lists)
     uint64_t base;
     if (off) {
         base = off[bin];
@@ -353,16 +356,20 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
         h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 8, &h->keys_cap));
         h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(cap_total, 1) * 4, &h->lens_cap));
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
+        // a bin holds at most its slot's capacity: the 4096-key sort when a
+        // capacity exceeds 2048
+        const bool big = *std::max_element(sb.slot_cap_h.begin(), sb.slot_cap_h.end()) > LDS_SORT_CAP;
+        auto kern = big ? k_sort_bins<LDS_SORT_CAP_MAX> : k_sort_bins<LDS_SORT_CAP>;
         if (counts_host && bind_ready) {
             // pipelined scan: the list's ready event is bound to the sort's
             // own dispatch (no marker packet before the next scan's kernel)
             HIPCHK(hipEventCreate(&h->ready));
-            hipExtLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, nullptr, h->ready, 0u, sb.out,
+            hipExtLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, stream, nullptr, h->ready, 0u, sb.out,
                                   sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
                                   sb.nbins, total_out);
         } else {
-            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
-                               sb.cnt, nullptr, sh, h->keys, slot_len, h->lens, counts_host,
+            hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
+                               sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
                                (counts_host || total_out) ? sb.nbins : 0u, total_out);
         }
         HIPCHK(hipGetLastError());
@@ -394,7 +401,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                                                   &h->lens_cap));
         if (total == 0) return h;
         const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
-        const bool lds = maxc <= LDS_SORT_CAP;
+        const bool lds = maxc <= LDS_SORT_CAP_MAX;
         size_t sort_bytes = 0;
         if (!lds)
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
@@ -413,8 +420,10 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             HIPCHK(hipGetLastError());
         }
         if (lds) {
-            hipLaunchKernelGGL(k_sort_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt,
-                               inline_off ? nullptr : d_off, sh, h->keys, slot_len, h->lens);
+            auto kern = maxc > LDS_SORT_CAP ? k_sort_bins<LDS_SORT_CAP_MAX> : k_sort_bins<LDS_SORT_CAP>;
+            hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt,
+                               inline_off ? (const uint64_t*)nullptr : (const uint64_t*)d_off, sh, h->keys, slot_len,
+                               h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr);
             if (lens_done) *lens_done = slot_len != nullptr;
             HIPCHK(hipGetLastError());
         } else {

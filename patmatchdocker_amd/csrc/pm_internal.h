@@ -100,6 +100,7 @@ constexpr uint32_t NBINS = 1024;                     // hit bins (at least)
 constexpr uint32_t MAX_BINS = 8192;
 constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_nfa_rev
 constexpr uint32_t LDS_SORT_CAP = 2048;              // keys per bin sorted in LDS (16 KB: 8 sort blocks per CU)
+constexpr uint32_t LDS_SORT_CAP_MAX = 4096;          // the larger sort variant (32 KB), for bins above LDS_SORT_CAP
 constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
 constexpr int RUN_SKIP = 8;                          // run-interior lookahead (xint)
 
@@ -479,7 +480,7 @@ SinkBuffers make_sink_segments(pm_db* db, int n_slots, uint32_t per_slot, const 
 uint64_t sink_total(pm_db* db, const SinkBuffers& sb, std::vector<uint32_t>& counts, bool& overflow);
 // bins -> one sorted key list (pattern << 48 | pos) owned by the returned
 // hits; lens are left for the caller to fill.
-// Sorts every bin (<= 4096 bins, lists <= LDS_SORT_CAP keys) into a list
+// Sorts every bin (<= 4096 bins, lists <= LDS_SORT_CAP_MAX keys) into a list
 // sized for all capacities BEFORE the counts reach the host, so a scan needs
 // one host sync; count unset -- the caller validates the counts it reads
 // afterwards and keeps the result (count = total) or discards it.

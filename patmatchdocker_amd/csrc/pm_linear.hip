@@ -1385,7 +1385,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 const uint32_t rec_need = sb.aux;
                 if (!overflow && rec_need == 0) {
                     done = true;
-                    if (spec && total && *std::max_element(counts.begin(), counts.end()) <= LDS_SORT_CAP) {
+                    if (spec && total && *std::max_element(counts.begin(), counts.end()) <= LDS_SORT_CAP_MAX) {
                         spec->count = total;
                         hit_list = spec;
                     } else {
@@ -1493,7 +1493,7 @@ void hits_finalize(pm_hits* h) {
         overflow |= c > pd->slot_cap_h[b / pd->bins_per_pattern];
     }
     const bool rec_over = pd->counts_h[pd->nbins] != 0;
-    if (!overflow && !rec_over && maxc <= LDS_SORT_CAP) {   // the speculative list is the answer
+    if (!overflow && !rec_over && maxc <= LDS_SORT_CAP_MAX) {   // the speculative list is the answer
         h->count = pd->reported ? pd->counts_h[pd->nbins + 1] : total;
         double kms = 0.0;
         for (auto& e : pd->jev) kms += e->ms();

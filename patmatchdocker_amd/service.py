@@ -183,6 +183,11 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
     outputs = [""] * len(patterns)
     if not progs:
         return outputs
+    # shapes no GPU kernel takes raise UnsupportedOnGPU here, before the
+    # database is touched (run_patmatch answers them with an error)
+    types = engine.parse_error_types(k, types)
+    for prog in progs:
+        engine.route(prog, engine.NUC, k, types)
     world, rank = _world()
     if world > 1:
         # one process per GPU (torchrun): every rank scans its record-aligned
@@ -620,9 +625,16 @@ def run_patmatch(request, id):
         pattern, get_param(request, "seqtype"), get_param(request, "strand"),
         get_param(request, "insertion"), get_param(request, "deletion"),
         get_param(request, "substitution"), get_param(request, "mismatch"))
-    data, uniqueHits, totalHits, error_message = _search_and_collect(
-        pattern, comp_pattern, option, datafile, get_param(request, "max_hits"), begMatch, endMatch,
-        downloadFile, pattern)
+    try:
+        data, uniqueHits, totalHits, error_message = _search_and_collect(
+            pattern, comp_pattern, option, datafile, get_param(request, "max_hits"), begMatch, endMatch,
+            downloadFile, pattern)
+    except engine.UnsupportedOnGPU as exc:
+        # a query shape no GPU kernel takes (deletions with as many errors as
+        # the pattern's shortest match, > 256 automaton positions, > 15
+        # errors): an explicit error like check_pattern's, never a 500 and
+        # never a silent empty result (there is no CPU scan path)
+        return {"error": "This search is not supported by the GPU scan: %s" % exc}
     downloadUrl = ""
     if uniqueHits > 0:
         try:

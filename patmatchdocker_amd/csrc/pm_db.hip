@@ -52,6 +52,7 @@ __global__ void k_pack_nuc(const uint8_t* __restrict__ raw, uint64_t n, uint64_t
             br |= 1u << b;
         } else {
             ot |= 1u << b;
+            if ((raw[p] & 0xdf) == 'N') h |= 1u << b;   // an "other" byte's hi bit: it is N (NUC_N_MARK)
         }
     }
     const uint64_t pw = phys_word(t, w);
@@ -94,7 +95,7 @@ __global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint
     const uint32_t w = (uint32_t)(g % STREAM);
     const uint64_t stride = SYN_HDR + 1 + rec_len + 1;
     const uint64_t r = mix64(seed * 0x9e3779b97f4a7c15ull + g);
-    uint32_t br = 0, ot = 0;
+    uint32_t br = 0, ot = 0, nn = 0;
     const uint64_t p0 = pos_of(t, w, 0);
     uint64_t q = p0 % stride;
     const uint64_t d = STREAM % stride;
@@ -102,12 +103,15 @@ __global__ void k_pack_synth(uint64_t n, uint64_t ntiles, uint64_t rec_len, uint
         const uint64_t p = p0 + (uint64_t)b * STREAM;
         const bool is_base = p < n && q >= SYN_HDR + 1 && q < SYN_HDR + 1 + rec_len;
         if (!is_base) br |= 1u << b;
-        else if (synth_other(p / stride, q - (SYN_HDR + 1), p, rec_len, seed)) ot |= 1u << b;
+        else if (const uint8_t x = synth_other(p / stride, q - (SYN_HDR + 1), p, rec_len, seed)) {
+            ot |= 1u << b;
+            if (x == 'N') nn |= 1u << b;
+        }
         q += d;
         if (q >= stride) q -= stride;
     }
     const uint64_t pw = phys_word(t, w);
-    hl[pw] = make_uint2((uint32_t)(r >> 32) & ~(br | ot), (uint32_t)r & ~(br | ot));
+    hl[pw] = make_uint2(((uint32_t)(r >> 32) & ~(br | ot)) | nn, (uint32_t)r & ~(br | ot));
     bo[pw] = make_uint2(br, ot);
 }
 

@@ -147,6 +147,10 @@ inline uint32_t blocks_for(uint64_t n, uint32_t threads) {
 // ---------------------------------------------------------------------------
 // device views
 // ---------------------------------------------------------------------------
+// NUC_N_MARK: at an "other" position (bo.y bit set, no break) the hi plane
+// bit is 1 iff the byte is N -- the common exception byte, whose class
+// membership then needs no side-table lookup (k_others_lane); every other
+// reader takes exception bytes from xbytes and ignores the planes there.
 struct NucView {
     const uint2 *hl, *bo;
     const uint32_t *sbflag, *sbbase;

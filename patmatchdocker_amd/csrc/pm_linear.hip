@@ -310,6 +310,165 @@ __device__ inline void other_windows(const OthersArgs& a, const uint32_t (*s_mem
     }
 }
 
+// Phase 2, lane form (patterns of <= 32 positions): one LANE per selected
+// word, bit-parallel over the windows that hold an exception e.  The
+// 2 * maxlen - 1 positions around e (e - maxlen + 1 .. e + maxlen - 1, all
+// in e's stream) are gathered into bit vectors -- bit i = position
+// e - maxlen + 1 + i: the two base planes H / L, breaks, "other" bytes,
+// positions outside the file -- and for each pattern the mismatch count of
+// every window start u at once is a bit-sliced sum of the per-position
+// mismatch vectors shifted by the position (V_j >> j), exception bytes
+// added from their class membership.  A window is evaluated by the first
+// exception it holds (the ones before e own the others), breaks kill it
+// unless the simple engine runs (cross), and windows off the file are dead:
+// the same windows, the same verdicts as the wave form below.
+constexpr int JIT_MAX_P_ = 8;         // = JIT_MAX_P (declared further down)
+constexpr int OTH_LANE_MAXLEN = 32;   // 2 * maxlen - 1 <= 63 positions in a 64-bit vector
+
+__device__ inline uint64_t vec_mismatch(uint64_t H, uint64_t L, uint32_t sub) {
+    const uint64_t sA = (sub & 1) ? ~0ull : 0ull, sC = (sub & 2) ? ~0ull : 0ull;
+    const uint64_t sG = (sub & 4) ? ~0ull : 0ull, sT = (sub & 8) ? ~0ull : 0ull;
+    const uint64_t match = (~H & ((~L & sA) | (L & sC))) | (H & ((~L & sG) | (L & sT)));
+    return ~match;
+}
+
+__device__ inline void vec_add(uint64_t x, uint64_t& c0, uint64_t& c1, uint64_t& ge4) {
+    const uint64_t cy0 = c0 & x;
+    c0 ^= x;
+    const uint64_t cy1 = c1 & cy0;
+    c1 ^= cy0;
+    ge4 |= cy1;
+}
+
+__global__ __launch_bounds__(256) void k_others_lane(OthersArgs a) {
+    // per (pattern p, position j) at p * maxlen + j: byte membership of its
+    // class ('.' all ones) and its A/C/G/T subset (+ 16: accepts N)
+    __shared__ uint32_t s_memb[JIT_MAX_P_ * OTH_LANE_MAXLEN][8];
+    __shared__ uint8_t s_sub[JIT_MAX_P_ * OTH_LANE_MAXLEN];
+    for (int i = threadIdx.x; i < a.P * a.maxlen * 8; i += blockDim.x) {
+        const int e = i >> 3, p = e / a.maxlen, j = e % a.maxlen;
+        uint32_t m = 0;
+        if (j < a.lengths[p]) {
+            const int cl = a.pos_class[p * 64 + j];
+            m = a.class_any[cl] ? ~0u : a.class_bytes[cl * 8 + (i & 7)];
+        }
+        s_memb[e][i & 7] = m;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < a.P * a.maxlen; e += blockDim.x) {
+        uint32_t sub = 0;
+        const char* acgt = "ACGT";
+        for (int x = 0; x < 4; ++x) {
+            const uint8_t c = (uint8_t)acgt[x];
+            if ((s_memb[e][c >> 5] >> (c & 31)) & 1) sub |= 1u << x;
+        }
+        if ((s_memb[e]['N' >> 5] >> ('N' & 31)) & 1) sub |= 16;   // accepts N
+        s_sub[e] = (uint8_t)sub;
+    }
+    __syncthreads();
+    const int ML = a.maxlen, span = 2 * ML - 1;
+    const uint32_t nsel = *a.nsel;
+    for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < nsel; it += gridDim.x * blockDim.x) {
+        const OtherSel sv = a.sel[it];
+        const uint64_t tile = sv.word / TILE_WORDS;
+        const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
+        for (uint32_t bits = sv.bits; bits; bits &= bits - 1) {
+            const uint64_t e = pos_of(tile, lw, __builtin_ctz(bits));
+            if (e >= a.n) continue;
+            const int64_t q0 = (int64_t)e - (ML - 1);
+            uint64_t H = 0, L = 0, BR = 0, OT = 0, OUT = 0;
+#pragma unroll 8
+            for (int i = 0; i < span; ++i) {
+                const int64_t q = q0 + i;
+                if (q < 0 || (uint64_t)q >= a.n) {
+                    OUT |= 1ull << i;
+                    continue;
+                }
+                const Loc l = loc_of((uint64_t)q);
+                const uint2 ex = a.nuc.bo[l.word];
+                const uint2 hv = a.nuc.hl[l.word];
+                H |= (uint64_t)((hv.x >> l.bit) & 1) << i;
+                L |= (uint64_t)((hv.y >> l.bit) & 1) << i;
+                BR |= (uint64_t)((ex.x >> l.bit) & 1) << i;
+                OT |= (uint64_t)((ex.y >> l.bit) & 1) << i;
+            }
+            // bytes compared by value (class membership): "other" bytes, and
+            // the breaks too when windows may span lines; kills otherwise.
+            // N (hi plane bit set at an "other" position, NUC_N_MARK) takes
+            // its membership from s_nm; the rest from the side table
+            const uint64_t EX = OT | (a.cross ? BR : 0ull);
+            const uint64_t EXN = OT & ~BR & H;
+            const uint64_t EXL = EX & ~EXN;
+            const uint64_t KILL = OUT | (a.cross ? 0ull : BR);
+            // windows u <= h hold an exception before e: owned by it
+            const uint64_t before = (OT | BR) & ((1ull << (ML - 1)) - 1);
+            const uint64_t owned = before ? ~0ull >> __builtin_clzll(before) : 0ull;
+            // the looked-up bytes (up to 8 kept in registers: their span
+            // index and byte; more -- rare -- are looked up again per pattern)
+            const int nxl = __popcll(EXL);
+            uint64_t xl_pos = 0, xl_byte = 0;
+            if (nxl <= 8) {
+                int q = 0;
+                for (uint64_t x = EXL; x; x &= x - 1, ++q) {
+                    const int i = __builtin_ctzll(x);
+                    const Loc l = loc_of((uint64_t)(q0 + i));
+                    const uint8_t ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
+                    xl_pos |= (uint64_t)i << (8 * q);
+                    xl_byte |= (uint64_t)ch << (8 * q);
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < JIT_MAX_P_; ++p) {
+                if (p >= a.P) break;
+                const int len = a.lengths[p];
+                uint64_t c0 = 0, c1 = 0, ge4 = 0, killw = 0;
+                for (int j = 0; j < len; ++j) {
+                    const uint8_t sub = s_sub[p * ML + j];
+                    const uint64_t nmis = (sub & 16) ? 0ull : EXN;   // N rejected by this class
+                    vec_add(((vec_mismatch(H, L, sub) & ~EX) | nmis) >> j, c0, c1, ge4);
+                    killw |= KILL >> j;
+                }
+                // each looked-up byte is its own addend (two of them may fall
+                // in one window)
+                uint64_t xl = EXL;
+                for (int q = 0; q < nxl; ++q) {
+                    int i;
+                    uint8_t ch;
+                    if (nxl <= 8) {
+                        i = (int)((xl_pos >> (8 * q)) & 255);
+                        ch = (uint8_t)((xl_byte >> (8 * q)) & 255);
+                    } else {
+                        i = __builtin_ctzll(xl);
+                        xl &= xl - 1;
+                        const Loc l = loc_of((uint64_t)(q0 + i));
+                        ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
+                    }
+                    uint64_t mm = 0;
+                    for (int j = 0; j < len && j <= i; ++j)
+                        if (!((s_memb[p * ML + j][ch >> 5] >> (ch & 31)) & 1)) mm |= 1ull << (i - j);
+                    vec_add(mm, c0, c1, ge4);
+                }
+                uint64_t dead;
+                switch (a.k) {
+                    case 0: dead = c0 | c1 | ge4; break;
+                    case 1: dead = c1 | ge4; break;
+                    case 2: dead = (c1 & c0) | ge4; break;
+                    default: dead = ge4; break;
+                }
+                // starts whose window holds e: u in [ML - len, ML - 1]
+                const uint64_t range = ((1ull << len) - 1) << (ML - len);
+                for (uint64_t alive = range & ~dead & ~killw & ~owned; alive; alive &= alive - 1) {
+                    const uint64_t s = (uint64_t)(q0 + __builtin_ctzll(alive));
+                    const uint32_t slot = (uint32_t)(a.pattern_base + p);
+                    const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
+                    const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
+                    if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
+                }
+            }
+        }
+    }
+}
+
 // Phase 2: one wave per selected word, waves loop over the list (its length
 // is on the device), so every wave reaches the end of the list and exits.
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
@@ -381,6 +540,7 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
 constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
+static_assert(JIT_MAX_P == JIT_MAX_P_, "k_others_lane stages a chunk's classes in LDS");
 
 // Hit records of pm_linear_jit -> hit keys.  A record is (tile, lane, step,
 // pattern) and the live mask of that window word, exact for the ACGT fast
@@ -1293,8 +1453,16 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
                     hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
                     HIPCHK(hipGetLastError());
-                    hipLaunchKernelGGL(k_linear_others, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
-                                       dim3(256), 0, os, oa);
+                    // PM_OTHERS_LANE=1: the lane form (measured 0.20 vs 0.18 ms on
+                    // the bench database: both are bound by the random gathers,
+                    // ~58 cache lines per exception bit)
+                    if (oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
+                        hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
+                                           dim3(256), 0, os, oa);
+                    else
+                        hipLaunchKernelGGL(k_linear_others,
+                                           dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
+                                           dim3(256), 0, os, oa);
                     HIPCHK(hipGetLastError());
                 };
                 if (exc_conc) {

@@ -347,8 +347,17 @@ def main():
             # query (the batch is split into kernels of <= 8 patterns, each
             # streaming the planes), so achieved = one read / all launches --
             # the honest HBM fraction of a VALU-bound query
-            line["roofline"]["note"] = ("one database read per query; kernel_ms = the sum of the query's "
-                                        "specialized launches (<= 8 patterns each); VALU-bound, see DESIGN.md §4")
+            batch_filter = (jit and args.k == 0 and len(progs) >= int(os.environ.get("PM_BATCH_MIN", "16"))
+                            and os.environ.get("PM_BATCH", "1") != "0")
+            if batch_filter:
+                # one k_batch_scan launch reads the planes once (0.25 B/base)
+                # and probes a 10-mer table in LDS per position (pm_batch.hip)
+                line["roofline"]["kernel"] = "k_batch_scan (q-gram filter: register transpose + LDS table probe per position)"
+                line["roofline"]["note"] = ("one database read per query in one launch; VALU/LDS-issue bound "
+                                            "(~5 VALU + 1 ds_read per position), see DESIGN.md §3")
+            else:
+                line["roofline"]["note"] = ("one database read per query; kernel_ms = the sum of the query's "
+                                            "specialized launches (<= 8 patterns each); VALU-bound, see DESIGN.md §4")
             line["roofline"]["traffic"] = None
         if indel:
             line["roofline"].update({

@@ -429,6 +429,67 @@ struct IdsSpec {
 };
 bool ids_rev_scan(pm_db* db, const IdsSpec& spec, const Sink& sink, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b);
 
+// Large k = 0 batches of fixed-length patterns: a q-gram filter in one pass
+// over the planes (pm_batch.hip).
+constexpr int BQ = 10;                                     // q-gram length
+constexpr uint32_t BQ_TABLE_WORDS = 1u << (2 * BQ - 5);    // 2^20 bits: 128 KB of LDS
+constexpr int BATCH_WAVES = 16;                            // waves per workgroup (one workgroup per CU)
+constexpr int BATCH_THREADS = 64 * BATCH_WAVES;
+constexpr int BATCH_MAX_P = 1024;
+constexpr int BATCH_MAX_LEN = 16;                          // a window's bases fit one 32-bit code word
+constexpr uint32_t BATCH_MAX_WPO = 16;                     // scan waves per output segment
+constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a quarter of the table)
+
+struct BatchIndex {
+    uint32_t omax = 0;
+    uint64_t expansions = 0;
+    std::vector<uint32_t> table, rank;   // [BQ_TABLE_WORDS]: codes present; set bits before each word
+    std::vector<uint32_t> list_off;      // [codes + 1]
+    std::vector<uint32_t> list;          // pattern << 8 | o_p, per code in increasing code order
+    std::vector<uint32_t> pmask;         // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
+    std::vector<uint32_t> plen;          // [P]: bits 2j + 1 for j < length
+    std::vector<uint32_t> popt;          // [P]: o_p, the indexed piece's offset
+};
+// false: the batch is not for the filter (lengths outside [BQ, BATCH_MAX_LEN],
+// too many patterns or expansions)
+bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, const uint8_t* class_acgt,
+                       const uint8_t* class_is_any, BatchIndex& bi);
+
+struct BatchScanArgs {
+    const uint2* hl;
+    uint64_t ntiles;
+    const uint32_t* table;
+    uint32_t omax, tiles_per_wave, nwaves, ccap;
+    uint4* cand;            // [nwaves][ccap] candidate entries
+    uint32_t* cand_cnt;     // [nwaves]
+    uint32_t *zero_a, *zero_b;   // counters zeroed by the first workgroup (the sink's aux counter, xcnt)
+};
+struct BatchVerifyArgs {
+    const uint4* cand;
+    const uint32_t* cand_cnt;
+    uint32_t ccap;
+    uint32_t* aux;          // the largest candidate count above ccap (0: none)
+    const uint32_t *table, *rank, *list_off, *list;
+    const uint4* pmask;
+    const uint32_t *plen, *popt;
+    const int32_t* lengths;
+    uint32_t omax, tiles_per_wave, wpo, nwaves, nout;
+    int P;
+    const uint2 *hl, *bo;
+    const uint64_t* lflag;
+    uint64_t ntiles, n;
+    uint64_t* out;
+    uint32_t* seg_cnt;
+    const uint64_t* slot_base;
+    const uint32_t* slot_cap;
+    uint64_t* xkeys;        // keys of the next segment
+    uint32_t* xcnt;
+    uint32_t xcap;
+};
+// k_batch_scan (timed by ev_a / ev_b), k_batch_verify, k_batch_fixup on s
+void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
+                  hipEvent_t ev_a, hipEvent_t ev_b);
+
 // Carves 256-byte aligned pieces out of one buffer.
 struct Carve {
     size_t off = 0;

@@ -190,6 +190,7 @@ struct OthersArgs {
     const uint32_t* slot_cap;
     uint32_t nwg, tiles_per_wg;
     int items_per_wave;  // k_linear_others: 1, 2 or 4 (2 * maxlen - 1 <= 64 / items_per_wave)
+    int n_classes;       // k_linear_others<true>: classes staged in LDS (<= 256)
 };
 
 // Phase 1, one thread per candidate word: the exception bits that can own a
@@ -242,7 +243,21 @@ constexpr uint32_t OTH_BLOCKS = 2048;   // phase 2: persistent blocks (8 per CU)
 
 // The windows owned by the exception bits `ot` of logical word lw of a tile
 // (one wave; a window is owned by the first exception it holds).
-__device__ inline void other_windows(const OthersArgs& a, const uint32_t (*s_memb)[8], uint64_t tile, uint32_t lw,
+// class membership of byte ch at (pattern p, position j), entry p * maxlen + j:
+// a table per entry (batches of <= 8 patterns) or a class id per entry and a
+// table per class (large batches, k_linear_others<true>)
+struct MembDirect {
+    const uint32_t (*t)[8];
+    __device__ bool operator()(int e, uint8_t ch) const { return (t[e][ch >> 5] >> (ch & 31)) & 1; }
+};
+struct MembClass {
+    const uint8_t* cls;
+    const uint32_t (*cm)[8];
+    __device__ bool operator()(int e, uint8_t ch) const { return (cm[cls[e]][ch >> 5] >> (ch & 31)) & 1; }
+};
+
+template <class Memb>
+__device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint64_t tile, uint32_t lw,
                                      uint32_t ot, int lane, int lanes, int slice) {
     // per exception bit e: the bytes of every window holding e --
     // positions e - maxlen + 1 .. e + maxlen - 1 -- are gathered once, one
@@ -298,7 +313,7 @@ __device__ inline void other_windows(const OthersArgs& a, const uint32_t (*s_mem
                 if ((f & 2) && !a.cross) { ok = false; break; }
                 if ((f & 1) && j < d) { ok = false; break; }   // owned by an earlier exception
                 const uint8_t ch = wch[i0 + j];
-                if (!((s_memb[p * a.maxlen + j][ch >> 5] >> (ch & 31)) & 1) && ++mm > a.k) { ok = false; break; }
+                if (!memb(p * a.maxlen + j, ch) && ++mm > a.k) { ok = false; break; }
             }
             if (ok) {
                 const uint32_t slot = (uint32_t)(a.pattern_base + p);
@@ -471,19 +486,35 @@ __global__ __launch_bounds__(256) void k_others_lane(OthersArgs a) {
 
 // Phase 2: one wave per selected word, waves loop over the list (its length
 // is on the device), so every wave reaches the end of the list and exits.
+// CLS: large batches (more than OTH_MAX_POS (pattern, position) entries) stage
+// a class id per entry and one membership table per class instead.
+constexpr int OTH_CLS_MAX_POS = 1024 * 16;   // BATCH_MAX_P patterns of <= BATCH_MAX_LEN positions
+template <bool CLS>
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     // membership of every byte in the class of (pattern p, position j), at
     // p * maxlen + j ('.' all ones), staged in LDS once per block: the window
     // tests below then touch no global table
-    __shared__ uint32_t s_memb[OTH_MAX_POS][8];
-    for (int i = threadIdx.x; i < a.P * a.maxlen * 8; i += blockDim.x) {
-        const int e = i >> 3, p = e / a.maxlen, j = e % a.maxlen;
-        uint32_t m = 0;
-        if (j < a.lengths[p]) {
-            const int cl = a.pos_class[p * 64 + j];
-            m = a.class_any[cl] ? ~0u : a.class_bytes[cl * 8 + (i & 7)];
+    __shared__ uint32_t s_memb[CLS ? 256 : OTH_MAX_POS][8];
+    __shared__ uint8_t s_cls[CLS ? OTH_CLS_MAX_POS : 1];
+    if (CLS) {
+        for (int i = threadIdx.x; i < 256 * 8; i += blockDim.x) {
+            const int c = i >> 3;
+            s_memb[c][i & 7] = c < a.n_classes ? (a.class_any[c] ? ~0u : a.class_bytes[c * 8 + (i & 7)]) : 0u;
         }
-        s_memb[e][i & 7] = m;
+        for (int e = threadIdx.x; e < a.P * a.maxlen; e += blockDim.x) {
+            const int p = e / a.maxlen, j = e % a.maxlen;
+            s_cls[e] = j < a.lengths[p] ? a.pos_class[p * 64 + j] : 0;
+        }
+    } else {
+        for (int i = threadIdx.x; i < a.P * a.maxlen * 8; i += blockDim.x) {
+            const int e = i >> 3, p = e / a.maxlen, j = e % a.maxlen;
+            uint32_t m = 0;
+            if (j < a.lengths[p]) {
+                const int cl = a.pos_class[p * 64 + j];
+                m = a.class_any[cl] ? ~0u : a.class_bytes[cl * 8 + (i & 7)];
+            }
+            s_memb[e][i & 7] = m;
+        }
     }
     __syncthreads();
     // items_per_wave (1, 2 or 4) items share a wave, 64 / items_per_wave
@@ -493,8 +524,12 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     const uint32_t nsel = *a.nsel, nitems = gridDim.x * (blockDim.x >> 6) * G;
     for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * G + slice; it < nsel; it += nitems) {
         const OtherSel sv = a.sel[it];
-        other_windows(a, s_memb, sv.word / TILE_WORDS, logical_word((uint32_t)(sv.word % TILE_WORDS)), sv.bits, lane,
-                      lanes, slice);
+        const uint64_t tile = sv.word / TILE_WORDS;
+        const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
+        if (CLS)
+            other_windows(a, MembClass{s_cls, s_memb}, tile, lw, sv.bits, lane, lanes, slice);
+        else
+            other_windows(a, MembDirect{s_memb}, tile, lw, sv.bits, lane, lanes, slice);
     }
 }
 
@@ -1311,9 +1346,26 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         const size_t o_acgt = up.add(class_acgt, (size_t)n_classes);
         const size_t o_any = up.add(class_is_any, (size_t)n_classes);
         const size_t o_jsel = up.add(jsel.data(), jsel.size());
+        // a large k = 0 batch: the q-gram filter (pm_batch.hip), one pass for
+        // the whole batch (PM_BATCH=0 off; PM_BATCH_MIN: smallest batch, 16)
+        BatchIndex bi;
+        static const int batch_min = getenv("PM_BATCH_MIN") ? std::max(1, atoi(getenv("PM_BATCH_MIN"))) : 16;
+        const bool batch = jit && k == 0 && n_patterns >= batch_min && env_flag("PM_BATCH", true) &&
+                           build_batch_index(n_patterns, lengths, pos_class, class_acgt, class_is_any, bi);
+        size_t o_btab = 0, o_brank = 0, o_boff = 0, o_blist = 0, o_bmask = 0, o_blen = 0, o_bopt = 0;
+        if (batch) {
+            o_btab = up.add(bi.table.data(), bi.table.size() * 4);
+            o_brank = up.add(bi.rank.data(), bi.rank.size() * 4);
+            o_boff = up.add(bi.list_off.data(), bi.list_off.size() * 4);
+            o_blist = up.add(bi.list.data(), std::max<size_t>(bi.list.size(), 1) * 4);
+            o_bmask = up.add(bi.pmask.data(), bi.pmask.size() * 4);
+            o_blen = up.add(bi.plen.data(), bi.plen.size() * 4);
+            o_bopt = up.add(bi.popt.data(), bi.popt.size() * 4);
+        }
         struct Chunk { int base, P; hipFunction_t jit; };
         std::vector<Chunk> chunks;
-        for (int base = 0; base < n_patterns;) {
+        if (batch) chunks.push_back({0, n_patterns, nullptr});
+        for (int base = batch ? n_patterns : 0; base < n_patterns;) {
             const int rem = n_patterns - base;
             // instantiated widths; a specialized kernel takes up to 8 (class
             // words shared by more patterns, one pass over HBM for all of them)
@@ -1354,7 +1406,131 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         pm_hits* spec = nullptr;       // speculatively sorted hit list
         pm_hits* hit_list = nullptr;   // accepted speculative list
         bool done = false;
-        if (jit) {
+        // the exception pass for the patterns of chunk `ch`, appending to the hit
+        // lists of `sb` (nout segments per pattern, tiles_per_out tiles each)
+        auto launch_others = [&](const Chunk& ch, hipStream_t os, const SinkBuffers& sb, uint64_t nout,
+                                 uint64_t tiles_per_out) {
+            const bool use_edge = edge_ok(ch.base, ch.P);
+            // line-bounded: only words with an "other" byte can own a window
+            const uint32_t* edge = cross ? db->xedge : db->xedge_oth;
+            const uint64_t nedge = cross ? db->nedge : db->nedge_oth;
+            const uint64_t words = use_edge ? nedge : db->nflag;
+            if (!words) return;
+            uint8_t* ws = static_cast<uint8_t*>(reserve(db, db->ws_oth, 256 + words * sizeof(OtherSel)));
+            OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
+                          d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
+                          d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
+                          cross ? 1 : 0, skip_ok(ch.base, ch.P) ? 1 : 0, d_up + o_jsel + 4 * ch.base,
+                          *std::max_element(lengths + ch.base, lengths + ch.base + ch.P),
+                          use_edge ? 1 : 0, db->xint, edge, nedge,
+                          reinterpret_cast<OtherSel*>(ws + 256), reinterpret_cast<uint32_t*>(ws),
+                          sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tiles_per_out), 1,
+                          n_classes};
+            const int span = 2 * oa.maxlen - 1;
+            oa.items_per_wave = span <= 16 ? 4 : span <= 32 ? 2 : 1;
+            // phase 1: one thread per candidate word selects the
+            // exception bits that can own a live window; phase 2:
+            // persistent waves evaluate them
+            HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
+            hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
+            HIPCHK(hipGetLastError());
+            // PM_OTHERS_LANE=1: the lane form (measured 0.20 vs 0.18 ms on
+            // the bench database: both are bound by the random gathers,
+            // ~58 cache lines per exception bit)
+            const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
+            require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
+            if (!cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
+                hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
+                                   dim3(256), 0, os, oa);
+            else
+                hipLaunchKernelGGL(cls ? k_linear_others<true> : k_linear_others<false>,
+                                   dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
+                                   dim3(256), 0, os, oa);
+            HIPCHK(hipGetLastError());
+        };
+        if (jit && batch) {
+            // k_batch_scan: one workgroup of BATCH_WAVES waves per CU, each
+            // wave a contiguous tile range; an output segment = wpo waves
+            int ncu = 0;
+            HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, db->device));
+            uint64_t nwaves = std::min<uint64_t>(db->ntiles, (uint64_t)std::max(ncu, 1) * BATCH_WAVES);
+            const uint64_t tpw = (db->ntiles + nwaves - 1) / nwaves;
+            nwaves = (db->ntiles + tpw - 1) / tpw;
+            const uint32_t nblocks = (uint32_t)((nwaves + BATCH_WAVES - 1) / BATCH_WAVES);
+            const uint64_t wpo = 4;
+            const uint64_t nout = (nwaves + wpo - 1) / wpo;
+            std::vector<uint32_t> slot_caps(n_patterns, 64);
+            // candidates per wave: ~1 % of the positions at configs[4]
+            uint32_t ccap = (uint32_t)std::min<uint64_t>(tpw * 16384, std::max<uint64_t>(4096, tpw * 512));
+            const std::string cap_key =
+                "batch|" + jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any);
+            {
+                std::lock_guard<std::mutex> lk(g_cap_mu);
+                auto it = g_cap_hint.find({db, cap_key});
+                if (it != g_cap_hint.end() && it->second.first.size() == slot_caps.size()) {
+                    slot_caps = it->second.first;
+                    ccap = std::max(ccap, it->second.second);
+                }
+            }
+            // keys whose start lies past a segment's last tile: at most o_max
+            // starts per pattern and segment boundary
+            const uint64_t xcap = std::max<uint64_t>(4096, nout * n_patterns * (bi.omax + 1));
+            const bool exc = db->nflag && (db->n_oth_words || cross);
+            for (int attempt = 0; attempt < 4 && !done; ++attempt) {
+                Carve cv;
+                const size_t o_cand = cv.take(nwaves * ccap * sizeof(uint4));
+                const size_t o_ccnt = cv.take(nwaves * sizeof(uint32_t));
+                const size_t o_xcnt = cv.take(sizeof(uint32_t));
+                const size_t o_x = cv.take(xcap * sizeof(uint64_t));
+                uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
+                // k_batch_verify stores every (pattern, segment) count
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
+                const uint32_t* d_tab = reinterpret_cast<const uint32_t*>(d_up + o_btab);
+                BatchScanArgs sa{db->hl, db->ntiles, d_tab, bi.omax, (uint32_t)tpw, (uint32_t)nwaves, ccap,
+                                 reinterpret_cast<uint4*>(rbase + o_cand), reinterpret_cast<uint32_t*>(rbase + o_ccnt),
+                                 sb.cnt + sb.nbins, reinterpret_cast<uint32_t*>(rbase + o_xcnt)};
+                BatchVerifyArgs va{reinterpret_cast<const uint4*>(rbase + o_cand),
+                                   reinterpret_cast<const uint32_t*>(rbase + o_ccnt), ccap, sb.cnt + sb.nbins, d_tab,
+                                   reinterpret_cast<const uint32_t*>(d_up + o_brank),
+                                   reinterpret_cast<const uint32_t*>(d_up + o_boff),
+                                   reinterpret_cast<const uint32_t*>(d_up + o_blist),
+                                   reinterpret_cast<const uint4*>(d_up + o_bmask),
+                                   reinterpret_cast<const uint32_t*>(d_up + o_blen),
+                                   reinterpret_cast<const uint32_t*>(d_up + o_bopt),
+                                   reinterpret_cast<const int32_t*>(d_up + o_len), bi.omax, (uint32_t)tpw,
+                                   (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, db->hl, db->bo,
+                                   db->lflag, db->ntiles, db->n, sb.out, sb.cnt, sb.slot_base, sb.slot_cap,
+                                   reinterpret_cast<uint64_t*>(rbase + o_x), reinterpret_cast<uint32_t*>(rbase + o_xcnt),
+                                   (uint32_t)xcap};
+                jev.clear();
+                jev.emplace_back(new EventPair());
+                batch_launch(sa, va, nblocks, s, jev.back()->a, jev.back()->b);
+                if (exc) launch_others(chunks[0], s, sb, nout, tpw * wpo);
+                bool overflow = false;
+                total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
+                const uint32_t cneed = sb.aux;
+                if (!overflow && cneed == 0) {
+                    done = true;
+                    std::lock_guard<std::mutex> lk(g_cap_mu);
+                    if (g_cap_hint.size() > 256) g_cap_hint.clear();
+                    g_cap_hint[{db, cap_key}] = {slot_caps, ccap};
+                    break;
+                }
+                if (cneed) ccap = std::max<uint32_t>(ccap, cneed + cneed / 8 + 64);
+                if (overflow) {
+                    uint64_t keys_total = 0;
+                    for (int p = 0; p < n_patterns; ++p) {
+                        const uint32_t* c = counts.data() + (uint64_t)p * nout;
+                        const uint32_t m = *std::max_element(c, c + nout);
+                        while (slot_caps[p] < m) slot_caps[p] *= 2;
+                        keys_total += (uint64_t)slot_caps[p] * nout;
+                    }
+                    require(keys_total * 8 <= (16ull << 30), "hit list larger than 16 GB of segments",
+                            PM_E_UNSUPPORTED);
+                }
+            }
+            require(done, "internal: batch scan capacities did not converge");
+        } else if (jit) {
             // one output segment per (pattern, workgroup); workgroups own
             // contiguous tile ranges (3 per CU resident)
             // more workgroups than resident slots (PM_JIT_SPLIT x): the
@@ -1429,49 +1605,13 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 // expansion, others and the sort: on the post stream after the
                 // kernel's event when this scan returns pipelined in one launch
                 const hipStream_t xs = spec_async && offload ? post_stream(db) : s;
-                auto launch_others = [&](const Chunk& ch, hipStream_t os) {
-                    const bool use_edge = edge_ok(ch.base, ch.P);
-                    // line-bounded: only words with an "other" byte can own a window
-                    const uint32_t* edge = cross ? db->xedge : db->xedge_oth;
-                    const uint64_t nedge = cross ? db->nedge : db->nedge_oth;
-                    const uint64_t words = use_edge ? nedge : db->nflag;
-                    if (!words) return;
-                    uint8_t* ws = static_cast<uint8_t*>(reserve(db, db->ws_oth, 256 + words * sizeof(OtherSel)));
-                    OthersArgs oa{nuc_view(db), db->xoth, db->xbrk, db->xword, db->nflag, db->n,
-                                  d_up + o_pc + 64 * ch.base, reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base,
-                                  d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), ch.P, k, ch.base,
-                                  cross ? 1 : 0, skip_ok(ch.base, ch.P) ? 1 : 0, d_up + o_jsel + 4 * ch.base,
-                                  *std::max_element(lengths + ch.base, lengths + ch.base + ch.P),
-                                  use_edge ? 1 : 0, db->xint, edge, nedge,
-                                  reinterpret_cast<OtherSel*>(ws + 256), reinterpret_cast<uint32_t*>(ws),
-                                  sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tpw * group), 1};
-                    const int span = 2 * oa.maxlen - 1;
-                    oa.items_per_wave = span <= 16 ? 4 : span <= 32 ? 2 : 1;
-                    // phase 1: one thread per candidate word selects the
-                    // exception bits that can own a live window; phase 2:
-                    // persistent waves evaluate them
-                    HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
-                    hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
-                    HIPCHK(hipGetLastError());
-                    // PM_OTHERS_LANE=1: the lane form (measured 0.20 vs 0.18 ms on
-                    // the bench database: both are bound by the random gathers,
-                    // ~58 cache lines per exception bit)
-                    if (oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
-                        hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
-                                           dim3(256), 0, os, oa);
-                    else
-                        hipLaunchKernelGGL(k_linear_others,
-                                           dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
-                                           dim3(256), 0, os, oa);
-                    HIPCHK(hipGetLastError());
-                };
                 if (exc_conc) {
                     // forked after the counter memset and the table uploads
                     // (both on s, behind lane_begin's wait for the lane)
                     const hipStream_t es = exc_stream(db);
                     HIPCHK(hipEventRecord(db->exc_fork, s));
                     HIPCHK(hipStreamWaitEvent(es, db->exc_fork, 0));
-                    for (const Chunk& ch : chunks) launch_others(ch, es);
+                    for (const Chunk& ch : chunks) launch_others(ch, es, sb, nout, tpw * group);
                     HIPCHK(hipEventRecord(db->exc_join, es));
                 }
                 for (const Chunk& ch : chunks) {
@@ -1489,7 +1629,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                   (uint32_t)tpw, exc_conc ? 1 : 0};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
-                    if (exc && !exc_conc) launch_others(ch, xs);
+                    if (exc && !exc_conc) launch_others(ch, xs, sb, nout, tpw * group);
                 }
                 if (exc_conc) HIPCHK(hipStreamWaitEvent(xs, db->exc_join, 0));
                 if (spec_async) {

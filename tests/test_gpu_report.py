@@ -196,3 +196,63 @@ def test_config4_batch_of_256_patterns(engine, oracle_mod, monkeypatch, k, mbp):
         assert _pairs(r) == want, (prog.source, k)
         total += len(want)
     assert total > 1000
+
+
+def _exception_rich_fasta(seed, mbp, width, headless):
+    """Multi-line records with N runs, IUPAC letters and lower case: windows
+    over breaks (the simple engine's cross windows) and over "other" bytes
+    are the exception pass's, the rest the q-gram filter's."""
+    rng = random.Random(seed)
+    out = bytearray()
+    r = 0
+    while len(out) < mbp * 1e6:
+        if r or not headless:
+            out += b">chr%d q-gram batch %d\n" % (r, rng.randint(0, 99))
+        n = rng.randint(50000, 400000)
+        s = bytearray(rng.choice(b"ACGT") for _ in range(n))
+        for _ in range(rng.randint(0, 3)):   # N runs
+            a = rng.randrange(n)
+            s[a:a + rng.randint(5, 300)] = b"N" * len(s[a:a + rng.randint(5, 300)])
+        for _ in range(n // 20000):          # IUPAC letters
+            s[rng.randrange(n)] = rng.choice(b"RYKMSWBDHV")
+        a = rng.randrange(n)
+        s[a:a + 500] = s[a:a + 500].lower()
+        s = bytes(s[:n])
+        for i in range(0, len(s), width):
+            out += s[i:i + width] + b"\n"
+        r += 1
+    return bytes(out)
+
+
+@pytest.mark.parametrize("width,headless", [(60, False), (80, True)])
+def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, headless):
+    """The q-gram batch filter (pm_batch.hip, k = 0, >= 16 patterns of 10-16
+    positions) on a multi-tile database full of exceptions, patterns of
+    every length 10..16 (different piece offsets o_p) + configs[4]'s motifs,
+    every pattern's report list vs the oracle; and the same query with the
+    filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks)."""
+    import bench
+    monkeypatch.setenv("PM_JIT", "1")
+    text = _exception_rich_fasta(21 + width, 3.0, width, headless)
+    rng = random.Random(width)
+    motifs = bench.batch_patterns(40, seed=width)
+    for L in range(10, 17):
+        for _ in range(3):
+            motifs.append("".join(rng.choice("ACGT") if rng.random() < 0.75 else rng.choice("RYSWKMN")
+                                  for _ in range(L)))
+    motifs += ["GAATTCGAATTC", "TATATATATA", "NNNNNNNNNNAC", "AAAAAAAAAAAAAAAA"]
+    progs = [compile_pattern(convert("-n", m)) for m in motifs]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, progs, k=0, types="s")
+        monkeypatch.setenv("PM_BATCH", "0")
+        res_chunks, _ = engine.scan(db, progs, k=0, types="s")
+    finally:
+        db.close()
+    total = 0
+    for prog, r, rc in zip(progs, res, res_chunks):
+        want = oracle_mod.scan_threads(text, prog, 0, "s", skip_headers=True, threads=16, report="nrgrep")
+        assert _pairs(r) == want, prog.source
+        assert _pairs(rc) == want, prog.source
+        total += len(want)
+    assert total > 1000

@@ -172,76 +172,100 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
     if (lane == 0) a.cand_cnt[wave] = ccnt;
 }
 
+// The matches among one candidate's entries: key per match, into this
+// segment's lists (LDS counters) or the next segment's list (xkeys).
+__device__ __forceinline__ void verify_candidate(const BatchVerifyArgs& a, uint32_t og, uint32_t* cnt_p, uint4 e,
+                                                 uint32_t co) {
+    const uint32_t x0 = e.z, x1 = e.w;
+    const uint32_t i = e.y & 63u, st0 = (e.y >> 6) & 31u, bl = e.y >> 11;
+    const uint32_t lo = co >> 8, hi = lo + (co & 255u);
+    for (uint32_t t = lo; t < hi; ++t) {
+        const uint4 h = a.ents[2 * t], mk = a.ents[2 * t + 1];
+        const uint32_t p = h.x & 0xFFFFu, op = (h.x >> 16) & 255u;
+        const int len = (int)(h.x >> 24);
+        // the window's 16 bases; per position the class's bit for its base
+        // (A/C by lo, G/T by lo, then by hi), at odd bits
+        const uint32_t wc = alignb(x1, x0, 2u * (a.omax - op));
+        const uint32_t lsh = wc << 1;
+        const uint32_t s1 = (lsh & mk.y) | (~lsh & mk.x);
+        const uint32_t s2 = (lsh & mk.w) | (~lsh & mk.z);
+        const uint32_t res = (wc & s2) | (~wc & s1);
+        if ((res & h.y) != h.y) continue;
+        uint64_t tile = e.x;
+        uint32_t w = 32u * bl + a.omax + i - op, st = st0;
+        if (w >= STREAM) {   // the start lies in the next stream (or tile)
+            w -= (uint32_t)STREAM;
+            if (++st == 32) {
+                st = 0;
+                ++tile;
+            }
+        }
+        const uint64_t pos = pos_of(tile, w, st);
+        if (tile >= a.ntiles || pos + (uint64_t)len > a.n) continue;
+        if ((a.lflag[tile] >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
+            uint32_t kill = 0;
+            for (int j = 0; j < len; ++j) {
+                const Loc l = loc_of(pos + j);
+                const uint2 b = a.bo[l.word];
+                kill |= ((b.x | b.y) >> l.bit) & 1u;
+            }
+            if (kill) continue;
+        }
+        const uint64_t key = ((uint64_t)p << 48) | pos;
+        const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
+        if (ogr == og) {
+            const uint32_t o = atomicAdd(&cnt_p[p], 1u);
+            if (o < a.slot_cap[p]) a.out[a.slot_base[p] + (uint64_t)og * a.slot_cap[p] + o] = key;
+        } else {
+            const uint32_t o = atomicAdd(a.xcnt, 1u);
+            if (o < a.xcap) a.xkeys[o] = key;
+        }
+    }
+}
+
+// One block per output segment (wpo scan waves).  A thread takes VU
+// candidates at a time: their code -> entry lookups are independent loads in
+// flight together (two dependent L2 round trips per candidate: code_off,
+// then its entries).
+constexpr int VU = 4;
 __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
     __shared__ uint32_t cnt_p[BATCH_MAX_P];
-    __shared__ uint32_t s_n[BATCH_MAX_WPO];
+    __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
     const uint32_t og = blockIdx.x;
     for (int p = threadIdx.x; p < a.P; p += blockDim.x) cnt_p[p] = 0;
     const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
-    if (threadIdx.x < nw) {
-        uint32_t c = a.cand_cnt[w0 + threadIdx.x];
-        if (c > a.ccap) {
-            atomicMax(a.aux, c);
-            c = a.ccap;
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < nw; ++k) {
+            uint32_t c = a.cand_cnt[w0 + k];
+            if (c > a.ccap) {
+                atomicMax(a.aux, c);
+                c = a.ccap;
+            }
+            s_n[k] = run;
+            run += c;
         }
-        s_n[threadIdx.x] = c;
+        s_n[nw] = run;
     }
     __syncthreads();
-    for (uint32_t kw = 0; kw < nw; ++kw) {
-        const uint4* cs = a.cand + (uint64_t)(w0 + kw) * a.ccap;
-        for (uint32_t q = threadIdx.x; q < s_n[kw]; q += blockDim.x) {
-            const uint4 e = cs[q];
-            const uint32_t x0 = e.z, x1 = e.w;
-            const uint32_t code = alignb(x1, x0, 2u * a.omax) & 0xFFFFFu;
-            const uint32_t tw = a.table[code >> 5];
-            const uint32_t r = a.rank[code >> 5] + __popc(tw & ((1u << (code & 31u)) - 1u));
-            const uint32_t lo = a.list_off[r], hi = a.list_off[r + 1];
-            const uint32_t i = e.y & 63u, st0 = (e.y >> 6) & 31u, bl = e.y >> 11;
-            for (uint32_t t = lo; t < hi; ++t) {
-                const uint32_t ent = a.list[t];
-                const uint32_t p = ent >> 8, op = ent & 255u;
-                // the window's 16 bases; per position the class's bit for
-                // its base (A/C by lo, G/T by lo, then by hi), at odd bits
-                const uint32_t wc = alignb(x1, x0, 2u * (a.omax - op));
-                const uint4 mk = a.pmask[p];
-                const uint32_t lsh = wc << 1;
-                const uint32_t s1 = (lsh & mk.y) | (~lsh & mk.x);
-                const uint32_t s2 = (lsh & mk.w) | (~lsh & mk.z);
-                const uint32_t res = (wc & s2) | (~wc & s1);
-                const uint32_t lm = a.plen[p];
-                if ((res & lm) != lm) continue;
-                uint64_t tile = e.x;
-                uint32_t w = 32u * bl + a.omax + i - op, st = st0;
-                if (w >= STREAM) {   // the start lies in the next stream (or tile)
-                    w -= (uint32_t)STREAM;
-                    if (++st == 32) {
-                        st = 0;
-                        ++tile;
-                    }
-                }
-                const uint64_t pos = pos_of(tile, w, st);
-                const int len = a.lengths[p];
-                if (tile >= a.ntiles || pos + (uint64_t)len > a.n) continue;
-                if ((a.lflag[tile] >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
-                    uint32_t kill = 0;
-                    for (int j = 0; j < len; ++j) {
-                        const Loc l = loc_of(pos + j);
-                        const uint2 b = a.bo[l.word];
-                        kill |= ((b.x | b.y) >> l.bit) & 1u;
-                    }
-                    if (kill) continue;
-                }
-                const uint64_t key = ((uint64_t)p << 48) | pos;
-                const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
-                if (ogr == og) {
-                    const uint32_t o = atomicAdd(&cnt_p[p], 1u);
-                    if (o < a.slot_cap[p]) a.out[a.slot_base[p] + (uint64_t)og * a.slot_cap[p] + o] = key;
-                } else {
-                    const uint32_t o = atomicAdd(a.xcnt, 1u);
-                    if (o < a.xcap) a.xkeys[o] = key;
-                }
-            }
-        }
+    const uint32_t total = s_n[nw];
+    // candidate q of the segment: wave k with s_n[k] <= q < s_n[k + 1]
+    auto at = [&](uint32_t q) {
+        uint32_t k = 0;
+        while (q >= s_n[k + 1]) ++k;
+        return a.cand + (uint64_t)(w0 + k) * a.ccap + (q - s_n[k]);
+    };
+    for (uint32_t q0 = threadIdx.x * VU; q0 < total; q0 += blockDim.x * VU) {
+        uint4 e[VU];
+        uint32_t co[VU];
+#pragma unroll
+        for (int u = 0; u < VU; ++u) e[u] = q0 + u < total ? *at(q0 + u) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < VU; ++u)
+            co[u] = q0 + u < total ? a.code_off[alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u)] : 0u;
+#pragma unroll
+        for (int u = 0; u < VU; ++u)
+            if (co[u]) verify_candidate(a, og, cnt_p, e[u], co[u]);
     }
     __syncthreads();
     for (int p = threadIdx.x; p < a.P; p += blockDim.x) a.seg_cnt[(uint64_t)p * a.nout + og] = cnt_p[p];
@@ -297,8 +321,8 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         uint32_t code, p;
     };
     std::vector<Ent> ents;
+    std::vector<uint32_t> plen(P, 0);
     bi.popt.assign(P, 0);
-    bi.plen.assign(P, 0);
     bi.pmask.assign((size_t)4 * P, 0);
     for (int p = 0; p < P; ++p) {
         const int L = lengths[p];
@@ -307,7 +331,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
             const int c = pos_class[64 * p + j];
             sub[j] = class_is_any[c] ? 15u : (class_acgt[c] & 15u);
             for (int b = 0; b < 4; ++b) bi.pmask[(size_t)4 * p + b] |= ((sub[j] >> b) & 1u) << (2 * j + 1);
-            bi.plen[p] |= 1u << (2 * j + 1);
+            plen[p] |= 1u << (2 * j + 1);
         }
         // the piece with the fewest expansions (0: the pattern matches no
         // ACGT-only window, nothing to index)
@@ -341,22 +365,28 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         return x.code != y.code ? x.code < y.code : x.p < y.p;
     });
     bi.table.assign(BQ_TABLE_WORDS, 0u);
-    bi.rank.assign(BQ_TABLE_WORDS, 0u);
-    bi.list.clear();
-    bi.list_off.clear();
+    bi.code_off.assign((size_t)1 << (2 * BQ), 0u);
+    bi.ents.assign(ents.size() * BATCH_ENT_WORDS, 0u);
     for (size_t i = 0; i < ents.size(); ++i) {
-        if (i == 0 || ents[i].code != ents[i - 1].code) {
-            bi.list_off.push_back((uint32_t)bi.list.size());
-            bi.table[ents[i].code >> 5] |= 1u << (ents[i].code & 31);
+        const uint32_t c = ents[i].code, p = ents[i].p;
+        if (i == 0 || c != ents[i - 1].code) {
+            bi.table[c >> 5] |= 1u << (c & 31);
+            bi.code_off[c] = (uint32_t)i << 8;
         }
-        bi.list.push_back(ents[i].p << 8 | bi.popt[ents[i].p]);
+        if ((bi.code_off[c] & 255u) == 255u || i >= (1u << 24)) return false;
+        ++bi.code_off[c];
+        uint32_t* e = &bi.ents[i * BATCH_ENT_WORDS];
+        e[0] = p | bi.popt[p] << 16 | (uint32_t)lengths[p] << 24;
+        e[1] = plen[p];
+        for (int b = 0; b < 4; ++b) e[4 + b] = bi.pmask[(size_t)4 * p + b];   // the second uint4
     }
-    bi.list_off.push_back((uint32_t)bi.list.size());
-    uint32_t run = 0;
-    for (uint32_t w = 0; w < BQ_TABLE_WORDS; ++w) {
-        bi.rank[w] = run;
-        run += (uint32_t)__builtin_popcount(bi.table[w]);
-    }
+    Carve cv;
+    bi.o_table = cv.take(bi.table.size() * 4);
+    bi.o_code = cv.take(bi.code_off.size() * 4);
+    bi.o_ents = cv.take(std::max<size_t>(bi.ents.size(), BATCH_ENT_WORDS) * 4);
+    bi.o_pmask = cv.take(bi.pmask.size() * 4);
+    bi.o_popt = cv.take(bi.popt.size() * 4);
+    bi.bytes = cv.off;
     return true;
 }
 

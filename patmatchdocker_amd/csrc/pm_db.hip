@@ -432,7 +432,8 @@ void free_db(pm_db* db) {
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
     void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->bytes, db->bytes_raw, db->ws_post.p};
+                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->bytes, db->bytes_raw, db->ws_post.p,
+                    db->ws_batch.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);

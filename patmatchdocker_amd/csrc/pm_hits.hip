@@ -20,8 +20,6 @@
 namespace pm {
 namespace {
 
-// bin counters -> exclusive offsets; one block of 1024 threads, each owning a
-// contiguous run of bins
 struct BinShape {
     const uint64_t* slot_base;
     const uint32_t* slot_cap;
@@ -33,53 +31,16 @@ struct BinShape {
     }
 };
 
-__global__ __launch_bounds__(1024) void k_bin_offsets(const uint32_t* __restrict__ cnt, uint32_t nbins,
-                                                      BinShape sh, uint64_t* __restrict__ off) {
-    __shared__ uint64_t part[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (nbins + 1023) / 1024;
-    const uint32_t b0 = t * per, b1 = min(nbins, b0 + per);
-    uint64_t s = 0;
-    for (uint32_t b = b0; b < b1; ++b) s += min(cnt[b], sh.cap(b));
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint64_t v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint64_t acc = part[t] - s;
-    for (uint32_t b = b0; b < b1; ++b) {
-        off[b] = acc;
-        acc += min(cnt[b], sh.cap(b));
-    }
-}
-
 // One workgroup per bin: bitonic sort in LDS, write at the bin's offset.
 // CAP keys per bin at most (2048: 16 KB of LDS; 4096 when a bin may hold
 // more, 32 KB); larger bins are left to the caller.
+// One bin, sorted by the whole block (uniform control flow: c is the same
+// for every thread).
 template <uint32_t CAP>
-__global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
-                                                   const uint64_t* __restrict__ off, BinShape sh,
-                                                   uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
-                                                   uint32_t* __restrict__ lens, uint32_t* counts_host = nullptr,
-                                                   uint32_t nbins = 0, uint64_t* total_out = nullptr) {
-    __shared__ uint64_t s[CAP];
-    const uint32_t bin = blockIdx.x;
-    if (counts_host && bin == 0) {   // the pipelined scan's count readback (mapped host memory)
-        for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
-        __threadfence_system();
-    }
-    if (total_out && bin == 0) {     // list length for the report pass (device-side count)
-        uint64_t acc = 0;
-        for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) acc += min(cnt[b], sh.cap(b));
-        for (int d2 = 32; d2 > 0; d2 >>= 1) acc += __shfl_xor(acc, d2, 64);
-        __shared__ uint64_t wsum[4];
-        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) *total_out = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    }
+__device__ __forceinline__ void sort_one_bin(uint64_t* s, uint32_t bin, const uint64_t* __restrict__ out,
+                                             const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                             const BinShape& sh, uint64_t* __restrict__ dst,
+                                             const int32_t* __restrict__ slot_len, uint32_t* __restrict__ lens) {
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     if (c == 0 || c > CAP) return;   // (a speculative sort's caller redoes such lists)
     uint64_t base;
@@ -143,6 +104,49 @@ __global__ __launch_bounds__(256) void k_sort_bins(const uint64_t* __restrict__ 
     }
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) d[i] = s[i];
 }
+
+// One workgroup per bin at a time (item it -> bin it, or bin_list[it]; the
+// grid strides over nitems): bitonic sort in LDS, write at the bin's offset.
+// CAP keys per bin at most (2048: 16 KB of LDS; 4096 when a bin may hold
+// more, 32 KB; 16384 for the large-bin pass, 128 KB); larger bins are left
+// to the caller.
+template <uint32_t CAP, int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void k_sort_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
+                                                       const uint64_t* __restrict__ off, BinShape sh,
+                                                       uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
+                                                       uint32_t* __restrict__ lens, uint32_t* counts_host,
+                                                       uint32_t nbins, uint64_t* total_out,
+                                                       const uint32_t* __restrict__ bin_list, uint32_t nitems) {
+    __shared__ uint64_t s[CAP];
+    if (counts_host && blockIdx.x == 0) {   // the pipelined scan's count readback (mapped host memory)
+        for (uint32_t i = threadIdx.x; i <= nbins; i += blockDim.x) counts_host[i] = cnt[i];
+        __threadfence_system();
+    }
+    if (total_out && blockIdx.x == 0) {     // list length for the report pass (device-side count)
+        uint64_t acc = 0;
+        for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) acc += min(cnt[b], sh.cap(b));
+        for (int d2 = 32; d2 > 0; d2 >>= 1) acc += __shfl_xor(acc, d2, 64);
+        __shared__ uint64_t wsum[THREADS / 64];
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t t = 0;
+            for (int w = 0; w < THREADS / 64; ++w) t += wsum[w];
+            *total_out = t;
+        }
+    }
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        sort_one_bin<CAP>(s, bin_list ? bin_list[it] : it, out, cnt, off, sh, dst, slot_len, lens);
+        __syncthreads();   // s is reused by the next bin
+    }
+}
+
+// clamped bin count (the keys a bin contributes to the list)
+struct BinCount {
+    const uint32_t* cnt;
+    BinShape sh;
+    __device__ uint64_t operator()(uint32_t b) const { return min(cnt[b], sh.cap(b)); }
+};
 
 __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
                               const uint64_t* __restrict__ off, BinShape sh, uint64_t* __restrict__ dst) {
@@ -366,11 +370,11 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
             HIPCHK(hipEventCreate(&h->ready));
             hipExtLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, stream, nullptr, h->ready, 0u, sb.out,
                                   sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
-                                  sb.nbins, total_out);
+                                  sb.nbins, total_out, (const uint32_t*)nullptr, sb.nbins);
         } else {
             hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, stream, sb.out,
                                sb.cnt, (const uint64_t*)nullptr, sh, h->keys, slot_len, h->lens, counts_host,
-                               (counts_host || total_out) ? sb.nbins : 0u, total_out);
+                               (counts_host || total_out) ? sb.nbins : 0u, total_out, (const uint32_t*)nullptr, sb.nbins);
         }
         HIPCHK(hipGetLastError());
     } catch (...) {
@@ -401,31 +405,60 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                                                   &h->lens_cap));
         if (total == 0) return h;
         const uint32_t maxc = *std::max_element(counts.begin(), counts.end());
-        const bool lds = maxc <= LDS_SORT_CAP_MAX;
-        size_t sort_bytes = 0;
+        // bins of up to LDS_SORT_CAP_MAX keys: one LDS sort block each; a few
+        // larger ones (dense patterns of a big batch) up to LDS_SORT_CAP_HUGE:
+        // a second pass over their list, 128 KB of LDS per block; beyond
+        // that one radix sort of the whole list
+        const bool lds = maxc <= LDS_SORT_CAP_HUGE;
+        std::vector<uint32_t> big;
+        if (lds && maxc > LDS_SORT_CAP_MAX)
+            for (uint32_t b = 0; b < sb.nbins; ++b)
+                if (std::min(counts[b], sb.slot_cap_h[b / sb.bins_per_pattern]) > LDS_SORT_CAP_MAX) big.push_back(b);
+        const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
+        // up to 4096 bins each sort block sums the counts before it itself
+        const bool inline_off = lds && sb.nbins <= 4096 && big.empty();
+        auto counted = hipcub::TransformInputIterator<uint64_t, BinCount, hipcub::CountingInputIterator<uint32_t>>(
+            hipcub::CountingInputIterator<uint32_t>(0u), BinCount{sb.cnt, sh});
+        size_t sort_bytes = 0, scan_bytes = 0;
         if (!lds)
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
                                                      (int)total, 0, 64, s));
+        if (!inline_off)
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)sb.nbins, s));
         Carve c;
         const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
         const size_t o_uns = lds ? 0 : c.take(total * sizeof(uint64_t));
         const size_t o_tmp = lds ? 0 : c.take(sort_bytes);
+        const size_t o_scan = c.take(scan_bytes);
+        const size_t o_big = c.take(big.size() * sizeof(uint32_t));
         uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
-        const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
-        // up to 4096 bins each sort block sums the counts before it itself
-        const bool inline_off = lds && sb.nbins <= 4096;
         if (!inline_off) {
-            hipLaunchKernelGGL(k_bin_offsets, dim3(1), dim3(1024), 0, s, sb.cnt, sb.nbins, sh, d_off);
-            HIPCHK(hipGetLastError());
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)sb.nbins, s));
+            // rocPRIM's scan leaves a stale "stream is capturing" status from
+            // its capture query behind (the call itself succeeded): clear it so
+            // the next launch check does not report it
+            (void)hipGetLastError();
         }
         if (lds) {
             auto kern = maxc > LDS_SORT_CAP ? k_sort_bins<LDS_SORT_CAP_MAX> : k_sort_bins<LDS_SORT_CAP>;
-            hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt,
+            // many bins (a large batch: patterns x segments): each block
+            // sorts a strided run of bins instead of one block per bin
+            hipLaunchKernelGGL(kern, dim3(std::min<uint32_t>(sb.nbins, 8192)), dim3(256), 0, s, sb.out, sb.cnt,
                                inline_off ? (const uint64_t*)nullptr : (const uint64_t*)d_off, sh, h->keys, slot_len,
-                               h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr);
-            if (lens_done) *lens_done = slot_len != nullptr;
+                               h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)nullptr, sb.nbins);
             HIPCHK(hipGetLastError());
+            if (!big.empty()) {
+                uint32_t* d_big = reinterpret_cast<uint32_t*>(base + o_big);
+                HIPCHK(hipMemcpyAsync(d_big, big.data(), big.size() * 4, hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_HUGE, 1024>), dim3((uint32_t)big.size()), dim3(1024), 0, s,
+                                   sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
+                                   (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_big,
+                                   (uint32_t)big.size());
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamSynchronize(s));   // `big` (pageable) was read by the copy
+            }
+            if (lens_done) *lens_done = slot_len != nullptr;
         } else {
             uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
             hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh,
@@ -460,7 +493,8 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
 // so one thread walks each list sequentially (anchored queries only).
 namespace {
 
-constexpr uint32_t REP_G = 512;           // chunks (blocks) of the list
+constexpr uint32_t REP_G = 512;           // chunks (blocks) of the list (at least)
+constexpr uint32_t REP_G_MAX = 8192;      // long lists: ~16 Ki candidates per chunk
 constexpr uint32_t REP_T = 256;           // threads per block
 constexpr uint64_t POS_MASK = (1ull << 48) - 1;
 
@@ -757,7 +791,7 @@ bool report_needed(uint32_t flags, bool cross) {
 
 ReportWs report_ws(pm_db* db, uint64_t cap_items) {
     Carve c;
-    const size_t o_t = c.take(8), o_c = c.take(8), o_m = c.take(REP_G * 8), o_b = c.take(REP_G * 4),
+    const size_t o_t = c.take(8), o_c = c.take(8), o_m = c.take(REP_G_MAX * 8), o_b = c.take(REP_G_MAX * 4),
                  o_a = c.take(std::max<uint64_t>(cap_items, 1));
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_rep, c.off));
     ReportWs ws;
@@ -795,7 +829,11 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     a.hdr = hdr && !keep_hdr && !(flags & PM_KEEP_HEADERS) ? 1 : 0;
     a.debug = getenv("PM_REPORT_DEBUG") ? 1 : 0;
     (void)cap_items;   // every acc entry below the list length is written by k_rep_walk (no memset)
-    static const uint32_t G = getenv("PM_REPORT_G") ? std::min<uint32_t>(REP_G, std::max(1, atoi(getenv("PM_REPORT_G")))) : REP_G;
+    // chunks: REP_G, more for long lists (a big batch's tens of millions of
+    // candidates: every block's serial tile scans then stay short)
+    static const int g_env = getenv("PM_REPORT_G") ? std::max(1, atoi(getenv("PM_REPORT_G"))) : 0;
+    const uint32_t G = g_env ? std::min<uint32_t>(REP_G_MAX, (uint32_t)g_env)
+                             : (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
     hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
     hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
     if (a.debug) hipLaunchKernelGGL(k_rep_check, dim3(G), dim3(REP_T), 0, s, a);

@@ -101,6 +101,7 @@ constexpr uint32_t MAX_BINS = 8192;
 constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_nfa_rev
 constexpr uint32_t LDS_SORT_CAP = 2048;              // keys per bin sorted in LDS (16 KB: 8 sort blocks per CU)
 constexpr uint32_t LDS_SORT_CAP_MAX = 4096;          // the larger sort variant (32 KB), for bins above LDS_SORT_CAP
+constexpr uint32_t LDS_SORT_CAP_HUGE = 16384;        // large bins, sorted in a second pass (128 KB of LDS)
 constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
 constexpr int RUN_SKIP = 8;                          // run-interior lookahead (xint)
 
@@ -326,6 +327,10 @@ struct pm_db : pm_lane {
     bool own_stream = false;
     // synchronous-path workspaces
     pm_devbuf ws_post;
+    // the q-gram batch filter's device tables (pm_batch.hip) and the batch
+    // signature they were built for: a repeated batch uploads nothing
+    pm_devbuf ws_batch;
+    std::string batch_sig;
     pm_hostbuf pin_down;
     // pipelined scans: record expansion + sort of scan i run on `post` while
     // scan i+1's kernel runs on `stream`, each on its own workspace lane (the
@@ -443,15 +448,19 @@ constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a q
 struct BatchIndex {
     uint32_t omax = 0;
     uint64_t expansions = 0;
-    std::vector<uint32_t> table, rank;   // [BQ_TABLE_WORDS]: codes present; set bits before each word
-    std::vector<uint32_t> list_off;      // [codes + 1]
-    std::vector<uint32_t> list;          // pattern << 8 | o_p, per code in increasing code order
-    std::vector<uint32_t> pmask;         // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
-    std::vector<uint32_t> plen;          // [P]: bits 2j + 1 for j < length
-    std::vector<uint32_t> popt;          // [P]: o_p, the indexed piece's offset
+    std::vector<uint32_t> table;      // [BQ_TABLE_WORDS]: the codes present (bit code & 31 of word code >> 5)
+    std::vector<uint32_t> code_off;   // [2^(2 BQ)]: first entry << 8 | entries, per code
+    std::vector<uint32_t> ents;       // BATCH_ENT_WORDS per (code, pattern) entry, in increasing code order
+    std::vector<uint32_t> pmask;      // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
+    std::vector<uint32_t> popt;       // [P]: o_p, the indexed piece's offset
+    // device image (ws_batch): table | code_off | ents | pmask | popt
+    size_t o_table = 0, o_code = 0, o_ents = 0, o_pmask = 0, o_popt = 0, bytes = 0;
 };
+// one verification entry (two uint4): {p | o_p << 16 | len << 24, length mask
+// (bits 2j + 1), 0, 0}, {mA, mC, mG, mT}
+constexpr int BATCH_ENT_WORDS = 8;
 // false: the batch is not for the filter (lengths outside [BQ, BATCH_MAX_LEN],
-// too many patterns or expansions)
+// too many patterns or expansions, a code shared by more than 255 patterns)
 bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, const uint8_t* class_acgt,
                        const uint8_t* class_is_any, BatchIndex& bi);
 
@@ -469,9 +478,10 @@ struct BatchVerifyArgs {
     const uint32_t* cand_cnt;
     uint32_t ccap;
     uint32_t* aux;          // the largest candidate count above ccap (0: none)
-    const uint32_t *table, *rank, *list_off, *list;
+    const uint32_t* code_off;
+    const uint4* ents;      // two uint4 per entry
     const uint4* pmask;
-    const uint32_t *plen, *popt;
+    const uint32_t* popt;
     const int32_t* lengths;
     uint32_t omax, tiles_per_wave, wpo, nwaves, nout;
     int P;

@@ -338,6 +338,7 @@ __device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint
 // unless the simple engine runs (cross), and windows off the file are dead:
 // the same windows, the same verdicts as the wave form below.
 constexpr int JIT_MAX_P_ = 8;         // = JIT_MAX_P (declared further down)
+constexpr int OTH_CLS_MAX_POS = BATCH_MAX_P * BATCH_MAX_LEN;   // (pattern, position) entries of a q-gram batch
 constexpr int OTH_LANE_MAXLEN = 32;   // 2 * maxlen - 1 <= 63 positions in a 64-bit vector
 
 __device__ inline uint64_t vec_mismatch(uint64_t H, uint64_t L, uint32_t sub) {
@@ -484,11 +485,133 @@ __global__ __launch_bounds__(256) void k_others_lane(OthersArgs a) {
     }
 }
 
+// Phase 2 for large batches (k_batch_scan's exception windows), one WAVE per
+// exception bit e, with the work split per CLASS: a batch of hundreds of
+// IUPAC motifs uses a handful of classes (A, C, G, T, the two-base codes,
+// '.').  Lane i gathers position e - maxlen + 1 + i (one round trip for the
+// whole window span); ballots turn the lanes' bits into 64-bit span vectors
+// (planes, breaks, "other" bytes, off-file); the match vector of every class
+// over the span (bit i = position i accepted: ACGT from the planes, N from
+// its mark, other bytes by value) is one ballot per class, kept in LDS.
+// Then lane l takes patterns l, l + 64, ...: one LDS read, a 64-bit shift and
+// two ANDs per position give the windows of every start u holding e, alive
+// iff every position accepts its byte (k > 0: mismatches counted
+// bit-sliced).  Ownership, kills and the file end as in k_others_lane.
+constexpr int OTH_BATCH_THREADS = 256;
+constexpr int OTH_BATCH_MAX_CLASSES = 32;
+
+__global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a) {
+    __shared__ uint4 s_cls[BATCH_MAX_P];                          // 16 class ids per pattern
+    __shared__ uint32_t s_cm[OTH_BATCH_MAX_CLASSES][8];           // byte membership per class
+    __shared__ uint8_t s_csub[OTH_BATCH_MAX_CLASSES];             // A/C/G/T subset + 16: accepts N
+    __shared__ uint64_t s_mv[OTH_BATCH_THREADS / 64][OTH_BATCH_MAX_CLASSES];   // per wave: match vector per class
+    const int nc = a.n_classes;
+    for (int i = threadIdx.x; i < nc * 8; i += blockDim.x) {
+        const int c = i >> 3;
+        s_cm[c][i & 7] = a.class_any[c] ? ~0u : a.class_bytes[c * 8 + (i & 7)];
+    }
+    uint8_t* cls8 = reinterpret_cast<uint8_t*>(s_cls);
+    for (int e = threadIdx.x; e < a.P * 16; e += blockDim.x) {
+        const int p = e >> 4, j = e & 15;
+        cls8[e] = j < a.lengths[p] ? a.pos_class[p * 64 + j] : 0;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        uint32_t sub = 0;
+        const char* acgt = "ACGT";
+        for (int x = 0; x < 4; ++x) {
+            const uint8_t ch = (uint8_t)acgt[x];
+            if ((s_cm[c][ch >> 5] >> (ch & 31)) & 1) sub |= 1u << x;
+        }
+        if ((s_cm[c]['N' >> 5] >> ('N' & 31)) & 1) sub |= 16;
+        s_csub[c] = (uint8_t)sub;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t* const mv = s_mv[wid];
+    const int ML = a.maxlen, span = 2 * ML - 1;
+    const uint32_t nsel = *a.nsel;
+    for (uint32_t it = blockIdx.x * (OTH_BATCH_THREADS / 64) + wid; it < nsel; it += gridDim.x * (OTH_BATCH_THREADS / 64)) {
+        const OtherSel sv = a.sel[it];
+        const uint64_t tile = sv.word / TILE_WORDS;
+        const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
+        for (uint32_t bits = sv.bits; bits; bits &= bits - 1) {
+            const uint64_t e = pos_of(tile, lw, __builtin_ctz(bits));
+            if (e >= a.n) continue;   // wave-uniform
+            const int64_t q0 = (int64_t)e - (ML - 1);
+            const int64_t q = q0 + lane;
+            const bool in_span = lane < span, in_file = in_span && q >= 0 && (uint64_t)q < a.n;
+            uint32_t h = 0, l = 0, br = 0, ot = 0;
+            Loc lc{0, 0};
+            if (in_file) {
+                lc = loc_of((uint64_t)q);
+                const uint2 ex = a.nuc.bo[lc.word];
+                const uint2 hv = a.nuc.hl[lc.word];
+                h = (hv.x >> lc.bit) & 1;
+                l = (hv.y >> lc.bit) & 1;
+                br = (ex.x >> lc.bit) & 1;
+                ot = (ex.y >> lc.bit) & 1;
+            }
+            const uint64_t H = __builtin_amdgcn_ballot_w64(h != 0), L = __builtin_amdgcn_ballot_w64(l != 0);
+            const uint64_t BR = __builtin_amdgcn_ballot_w64(br != 0), OT = __builtin_amdgcn_ballot_w64(ot != 0);
+            const uint64_t OUT = __builtin_amdgcn_ballot_w64(in_span && !in_file);
+            const uint64_t EX = OT | (a.cross ? BR : 0ull);
+            const uint64_t EXN = OT & ~BR & H;   // N (NUC_N_MARK)
+            const uint64_t EXL = EX & ~EXN;       // bytes compared by value
+            const uint64_t KILL = OUT | (a.cross ? 0ull : BR);
+            const uint64_t before = (OT | BR) & ((1ull << (ML - 1)) - 1);
+            const uint64_t owned = before ? ~0ull >> __builtin_clzll(before) : 0ull;
+            // the lane's byte when it is compared by value (N: its mark)
+            uint8_t ch = 'N';
+            const bool byval = ((EXN | EXL) >> lane) & 1;
+            if ((EXL >> lane) & 1)
+                ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, lc.word) * 32 + lc.bit];
+            for (int c = 0; c < nc; ++c) {
+                const uint64_t vb = __builtin_amdgcn_ballot_w64(byval && ((s_cm[c][ch >> 5] >> (ch & 31)) & 1));
+                if (lane == c) mv[c] = (~vec_mismatch(H, L, s_csub[c]) & ~EX) | vb;
+            }
+            wave_lds_sync();
+            for (int p = lane; p < a.P; p += 64) {
+                const int len = a.lengths[p];
+                const uint4 cl = s_cls[p];
+                const uint32_t cw[4] = {cl.x, cl.y, cl.z, cl.w};
+                // starts u whose window holds e: u in [ML - len, ML - 1]
+                uint64_t alive = (((1ull << len) - 1) << (ML - len)) & ~owned;
+                uint64_t c0 = 0, c1 = 0, ge4 = 0;
+#pragma unroll
+                for (int j = 0; j < BATCH_MAX_LEN; ++j) {
+                    if (j >= len) break;
+                    const uint64_t m = mv[(cw[j >> 2] >> (8 * (j & 3))) & 255u] >> j;
+                    alive &= ~(KILL >> j);
+                    if (a.k == 0) alive &= m;
+                    else vec_add(~m, c0, c1, ge4);
+                }
+                if (a.k) {
+                    uint64_t dead;
+                    switch (a.k) {
+                        case 1: dead = c1 | ge4; break;
+                        case 2: dead = (c1 & c0) | ge4; break;
+                        default: dead = ge4; break;
+                    }
+                    alive &= ~dead;
+                }
+                for (; alive; alive &= alive - 1) {
+                    const uint64_t s0 = (uint64_t)(q0 + __builtin_ctzll(alive));
+                    const uint32_t slot = (uint32_t)(a.pattern_base + p);
+                    const uint64_t og = (s0 / TILE_POS) / a.tiles_per_wg;
+                    const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
+                    if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s0;
+                }
+            }
+            wave_lds_sync();   // mv is rewritten for the next bit
+        }
+    }
+}
+
 // Phase 2: one wave per selected word, waves loop over the list (its length
 // is on the device), so every wave reaches the end of the list and exits.
 // CLS: large batches (more than OTH_MAX_POS (pattern, position) entries) stage
 // a class id per entry and one membership table per class instead.
-constexpr int OTH_CLS_MAX_POS = 1024 * 16;   // BATCH_MAX_P patterns of <= BATCH_MAX_LEN positions
 template <bool CLS>
 __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     // membership of every byte in the class of (pattern p, position j), at
@@ -1229,6 +1352,47 @@ namespace {
 std::mutex g_nospec_mu;
 std::set<std::pair<const pm_db*, std::string>> g_nospec;
 
+// q-gram batch indexes by batch signature (host), and the device image of
+// the last one per database (ws_batch): a repeated batch rebuilds and
+// uploads nothing
+std::mutex g_bidx_mu;
+std::map<std::string, std::shared_ptr<const BatchIndex>> g_bidx;   // null: not for the filter
+
+std::shared_ptr<const BatchIndex> batch_index_cached(const std::string& sig, int P, const int32_t* lengths,
+                                                     const uint8_t* pos_class, const uint8_t* class_acgt,
+                                                     const uint8_t* class_is_any) {
+    {
+        std::lock_guard<std::mutex> lk(g_bidx_mu);
+        auto it = g_bidx.find(sig);
+        if (it != g_bidx.end()) return it->second;
+    }
+    auto bi = std::make_shared<BatchIndex>();
+    std::shared_ptr<const BatchIndex> r;
+    if (build_batch_index(P, lengths, pos_class, class_acgt, class_is_any, *bi)) r = bi;
+    std::lock_guard<std::mutex> lk(g_bidx_mu);
+    if (g_bidx.size() > 64) g_bidx.clear();
+    g_bidx[sig] = r;
+    return r;
+}
+
+uint8_t* batch_tables(pm_db* db, const BatchIndex& bi, const std::string& sig) {
+    if (db->batch_sig == sig && db->ws_batch.p) return static_cast<uint8_t*>(db->ws_batch.p);
+    // queued scans may still read the old tables
+    HIPCHK(hipStreamSynchronize(db->stream));
+    if (db->post) HIPCHK(hipStreamSynchronize(db->post));
+    uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_batch, bi.bytes));
+    std::vector<uint8_t> img(bi.bytes, 0);
+    memcpy(img.data() + bi.o_table, bi.table.data(), bi.table.size() * 4);
+    memcpy(img.data() + bi.o_code, bi.code_off.data(), bi.code_off.size() * 4);
+    memcpy(img.data() + bi.o_ents, bi.ents.data(), bi.ents.size() * 4);
+    memcpy(img.data() + bi.o_pmask, bi.pmask.data(), bi.pmask.size() * 4);
+    memcpy(img.data() + bi.o_popt, bi.popt.data(), bi.popt.size() * 4);
+    HIPCHK(hipMemcpyAsync(d, img.data(), img.size(), hipMemcpyHostToDevice, db->stream));
+    HIPCHK(hipStreamSynchronize(db->stream));
+    db->batch_sig = sig;
+    return d;
+}
+
 // pm_scan_linear on the byte layout (synchronous; the pipelined entry point
 // runs it too)
 void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
@@ -1348,20 +1512,16 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         const size_t o_jsel = up.add(jsel.data(), jsel.size());
         // a large k = 0 batch: the q-gram filter (pm_batch.hip), one pass for
         // the whole batch (PM_BATCH=0 off; PM_BATCH_MIN: smallest batch, 16)
-        BatchIndex bi;
         static const int batch_min = getenv("PM_BATCH_MIN") ? std::max(1, atoi(getenv("PM_BATCH_MIN"))) : 16;
-        const bool batch = jit && k == 0 && n_patterns >= batch_min && env_flag("PM_BATCH", true) &&
-                           build_batch_index(n_patterns, lengths, pos_class, class_acgt, class_is_any, bi);
-        size_t o_btab = 0, o_brank = 0, o_boff = 0, o_blist = 0, o_bmask = 0, o_blen = 0, o_bopt = 0;
-        if (batch) {
-            o_btab = up.add(bi.table.data(), bi.table.size() * 4);
-            o_brank = up.add(bi.rank.data(), bi.rank.size() * 4);
-            o_boff = up.add(bi.list_off.data(), bi.list_off.size() * 4);
-            o_blist = up.add(bi.list.data(), std::max<size_t>(bi.list.size(), 1) * 4);
-            o_bmask = up.add(bi.pmask.data(), bi.pmask.size() * 4);
-            o_blen = up.add(bi.plen.data(), bi.plen.size() * 4);
-            o_bopt = up.add(bi.popt.data(), bi.popt.size() * 4);
+        std::shared_ptr<const BatchIndex> bip;
+        std::string batch_sig;
+        if (jit && k == 0 && n_patterns >= batch_min && env_flag("PM_BATCH", true)) {
+            batch_sig = jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any);
+            bip = batch_index_cached(batch_sig, n_patterns, lengths, pos_class, class_acgt, class_is_any);
         }
+        const bool batch = bip != nullptr;
+        uint8_t* d_batch = nullptr;
+        if (batch) d_batch = batch_tables(db, *bip, batch_sig);
         struct Chunk { int base, P; hipFunction_t jit; };
         std::vector<Chunk> chunks;
         if (batch) chunks.push_back({0, n_patterns, nullptr});
@@ -1439,7 +1599,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // ~58 cache lines per exception bit)
             const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
             require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
-            if (!cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
+            if (cls && n_classes <= OTH_BATCH_MAX_CLASSES && oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P &&
+                env_flag("PM_OTHERS_BATCH", true))
+                hipLaunchKernelGGL(k_others_batch,
+                                   dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, OTH_BATCH_THREADS))),
+                                   dim3(OTH_BATCH_THREADS), 0, os, oa);
+            else if (!cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
                 hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
                                    dim3(256), 0, os, oa);
             else
@@ -1474,7 +1639,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             }
             // keys whose start lies past a segment's last tile: at most o_max
             // starts per pattern and segment boundary
-            const uint64_t xcap = std::max<uint64_t>(4096, nout * n_patterns * (bi.omax + 1));
+            const uint64_t xcap = std::max<uint64_t>(4096, nout * n_patterns * (bip->omax + 1));
             const bool exc = db->nflag && (db->n_oth_words || cross);
             for (int attempt = 0; attempt < 4 && !done; ++attempt) {
                 Carve cv;
@@ -1485,18 +1650,17 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
                 // k_batch_verify stores every (pattern, segment) count
                 sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
-                const uint32_t* d_tab = reinterpret_cast<const uint32_t*>(d_up + o_btab);
+                const BatchIndex& bi = *bip;
+                const uint32_t* d_tab = reinterpret_cast<const uint32_t*>(d_batch + bi.o_table);
                 BatchScanArgs sa{db->hl, db->ntiles, d_tab, bi.omax, (uint32_t)tpw, (uint32_t)nwaves, ccap,
                                  reinterpret_cast<uint4*>(rbase + o_cand), reinterpret_cast<uint32_t*>(rbase + o_ccnt),
                                  sb.cnt + sb.nbins, reinterpret_cast<uint32_t*>(rbase + o_xcnt)};
                 BatchVerifyArgs va{reinterpret_cast<const uint4*>(rbase + o_cand),
-                                   reinterpret_cast<const uint32_t*>(rbase + o_ccnt), ccap, sb.cnt + sb.nbins, d_tab,
-                                   reinterpret_cast<const uint32_t*>(d_up + o_brank),
-                                   reinterpret_cast<const uint32_t*>(d_up + o_boff),
-                                   reinterpret_cast<const uint32_t*>(d_up + o_blist),
-                                   reinterpret_cast<const uint4*>(d_up + o_bmask),
-                                   reinterpret_cast<const uint32_t*>(d_up + o_blen),
-                                   reinterpret_cast<const uint32_t*>(d_up + o_bopt),
+                                   reinterpret_cast<const uint32_t*>(rbase + o_ccnt), ccap, sb.cnt + sb.nbins,
+                                   reinterpret_cast<const uint32_t*>(d_batch + bi.o_code),
+                                   reinterpret_cast<const uint4*>(d_batch + bi.o_ents),
+                                   reinterpret_cast<const uint4*>(d_batch + bi.o_pmask),
+                                   reinterpret_cast<const uint32_t*>(d_batch + bi.o_popt),
                                    reinterpret_cast<const int32_t*>(d_up + o_len), bi.omax, (uint32_t)tpw,
                                    (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, db->hl, db->bo,
                                    db->lflag, db->ntiles, db->n, sb.out, sb.cnt, sb.slot_base, sb.slot_cap,

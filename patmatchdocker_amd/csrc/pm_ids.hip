@@ -128,10 +128,9 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    sg << "ids2:" << m << ":" << k << ":" << sp.errs << ":";
+    sg << "ids5:" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
     for (int j = 0; j <= k; ++j) sg << ":" << sp.rev_pre[j] << "," << sp.rev_ins[j];
-    *sig = sg.str();
 
     // two register banks, r and s: a step reads one and writes the other,
     // and the loop body is two steps (r -> s, s -> r), so no state moves
@@ -148,24 +147,50 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
                     if (bit(sp.rev_pre[jj], i)) return "0xffffffffu";
                     return i + 1 < m ? V(src, jj, i + 1) : "0u";
                 };
-                std::string t;
+                // match term: A & M (or A, or M alone), then the error terms
+                // ORed in; emitted as explicit v_bitop3 ((a & m) | x: 0xEA,
+                // a | b | c: 0xFE) -- written as C the compiler picks
+                // v_or3_b32 / v_and_or_b32, which issue ~1.5x slower on
+                // gfx950 (profiles/r01c_valu_rates.txt)
                 const std::string a = A(j);
-                if (a == "0xffffffffu") t = pc[i].any ? "0xffffffffu" : "M" + std::to_string(ci[i]);
-                else if (a == "0u") t = "0u";
-                else t = pc[i].any ? a : "(" + a + " & M" + std::to_string(ci[i]) + ")";
-                std::vector<std::string> terms{t};
-                if (j > 0 && SUB) terms.push_back(A(j - 1));
-                if (j > 0 && INS) terms.push_back(bit(sp.rev_ins[j - 1], i) ? "0xffffffffu" : V(src, j - 1, i));
+                std::string ta, tm;   // the match term as (ta & tm), or ta alone (tm empty)
+                if (a == "0xffffffffu") ta = pc[i].any ? "0xffffffffu" : "M" + std::to_string(ci[i]);
+                else if (a == "0u") ta = "0u";
+                else {
+                    ta = a;
+                    if (!pc[i].any) tm = "M" + std::to_string(ci[i]);
+                }
+                std::vector<std::string> rest;
+                if (j > 0 && SUB) rest.push_back(A(j - 1));
+                if (j > 0 && INS) rest.push_back(bit(sp.rev_ins[j - 1], i) ? "0xffffffffu" : V(src, j - 1, i));
                 if (j > 0 && DEL) {
-                    if (i + 1 < m) terms.push_back(V(dst, j - 1, i + 1));
-                    if (j >= 2 && INS && i == m - 1) terms.push_back("0xffffffffu");
+                    if (i + 1 < m) rest.push_back(V(dst, j - 1, i + 1));
+                    if (j >= 2 && INS && i == m - 1) rest.push_back("0xffffffffu");
+                }
+                std::vector<std::string> terms;
+                bool ones = ta == "0xffffffffu" && tm.empty();
+                for (const std::string& x : rest) {
+                    if (x == "0xffffffffu") ones = true;
+                    else if (x != "0u") terms.push_back(x);
                 }
                 std::string e;
-                for (const std::string& x : terms) {
-                    if (x == "0u") continue;
-                    e += (e.empty() ? "" : " | ") + x;
+                if (ones) {
+                    e = "0xffffffffu";
+                } else {
+                    size_t q = 0;
+                    if (ta == "0u") e = "";
+                    else if (tm.empty()) e = ta;
+                    else if (!terms.empty()) e = "B3(" + ta + ", " + tm + ", " + terms[q++] + ", 0xEA)";
+                    else e = "(" + ta + " & " + tm + ")";
+                    for (; q < terms.size();) {
+                        if (e.empty()) e = terms[q++];
+                        else if (q + 1 < terms.size()) {
+                            e = "B3(" + e + ", " + terms[q] + ", " + terms[q + 1] + ", 0xFE)";
+                            q += 2;
+                        } else e = "(" + e + " | " + terms[q++] + ")";
+                    }
+                    if (e.empty()) e = "0u";
                 }
-                if (e.empty()) e = "0u";
                 o << ind << V(dst, j, i) << " = " << (kill ? "(" + e + ") & nb" : e) << ";\n";
             }
     };
@@ -173,16 +198,24 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     // exception words are `vv` / `ev` and whose plane word is at pointer `pv`;
     // `emit`: t < 32 (the lane's own column) -- report starts
     auto step = [&](std::ostringstream& o, char src, char dst, const std::string& tv, const std::string& vv,
-                    const std::string& ev, const std::string& pv, bool emit) {
+                    const std::string& pv, bool emit) {
         const std::string in = "            ";
         o << in << "{\n";
-        o << in << "    const uint2 v = " << vv << ", e = " << ev << ";\n";
+        o << in << "    const uint2 v = " << vv << ";\n";
         for (size_t c = 0; c < rep.size(); ++c) {
             const PosClass& p = pc[rep[c]];
             if (p.any) o << in << "    u32 M" << c << " = 0xffffffffu;\n";
             else o << in << "    u32 M" << c << " = B3(v.x, v.y, v.y, " << subset_table(p.acgt) << ");\n";
         }
-        o << in << "    if (__ballot((e.x | e.y) != 0)) {   // wave-uniform\n";
+        // the row's exception flags (sbflag, fetched per tile): only a row
+        // with a break or an "other" byte in some lane reads the exception
+        // plane (emit: own row t; warm-up: row t - 32 of the next column, or
+        // the halo for lane 63)
+        o << in << "    const u32 rr = (u32)(" << tv << ")" << (emit ? "" : " - 32u") << ";\n";
+        o << in << "    const u32 rf = (u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr) | "
+                   "(u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr);\n";
+        o << in << "    if (rf != 0u" << (emit ? "" : " || ((halof >> rr) & 1ull)") << ") {   // wave-uniform, rare\n";
+        o << in << "        const uint2 e = " << pv << "[dbo];\n";
         o << in << "        const u32 nb = ~e.x;\n";
         // "other" bytes: the byte's own class membership
         o << in << "        if (e.y) {\n";
@@ -217,36 +250,83 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     std::ostringstream o;
     o << kIdsCommon;
     o << "#define WU " << WU << "\n";
+    // PM_IDS_LDS=1 (experiment): copy each tile into LDS by LDS-DMA first
+    // (one HBM round trip per tile; 2 waves/SIMD for the LDS)
+    const bool lds = env_flag("PM_IDS_LDS", false);
+    sg << (lds ? ":lds" : ":dir");
+    if (lds) o << "#define IDS_LDS 1\n";
+    // workgroups per CU the register budget is cut for (PM_IDS_WG, default 4:
+    // <= 128 VGPRs, 4 waves per SIMD)
+    const int wg = getenv("PM_IDS_WG") ? std::max(1, atoi(getenv("PM_IDS_WG"))) : 4;
+    o << "#define IDS_WG " << wg << "\n";
+    sg << ":wg" << wg;
+    *sig = sg.str();
     o << R"IDS(
 // One wave per tile; lane c owns stream column c (logical words 32c ..
 // 32c + 31, physical word t * 64 + c at step t): it scans the next column's
 // first WU words (or the tile's halo, lane 63) right to left as warm-up,
-// then its own 32 words, reporting starts.
-extern "C" __global__ __launch_bounds__(256) void pm_ids_rev(IArgs a) {
+// then its own 32 words, reporting starts.  The exception plane is read only
+// for rows whose sbflag bits show a break or an "other" byte in some lane:
+// lane r < 32 holds row r's 64 flag bits (one load per tile), a step reads
+// its row's with v_readlane.
+extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) {   // IDS_WG workgroups per CU
+#ifdef IDS_LDS
+    __shared__ __attribute__((aligned(1024))) uint4 s_tile[4][(TILE_WORDS / 2 + 63) / 64 * 64];
+#endif
     const u32 col = threadIdx.x & 63;
-    const u64 wave = (blockIdx.x * 256ull + threadIdx.x) >> 6, nwaves = gridDim.x * 4ull;
+    const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u64 wave = (u64)blockIdx.x * 4u + wid, nwaves = gridDim.x * 4ull;
     const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
+#ifdef IDS_LDS
+    const uint2* const lt = reinterpret_cast<const uint2*>(s_tile[wid]);
+    const u32 lds_base = (u32)reinterpret_cast<u64>(s_tile[wid]);   // LDS byte address
+#endif
     for (u64 tile = wave; tile < a.ntiles; tile += nwaves) {
-        // lflag bit c: column c and the 63 words after it hold an exception
-        const bool flagged = (a.lflag[tile] >> col) & 1ull;
-        const uint2* tb = a.hl + tile * TILE_WORDS;
+        const u64 base = tile * TILE_WORDS;   // a multiple of 32: rows are sbflag word pairs
+        const uint2* tb = a.hl + base;
+        u64 rowf = 0;
+        if (col < 32u) {
+            const u32* sf = a.sbflag + (base >> 5) + 2u * col;
+            rowf = (u64)sf[0] | ((u64)sf[1] << 32);
+        }
+        const u32* hf = a.sbflag + ((base + STREAM) >> 5);
+        const u64 halof = (u64)hf[0] | ((u64)hf[1] << 32);   // halo words 2048 .. 2111
+#ifdef IDS_LDS
+        {
+            const unsigned char* tbb = reinterpret_cast<const unsigned char*>(tb);
+            const u32 voff = col * 16u;
+#pragma unroll
+            for (int q = 0; q < (int)((TILE_WORDS * 8 + 1023) / 1024); ++q) {
+                if ((q + 1) * 1024 > (int)(TILE_WORDS * 8) && (int)col * 16 >= (int)(TILE_WORDS * 8) % 1024) continue;
+                const u32 dst = __builtin_amdgcn_readfirstlane(lds_base + q * 1024);
+                const unsigned char* pb = tbb + q * 1024;
+                u32 keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(voff), "s"(pb), "s"(dst) : "memory");
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint2* ln = col < 63u ? lt + col + 1 : lt + STREAM;   // the words in LDS
+        const uint2* lm = lt + col;
+#endif
         const uint2* pn = col < 63u ? tb + col + 1 : tb + STREAM;   // warm-up words: t - 32 ..
         const long sn = col < 63u ? 64 : 1;
         const uint2* pm = tb + col;                                  // own words: t * 64
 )IDS";
     for (int j = 0; j <= k; ++j)
         for (int i = 0; i < m; ++i) o << "        u32 " << V('r', j, i) << " = 0, " << V('s', j, i) << " = 0;\n";
-    o << "        uint2 v0, e0, v1, e1;\n";
-    o << "        const uint2* p0;\n";
-    o << "        const uint2* p1;\n";
-    auto ptr = [](bool own, const std::string& tv) {
-        return own ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn";
+    o << "        uint2 v0, v1;\n";
+    o << "        uint2 w0 = make_uint2(0u, 0u), w1 = make_uint2(0u, 0u);\n";
+    o << "        const uint2 *p0, *p1, *q0 = tb, *q1 = tb;\n";
+    auto ptr = [](bool own, const std::string& tv, const char* g) {
+        const std::string m = g[0] == 'p' ? "pm" : "lm", n = g[0] == 'p' ? "pn" : "ln";
+        return own ? m + " + (long)(" + tv + ") * 64" : n + " + (long)((" + tv + ") - 32) * sn";
     };
     auto load = [&](const std::string& pv, const std::string& vv, const std::string& ev, bool own,
                     const std::string& tv, const std::string& ind) {
-        o << ind << pv << " = " << ptr(own, tv) << ";\n";
-        o << ind << vv << " = *" << pv << ";\n";
-        o << ind << ev << " = flagged ? " << pv << "[dbo] : make_uint2(0u, 0u);\n";
+        o << ind << pv << " = " << ptr(own, tv, "p") << ";\n";
+        o << ind << vv << " = *(" << ptr(own, tv, lds ? "l" : "p") << ");\n";
+        (void)ev;
     };
     // a phase: `n` steps from t = `t0` down, pointer form `own`; pairs of
     // steps alternate the register banks and the word buffers (each step's
@@ -257,24 +337,30 @@ extern "C" __global__ __launch_bounds__(256) void pm_ids_rev(IArgs a) {
         if (n % 2) {   // a single step first
             o << "        {\n";
             load("p0", "v0", "e0", own, std::to_string(t), "            ");
-            step(o, b0, b1, std::to_string(t), "v0", "e0", "p0", own);
+            step(o, b0, b1, std::to_string(t), "v0", "p0", own);
             o << "        }\n";
             std::swap(b0, b1);
             --t;
             --n;
         }
         if (!n) return;
+        // the words of steps t and t - 1 are in v0 / v1 when an iteration
+        // starts; it issues the loads of t - 2 and t - 3 first (two steps
+        // ahead of their use)
         const std::string ind = "            ";
+        const int last = t - n + 1;
         o << "        {\n";
         load("p0", "v0", "e0", own, std::to_string(t), ind);
+        load("p1", "v1", "e1", own, std::to_string(t - 1), ind);
         o << "        }\n";
-        o << "        for (int t = " << t << "; t >= " << t - n + 2 << "; t -= 2) {\n";
-        load("p1", "v1", "e1", own, "t - 1", ind);
-        step(o, b0, b1, "t", "v0", "e0", "p0", own);
-        o << ind << "if (t - 2 >= " << t - n + 1 << ") {\n";
-        load("p0", "v0", "e0", own, "t - 2", ind + "    ");
+        o << "        for (int t = " << t << "; t >= " << last + 1 << "; t -= 2) {\n";
+        o << ind << "if (t - 2 >= " << last << ") {\n";
+        load("q0", "w0", "e0", own, "t - 2", ind + "    ");
+        load("q1", "w1", "e1", own, "t - 3", ind + "    ");
         o << ind << "}\n";
-        step(o, b1, b0, "t - 1", "v1", "e1", "p1", own);
+        step(o, b0, b1, "t", "v0", "p0", own);
+        step(o, b1, b0, "t - 1", "v1", "p1", own);
+        o << ind << "v0 = w0; v1 = w1; p0 = q0; p1 = q1;\n";
         o << "        }\n";
     };
     phase(31 + WU, WU, false);   // warm-up: t = 32 + WU - 1 .. 32
@@ -316,8 +402,14 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     IArgsHost a{nv.hl, nv.bo, nv.sbflag, nv.sbbase, nv.xbytes, db->lflag, sp.d_bmask, db->ntiles, db->n,
                 sink.out, sink.bin_cnt, sink.cap, sink.bins_per_pattern, sink.pos_shift, (uint32_t)sp.pattern_id};
     void* params[] = {&a};
-    // one wave per tile, waves loop over tiles (every wave reaches the end)
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((db->ntiles + 3) / 4, 256 * 8));
+    // one wave per tile, waves loop over tiles (every wave reaches the end);
+    // as many waves as are resident at once (4 per SIMD at <= 128 VGPRs):
+    // a second round of waves would start only as the first drains (PMC:
+    // ~2.9 of 4 waves resident on average with 2 rounds)
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, db->device));
+    const uint64_t resident = (uint64_t)std::max(ncu, 1) * 4;   // blocks of 4 waves: 16 waves per CU
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((db->ntiles + 3) / 4, resident));
     HIPCHK(hipExtModuleLaunchKernel(fn, blocks * 256u, 1, 1, 256, 1, 1, 0, s, params, nullptr, ev_a, ev_b, 0));
     return true;
 }

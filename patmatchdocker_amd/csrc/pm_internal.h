@@ -449,11 +449,16 @@ struct BatchIndex {
     uint32_t omax = 0;
     uint64_t expansions = 0;
     std::vector<uint32_t> table;      // [BQ_TABLE_WORDS]: the codes present (bit code & 31 of word code >> 5)
-    std::vector<uint32_t> code_off;   // [2^(2 BQ)]: first entry << 8 | entries, per code
+    // code -> first entry << 8 | entries: open-addressing hash table of
+    // 2^hbits slots {code + 1 (0: empty), value}, at most half full -- a few
+    // hundred KB, L2-resident (a direct 2^20-entry array is 4 MB of random
+    // reads)
+    std::vector<uint32_t> htab;
+    uint32_t hbits = 0;
     std::vector<uint32_t> ents;       // BATCH_ENT_WORDS per (code, pattern) entry, in increasing code order
     std::vector<uint32_t> pmask;      // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
     std::vector<uint32_t> popt;       // [P]: o_p, the indexed piece's offset
-    // device image (ws_batch): table | code_off | ents | pmask | popt
+    // device image (ws_batch): table | htab | ents | pmask | popt
     size_t o_table = 0, o_code = 0, o_ents = 0, o_pmask = 0, o_popt = 0, bytes = 0;
 };
 // one verification entry (two uint4): {p | o_p << 16 | len << 24, length mask
@@ -478,7 +483,8 @@ struct BatchVerifyArgs {
     const uint32_t* cand_cnt;
     uint32_t ccap;
     uint32_t* aux;          // the largest candidate count above ccap (0: none)
-    const uint32_t* code_off;
+    const uint2* htab;      // BatchIndex::htab
+    uint32_t hbits;
     const uint4* ents;      // two uint4 per entry
     const uint4* pmask;
     const uint32_t* popt;
@@ -598,6 +604,7 @@ struct TextView {
     const uint8_t* raw;     // BYTE layout, the file's own bytes
     uint64_t n;
     int nuc_layout;
+    const uint64_t* lflag;  // NUC: per tile, the lanes with an exception (a clean lane holds no header byte)
 };
 TextView text_view(const pm_db* db);
 // true when the pass changes anything for `flags` (cross: candidates may

@@ -44,10 +44,6 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
     return __builtin_amdgcn_alignbit(hi, lo, s);
 }
 
-__host__ __device__ inline uint32_t batch_hash(uint32_t code, uint32_t bits) {
-    return (code * 0x9E3779B1u) >> (32 - bits);
-}
-
 // one level of the 32x32 bit transpose: swaps the (rows r, columns c + J)
 // block with the (rows r + J, columns c) block, r and c with bit J clear
 template <int J, uint32_t M>
@@ -264,27 +260,9 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
         uint32_t co[VU];
 #pragma unroll
         for (int u = 0; u < VU; ++u) e[u] = q0 + u < total ? *at(q0 + u) : make_uint4(0u, 0u, 0u, 0u);
-        uint32_t h[VU], code[VU];
 #pragma unroll
-        for (int u = 0; u < VU; ++u) {
-            code[u] = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
-            h[u] = batch_hash(code[u], a.hbits);
-            co[u] = 0u;
-        }
-        // first probes of the VU candidates together, then the rare collisions
-#pragma unroll
-        for (int u = 0; u < VU; ++u) {
-            if (q0 + u >= total) continue;
-            for (uint32_t g = 0; g < (1u << a.hbits); ++g) {
-                const uint2 sl = a.htab[h[u]];
-                if (sl.x == code[u] + 1u) {
-                    co[u] = sl.y;
-                    break;
-                }
-                if (sl.x == 0u) break;   // absent (cannot happen for a probed code)
-                h[u] = (h[u] + 1u) & ((1u << a.hbits) - 1u);
-            }
-        }
+        for (int u = 0; u < VU; ++u)
+            co[u] = q0 + u < total ? a.code_off[alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u)] : 0u;
 #pragma unroll
         for (int u = 0; u < VU; ++u)
             if (co[u]) verify_candidate(a, og, cnt_p, e[u], co[u]);
@@ -387,38 +365,24 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         return x.code != y.code ? x.code < y.code : x.p < y.p;
     });
     bi.table.assign(BQ_TABLE_WORDS, 0u);
-    std::vector<uint32_t> code_off((size_t)1 << (2 * BQ), 0u);
+    bi.code_off.assign((size_t)1 << (2 * BQ), 0u);
     bi.ents.assign(ents.size() * BATCH_ENT_WORDS, 0u);
     for (size_t i = 0; i < ents.size(); ++i) {
         const uint32_t c = ents[i].code, p = ents[i].p;
         if (i == 0 || c != ents[i - 1].code) {
             bi.table[c >> 5] |= 1u << (c & 31);
-            code_off[c] = (uint32_t)i << 8;
+            bi.code_off[c] = (uint32_t)i << 8;
         }
-        if ((code_off[c] & 255u) == 255u || i >= (1u << 24)) return false;
-        ++code_off[c];
+        if ((bi.code_off[c] & 255u) == 255u || i >= (1u << 24)) return false;
+        ++bi.code_off[c];
         uint32_t* e = &bi.ents[i * BATCH_ENT_WORDS];
         e[0] = p | bi.popt[p] << 16 | (uint32_t)lengths[p] << 24;
         e[1] = plen[p];
         for (int b = 0; b < 4; ++b) e[4 + b] = bi.pmask[(size_t)4 * p + b];   // the second uint4
     }
-    // the present codes into the hash table (at most half full)
-    uint32_t ncodes = 0;
-    for (uint32_t w : bi.table) ncodes += (uint32_t)__builtin_popcount(w);
-    bi.hbits = 10;
-    while ((1u << bi.hbits) < 2 * ncodes) ++bi.hbits;
-    bi.htab.assign((size_t)2 << bi.hbits, 0u);
-    for (size_t i = 0; i < ents.size(); ++i) {
-        const uint32_t c = ents[i].code;
-        if (i && c == ents[i - 1].code) continue;
-        uint32_t h = batch_hash(c, bi.hbits);
-        while (bi.htab[2 * h]) h = (h + 1) & ((1u << bi.hbits) - 1);
-        bi.htab[2 * h] = c + 1;
-        bi.htab[2 * h + 1] = code_off[c];
-    }
     Carve cv;
     bi.o_table = cv.take(bi.table.size() * 4);
-    bi.o_code = cv.take(bi.htab.size() * 4);
+    bi.o_code = cv.take(bi.code_off.size() * 4);
     bi.o_ents = cv.take(std::max<size_t>(bi.ents.size(), BATCH_ENT_WORDS) * 4);
     bi.o_pmask = cv.take(bi.pmask.size() * 4);
     bi.o_popt = cv.take(bi.popt.size() * 4);

@@ -1383,7 +1383,7 @@ uint8_t* batch_tables(pm_db* db, const BatchIndex& bi, const std::string& sig) {
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_batch, bi.bytes));
     std::vector<uint8_t> img(bi.bytes, 0);
     memcpy(img.data() + bi.o_table, bi.table.data(), bi.table.size() * 4);
-    memcpy(img.data() + bi.o_code, bi.htab.data(), bi.htab.size() * 4);
+    memcpy(img.data() + bi.o_code, bi.code_off.data(), bi.code_off.size() * 4);
     memcpy(img.data() + bi.o_ents, bi.ents.data(), bi.ents.size() * 4);
     memcpy(img.data() + bi.o_pmask, bi.pmask.data(), bi.pmask.size() * 4);
     memcpy(img.data() + bi.o_popt, bi.popt.data(), bi.popt.size() * 4);
@@ -1657,7 +1657,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                  sb.cnt + sb.nbins, reinterpret_cast<uint32_t*>(rbase + o_xcnt)};
                 BatchVerifyArgs va{reinterpret_cast<const uint4*>(rbase + o_cand),
                                    reinterpret_cast<const uint32_t*>(rbase + o_ccnt), ccap, sb.cnt + sb.nbins,
-                                   reinterpret_cast<const uint2*>(d_batch + bi.o_code), bi.hbits,
+                                   reinterpret_cast<const uint32_t*>(d_batch + bi.o_code),
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_ents),
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_pmask),
                                    reinterpret_cast<const uint32_t*>(d_batch + bi.o_popt),

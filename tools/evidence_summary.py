@@ -41,7 +41,7 @@ def pmc(dirs, needle):
 
 for name in ("bench", "bench100", "bench_ids", "bench_cfg4", "configs"):
     copy(os.path.join(root, name + ".json"), "%s_%s.json" % (rnd, name))
-for d in ("prof", "prof100", "prof_ids"):
+for d in ("prof", "prof100", "prof_ids", "prof_cfg4"):
     copy(os.path.join(root, d, "run_kernel_stats.csv"), "%s_%s_kernel_stats.csv" % (rnd, d))
 copy(os.path.join(root, "prof", "run_kernel_trace.csv"), "%s_prof_kernel_trace.csv" % rnd)
 

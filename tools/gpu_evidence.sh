@@ -21,6 +21,7 @@ P 400 prof100 --gbp 100 --steps 10 --warmup 3
 B 300 bench_ids --types ids --steps 10 --warmup 3
 P 300 prof_ids --types ids --steps 10 --warmup 3
 B 400 bench_cfg4 --config 4 --steps 3 --warmup 1 --no-cpu-baseline
+P 400 prof_cfg4 --config 4 --steps 3 --warmup 1
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \

@@ -430,7 +430,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         const size_t o_uns = lds ? 0 : c.take(total * sizeof(uint64_t));
         const size_t o_tmp = lds ? 0 : c.take(sort_bytes);
         const size_t o_scan = c.take(scan_bytes);
-        const size_t o_big = c.take(big.size() * sizeof(uint32_t));
+        const size_t o_big = c.take(inline_off ? 0 : (size_t)sb.nbins * sizeof(uint32_t));   // bin lists
         uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
         if (!inline_off) {
@@ -440,23 +440,44 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             // the next launch check does not report it
             (void)hipGetLastError();
         }
-        if (lds) {
+        if (lds && inline_off) {
             auto kern = maxc > LDS_SORT_CAP ? k_sort_bins<LDS_SORT_CAP_MAX> : k_sort_bins<LDS_SORT_CAP>;
-            // many bins (a large batch: patterns x segments): each block
-            // sorts a strided run of bins instead of one block per bin
-            hipLaunchKernelGGL(kern, dim3(std::min<uint32_t>(sb.nbins, 8192)), dim3(256), 0, s, sb.out, sb.cnt,
-                               inline_off ? (const uint64_t*)nullptr : (const uint64_t*)d_off, sh, h->keys, slot_len,
-                               h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)nullptr, sb.nbins);
+            hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, (const uint64_t*)nullptr, sh,
+                               h->keys, slot_len, h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr,
+                               (const uint32_t*)nullptr, sb.nbins);
             HIPCHK(hipGetLastError());
-            if (!big.empty()) {
-                uint32_t* d_big = reinterpret_cast<uint32_t*>(base + o_big);
-                HIPCHK(hipMemcpyAsync(d_big, big.data(), big.size() * 4, hipMemcpyHostToDevice, s));
-                hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_HUGE, 1024>), dim3((uint32_t)big.size()), dim3(1024), 0, s,
-                                   sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
-                                   (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_big,
-                                   (uint32_t)big.size());
+        } else if (lds) {
+            // many bins (a large batch: patterns x segments), each pass a
+            // size class: a bin's sort is a short chain of dependent loads, so
+            // the small-bin pass (most bins, 2 KB of LDS) keeps many blocks
+            // in flight per CU; the larger classes go by bin lists
+            std::vector<uint32_t> mid;
+            for (uint32_t b = 0; b < sb.nbins; ++b) {
+                const uint32_t c = std::min(counts[b], sb.slot_cap_h[b / sb.bins_per_pattern]);
+                if (c > LDS_SORT_SMALL && c <= LDS_SORT_CAP_MAX) mid.push_back(b);
+            }
+            hipLaunchKernelGGL((k_sort_bins<LDS_SORT_SMALL, LDS_SORT_SMALL>), dim3(std::min<uint32_t>(sb.nbins, 65536)),
+                               dim3(LDS_SORT_SMALL), 0, s, sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys,
+                               slot_len, h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr,
+                               (const uint32_t*)nullptr, sb.nbins);
+            HIPCHK(hipGetLastError());
+            std::vector<uint32_t> lists(mid);
+            lists.insert(lists.end(), big.begin(), big.end());
+            if (!lists.empty()) {
+                uint32_t* d_lists = reinterpret_cast<uint32_t*>(base + o_big);
+                HIPCHK(hipMemcpyAsync(d_lists, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, s));
+                if (!mid.empty())
+                    hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_MAX, 256>), dim3((uint32_t)mid.size()), dim3(256), 0, s,
+                                       sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
+                                       (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_lists,
+                                       (uint32_t)mid.size());
+                if (!big.empty())
+                    hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_HUGE, 1024>), dim3((uint32_t)big.size()), dim3(1024), 0,
+                                       s, sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
+                                       (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_lists + mid.size(),
+                                       (uint32_t)big.size());
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipStreamSynchronize(s));   // `big` (pageable) was read by the copy
+                HIPCHK(hipStreamSynchronize(s));   // `lists` (pageable) was read by the copy
             }
             if (lens_done) *lens_done = slot_len != nullptr;
         } else {

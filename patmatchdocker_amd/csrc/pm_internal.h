@@ -102,6 +102,7 @@ constexpr int MAX_NFA_CHUNK = 4096;                  // positions per lane in k_
 constexpr uint32_t LDS_SORT_CAP = 2048;              // keys per bin sorted in LDS (16 KB: 8 sort blocks per CU)
 constexpr uint32_t LDS_SORT_CAP_MAX = 4096;          // the larger sort variant (32 KB), for bins above LDS_SORT_CAP
 constexpr uint32_t LDS_SORT_CAP_HUGE = 16384;        // large bins, sorted in a second pass (128 KB of LDS)
+constexpr uint32_t LDS_SORT_SMALL = 256;             // many-bin lists: the small-bin pass (rank sort, 2 KB of LDS)
 constexpr uint64_t BYTE_PAD = 2 * MAX_NFA_CHUNK + 4096;
 constexpr int RUN_SKIP = 8;                          // run-interior lookahead (xint)
 

@@ -1599,8 +1599,11 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // ~58 cache lines per exception bit)
             const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
             require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
-            if (cls && n_classes <= OTH_BATCH_MAX_CLASSES && oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P &&
-                env_flag("PM_OTHERS_BATCH", true))
+            // the per-class wave form: large batches (class-id staging), or any
+            // chunk with PM_OTHERS_BATCH=2 (experiment)
+            static const int others_batch = getenv("PM_OTHERS_BATCH") ? atoi(getenv("PM_OTHERS_BATCH")) : 1;
+            if ((cls ? others_batch >= 1 : others_batch >= 2) && n_classes <= OTH_BATCH_MAX_CLASSES &&
+                oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P)
                 hipLaunchKernelGGL(k_others_batch,
                                    dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, OTH_BATCH_THREADS))),
                                    dim3(OTH_BATCH_THREADS), 0, os, oa);

@@ -76,6 +76,11 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
     return x;
 }
 
+// STRIDE 2: only every other position is probed (PAR: the parity of the
+// probed block offsets i, so that o_max + i is even); every pattern is then
+// indexed by two consecutive pieces (o_p and o_p + 1), one of which starts at
+// an even position for any window -- half the LDS probes per position.
+template <int STRIDE, int PAR>
 __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
     __shared__ uint32_t s_tab[BQ_TABLE_WORDS];   // 128 KB: one workgroup per CU
     for (uint32_t i = threadIdx.x; i < BQ_TABLE_WORDS; i += BATCH_THREADS) s_tab[i] = a.table[i];
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             const uint32_t d[3] = {alignb(c1, c0, sh), alignb(c2, c1, sh), alignb(c3, c2, sh)};
             uint32_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < 32; ++i) {
+            for (int i = PAR; i < 32; i += STRIDE) {
                 const int b0 = 2 * i, b3 = 2 * i + 3;
                 const uint32_t code = (b0 & 31) ? alignb(d[(b0 >> 5) + 1], d[b0 >> 5], b0 & 31) : d[b0 >> 5];
                 // code bits 5..19 (the table word) at bits 2..16: its LDS byte address
@@ -148,12 +153,12 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             }
             // candidates: probe i -> 16-byte entry {tile, lane << 11 | s << 6
             // | i, the 32 bases from position i of the block}
-            uint32_t m = acc;
+            uint32_t m = STRIDE == 2 ? acc >> 16 : acc;   // stride 2: probe i = 2k + PAR at bit k
             while (__builtin_amdgcn_ballot_w64(m != 0u)) {
                 const bool has = m != 0u;
                 uint4 e = make_uint4(0u, 0u, 0u, 0u);
                 if (has) {
-                    const uint32_t i = (uint32_t)__builtin_ctz(m);
+                    const uint32_t i = STRIDE == 2 ? 2u * (uint32_t)__builtin_ctz(m) + PAR : (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
                     const bool up = i >= 16u;
                     const uint32_t r = (2u * i) & 31u;
@@ -286,7 +291,10 @@ __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
     // the file's first starts st < o_max - o_p: probed by no block
     for (uint32_t q = tid; q < (uint32_t)a.P * a.omax; q += nth) {
         const uint32_t p = q / a.omax, st = q % a.omax;
-        if (st + a.popt[p] >= a.omax) continue;
+        // the position this start is probed at (stride 2: the even one of
+        // its two pieces); probes start at o_max
+        const uint32_t y = st + a.popt[p];
+        if ((a.stride == 2 ? y + (y & 1u) : y) >= a.omax) continue;
         const int len = a.lengths[p];
         if ((uint64_t)st + len > a.n) continue;
         const uint4 mk = a.pmask[p];
@@ -318,8 +326,17 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
     for (int p = 0; p < P; ++p)
         if (lengths[p] < BQ || lengths[p] > BATCH_MAX_LEN) return false;
     struct Ent {
-        uint32_t code, p;
+        uint32_t code, p, op;
     };
+    // PM_BATCH_STRIDE=2 (experiment; every pattern needs room for two
+    // pieces): every pattern indexed by two consecutive pieces, every other
+    // position probed.  Measured on configs[4]: scan 3.0 -> 2.16 ms, but the
+    // two pieces' expansions raise the candidates and verify 2.08 -> 2.74 ms
+    // (10.6 vs 9.9 ms per step), so every position is probed by default.
+    bi.stride = getenv("PM_BATCH_STRIDE") && atoi(getenv("PM_BATCH_STRIDE")) == 2 ? 2 : 1;
+    for (int p = 0; p < P; ++p)
+        if (lengths[p] < BQ + 1) bi.stride = 1;
+    const int npieces = (int)bi.stride;
     std::vector<Ent> ents;
     std::vector<uint32_t> plen(P, 0);
     bi.popt.assign(P, 0);
@@ -337,38 +354,45 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         // ACGT-only window, nothing to index)
         uint64_t best = ~0ull;
         int bo = 0;
-        for (int o = 0; o + BQ <= L; ++o) {
+        auto expansions = [&](int o) {
             uint64_t prod = 1;
             for (int i = 0; i < BQ; ++i) prod *= (uint64_t)__builtin_popcount(sub[o + i]);
-            if (prod < best) {
-                best = prod;
+            return prod;
+        };
+        for (int o = 0; o + BQ + npieces - 1 <= L; ++o) {
+            uint64_t tot = 0;
+            for (int q = 0; q < npieces; ++q) tot += expansions(o + q);
+            if (tot < best) {
+                best = tot;
                 bo = o;
             }
         }
         bi.popt[p] = (uint32_t)bo;
-        bi.omax = std::max(bi.omax, (uint32_t)bo);
+        bi.omax = std::max(bi.omax, (uint32_t)(bo + npieces - 1));
         bi.expansions += best;
         if (bi.expansions > BATCH_MAX_EXPANSIONS) return false;
-        if (!best) continue;
-        std::vector<uint32_t> codes(1, 0u);
-        for (int i = 0; i < BQ; ++i) {
-            std::vector<uint32_t> nx;
-            nx.reserve(codes.size() * 4);
-            for (uint32_t c : codes)
-                for (uint32_t b = 0; b < 4; ++b)
-                    if ((sub[bo + i] >> b) & 1u) nx.push_back(c | (b << (2 * i)));
-            codes.swap(nx);
+        for (int q = 0; q < npieces; ++q) {
+            if (!expansions(bo + q)) continue;   // the pattern matches no ACGT-only window
+            std::vector<uint32_t> codes(1, 0u);
+            for (int i = 0; i < BQ; ++i) {
+                std::vector<uint32_t> nx;
+                nx.reserve(codes.size() * 4);
+                for (uint32_t c : codes)
+                    for (uint32_t b = 0; b < 4; ++b)
+                        if ((sub[bo + q + i] >> b) & 1u) nx.push_back(c | (b << (2 * i)));
+                codes.swap(nx);
+            }
+            for (uint32_t c : codes) ents.push_back({c, (uint32_t)p, (uint32_t)(bo + q)});
         }
-        for (uint32_t c : codes) ents.push_back({c, (uint32_t)p});
     }
     std::sort(ents.begin(), ents.end(), [](const Ent& x, const Ent& y) {
-        return x.code != y.code ? x.code < y.code : x.p < y.p;
+        return x.code != y.code ? x.code < y.code : x.p != y.p ? x.p < y.p : x.op < y.op;
     });
     bi.table.assign(BQ_TABLE_WORDS, 0u);
     bi.code_off.assign((size_t)1 << (2 * BQ), 0u);
     bi.ents.assign(ents.size() * BATCH_ENT_WORDS, 0u);
     for (size_t i = 0; i < ents.size(); ++i) {
-        const uint32_t c = ents[i].code, p = ents[i].p;
+        const uint32_t c = ents[i].code, p = ents[i].p, op = ents[i].op;
         if (i == 0 || c != ents[i - 1].code) {
             bi.table[c >> 5] |= 1u << (c & 31);
             bi.code_off[c] = (uint32_t)i << 8;
@@ -376,7 +400,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         if ((bi.code_off[c] & 255u) == 255u || i >= (1u << 24)) return false;
         ++bi.code_off[c];
         uint32_t* e = &bi.ents[i * BATCH_ENT_WORDS];
-        e[0] = p | bi.popt[p] << 16 | (uint32_t)lengths[p] << 24;
+        e[0] = p | op << 16 | (uint32_t)lengths[p] << 24;
         e[1] = plen[p];
         for (int b = 0; b < 4; ++b) e[4 + b] = bi.pmask[(size_t)4 * p + b];   // the second uint4
     }
@@ -393,7 +417,8 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
                   hipEvent_t ev_a, hipEvent_t ev_b) {
     // the kernel's own dispatch timestamps (no marker packets)
-    hipExtLaunchKernelGGL(k_batch_scan, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
+    auto kern = va.stride == 1 ? k_batch_scan<1, 0> : (sa.omax & 1u) ? k_batch_scan<2, 1> : k_batch_scan<2, 0>;
+    hipExtLaunchKernelGGL(kern, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_batch_verify, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());

@@ -1516,7 +1516,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         std::shared_ptr<const BatchIndex> bip;
         std::string batch_sig;
         if (jit && k == 0 && n_patterns >= batch_min && env_flag("PM_BATCH", true)) {
-            batch_sig = jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any);
+            batch_sig = jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any) +
+                        (getenv("PM_BATCH_STRIDE") ? std::string(";stride=") + getenv("PM_BATCH_STRIDE") : "");
             bip = batch_index_cached(batch_sig, n_patterns, lengths, pos_class, class_acgt, class_is_any);
         }
         const bool batch = bip != nullptr;
@@ -1665,7 +1666,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_pmask),
                                    reinterpret_cast<const uint32_t*>(d_batch + bi.o_popt),
                                    reinterpret_cast<const int32_t*>(d_up + o_len), bi.omax, (uint32_t)tpw,
-                                   (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, db->hl, db->bo,
+                                   (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, bi.stride, db->hl, db->bo,
                                    db->lflag, db->ntiles, db->n, sb.out, sb.cnt, sb.slot_base, sb.slot_cap,
                                    reinterpret_cast<uint64_t*>(rbase + o_x), reinterpret_cast<uint32_t*>(rbase + o_xcnt),
                                    (uint32_t)xcap};

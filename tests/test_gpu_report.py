@@ -224,35 +224,44 @@ def _exception_rich_fasta(seed, mbp, width, headless):
     return bytes(out)
 
 
-@pytest.mark.parametrize("width,headless", [(60, False), (80, True)])
-def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, headless):
+@pytest.mark.parametrize("width,headless,minlen", [(60, False, 10), (80, True, 11)])
+def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, headless, minlen):
     """The q-gram batch filter (pm_batch.hip, k = 0, >= 16 patterns of 10-16
     positions) on a multi-tile database full of exceptions, patterns of
     every length 10..16 (different piece offsets o_p) + configs[4]'s motifs,
     every pattern's report list vs the oracle; and the same query with the
-    filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks)."""
+    filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks).
+    minlen 11 also runs the stride-2 probes (PM_BATCH_STRIDE=2: every other
+    position, two indexed pieces per pattern)."""
     import bench
     monkeypatch.setenv("PM_JIT", "1")
     text = _exception_rich_fasta(21 + width, 3.0, width, headless)
     rng = random.Random(width)
     motifs = bench.batch_patterns(40, seed=width)
-    for L in range(10, 17):
+    for L in range(minlen, 17):
         for _ in range(3):
             motifs.append("".join(rng.choice("ACGT") if rng.random() < 0.75 else rng.choice("RYSWKMN")
                                   for _ in range(L)))
-    motifs += ["GAATTCGAATTC", "TATATATATA", "NNNNNNNNNNAC", "AAAAAAAAAAAAAAAA"]
+    motifs += [m for m in ("GAATTCGAATTC", "TATATATATA", "NNNNNNNNNNAC", "AAAAAAAAAAAAAAAA") if len(m) >= minlen]
     progs = [compile_pattern(convert("-n", m)) for m in motifs]
     db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
     try:
         res, _ = engine.scan(db, progs, k=0, types="s")
+        res_s2 = None
+        if minlen >= 11:
+            monkeypatch.setenv("PM_BATCH_STRIDE", "2")
+            res_s2, _ = engine.scan(db, progs, k=0, types="s")
+            monkeypatch.delenv("PM_BATCH_STRIDE")
         monkeypatch.setenv("PM_BATCH", "0")
         res_chunks, _ = engine.scan(db, progs, k=0, types="s")
     finally:
         db.close()
     total = 0
-    for prog, r, rc in zip(progs, res, res_chunks):
+    for i, (prog, r, rc) in enumerate(zip(progs, res, res_chunks)):
         want = oracle_mod.scan_threads(text, prog, 0, "s", skip_headers=True, threads=16, report="nrgrep")
         assert _pairs(r) == want, prog.source
         assert _pairs(rc) == want, prog.source
+        if res_s2 is not None:
+            assert _pairs(res_s2[i]) == want, prog.source
         total += len(want)
     assert total > 1000

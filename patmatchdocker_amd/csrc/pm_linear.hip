@@ -283,9 +283,18 @@ __device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint
             uint8_t c = 0, f = 0;
             if (q >= 0 && (uint64_t)q < a.n) {
                 const Loc l = loc_of((uint64_t)q);
-                const uint2 ex = a.nuc.bo[l.word];
-                const uint2 hv = a.nuc.hl[l.word];   // issued with bo: one round trip for a base
-                const uint32_t brk = (ex.x >> l.bit) & 1, oth = (ex.y >> l.bit) & 1;
+                // the exception plane only for words that hold an exception
+                // (sbflag: 1 bit per word, 1/64 of the plane, cache-resident):
+                // most of a window's words are clean, so about half the HBM
+                // lines of a gather
+                const uint32_t sf = a.nuc.sbflag[l.word >> 5];
+                const uint2 hv = a.nuc.hl[l.word];
+                uint32_t brk = 0, oth = 0;
+                if ((sf >> (l.word & 31)) & 1) {
+                    const uint2 ex = a.nuc.bo[l.word];
+                    brk = (ex.x >> l.bit) & 1;
+                    oth = (ex.y >> l.bit) & 1;
+                }
                 f = (uint8_t)((brk | oth) | (brk << 1));
                 if (brk | oth)
                     c = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
@@ -545,12 +554,15 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
             Loc lc{0, 0};
             if (in_file) {
                 lc = loc_of((uint64_t)q);
-                const uint2 ex = a.nuc.bo[lc.word];
+                const uint32_t sf = a.nuc.sbflag[lc.word >> 5];   // the exception plane only for flagged words
                 const uint2 hv = a.nuc.hl[lc.word];
                 h = (hv.x >> lc.bit) & 1;
                 l = (hv.y >> lc.bit) & 1;
-                br = (ex.x >> lc.bit) & 1;
-                ot = (ex.y >> lc.bit) & 1;
+                if ((sf >> (lc.word & 31)) & 1) {
+                    const uint2 ex = a.nuc.bo[lc.word];
+                    br = (ex.x >> lc.bit) & 1;
+                    ot = (ex.y >> lc.bit) & 1;
+                }
             }
             const uint64_t H = __builtin_amdgcn_ballot_w64(h != 0), L = __builtin_amdgcn_ballot_w64(l != 0);
             const uint64_t BR = __builtin_amdgcn_ballot_w64(br != 0), OT = __builtin_amdgcn_ballot_w64(ot != 0);

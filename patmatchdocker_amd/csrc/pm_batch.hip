@@ -177,67 +177,79 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
     if (lane == 0) a.cand_cnt[wave] = ccnt;
 }
 
-// The matches among one candidate's entries: key per match, into this
-// segment's lists (LDS counters) or the next segment's list (xkeys).
-__device__ __forceinline__ void verify_candidate(const BatchVerifyArgs& a, uint32_t og, uint32_t* cnt_p, uint4 e,
-                                                 uint32_t co) {
+// Slot tables of the block's hit lists, staged in LDS.
+struct VerifySlots {
+    uint64_t* base;   // [P] this segment's list of pattern p: out + slot_base[p] + og * slot_cap[p]
+    uint32_t* cap;    // [P]
+    uint32_t* cnt;    // [P] keys so far
+};
+
+// One entry (h, mk) of a candidate: on a match, its key into this segment's
+// list (LDS counter) or the next segment's list (xkeys).  lf: the lane flags
+// of the candidate's tile (prefetched).
+__device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t og, const VerifySlots& vs, uint4 e,
+                                             uint64_t lf, uint4 h, uint4 mk) {
     const uint32_t x0 = e.z, x1 = e.w;
     const uint32_t i = e.y & 63u, st0 = (e.y >> 6) & 31u, bl = e.y >> 11;
-    const uint32_t lo = co >> 8, hi = lo + (co & 255u);
-    for (uint32_t t = lo; t < hi; ++t) {
-        const uint4 h = a.ents[2 * t], mk = a.ents[2 * t + 1];
-        const uint32_t p = h.x & 0xFFFFu, op = (h.x >> 16) & 255u;
-        const int len = (int)(h.x >> 24);
-        // the window's 16 bases; per position the class's bit for its base
-        // (A/C by lo, G/T by lo, then by hi), at odd bits
-        const uint32_t wc = alignb(x1, x0, 2u * (a.omax - op));
-        const uint32_t lsh = wc << 1;
-        const uint32_t s1 = (lsh & mk.y) | (~lsh & mk.x);
-        const uint32_t s2 = (lsh & mk.w) | (~lsh & mk.z);
-        const uint32_t res = (wc & s2) | (~wc & s1);
-        if ((res & h.y) != h.y) continue;
-        uint64_t tile = e.x;
-        uint32_t w = 32u * bl + a.omax + i - op, st = st0;
-        if (w >= STREAM) {   // the start lies in the next stream (or tile)
-            w -= (uint32_t)STREAM;
-            if (++st == 32) {
-                st = 0;
-                ++tile;
-            }
+    const uint32_t p = h.x & 0xFFFFu, op = (h.x >> 16) & 255u;
+    const int len = (int)(h.x >> 24);
+    // the window's 16 bases; per position the class's bit for its base
+    // (A/C by lo, G/T by lo, then by hi), at odd bits
+    const uint32_t wc = alignb(x1, x0, 2u * (a.omax - op));
+    const uint32_t lsh = wc << 1;
+    const uint32_t s1 = (lsh & mk.y) | (~lsh & mk.x);
+    const uint32_t s2 = (lsh & mk.w) | (~lsh & mk.z);
+    const uint32_t res = (wc & s2) | (~wc & s1);
+    if ((res & h.y) != h.y) return;
+    uint64_t tile = e.x;
+    uint32_t w = 32u * bl + a.omax + i - op, st = st0;
+    if (w >= STREAM) {   // the start lies in the next stream (or tile)
+        w -= (uint32_t)STREAM;
+        if (++st == 32) {
+            st = 0;
+            ++tile;
+            if (tile < a.ntiles) lf = a.lflag[tile];
         }
-        const uint64_t pos = pos_of(tile, w, st);
-        if (tile >= a.ntiles || pos + (uint64_t)len > a.n) continue;
-        if ((a.lflag[tile] >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
-            uint32_t kill = 0;
-            for (int j = 0; j < len; ++j) {
-                const Loc l = loc_of(pos + j);
-                const uint2 b = a.bo[l.word];
-                kill |= ((b.x | b.y) >> l.bit) & 1u;
-            }
-            if (kill) continue;
+    }
+    const uint64_t pos = pos_of(tile, w, st);
+    if (tile >= a.ntiles || pos + (uint64_t)len > a.n) return;
+    if ((lf >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
+        uint32_t kill = 0;
+        for (int j = 0; j < len; ++j) {
+            const Loc l = loc_of(pos + j);
+            const uint2 b = a.bo[l.word];
+            kill |= ((b.x | b.y) >> l.bit) & 1u;
         }
-        const uint64_t key = ((uint64_t)p << 48) | pos;
-        const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
-        if (ogr == og) {
-            const uint32_t o = atomicAdd(&cnt_p[p], 1u);
-            if (o < a.slot_cap[p]) a.out[a.slot_base[p] + (uint64_t)og * a.slot_cap[p] + o] = key;
-        } else {
-            const uint32_t o = atomicAdd(a.xcnt, 1u);
-            if (o < a.xcap) a.xkeys[o] = key;
-        }
+        if (kill) return;
+    }
+    const uint64_t key = ((uint64_t)p << 48) | pos;
+    const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
+    if (ogr == og) {
+        const uint32_t o = atomicAdd(&vs.cnt[p], 1u);
+        if (o < vs.cap[p]) a.out[vs.base[p] + o] = key;
+    } else {
+        const uint32_t o = atomicAdd(a.xcnt, 1u);
+        if (o < a.xcap) a.xkeys[o] = key;
     }
 }
 
 // One block per output segment (wpo scan waves).  A thread takes VU
-// candidates at a time: their code -> entry lookups are independent loads in
-// flight together (two dependent L2 round trips per candidate: code_off,
-// then its entries).
+// candidates at a time, and every dependent load of them is issued for all
+// VU together: the candidates, then their code -> entry offsets and tiles'
+// lane flags, then their first entries (a candidate code lists ~1 entry;
+// further ones are loaded as needed).  The slot tables are staged in LDS.
 constexpr int VU = 4;
 __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
     __shared__ uint32_t cnt_p[BATCH_MAX_P];
+    __shared__ uint32_t cap_p[BATCH_MAX_P];
+    __shared__ uint64_t base_p[BATCH_MAX_P];
     __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
     const uint32_t og = blockIdx.x;
-    for (int p = threadIdx.x; p < a.P; p += blockDim.x) cnt_p[p] = 0;
+    for (int p = threadIdx.x; p < a.P; p += blockDim.x) {
+        cnt_p[p] = 0;
+        cap_p[p] = a.slot_cap[p];
+        base_p[p] = a.slot_base[p] + (uint64_t)og * a.slot_cap[p];
+    }
     const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
     if (threadIdx.x == 0) {
         uint32_t run = 0;
@@ -253,6 +265,7 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
         s_n[nw] = run;
     }
     __syncthreads();
+    const VerifySlots vs{base_p, cap_p, cnt_p};
     const uint32_t total = s_n[nw];
     // candidate q of the segment: wave k with s_n[k] <= q < s_n[k + 1]
     auto at = [&](uint32_t q) {
@@ -260,17 +273,36 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
         while (q >= s_n[k + 1]) ++k;
         return a.cand + (uint64_t)(w0 + k) * a.ccap + (q - s_n[k]);
     };
-    for (uint32_t q0 = threadIdx.x * VU; q0 < total; q0 += blockDim.x * VU) {
-        uint4 e[VU];
+    // candidate base + u * blockDim + thread: a wave's loads are 64
+    // consecutive 16-byte entries
+    for (uint32_t base = 0; base < total; base += blockDim.x * VU) {
+        uint4 e[VU], h[VU], mk[VU];
         uint32_t co[VU];
+        uint64_t lf[VU];
 #pragma unroll
-        for (int u = 0; u < VU; ++u) e[u] = q0 + u < total ? *at(q0 + u) : make_uint4(0u, 0u, 0u, 0u);
+        for (int u = 0; u < VU; ++u) {
+            const uint32_t q = base + u * blockDim.x + threadIdx.x;
+            e[u] = q < total ? *at(q) : make_uint4(0u, 0u, 0u, 0u);
+        }
 #pragma unroll
-        for (int u = 0; u < VU; ++u)
-            co[u] = q0 + u < total ? a.code_off[alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u)] : 0u;
+        for (int u = 0; u < VU; ++u) {
+            const bool ok = base + u * blockDim.x + threadIdx.x < total;
+            co[u] = ok ? a.code_off[alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u)] : 0u;
+            lf[u] = ok && e[u].x < a.ntiles ? a.lflag[e[u].x] : 0ull;
+        }
 #pragma unroll
-        for (int u = 0; u < VU; ++u)
-            if (co[u]) verify_candidate(a, og, cnt_p, e[u], co[u]);
+        for (int u = 0; u < VU; ++u) {
+            const uint32_t lo = co[u] >> 8;
+            h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
+            mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            if (!co[u]) continue;
+            verify_entry(a, og, vs, e[u], lf[u], h[u], mk[u]);
+            const uint32_t lo = co[u] >> 8, hi = lo + (co[u] & 255u);
+            for (uint32_t t = lo + 1; t < hi; ++t) verify_entry(a, og, vs, e[u], lf[u], a.ents[2 * t], a.ents[2 * t + 1]);
+        }
     }
     __syncthreads();
     for (int p = threadIdx.x; p < a.P; p += blockDim.x) a.seg_cnt[(uint64_t)p * a.nout + og] = cnt_p[p];

@@ -1134,7 +1134,15 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     }
     // `waves`: __launch_bounds__ minimum workgroups per CU (4 -> at most
     // 128 VGPRs; jit_function falls back to 3 when that would spill)
-    o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << DMA_PIECES << "\n";
+    // bytes DMA'd per tile: the 2048 words and only the halo words a window
+    // reads (Lmax - 1 of the 64; PM_JIT_FULL_HALO=1: all) -- ~2 % fewer HBM
+    // lines per tile for a 15-mer
+    const int halo_used = getenv("PM_JIT_FULL_HALO") ? HALO : std::min(HALO, std::max(1, Lmax - 1));
+    const int LOAD_BYTES = std::min(TILE_BYTES, (int)(((STREAM + halo_used) * 8 + 15) / 16 * 16));
+    const int LOAD_PIECES = (LOAD_BYTES + 1023) / 1024;
+    (void)DMA_PIECES;
+    o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << LOAD_PIECES
+      << "\n#define LOAD_BYTES " << LOAD_BYTES << "\n";
     // experiment knobs: PM_JIT_NOCOMPUTE=1 only streams the tiles,
     // PM_JIT_NODMA=1 rescans each workgroup's first tiles (no HBM stream)
     const bool nocompute = getenv("PM_JIT_NOCOMPUTE") && getenv("PM_JIT_NOCOMPUTE")[0] == '1';
@@ -1162,7 +1170,7 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
 #pragma unroll
   for (int q = 0; q < DMA_PIECES; q += 4) {
     if (q + (int)wid >= DMA_PIECES) break;
-    if ((q + (int)wid + 1) * 1024 > LDS_TILE && lane * 16 >= LDS_TILE % 1024) continue;   // half last piece
+    if ((q + (int)wid + 1) * 1024 > LOAD_BYTES && lane * 16 >= LOAD_BYTES % 1024) continue;   // partial last piece
     const u32 dst = __builtin_amdgcn_readfirstlane(dst0 + (q + wid) * 1024);
     const unsigned char* pb = tb + (q + wid) * 1024;
     u32 keep;
@@ -1311,7 +1319,8 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
         sig += "]";
     }
     for (const char* knob :
-         {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT", "PM_JIT_NOSHARE"})
+         {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT", "PM_JIT_NOSHARE",
+          "PM_JIT_FULL_HALO"})
         if (const char* e = getenv(knob)) sig += std::string(";") + knob + "=" + e;
     return sig;
 }

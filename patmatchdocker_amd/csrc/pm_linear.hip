@@ -191,21 +191,24 @@ struct OthersArgs {
     uint32_t nwg, tiles_per_wg;
     int items_per_wave;  // k_linear_others: 1, 2 or 4 (2 * maxlen - 1 <= 64 / items_per_wave)
     int n_classes;       // k_linear_others<true>: classes staged in LDS (<= 256)
+    int direct;          // k_linear_others: iterate the candidate words themselves (selection inline, no
+                         // k_others_select pass)
 };
 
 // Phase 1, one thread per candidate word: the exception bits that can own a
 // live window, compacted into `sel`.
-__global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= (a.use_edge ? a.nedge : a.nflag)) return;
+// The exception bits of candidate word t that can own a live window (0:
+// none), and the word's physical index.
+__device__ inline uint32_t select_bits(const OthersArgs& a, uint64_t t, uint64_t* word) {
     const uint64_t idx = a.use_edge ? a.xedge[t] : t;   // run interiors removed at build (k_run_interior)
     uint32_t ot = a.xoth[idx] | (a.cross ? a.xbrk[idx] : 0u);
     if (a.use_edge) ot &= ~a.xint[idx];
-    if (!ot) return;
+    if (!ot) return 0u;
     const uint64_t w = a.xword[idx];
+    *word = w;
     const uint64_t tile = w / TILE_WORDS;
     const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
-    if (lw >= STREAM) return;   // halo copy of a main word
+    if (lw >= STREAM) return 0u;   // halo copy of a main word
     if (lw >= 1 && a.skip_ok) {
         // exceptions right before each bit's position (bit b of word lw - 1
         // is position e - 1)
@@ -235,6 +238,14 @@ __global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
             ot &= ~m;
         }
     }
+    return ot;
+}
+
+__global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= (a.use_edge ? a.nedge : a.nflag)) return;
+    uint64_t w = 0;
+    const uint32_t ot = select_bits(a, t, &w);
     if (ot) a.sel[atomicAdd(a.nsel, 1u)] = OtherSel{w, ot, 0u};
 }
 
@@ -656,9 +667,17 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     // lanes each (an item's window span fits them): more gathers in flight
     const int G = a.items_per_wave, lanes = 64 / G;
     const int lane = (threadIdx.x & 63) % lanes, slice = (threadIdx.x & 63) / lanes;
-    const uint32_t nsel = *a.nsel, nitems = gridDim.x * (blockDim.x >> 6) * G;
-    for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * G + slice; it < nsel; it += nitems) {
-        const OtherSel sv = a.sel[it];
+    const uint64_t nsel = a.direct ? (a.use_edge ? a.nedge : a.nflag) : *a.nsel;
+    const uint32_t nitems = gridDim.x * (blockDim.x >> 6) * G;
+    for (uint64_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * G + slice; it < nsel; it += nitems) {
+        OtherSel sv;
+        if (a.direct) {   // the item's lanes select its bits themselves (same loads: broadcast)
+            sv.word = 0;
+            sv.bits = select_bits(a, it, &sv.word);
+            if (!sv.bits) continue;
+        } else {
+            sv = a.sel[it];
+        }
         const uint64_t tile = sv.word / TILE_WORDS;
         const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
         if (CLS)
@@ -1613,23 +1632,33 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // phase 1: one thread per candidate word selects the
             // exception bits that can own a live window; phase 2:
             // persistent waves evaluate them
-            HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
-            hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
-            HIPCHK(hipGetLastError());
+            const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
+            require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
+            static const int others_batch = getenv("PM_OTHERS_BATCH") ? atoi(getenv("PM_OTHERS_BATCH")) : 1;
+            const bool batch_form = (cls ? others_batch >= 1 : others_batch >= 2) && n_classes <= OTH_BATCH_MAX_CLASSES &&
+                                    oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P;
+            const bool lane_form = !batch_form && !cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN &&
+                                   env_flag("PM_OTHERS_LANE", false);
+            // a selection pass compacts the words first (PM_OTHERS_DIRECT=1:
+            // the wave form selects inline instead -- measured slower, 0.231
+            // vs 0.138 + 0.046 ms on configs[2]: the persistent waves then
+            // wait on the selection loads of every filtered-out word)
+            oa.direct = !batch_form && !lane_form && env_flag("PM_OTHERS_DIRECT", false) ? 1 : 0;
+            if (!oa.direct) {
+                HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
+                hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
+                HIPCHK(hipGetLastError());
+            }
             // PM_OTHERS_LANE=1: the lane form (measured 0.20 vs 0.18 ms on
             // the bench database: both are bound by the random gathers,
             // ~58 cache lines per exception bit)
-            const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
-            require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
             // the per-class wave form: large batches (class-id staging), or any
             // chunk with PM_OTHERS_BATCH=2 (experiment)
-            static const int others_batch = getenv("PM_OTHERS_BATCH") ? atoi(getenv("PM_OTHERS_BATCH")) : 1;
-            if ((cls ? others_batch >= 1 : others_batch >= 2) && n_classes <= OTH_BATCH_MAX_CLASSES &&
-                oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P)
+            if (batch_form)
                 hipLaunchKernelGGL(k_others_batch,
                                    dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, OTH_BATCH_THREADS))),
                                    dim3(OTH_BATCH_THREADS), 0, os, oa);
-            else if (!cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN && env_flag("PM_OTHERS_LANE", false))
+            else if (lane_form)
                 hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
                                    dim3(256), 0, os, oa);
             else

@@ -172,17 +172,23 @@ def test_specialized_shared_blocks(engine, oracle_mod, monkeypatch, k):
         db.close()
 
 
-def test_specialized_matches_generic_on_synthetic(engine, monkeypatch):
+def test_specialized_matches_generic_on_synthetic(engine, oracle_mod, monkeypatch):
+    """Both linear kernels on the bench's synthetic database (N runs, IUPAC
+    letters, headers generated on the device), each vs the oracle on the
+    decoded text (the bench motif, both strands, k = 2)."""
     db = engine.SequenceDatabase.synthetic(n_records=40, rec_len=100_003, seed=9)
     try:
+        text = db.decode(0, db.info()["positions"])
         fwd = convert("-n", "TGCTGASTCAGCANW")
         progs = [compile_pattern(fwd), compile_pattern(convert("-c", fwd))]
         monkeypatch.setenv("PM_JIT", "0")
         generic, _ = engine.scan(db, progs, k=2, types="s")
         monkeypatch.setenv("PM_JIT", "1")
         special, _ = engine.scan(db, progs, k=2, types="s")
-        for g, s_ in zip(generic, special):
-            assert _gpu_pairs(g) == _gpu_pairs(s_)
+        for prog, g, s_ in zip(progs, generic, special):
+            want = oracle_mod.scan_threads(text, prog, 2, "s", skip_headers=True, threads=16, report="nrgrep")
+            assert _gpu_pairs(g) == want, prog.source
+            assert _gpu_pairs(s_) == want, prog.source
     finally:
         db.close()
 

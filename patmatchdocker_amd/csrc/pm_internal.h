@@ -443,7 +443,7 @@ constexpr int BATCH_WAVES = 16;                            // waves per workgrou
 constexpr int BATCH_THREADS = 64 * BATCH_WAVES;
 constexpr int BATCH_MAX_P = 1024;
 constexpr int BATCH_MAX_LEN = 16;                          // a window's bases fit one 32-bit code word
-constexpr uint32_t BATCH_MAX_WPO = 16;                     // scan waves per output segment
+constexpr uint32_t BATCH_MAX_WPO = 64;                     // scan waves per output segment
 constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a quarter of the table)
 
 struct BatchIndex {

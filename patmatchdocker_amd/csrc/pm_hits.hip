@@ -148,13 +148,26 @@ struct BinCount {
     __device__ uint64_t operator()(uint32_t b) const { return min(cnt[b], sh.cap(b)); }
 };
 
+// pos_bits > 0: keys packed as pattern << pos_bits | position, so the radix
+// sort runs over the significant bits only (k_unpack_keys restores them)
 __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
-                              const uint64_t* __restrict__ off, BinShape sh, uint64_t* __restrict__ dst) {
+                              const uint64_t* __restrict__ off, BinShape sh, uint64_t* __restrict__ dst,
+                              uint32_t pos_bits) {
     const uint32_t bin = blockIdx.x;
     const uint32_t c = min(cnt[bin], sh.cap(bin));
     const uint64_t o = off[bin];
     const uint64_t* src = sh.src(out, bin);
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = src[i];
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+        const uint64_t k = src[i];
+        dst[o + i] = pos_bits ? ((k >> 48) << pos_bits) | (k & ((1ull << 48) - 1)) : k;
+    }
+}
+
+__global__ void k_unpack_keys(uint64_t* __restrict__ keys, uint64_t n, uint32_t pos_bits) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    keys[i] = ((k >> pos_bits) << 48) | (k & ((1ull << pos_bits) - 1));
 }
 
 std::mutex g_pool_mu;
@@ -482,11 +495,22 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             if (lens_done) *lens_done = slot_len != nullptr;
         } else {
             uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
+            // sort only the significant bits: positions < 2^pos_bits, pattern
+            // slots < 2^slot_bits
+            uint32_t pos_bits = 1, slot_bits = 1;
+            while (pos_bits < 48 && (db->n >> pos_bits)) ++pos_bits;
+            while (slot_bits < 16 && ((uint64_t)(sb.nbins / sb.bins_per_pattern - 1) >> slot_bits)) ++slot_bits;
+            const bool pack = pos_bits + slot_bits < 56;
             hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh,
-                               unsorted);
+                               unsorted, pack ? pos_bits : 0u);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0, 64,
-                                                     s));
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
+                                                     pack ? (int)(pos_bits + slot_bits) : 64, s));
+            if (pack) {
+                hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
+                                   pos_bits);
+                HIPCHK(hipGetLastError());
+            }
         }
     } catch (...) {
         pool_put(h->device, h->keys, h->keys_cap);

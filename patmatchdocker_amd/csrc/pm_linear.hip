@@ -600,14 +600,22 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
                 const uint32_t cw[4] = {cl.x, cl.y, cl.z, cl.w};
                 // starts u whose window holds e: u in [ML - len, ML - 1]
                 uint64_t alive = (((1ull << len) - 1) << (ML - len)) & ~owned;
+                if (KILL) {   // wave-uniform; rare with the simple engine (off-file positions only)
+                    uint64_t kw = 0;
+                    for (int j = 0; j < len; ++j) kw |= KILL >> j;
+                    alive &= ~kw;
+                }
                 uint64_t c0 = 0, c1 = 0, ge4 = 0;
 #pragma unroll
                 for (int j = 0; j < BATCH_MAX_LEN; ++j) {
                     if (j >= len) break;
                     const uint64_t m = mv[(cw[j >> 2] >> (8 * (j & 3))) & 255u] >> j;
-                    alive &= ~(KILL >> j);
-                    if (a.k == 0) alive &= m;
-                    else vec_add(~m, c0, c1, ge4);
+                    if (a.k == 0) {
+                        alive &= m;
+                        if (!alive) break;   // most windows around an exception die within a few positions
+                    } else {
+                        vec_add(~m, c0, c1, ge4);
+                    }
                 }
                 if (a.k) {
                     uint64_t dead;

@@ -606,9 +606,7 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
                     alive &= ~kw;
                 }
                 uint64_t c0 = 0, c1 = 0, ge4 = 0;
-#pragma unroll
-                for (int j = 0; j < BATCH_MAX_LEN; ++j) {
-                    if (j >= len) break;
+                for (int j = 0; j < len; ++j) {   // (not unrolled: dead windows leave early)
                     const uint64_t m = mv[(cw[j >> 2] >> (8 * (j & 3))) & 255u] >> j;
                     if (a.k == 0) {
                         alive &= m;

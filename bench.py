@@ -16,11 +16,16 @@ Reported beside the throughput:
                 words) / its HIP-event duration vs the 8 TB/s HBM peak;
                 traffic = PMC HBM bytes per launch from profiles/ when a
                 counter run of this workload is committed there, else null;
-  cpu_baseline  the bit-parallel Shift-Add scan (oracle/pm_cpuscan.c, one
-                thread per host core of the box's CPU share, at most 16) timed
-                on a bounded sample of the same database (decoded from HBM);
-                its hits and the oracle's (pm_oracle.c, on a smaller prefix)
-                are bit-exact parity spot checks of the GPU hits.
+  cpu_baseline  nrgrep's own esimple engine restated from the binary
+                (oracle/pm_nrgrep.c: its piece BNDM scan, two-phase verify
+                and report rule), one thread per host core of the box's CPU
+                share (at most 16), timed on a bounded sample of the same
+                database (decoded from HBM); its matches are a bit-exact
+                parity spot check of the GPU's.
+
+`--gpus N` without torchrun: the bench starts `torch.distributed.run` with
+N local ranks itself (a child process, before any GPU call) and exits with
+its code; under torchrun, N must equal WORLD_SIZE.
 """
 
 import argparse
@@ -50,7 +55,7 @@ def parse_args():
                     help="error types of '-k <k><types>': s = mismatches (default, the metric's workload); "
                          "ids = the web form's default (insertions, deletions, substitutions)")
     ap.add_argument("--sample-mbp", type=float, default=None,
-                    help="CPU-baseline sample (Mbp; default 200 per CPU thread)")
+                    help="CPU-baseline sample (Mbp; default 100 per CPU thread)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the box's CPU share, at most 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -103,80 +108,66 @@ def cpu_threads_default():
     return max(1, min(16, n))
 
 
-def cpu_baseline(db, progs, k, sample_bp, gpu_hits, threads, parity_bp=320e6):
-    """CPU baseline + parity spot checks on the first `sample_bp` positions
-    (decoded from HBM, so the exact bytes the GPU scanned): the reported
-    matches of every strand by the bit-parallel Shift-Add scan
-    (oracle/pm_cpuscan.c -- the automaton family nrgrep itself runs) over
-    `threads` host threads, timed; its hits must equal the GPU's, and the
-    first `parity_bp` positions are also checked against the oracle
-    (pm_oracle.c, a different algorithm).  Returns (dict, parity_ok)."""
+def cpu_baseline(db, progs, k, types, sample_bp, gpu_hits, threads):
+    """CPU baseline + parity spot check on the first `sample_bp` positions
+    (decoded from HBM, so the exact bytes the GPU scanned): what
+    nrgrep_coords prints for every strand, by nrgrep's own esimple engine
+    restated from the binary (oracle/pm_nrgrep.c -- its cost-model plan,
+    piece BNDM scan, two-phase verify and report rule) over `threads` host
+    threads (the text cut at line breaks: e* matches never span one), timed;
+    its matches must equal the GPU's.  Returns (dict, parity_ok)."""
     from oracle import oracle
     text = db.decode(0, int(sample_bp))
+    text = text[:text.rfind(b"\n") + 1]
     t0, c0 = time.perf_counter(), time.process_time()
-    base = [oracle.shiftadd_threads(text, p, k, skip_headers=True, threads=threads) for p in progs]
-    dt = time.perf_counter() - t0
-    cpu_s = time.process_time() - c0
-    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
-    ptext = text[:int(parity_bp)]
-    cut = ptext.rfind(b"\n") + 1
-    ptext = ptext[:cut]
-    want = [oracle.scan_threads(ptext, p, k, "s", skip_headers=True, threads=threads, report="nrgrep") for p in progs]
-    ok = True
-    keys, lens = gpu_hits
-    keys = keys.cpu().tolist()
-    lens = lens.cpu().tolist()
-    for pid, (b, w) in enumerate(zip(base, want)):
-        got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
-               if (kk >> 48) == pid]
-        ok &= [h for h in got if h[1] <= len(text)] == [h for h in b if h[1] <= len(text)]
-        ok &= [h for h in got if h[1] <= len(ptext)] == w
-    return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
-            "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands: "
-                      "bit-parallel Shift-Add scan (oracle/pm_cpuscan.c, nrgrep's automaton family, "
-                      "same reported matches) on %d host threads, text cut at line breaks; "
-                      "%.1f s wall, %.1f s CPU, %d CPUs in the affinity mask"
-                      % (sample_bp / 1e6, threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok
-
-
-def cpu_baseline_ids(db, progs, k, types, sample_bp, gpu_hits, threads, parity_bp=40e6):
-    """`-k <k>ids` CPU baseline: the bit-parallel Wu-Manber scan
-    (oracle/pm_cpuscan.c pmc_ids_scan, nrgrep's e* engines' recurrence)
-    on `threads` host threads over the first `sample_bp` positions, timed;
-    its reported matches must equal the GPU's, and the first `parity_bp`
-    positions are also checked against pm_oracle.c."""
-    from oracle import oracle
-    text = db.decode(0, int(sample_bp))
-    cut = text.rfind(b"\n") + 1
-    text = text[:cut]
-    t0, c0 = time.perf_counter(), time.process_time()
-    base = [oracle.ids_threads(text, p, k, types, skip_headers=True, threads=threads) for p in progs]
-    dt = time.perf_counter() - t0
-    cpu_s = time.process_time() - c0
-    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
-    ptext = text[:int(parity_bp)]
-    ptext = ptext[:ptext.rfind(b"\n") + 1]
-    want = [oracle.scan_threads(ptext, p, k, types, skip_headers=True, threads=threads, report="nrgrep")
+    base = [oracle.scan_threads(text, p, k, types, skip_headers=True, threads=threads, report="nrgrep")
             for p in progs]
+    dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0
+    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
+    ok = True
     keys, lens = gpu_hits
     keys = keys.cpu().tolist()
     lens = lens.cpu().tolist()
-    ok = True
-    for pid, (b, w) in enumerate(zip(base, want)):
+    for pid, b in enumerate(base):
         got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
                if (kk >> 48) == pid]
         ok &= [h for h in got if h[1] <= len(text)] == b
-        ok &= [h for h in got if h[1] <= len(ptext)] == w
+    plan = oracle.nrgrep_plan(progs[0], k)
     return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
             "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, -k %d%s: "
-                      "bit-parallel Wu-Manber scan (oracle/pm_cpuscan.c pmc_ids_scan, reverse pass for starts + "
-                      "forward pass for the shortest end + report rule, same reported matches) on %d host "
-                      "threads, text cut at line breaks; %.1f s wall, %.1f s CPU"
-                      % (sample_bp / 1e6, k, types, threads, dt, cpu_s)}, ok
+                      "nrgrep's esimple engine restated from the binary (oracle/pm_nrgrep.c; plan type %d, "
+                      "%s) on %d host threads, text cut at line breaks; %.1f s wall, %.1f s CPU, "
+                      "%d CPUs in the affinity mask"
+                      % (sample_bp / 1e6, k, types, plan["type"],
+                         "%d pieces of %d found by BNDM" % (len(plan["L"]), plan["piece_len"])
+                         if plan["type"] == 1 else "window %s" % (plan["window"],),
+                         threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok
+
+
+def spawn_ranks(args):
+    """`--gpus N` outside torchrun: run this script under
+    torch.distributed.run with N local ranks (a child process, started
+    before this process touches a GPU) and return its exit code."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, os.environ.get("WORLD_SIZE")))
     import torch
     import torch.distributed as dist
 
@@ -234,7 +225,9 @@ def main():
         finally:
             engine.destroy_hits(h)
         keys = shards.to_global(keys, offset)
-        out = shards.gather_hits(keys, lens)
+        # substitutions only: every hit of pattern p is prog.m long, so only
+        # the keys travel (to rank 0)
+        out = shards.gather_hits(keys, None, fixed_len=[p.m for p in progs])
         return out, ms
 
     def ids_step():
@@ -367,12 +360,9 @@ def main():
             line["roofline"]["traffic"] = None
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
             thr = args.cpu_threads or cpu_threads_default()
-            if indel:
-                mbp = args.sample_mbp if args.sample_mbp is not None else 40.0 * thr
-                cb, ok = cpu_baseline_ids(db, progs, args.k, args.types, mbp * 1e6, result, thr)
-            else:
-                mbp = args.sample_mbp if args.sample_mbp is not None else 200.0 * thr
-                cb, ok = cpu_baseline(db, progs, args.k, mbp * 1e6, result, thr)
+            # ~10-30 s of CPU work (nrgrep's engine runs ~0.1 Gbases/s per thread)
+            mbp = args.sample_mbp if args.sample_mbp is not None else 100.0 * thr
+            cb, ok = cpu_baseline(db, progs, args.k, args.types if args.k else "", mbp * 1e6, result, thr)
             line["cpu_baseline"] = cb
             line["parity_sample_bit_exact"] = ok
         else:

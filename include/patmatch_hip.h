@@ -91,6 +91,21 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
  * windows are checked against the file's own bytes and may span a line
  * break (pm_scan_linear decides this by itself).                          */
 #define PM_CROSS_LINES 16
+/* The pattern is a class sequence (nrgrep's detClass() == 1) searched with
+ * k > 0 errors: nrgrep_coords runs its "esimple" engine (searchPreproc
+ * 0x402710), whose own candidate order and two-phase verification decide
+ * which overlapping match is printed.  pm_scan_linear sets it
+ * by itself for k > 0; pm_scan_nfa_wide takes it from the caller.        */
+#define PM_ESIMPLE 64
+/* The scan plan nrgrep's esimplePreproc (0x415540) derives from the classes
+ * of a class sequence with k errors (cost model over its letterProb table):
+ * out[0] = 1 (k+1 pieces, BNDM), 2 (a window, ABNDM) or 3 (the prefix,
+ * forward shift-or); out[1] = piece length; out[2..3] = simpleFindBest's
+ * window; out[4] = number of pieces P; out[5 .. 5+P) = pattern positions
+ * left of each piece / window.  byte_mask as in pm_scan_nfa_wide (the folded
+ * byte's positions; classes hold both cases, as `-i` builds them).  Host
+ * only, no GPU needed.  out must hold 5 + k + 1 ints.                    */
+int pm_esimple_plan(int m, int words, const uint64_t* byte_mask, int k, int32_t* out);
 
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched

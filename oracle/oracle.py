@@ -25,7 +25,7 @@ ERR_INS, ERR_DEL, ERR_SUB = 1, 2, 4
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "Makefile")]
+    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "pm_nrgrep.c", "Makefile")]
     if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return path
@@ -52,6 +52,11 @@ def lib():
         _LIB.pmc_shiftadd.restype = ctypes.c_int64
         _LIB.pmc_shiftadd.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, p64, ctypes.c_int64]
+        _LIB.pmn_plan.restype = ctypes.c_int
+        _LIB.pmn_plan.argtypes = [pu64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        _LIB.pmn_esimple.restype = ctypes.c_int64
+        _LIB.pmn_esimple.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -97,8 +102,8 @@ PMO_NRGREP, PMO_START, PMO_END, PMO_SIMPLE = 1, 2, 4, 8
 def mode_of(prog, k: int, report: str = "nrgrep", simple=None) -> int:
     """pmo_scan2 mode bits for a compiled program: nrgrep's engine choice
     (simple = k 0 + class sequence, searchPreproc 0x402660), the anchors and
-    the report rule."""
-    m = PMO_NRGREP if report == "nrgrep" else 0
+    the report rule ("nrgrep" / "leftmost": first found = leftmost start)."""
+    m = PMO_NRGREP if report in ("nrgrep", "leftmost") else 0
     if prog.anchor_start:
         m |= PMO_START
     if prog.anchor_end:
@@ -118,12 +123,18 @@ def scan_candidates(text: bytes, prog, k: int = 0, types: str = "ids"):
 
 def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
                   report: str = "nrgrep", simple=None, mode=None):
-    """What ``nrgrep_coords`` prints for ``prog`` (pmo_scan2): the candidates
-    of ``scan`` (or the simple engine's whole-text windows at k = 0) reduced
-    by the binary's report rule -- first found wins, the scan resumes at the
-    match end -- and its '^'/'$' checks; ``skip_headers`` then drops the
-    header-line hits process_output throws away.  ``simple`` overrides the
-    engine choice (False: line-bounded windows even at k = 0)."""
+    """What ``nrgrep_coords`` prints for ``prog``.  A class sequence at
+    k > 0 runs nrgrep's esimple engine (``scan_esimple``, pm_nrgrep.c: its
+    own candidate order and verify).  Everything else (pmo_scan2): the
+    candidates of ``scan`` (or the simple engine's whole-text windows at
+    k = 0) reduced by the binary's report rule -- first found wins, the
+    scan resumes at the match end -- and its '^'/'$' checks, the first found
+    being the leftmost start (``report="leftmost"`` forces that rule for a
+    class sequence too).  ``skip_headers`` then drops the header-line hits
+    process_output throws away.  ``simple`` overrides the engine choice
+    (False: line-bounded windows even at k = 0)."""
+    if report == "nrgrep" and simple is None and mode is None and k > 0 and is_esimple(prog):
+        return scan_esimple(text, prog, k, types, skip_headers)
     L = lib()
     B = np.array(prog.byte_masks(), dtype=np.uint64)
     F = np.array(prog.follow + [0], dtype=np.uint64)
@@ -222,6 +233,64 @@ def record_index(text: bytes):
 
 
 # ---------------------------------------------------------------------------
+# nrgrep's esimple engine (pm_nrgrep.c): the -k <k><ids> path of a class
+# sequence, restated from the binary's disassembly
+# ---------------------------------------------------------------------------
+
+def is_esimple(prog) -> bool:
+    """nrgrep's esimple engine (searchPreproc 0x402710): a plain class
+    sequence (detClass 1) searched with errors."""
+    return prog.linear and prog.kind == "simple"
+
+
+def wide_masks(prog) -> np.ndarray:
+    """[256][4] uint64 position sets (bit i = position i accepts the folded
+    byte), up to 256 positions."""
+    B = np.zeros((256, 4), dtype=np.uint64)
+    for i, cls in enumerate(prog.classes):
+        for b in cls:
+            B[b, i >> 6] |= np.uint64(1 << (i & 63))
+    return B
+
+
+def nrgrep_plan(prog, k: int):
+    """nrgrep's scan plan for ``prog`` at k errors (esimplePreproc): a dict
+    with ``type`` (1 pieces, 2 backward window, 3 forward window),
+    ``piece_len``, ``window`` and ``L`` (left length of every piece)."""
+    B = wide_masks(prog)
+    out = (ctypes.c_int * 24)()
+    n = lib().pmn_plan(B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), prog.m, k,
+                       1 if prog.ignore_case else 0, out)
+    if n < 0:
+        raise ValueError("no esimple plan for m=%d k=%d" % (prog.m, k))
+    return {"type": out[0], "piece_len": out[1], "window": (out[2], out[3]),
+            "L": [out[4 + i] for i in range(n)]}
+
+
+def scan_esimple(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False):
+    """What nrgrep_coords prints for a class sequence at k > 0 (pmn_esimple:
+    nrgrep's own scanners, record lookup, two-phase verify and report rule)."""
+    if not prog.linear or k < 1:
+        raise ValueError("scan_esimple needs a class sequence and k > 0")
+    B = wide_masks(prog)
+    mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = lib().pmn_esimple(text, len(text), B.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), prog.m, k,
+                              err_flags(types), 1 if prog.ignore_case else 0, mode,
+                              beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                              end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pmn_esimple rejected m=%d k=%d" % (prog.m, k))
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+# ---------------------------------------------------------------------------
 # pure-Python restatement (explicit (position, errors) state sets), small n
 # ---------------------------------------------------------------------------
 
@@ -283,7 +352,10 @@ def scan_py_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_hea
     with no class accepting '\n'), restated in pure Python for automata of
     any size (pm_oracle.c holds 64 positions): the candidates of scan_py,
     the report rule (first found wins, resume at its end) and the '^'
-    check (a line start or the resume point, pmo_scan2)."""
+    check (a line start or the resume point, pmo_scan2).  A class sequence
+    at k > 0 is nrgrep's esimple engine: ``scan_esimple`` (256 positions)."""
+    if k > 0 and is_esimple(prog):
+        return scan_esimple(text, prog, k, types, skip_headers)
     out, R = [], 0
     for b, e in scan_py(text, prog, k, types, to_line_end=prog.anchor_end):
         if b < R:

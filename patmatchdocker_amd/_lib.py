@@ -23,6 +23,7 @@ PM_MAX_LINEAR_POSITIONS = 64  # pattern length, fixed-length kernel
 PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
 PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END, PM_KEEP_HEADERS = 0, 1, 2, 4, 8
 PM_CROSS_LINES = 16
+PM_ESIMPLE = 64               # a class sequence at k > 0: nrgrep's esimple report
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -31,7 +32,7 @@ EXPORTED = (
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
-    "pm_ids_jit_compile",
+    "pm_ids_jit_compile", "pm_esimple_plan",
 )
 
 
@@ -81,6 +82,7 @@ def _declare(lib):
     lib.pm_hits_destroy.argtypes = [P]
     lib.pm_hits_device.argtypes = [P, PP, PP, pu64]
     lib.pm_hits_copy_device.argtypes = [P, P, P, u64, P]
+    lib.pm_esimple_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
     lib.pm_linear_jit_compile.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, P, ctypes.c_int, pu64]
     for name in EXPORTED:
         if name not in ("pm_last_error", "pm_version"):

@@ -533,9 +533,11 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
 // thread then walks its cluster (the candidates up to the next head)
 // sequentially.  Clusters are short (overlapping matches), so the walk is
 // cheap; the running maximum comes from per-chunk maxima (k_rep_max) and an
-// in-block scan.  With '^' the acceptance of a candidate depends on where
-// the previous report ended (a start equal to R passes the check, 0x402182)
-// so one thread walks each list sequentially (anchored queries only).
+// in-block scan.  With '^' a start passes the check at a line start or
+// exactly at R (recCheckLeftContext 0x402182): a head must then lie strictly
+// after every earlier end (a candidate touching the running end joins its
+// cluster), and the head itself is reported only at a line start.  A class
+// sequence at k > 0 takes nrgrep's esimple order instead (pm_esimple.hip).
 namespace {
 
 constexpr uint32_t REP_G = 512;           // chunks (blocks) of the list (at least)
@@ -601,6 +603,10 @@ __device__ inline bool rep_keep(const RepArgs& a, uint64_t key) {
     }
     if (tv_header(a.tv, s)) return false;
     return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
+}
+
+__device__ inline bool rep_line_start(const RepArgs& a, uint64_t s) {
+    return s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n';
 }
 
 // 64-bit wave shuffle as two 32-bit halves (a (pattern, end) key does not
@@ -670,30 +676,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         if (threadIdx.x == 0) a.bcnt[blockIdx.x] = (uint32_t)own;
         return;
     }
-    if (a.flags & PM_ANCHOR_START) {
-        if (blockIdx.x != 0 || threadIdx.x != 0) return;
-        uint64_t R = 0, pat = ~0ull;
-        for (uint32_t c = 0; c < gridDim.x; ++c) {
-            uint32_t cnt = 0;
-            for (uint64_t i = c * C; i < umin64(total, (uint64_t)(c + 1) * C); ++i) {
-                const uint64_t key = a.keys[i];
-                const uint32_t len = a.lens[i];
-                uint8_t kept = 0;
-                if (rep_valid(a, key, len)) {
-                    if ((key >> 48) != pat) { pat = key >> 48; R = 0; }
-                    const uint64_t s = key & POS_MASK;
-                    if (s >= R && (s == R || s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n')) {
-                        R = s + len;
-                        kept = rep_keep(a, key) ? 1 : 0;
-                    }
-                }
-                a.acc[i] = kept;
-                cnt += kept;
-            }
-            a.bcnt[c] = cnt;
-        }
-        return;
-    }
+    const bool anch = (a.flags & PM_ANCHOR_START) != 0;
     // running maximum of every chunk before this one
     uint64_t carry = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
@@ -735,20 +718,26 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         const uint64_t tile_max = scan[REP_T - 1];
         __syncthreads();
         carry = umax64(carry, tile_max);
-        if (!valid || key < excl) continue;   // not a head: its head's walk writes it
-        // head: reported; walk its cluster
-        uint8_t kept = rep_keep(a, key) ? 1 : 0;
+        // '^': a start is reported only at a line start or exactly at the
+        // resume point R (recCheckLeftContext 0x402170), so a candidate that
+        // touches the previous cluster's end belongs to that cluster
+        if (!valid || (anch ? key <= excl : key < excl)) continue;   // not a head: its head's walk writes it
+        // head: every earlier report ends before it (R < its start)
+        const uint64_t s0 = key & POS_MASK;
+        const bool first = !anch || rep_line_start(a, s0);
+        uint8_t kept = first && rep_keep(a, key) ? 1 : 0;
         a.acc[i] = kept;
         own += kept;
-        uint64_t R = (key & POS_MASK) + len, run = val;
+        uint64_t R = first ? s0 + len : s0 - 1, run = val;   // s0 - 1: below every start of the cluster
         for (uint64_t j = i + 1; j < total; ++j) {
             const uint64_t kj = a.keys[j];
-            if (kj >= run) break;                    // the next head
+            if (anch ? kj > run : kj >= run) break;  // the next head
             const uint32_t lj = a.lens[j];
             kept = 0;
             if (rep_valid(a, kj, lj)) {
-                if ((kj & POS_MASK) >= R) {
-                    R = (kj & POS_MASK) + lj;
+                const uint64_t sj = kj & POS_MASK;
+                if (sj >= R && (!anch || sj == R || rep_line_start(a, sj))) {
+                    R = sj + lj;
                     kept = rep_keep(a, kj) ? 1 : 0;
                 }
                 run = umax64(run, rep_val(kj, lj));
@@ -770,8 +759,8 @@ __global__ __launch_bounds__(REP_T) void k_rep_check(RepArgs a) {   // PM_REPORT
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     uint64_t c = 0, bad = 0;
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
-        c += a.acc[i] == 1;
-        bad += a.acc[i] > 1;
+        c += a.acc[i] & 1;
+        bad += a.acc[i] > 3;
     }
     c = block_sum(c, red);
     bad = block_sum(bad, red);
@@ -798,7 +787,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
-        const uint32_t keep = (i < b1 && a.acc[i]) ? 1u : 0u;
+        const uint32_t keep = (i < b1 && (a.acc[i] & 1)) ? 1u : 0u;   // bit 1: a cluster head (k_es_walk)
         scan[threadIdx.x] = keep;
         __syncthreads();
         for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive sum-scan
@@ -859,7 +848,8 @@ ReportWs report_ws(pm_db* db, uint64_t cap_items) {
 }
 
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
-                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr) {
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr,
+                       const EsPrep* es) {
     // acc is indexed below the list length, which never exceeds the
     // capacity the workspace was sized for (the sort's slot capacities)
     const uint64_t cap_items = std::min<uint64_t>(h->keys_cap / 8, ws.cap);
@@ -888,8 +878,13 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     static const int g_env = getenv("PM_REPORT_G") ? std::max(1, atoi(getenv("PM_REPORT_G"))) : 0;
     const uint32_t G = g_env ? std::min<uint32_t>(REP_G_MAX, (uint32_t)g_env)
                              : (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
-    hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
-    hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
+    if (es && (flags & PM_REPORT_NRGREP)) {
+        // nrgrep's esimple engine: its own candidate order and verify
+        es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, a.acc, a.bcnt, G, a.tv, s);
+    } else {
+        hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
+        hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
+    }
     if (a.debug) hipLaunchKernelGGL(k_rep_check, dim3(G), dim3(REP_T), 0, s, a);
     if (done)
         hipExtLaunchKernelGGL(k_rep_scatter, dim3(G), dim3(REP_T), 0, s, nullptr, done, 0u, a);
@@ -903,13 +898,13 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     h->lens_cap = lc;
 }
 
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr) {
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es) {
     if (total == 0) {
         h->count = 0;
         return;
     }
     const ReportWs ws = report_ws(db, h->keys_cap / 8);
-    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr, hdr);
+    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr, hdr, es);
     uint32_t* hc = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
     HIPCHK(hipMemcpyAsync(hc, ws.count, 4, hipMemcpyDeviceToHost, db->stream));
     HIPCHK(hipStreamSynchronize(db->stream));

@@ -618,7 +618,8 @@ bool report_needed(uint32_t flags, bool cross);
 // Synchronous form: enqueue on db->stream, read the count back, set h->count.
 // hdr: candidates may start on a header line (the simple engine's cross
 // windows) -- only then is every start checked against the header bytes.
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr);
+struct EsPrep;
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es = nullptr);
 // Workspace of one pass (db's current lane), sized for `cap_items` keys;
 // reserve it BEFORE enqueueing the producer of *total (reserve() may move it).
 struct ReportWs {
@@ -630,7 +631,58 @@ struct ReportWs {
     uint64_t cap = 0;
 };
 ReportWs report_ws(pm_db* db, uint64_t cap_items);
+
+// ---------------------------------------------------------------------------
+// nrgrep's esimple engine (pm_esimple.hip): the report of a class sequence
+// at k > 0 (PM_ESIMPLE) -- nrgrep's own candidate order and two-phase verify
+// replayed per cluster of candidate starts
+// ---------------------------------------------------------------------------
+struct EsPlan {               // esimplePreproc 0x415540
+    int type = 0;             // 1 pieces (BNDM), 2 backward window (ABNDM), 3 forward prefix (shift-or)
+    int piece_len = 0;        // type 1
+    int wbeg = 0, wend = 0;   // simpleFindBest's window (types 2, 3)
+    int npieces = 0;          // k + 1 (type 1) or 1
+    int L[PM_MAX_K + 1] = {}; // pattern positions left of each piece / window
+};
+// B: [256][W] position sets of the folded bytes (bit i = position i)
+EsPlan es_plan(const uint64_t* B, int W, int m, int k);
+
+struct EsSlot {               // one pattern of a report (device, uploaded as is)
+    int32_t m, k, errs, type, mpc, wbeg, wend, W, np, anchors, pid, pad;
+    int32_t L[PM_MAX_K + 1];
+    uint64_t test[PM_MAX_K + 1];   // type 1: the piece test mask (0x41384b)
+    uint64_t o_B, o_TL, o_TR;      // word offsets of B / TL[np] / TR[np] ([256][W] each) in the table blob
+};
+struct EsBuild {
+    std::vector<EsSlot> slots;
+    std::vector<uint64_t> tab;
+};
+struct EsUpload {
+    size_t o_slots = 0, o_tab = 0;
+    int nslots = 0;
+    int32_t pid_base = 0;
+};
+struct EsPrep {
+    const EsSlot* slots = nullptr;
+    const uint64_t* tab = nullptr;
+    int nslots = 0;
+    int32_t pid_base = 0;   // slot = pattern id - pid_base
+    int32_t gap_max = 0;    // candidate starts further apart never interact
+};
+// slots get pattern ids pid, in increasing order
+void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, uint32_t flags, int32_t pid);
+void es_upload(const EsBuild& b, Upload& up, EsUpload& u);
+int32_t es_gap(const EsBuild& b);
+EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max);
+// k_es_heads + k_es_walk on s: rewrites keys/lens in place and sets acc
+// (bit 0 = reported) and the per-chunk counts bcnt for k_rep_scatter
+void es_launch(const EsPrep& P, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s);
+
+// es (optional): the list holds a class sequence's candidate starts at
+// k > 0 and the selection is nrgrep's esimple engine (pm_esimple.hip)
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
-                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr);
+                       uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr,
+                       const EsPrep* es = nullptr);
 
 }  // namespace pm

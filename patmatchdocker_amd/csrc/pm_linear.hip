@@ -1439,6 +1439,24 @@ uint8_t* batch_tables(pm_db* db, const BatchIndex& bi, const std::string& sig) {
     return d;
 }
 
+// k > 0 with nrgrep's report: every pattern of the batch is a class
+// sequence searched by nrgrep's esimple engine; its plan and tables
+bool linear_esimple(int n_patterns, const int32_t* lengths, const uint8_t* pos_class, const uint32_t* class_bytes,
+                    int k, uint32_t flags, EsBuild& esb) {
+    if (k == 0 || !(flags & PM_REPORT_NRGREP)) return false;
+    std::vector<uint64_t> B(256);
+    for (int p = 0; p < n_patterns; ++p) {
+        std::fill(B.begin(), B.end(), 0ull);
+        for (int j = 0; j < lengths[p]; ++j) {
+            const uint32_t* cb = class_bytes + 8 * pos_class[64 * p + j];
+            for (int c = 0; c < 256; ++c)
+                if ((cb[c >> 5] >> (c & 31)) & 1) B[c] |= 1ull << j;
+        }
+        es_add_slot(esb, B.data(), 1, lengths[p], k, PM_ERR_SUB, flags, p);
+    }
+    return true;
+}
+
 // pm_scan_linear on the byte layout (synchronous; the pipelined entry point
 // runs it too)
 void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const uint8_t* pos_class, int n_classes,
@@ -1452,7 +1470,12 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
     const size_t o_len = up.add(lengths, (size_t)n_patterns * 4);
     const size_t o_pc = up.add(pos_class, (size_t)n_patterns * 64);
     const size_t o_any = up.add(class_is_any, (size_t)n_classes);
+    EsBuild esb;
+    EsUpload esu;
+    const bool esimple = linear_esimple(n_patterns, lengths, pos_class, class_bytes, k, flags, esb);
+    if (esimple) es_upload(esb, up, esu);
     uint8_t* d_up = up.commit(db);
+    const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     ByteLinArgs a{db->bytes, db->bytes_raw, db->n, d_up + o_pc, reinterpret_cast<const int32_t*>(d_up + o_len),
                   d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), n_patterns, k, cross ? 1 : 0, Sink{}};
     uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
@@ -1482,7 +1505,7 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
                            reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
         HIPCHK(hipGetLastError());
     }
-    if (report_needed(flags, cross)) report_sync(db, h, flags, total, cross);
+    if (report_needed(flags, cross)) report_sync(db, h, flags, total, cross, esimple ? &esp : nullptr);
     hits_ready(db, h);
     *out = h;
 }
@@ -1503,7 +1526,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
             for (int j = 0; j < lengths[p]; ++j) require(pos_class[64 * p + j] < n_classes, "class id out of range");
         }
-        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS)) == 0, "bad flags");
+        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_ESIMPLE)) ==
+                    0,
+                "bad flags");
         DeviceGuard g(db->device);
         hipStream_t s = db->stream;
         const bool jit = use_jit(db);
@@ -1556,6 +1581,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         const size_t o_acgt = up.add(class_acgt, (size_t)n_classes);
         const size_t o_any = up.add(class_is_any, (size_t)n_classes);
         const size_t o_jsel = up.add(jsel.data(), jsel.size());
+        // k > 0: nrgrep's esimple engine decides which overlapping window
+        // is printed (pm_esimple.hip)
+        EsBuild esb;
+        EsUpload esu;
+        const bool esimple = linear_esimple(n_patterns, lengths, pos_class, class_bytes, k, flags, esb);
+        if (esimple) es_upload(esb, up, esu);
         // a large k = 0 batch: the q-gram filter (pm_batch.hip), one pass for
         // the whole batch (PM_BATCH=0 off; PM_BATCH_MIN: smallest batch, 16)
         static const int batch_min = getenv("PM_BATCH_MIN") ? std::max(1, atoi(getenv("PM_BATCH_MIN"))) : 16;
@@ -1604,6 +1635,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         if (offload) switch_lane(db);
         lane_begin(db);
         uint8_t* d_up = up.commit(db);
+        const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
+        const EsPrep* es = esimple ? &esp : nullptr;
 
         SinkBuffers sb;
         std::vector<uint32_t> counts;
@@ -1884,7 +1917,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                                      pd->counts_h, xs, ws.total, /*bind_ready=*/false);
                         HIPCHK(hipEventCreate(&spec->ready));
                         report_enqueue_ws(db, spec, flags, ws, true, 0, pd->counts_h + sb.nbins + 1, xs, spec->ready,
-                                          cross);
+                                          cross, es);
                         pd->reported = true;
                     } else {
                         spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len),
@@ -1997,7 +2030,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
             HIPCHK(hipGetLastError());
         }
-        if (report) report_sync(db, h, flags, total, cross);
+        if (report) report_sync(db, h, flags, total, cross, es);
         // no host sync here: consumers wait on h->ready (pm_hits_copy*,
         // pm_hits_device, pm_hits_destroy)
         hits_ready(db, h);

@@ -432,12 +432,26 @@ void launch_nfa_verify(int K, int W, const NfaArgs& a, uint32_t blocks, hipStrea
 namespace pm {
 namespace {
 
+// a plain class sequence: first = {0}, last = {m-1}, follow(i) = {i+1}
+bool a_shift_only(int m, int W, const uint64_t* first, const uint64_t* last, const uint64_t* follow) {
+    bool ok = true;
+    for (int q = 0; q < W; ++q) {
+        ok = ok && first[q] == (q == 0 ? 1ull : 0ull);
+        ok = ok && last[q] == (q == (m - 1) / 64 ? 1ull << ((m - 1) % 64) : 0ull);
+    }
+    for (int i = 0; i < m && ok; ++i)
+        for (int q = 0; q < W; ++q)
+            ok = ok && follow[(size_t)i * W + q] == ((i + 1 < m && (i + 1) / 64 == q) ? 1ull << ((i + 1) % 64) : 0ull);
+    return ok;
+}
+
 // The scan behind pm_scan_nfa_errs / pm_scan_nfa_wide: position sets of W
 // words (W = ceil(m / 64)).
 void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t* follow, const uint64_t* first,
               const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
               pm_hits** out) {
-    require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES)) == 0,
+    require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES |
+                       PM_ESIMPLE)) == 0,
             "bad flags");
     require(db != nullptr, "db is NULL");
     std::lock_guard<std::recursive_mutex> lk(db->mu);
@@ -458,6 +472,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (k == 0) errs = PM_ERR_SUB;   // no errors: the type letters are irrelevant
     const bool cross = (flags & PM_CROSS_LINES) != 0;
     require(!cross || (k == 0 && !unbounded), "PM_CROSS_LINES is nrgrep's simple engine: k = 0, bounded");
+    // PM_ESIMPLE: a class sequence at k > 0 reported as nrgrep's esimple
+    // engine does (pm_esimple.hip); its walk computes the ends itself
+    const bool esimple = (flags & PM_ESIMPLE) && k > 0 && (flags & PM_REPORT_NRGREP);
     // a match must consume a pattern position (pm_oracle.c reports
     // non-empty matches only): with deletions that needs min_len > k
     require(!(errs & PM_ERR_DEL) || min_len > k,
@@ -521,7 +538,15 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     const size_t o_f = up.add(tf.data(), tf.size() * 8);
     const size_t o_p = up.add(tp.data(), tp.size() * 8);
     const size_t o_b = up.add(bm.data(), bm.size() * 8);
+    EsBuild esb;
+    EsUpload esu;
+    if (esimple) {
+        require(a_shift_only(m, W, first, last, follow), "PM_ESIMPLE needs a class sequence");
+        es_add_slot(esb, byte_mask, W, m, k, errs, (uint32_t)flags, pattern_id);
+        es_upload(esb, up, esu);
+    }
     uint8_t* d_up = up.commit(db);
+    const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
 
     NfaArgs a{};
     a.nuc = nuc_view(db);
@@ -538,16 +563,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     }
     a.nt = nt;
     a.halo = unbounded ? 0 : max_len + ins_extra - 1;
-    // a plain class sequence: first = {0}, last = {m-1}, follow(i) = {i+1}
-    a.shift_only = true;
-    for (int q = 0; q < W; ++q) {
-        a.shift_only = a.shift_only && first[q] == (q == 0 ? 1ull : 0ull);
-        a.shift_only = a.shift_only && last[q] == (q == (m - 1) / 64 ? 1ull << ((m - 1) % 64) : 0ull);
-    }
-    for (int i = 0; i < m && a.shift_only; ++i)
-        for (int q = 0; q < W; ++q)
-            a.shift_only = a.shift_only && follow[(size_t)i * W + q] ==
-                                               ((i + 1 < m && (i + 1) / 64 == q) ? 1ull << ((i + 1) % 64) : 0ull);
+    a.shift_only = a_shift_only(m, W, first, last, follow);
     a.errs = errs;
     a.k = k;
     for (int j = 0; j <= k; ++j)
@@ -643,7 +659,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     }
     double kms = ev.ms() + carry_ms;
     pm_hits* h = sink_to_hits(db, sb, counts, total);
-    if (total) {
+    if (total && !esimple) {
         a.starts = h->keys;
         a.nstarts = total;
         a.lens = h->lens;
@@ -662,7 +678,12 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
     // header line, the pass only selects what nrgrep reports; the simple
     // engine (cross) also drops the windows starting on a header line
-    if (report_needed((uint32_t)flags, cross)) report_sync(db, h, (uint32_t)flags, total, cross);
+    if (esimple) {
+        // the walk replaces the lengths; until it runs they are unset
+        report_sync(db, h, (uint32_t)flags, total, false, &esp);
+    } else if (report_needed((uint32_t)flags, cross)) {
+        report_sync(db, h, (uint32_t)flags, total, cross);
+    }
     HIPCHK(hipStreamSynchronize(s));
     hits_ready(db, h);
     *out = h;

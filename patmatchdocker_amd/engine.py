@@ -282,6 +282,19 @@ def ids_jit_compile(prog: Program, k: int, types: str = "ids") -> int:
     return nbytes.value
 
 
+def esimple_plan(prog: Program, k: int) -> dict:
+    """The scan plan nrgrep's esimplePreproc derives for ``prog`` at ``k``
+    errors (pm_esimple_plan, host only): ``type`` 1 = k+1 pieces of
+    ``piece_len`` (BNDM), 2 = the ``window`` backward (ABNDM), 3 = the prefix
+    forward (shift-or); ``L`` = pattern positions left of each piece."""
+    w = nfa_words(prog.m)
+    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
+    out = (ctypes.c_int32 * (6 + _lib.PM_MAX_K))()
+    check(_lib.load().pm_esimple_plan(prog.m, w, bm.ctypes.data, k, out))
+    return {"type": out[0], "piece_len": out[1], "window": (out[2], out[3]),
+            "L": [out[5 + i] for i in range(out[4])]}
+
+
 def kernel_ms(handle) -> float:
     ms = ctypes.c_double()
     check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))
@@ -319,6 +332,8 @@ def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0,
     flags = report_flags(prog) if flags is None else flags
     if k == 0 and prog.linear and any(10 in c for c in prog.classes):
         flags |= _lib.PM_CROSS_LINES
+    if k > 0 and prog.linear and prog.kind == "simple":
+        flags |= _lib.PM_ESIMPLE   # nrgrep's esimple engine decides the report
     out = ctypes.c_void_p()
     check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                        last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,

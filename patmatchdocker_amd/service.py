@@ -144,6 +144,7 @@ class _DatabaseCache:
 
 
 DATABASES = _DatabaseCache()
+_SHARD_LOCK = threading.Lock()   # the multi-rank path: one request's collectives at a time
 
 
 # ---------------------------------------------------------------------------
@@ -192,13 +193,26 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
     if world > 1:
         # one process per GPU (torchrun): every rank scans its record-aligned
         # piece of the file, the reports are joined across the cuts and
-        # gathered, every rank returns the whole output
+        # gathered, every rank returns the whole output.  Collectives must
+        # pair up across ranks: one request at a time per process
+        # (_SHARD_LOCK), every rank serving the same request sequence
+        # (INTEGRATION.md §2); a rank that cannot open its piece still takes
+        # part in the first collective, so the others fail instead of hanging
         from . import shards
         device = int(os.environ.get("LOCAL_RANK", "0"))
-        with DATABASES.lease(datafile, device, shard=(world, rank)) as piece:
-            results = shards.scan_sharded(piece, progs, k=k, types=types)
-            for slot, prog, (beg, end) in zip(slots, progs, results):
-                outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(piece, beg, end)
+        with _SHARD_LOCK:
+            lease = DATABASES.lease(datafile, device, shard=(world, rank))
+            try:
+                piece = lease.__enter__()
+            except Exception:
+                shards.agree(False)
+                raise
+            try:
+                results = shards.scan_sharded(piece, progs, k=k, types=types)
+                for slot, prog, (beg, end) in zip(slots, progs, results):
+                    outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(piece, beg, end)
+            finally:
+                lease.__exit__(None, None, None)
         return outputs
     with DATABASES.lease(datafile) as db:
         results, _ = engine.scan(db, progs, k=k, types=types)

@@ -26,6 +26,7 @@ a cut), so the result equals the single-process scan byte for byte.
 
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -50,41 +51,78 @@ def to_global(keys: torch.Tensor, offset: int) -> torch.Tensor:
     return keys + offset          # the pattern field never overflows (beg + offset < 2^48)
 
 
-def gather_hits(keys: torch.Tensor, lens: torch.Tensor, group=None, dst: Optional[int] = 0
-                ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+def gather_hits(keys: torch.Tensor, lens: Optional[torch.Tensor], group=None, dst: Optional[int] = 0,
+                fixed_len: Optional[Sequence[int]] = None) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
     """All ranks' (keys, lens) -> sorted (keys, lens) on rank ``dst``
     (``dst=None``: on every rank).
 
-    Works with any backend (RCCL for device tensors, gloo for CPU tensors).
-    Non-destination ranks return None.
+    Byte budget per query: one int64 count per rank (all_gather), then the
+    count-padded key vector of every rank moves to ``dst`` only
+    (``dist.gather``: (world - 1) x width x 8 bytes into dst over xGMI; with
+    ``dst=None`` an all_gather sends it to every rank).  ``fixed_len[p]``:
+    every hit of pattern p has that length (a class sequence searched with
+    substitutions), so the length vector is not sent at all and is rebuilt
+    from the pattern field.  Works with any backend (RCCL for device tensors,
+    gloo for CPU tensors).  Non-destination ranks return None.
     """
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        if lens is None:
+            lens = _fixed_lens(keys, fixed_len)
         return keys, lens          # one rank: the engine already sorted them
     if dist.get_backend(group) == "gloo" and keys.is_cuda:   # gloo gathers host tensors
-        out = gather_hits(keys.cpu(), lens.cpu(), group, dst)
-        return None if out is None else (out[0].to(keys.device), out[1].to(lens.device))
+        out = gather_hits(keys.cpu(), None if lens is None else lens.cpu(), group, dst, fixed_len)
+        return None if out is None else (out[0].to(keys.device), out[1].to(keys.device))
     world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    send_lens = fixed_len is None
+    if send_lens and lens is None:
+        raise ValueError("lens are needed unless fixed_len is given")
     count = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
     counts = [torch.zeros_like(count) for _ in range(world)]
     dist.all_gather(counts, count, group=group)
     sizes = [int(c.item()) for c in counts]
     width = max(max(sizes), 1)
     pk = torch.zeros(width, dtype=keys.dtype, device=keys.device)
-    pl = torch.zeros(width, dtype=lens.dtype, device=lens.device)
     pk[:keys.numel()] = keys
-    pl[:lens.numel()] = lens
-    all_k = [torch.empty_like(pk) for _ in range(world)]
-    all_l = [torch.empty_like(pl) for _ in range(world)]
-    dist.all_gather(all_k, pk, group=group)
-    dist.all_gather(all_l, pl, group=group)
-    if dst is not None and dist.get_rank(group) != dst:
-        return None
+    if send_lens:
+        pl = torch.zeros(width, dtype=lens.dtype, device=lens.device)
+        pl[:lens.numel()] = lens
+    if dst is None:
+        all_k = [torch.empty_like(pk) for _ in range(world)]
+        dist.all_gather(all_k, pk, group=group)
+        if send_lens:
+            all_l = [torch.empty_like(pl) for _ in range(world)]
+            dist.all_gather(all_l, pl, group=group)
+    else:
+        all_k = [torch.empty_like(pk) for _ in range(world)] if me == dst else None
+        dist.gather(pk, all_k, dst=dst, group=group)
+        if send_lens:
+            all_l = [torch.empty_like(pl) for _ in range(world)] if me == dst else None
+            dist.gather(pl, all_l, dst=dst, group=group)
+        if me != dst:
+            return None
     parts = [t[:n] for t, n in zip(all_k, sizes)]
     k = torch.cat(parts)
-    ln = torch.cat([t[:n] for t, n in zip(all_l, sizes)])
+    ln = torch.cat([t[:n] for t, n in zip(all_l, sizes)]) if send_lens else _fixed_lens(k, fixed_len)
     if k.numel() == 0:
         return k, ln
     return _merge(parts, k, ln)
+
+
+def _fixed_lens(keys: torch.Tensor, fixed_len: Optional[Sequence[int]]) -> torch.Tensor:
+    table = torch.tensor(list(fixed_len), dtype=torch.int32, device=keys.device)
+    return table[keys >> POS_BITS] if keys.numel() else torch.zeros(0, dtype=torch.int32, device=keys.device)
+
+
+def agree(ok: bool, group=None) -> bool:
+    """True on every rank iff ``ok`` on every rank (one all_reduce MIN): a
+    rank that failed locally makes the others fail instead of leaving them
+    blocked in the next collective."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_coll_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
 
 def _merge(parts, k, ln):
@@ -134,8 +172,18 @@ def hits_to_tensors(hits_handle, device: torch.device):
 # real FASTA files: record-aligned pieces, one per rank
 # ---------------------------------------------------------------------------
 
-HALO = 4096   # bytes held past a piece's end: >= any window that can cross a cut (<= 64 positions)
+# bytes held past a piece's end: >= any window that can cross a cut (the
+# simple engine's cross-line windows, up to PM_MAX_POSITIONS positions)
+HALO = 4096
 _SPACE = np.frombuffer(b" \t\n\r\f\x0b", dtype=np.uint8)
+
+
+def _check_halo():
+    from . import _lib
+    assert HALO >= _lib.PM_MAX_POSITIONS, "HALO must cover the longest automaton window"
+
+
+_check_halo()
 
 
 def header_lines(data: bytes) -> Tuple[np.ndarray, np.ndarray]:
@@ -158,17 +206,42 @@ def header_lines(data: bytes) -> Tuple[np.ndarray, np.ndarray]:
     return gt.astype(np.int64), ends
 
 
-def split_fasta(data: bytes, world: int) -> List[Tuple[int, int]]:
-    """``world`` contiguous byte ranges covering ``data``, cut only at header
-    lines, of about equal size (a range may be empty: fewer records than
-    ranks)."""
+_NAME_STOP = (b" ", b"\t", b"\n", b"\r", b"\f", b"\x0b")
+
+
+def _next_header(data, target: int) -> int:
+    """The first header-line start at or after ``target`` ('>' at a line
+    start, then a non-space, as header_lines), or len(data).  Reads only
+    from target - 1 on, so on a memory map it touches the pages around the
+    cut alone."""
     n = len(data)
-    starts, _ = header_lines(data)
+
+    def named(h):
+        return h + 1 < n and data[h + 1:h + 2] not in _NAME_STOP
+
+    if target <= 0:
+        if n and data[0:1] == b">" and named(0):
+            return 0
+        target = 1
+    pos = target - 1
+    while True:
+        q = data.find(b"\n>", pos)
+        if q < 0:
+            return n
+        if named(q + 1):
+            return q + 1
+        pos = q + 1
+
+
+def split_fasta(data, world: int) -> List[Tuple[int, int]]:
+    """``world`` contiguous byte ranges covering ``data`` (bytes or a memory
+    map), cut only at header lines, of about equal size (a range may be
+    empty: fewer records than ranks).  Cut i is the first header line at or
+    after n*i/world, found by scanning forward from there."""
+    n = len(data)
     cuts = [0]
     for i in range(1, world):
-        j = int(np.searchsorted(starts, (n * i) // world))
-        cut = int(starts[j]) if j < starts.size else n
-        cuts.append(max(cut, cuts[-1]))
+        cuts.append(max(_next_header(data, (n * i) // world), cuts[-1]))
     cuts.append(n)
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
@@ -186,28 +259,33 @@ def drop_header_starts(beg: np.ndarray, end: np.ndarray, hs: np.ndarray, he: np.
 class ShardedDatabase:
     """Rank ``rank``'s piece of a FASTA file (``split_fasta``) in HBM, with
     ``HALO`` bytes of the next piece so windows that start in the piece are
-    evaluated on the file's own bytes.  ``raw`` is the whole file (hit text
-    and line-start checks); hit offsets are file offsets."""
+    evaluated on the file's own bytes.  ``raw`` is the whole file as bytes
+    or, from :meth:`from_file`, a read-only memory map: a rank reads only its
+    piece (+ halo) and the pages around the cuts, and the hit text of any
+    piece is sliced from the map on demand.  Hit offsets are file offsets."""
 
-    def __init__(self, data: bytes, world: int, rank: int, device: int = 0, alphabet: Optional[str] = None,
+    def __init__(self, data, world: int, rank: int, device: int = 0, alphabet: Optional[str] = None,
                  halo: int = HALO, open_db: bool = True):
         self.raw = data
         self.world, self.rank = world, rank
         self.ranges = split_fasta(data, world)
         self.beg, self.end = self.ranges[rank]
         self.stop = min(len(data), self.end + halo) if self.end > self.beg else self.end
-        hs, he = header_lines(data[self.beg:self.end])
+        local = bytes(data[self.beg:self.stop])
+        hs, he = header_lines(local[:self.end - self.beg])
         self.headers = (hs, he)
         self.db = None
         if open_db and self.stop > self.beg:
             from . import engine
-            self.db = engine.SequenceDatabase.from_bytes(data[self.beg:self.stop],
-                                                         alphabet or engine.choose_alphabet(data), device)
+            self.db = engine.SequenceDatabase.from_bytes(local, alphabet or engine.choose_alphabet(local), device)
 
     @classmethod
-    def from_file(cls, path: str, world: int, rank: int, device: int = 0) -> "ShardedDatabase":
+    def from_file(cls, path: str, world: int, rank: int, device: int = 0, open_db: bool = True) -> "ShardedDatabase":
+        import mmap
         with open(path, "rb") as fh:
-            return cls(fh.read(), world, rank, device)
+            size = os.fstat(fh.fileno()).st_size
+            data = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_READ) if size else b""
+        return cls(data, world, rank, device, open_db=open_db)
 
     def __len__(self):
         return self.end - self.beg
@@ -279,20 +357,32 @@ def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str
                  scanner=None) -> List[Tuple[np.ndarray, np.ndarray]]:
     """Every rank scans its piece; returns, on every rank, [(beg, end) per
     program] in file offsets -- equal to the single-process scan of the
-    whole file (what nrgrep_coords reports, header-line starts dropped)."""
+    whole file (what nrgrep_coords reports, header-line starts dropped).
+
+    Collective: every rank of ``group`` must call it with the same programs,
+    in the same order as its other collective calls.  A rank whose local
+    scan raises still takes part in the first collective (``agree``), so the
+    other ranks raise too instead of blocking."""
     scanner = scanner or piece.scanner()
     P = len(progs)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     n_local = len(piece)
     empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64))
-    if n_local:
-        chains = []
-        for b, e in scanner.reported(progs, k, types):
-            b, e = np.asarray(b, dtype=np.int64), np.asarray(e, dtype=np.int64)
-            keep = b < n_local
-            chains.append((b[keep], e[keep]))
-    else:
-        chains = [empty] * P
+    failure = None
+    chains = [empty] * P
+    try:
+        if n_local:
+            chains = []
+            for b, e in scanner.reported(progs, k, types):
+                b, e = np.asarray(b, dtype=np.int64), np.asarray(e, dtype=np.int64)
+                keep = b < n_local
+                chains.append((b[keep], e[keep]))
+    except Exception as exc:   # every rank takes part in the agreement below
+        failure = exc
+    if not agree(failure is None, group):
+        if failure is not None:
+            raise failure
+        raise RuntimeError("scan_sharded: another rank's scan failed")
     if world > 1:
         # the chain state leaving each piece: the end of its last report
         dev = _coll_device(group)

@@ -10,7 +10,8 @@ The rules were read from the disassembly of the reference binary
   headers, line breaks, N runs, lower case and IUPAC letters;
 * the report rule (first found wins, resume at the match end) against a
   direct Python restatement over the candidate list, for line-bounded
-  patterns and k > 0;
+  patterns and k > 0 (the leftmost-start rule; a class sequence at k > 0
+  runs nrgrep's esimple engine instead, tests/test_nrgrep_esimple.py);
 * anchors, '.' accepting the delimiter, reversed ranges.
 """
 import json
@@ -91,7 +92,8 @@ def test_report_rule_on_candidates(oracle_mod, seed):
             if k == 0 and prog.linear:
                 continue   # the simple engine is not line-bounded (tested above)
             cands = oracle_mod.scan(text, prog, k, t)
-            assert oracle_mod.scan_reported(text, prog, k, t) == _greedy(cands, text), (p, k, t)
+            got = oracle_mod.scan_reported(text, prog, k, t, report="leftmost")
+            assert got == _greedy(cands, text), (p, k, t)
 
 
 def test_overlaps_are_not_reported(oracle_mod):

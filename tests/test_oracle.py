@@ -92,8 +92,9 @@ def test_oracle_threaded_scan_on_decoded_layout(oracle_mod):
 
 @pytest.mark.parametrize("seed", range(3))
 def test_shiftadd_cpu_scan_equals_reported_oracle(oracle_mod, seed):
-    """The bench's bit-parallel CPU baseline (pm_cpuscan.c, Shift-Add) reports
-    exactly what pmo_scan2 reports for class sequences with substitutions."""
+    """The bit-parallel Shift-Add CPU scan (pm_cpuscan.c) reports exactly what
+    pmo_scan2's leftmost-start rule reports for class sequences with
+    substitutions (nrgrep's own order: test_nrgrep_esimple.py)."""
     text = dna_fasta(seed + 60, n_records=5, max_len=4000, width=(70 if seed == 1 else None))
     for pat in ["TGCTGASTCAGCANW", "TATAWAWR", "GAATTC", "NNGCNN", "AAAA", "TANNNNTA"]:
         for strand in ("-n", "-c"):
@@ -102,7 +103,8 @@ def test_shiftadd_cpu_scan_equals_reported_oracle(oracle_mod, seed):
             for k in (0, 1, 2, 3):
                 if k >= prog.m:
                     continue
-                want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+                want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True,
+                                                report="leftmost" if k else "nrgrep")
                 assert oracle_mod.shiftadd_scan(text, prog, k, skip_headers=True) == want, (pat, k)
                 assert oracle_mod.shiftadd_threads(text, prog, k, skip_headers=True, threads=3) == want, (pat, k)
 
@@ -116,13 +118,15 @@ def test_python_reported_oracle_equals_c_oracle(oracle_mod, seed):
         prog = compile_pattern(p)
         for k, t in [(0, "s"), (1, "s"), (1, "ids"), (2, "id"), (2, "s")]:
             want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True, simple=False)
+            if k and oracle_mod.is_esimple(prog):
+                want = oracle_mod.scan_esimple(text, prog, k, t, skip_headers=True)
             assert oracle_mod.scan_py_reported(text, prog, k, t, skip_headers=True) == want, (p, k, t)
 
 
 @pytest.mark.parametrize("seed", range(4))
 def test_ids_cpu_scan_equals_reported_oracle(oracle_mod, seed):
-    """The bench's `-k <k>ids` CPU baseline (pmc_ids_scan, bit-parallel)
-    reports exactly what the oracle does."""
+    """The bit-parallel `-k <k>ids` CPU scan (pmc_ids_scan) reports exactly
+    what the oracle's leftmost-start rule does."""
     from tests.test_gpu_report import repeat_fasta
     text = dna_fasta(seed + 40, n_records=4, max_len=4000) if seed % 2 else repeat_fasta(seed + 40, 3, 1000, 4000)
     for pat in ["TGCTGASTCAGCANW", "TATAWAWR", "GAATTC", "AWA", "CAACAACAA", "TANNA"]:
@@ -130,6 +134,6 @@ def test_ids_cpu_scan_equals_reported_oracle(oracle_mod, seed):
         for k, t in [(1, "ids"), (2, "ids"), (2, "i"), (1, "d"), (3, "ds"), (2, "is"), (1, "s")]:
             if "d" in t and k >= prog.m:
                 continue
-            want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True)
+            want = oracle_mod.scan_reported(text, prog, k, t, skip_headers=True, report="leftmost")
             assert oracle_mod.ids_scan(text, prog, k, t, skip_headers=True) == want, (pat, k, t)
             assert oracle_mod.ids_threads(text, prog, k, t, skip_headers=True, threads=3) == want, (pat, k, t)

@@ -139,8 +139,9 @@ def _service_worker(rank, world, port, path, option, q):
     try:
         from patmatchdocker_amd import service
         # the pieces are scanned by the oracle (no GPU here)
+        real = shards.ShardedDatabase.from_file   # the memory-mapped reader, no HBM upload
         shards.ShardedDatabase.from_file = classmethod(
-            lambda cls, p, w, r, device=0: cls(open(p, "rb").read(), w, r, device, open_db=False))
+            lambda cls, p, w, r, device=0: real(p, w, r, device, open_db=False))
         shards.ShardedDatabase.scanner = lambda self: OracleScanner(self)
         q.put((rank, service.search_output(SERVICE_PATTERNS, option, path)))
     finally:

@@ -76,11 +76,10 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
     return x;
 }
 
-// STRIDE 2: only every other position is probed (PAR: the parity of the
-// probed block offsets i, so that o_max + i is even); every pattern is then
-// indexed by two consecutive pieces (o_p and o_p + 1), one of which starts at
-// an even position for any window -- half the LDS probes per position.
-template <int STRIDE, int PAR>
+// Every position is probed.  (Probing every other position with two
+// consecutive pieces per pattern measured: scan 3.0 -> 2.16 ms, but the two
+// pieces' expansions raise the candidates and verify 2.08 -> 2.74 ms, 10.6
+// vs 9.9 ms per configs[4] step; round 2.)
 __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
     __shared__ uint32_t s_tab[BQ_TABLE_WORDS];   // 128 KB: one workgroup per CU
     for (uint32_t i = threadIdx.x; i < BQ_TABLE_WORDS; i += BATCH_THREADS) s_tab[i] = a.table[i];
@@ -141,7 +140,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             const uint32_t d[3] = {alignb(c1, c0, sh), alignb(c2, c1, sh), alignb(c3, c2, sh)};
             uint32_t acc = 0;
 #pragma unroll
-            for (int i = PAR; i < 32; i += STRIDE) {
+            for (int i = 0; i < 32; ++i) {
                 const int b0 = 2 * i, b3 = 2 * i + 3;
                 const uint32_t code = (b0 & 31) ? alignb(d[(b0 >> 5) + 1], d[b0 >> 5], b0 & 31) : d[b0 >> 5];
                 // code bits 5..19 (the table word) at bits 2..16: its LDS byte address
@@ -153,12 +152,12 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             }
             // candidates: probe i -> 16-byte entry {tile, lane << 11 | s << 6
             // | i, the 32 bases from position i of the block}
-            uint32_t m = STRIDE == 2 ? acc >> 16 : acc;   // stride 2: probe i = 2k + PAR at bit k
+            uint32_t m = acc;
             while (__builtin_amdgcn_ballot_w64(m != 0u)) {
                 const bool has = m != 0u;
                 uint4 e = make_uint4(0u, 0u, 0u, 0u);
                 if (has) {
-                    const uint32_t i = STRIDE == 2 ? 2u * (uint32_t)__builtin_ctz(m) + PAR : (uint32_t)__builtin_ctz(m);
+                    const uint32_t i = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
                     const bool up = i >= 16u;
                     const uint32_t r = (2u * i) & 31u;
@@ -323,10 +322,9 @@ __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
     // the file's first starts st < o_max - o_p: probed by no block
     for (uint32_t q = tid; q < (uint32_t)a.P * a.omax; q += nth) {
         const uint32_t p = q / a.omax, st = q % a.omax;
-        // the position this start is probed at (stride 2: the even one of
-        // its two pieces); probes start at o_max
+        // the position this start is probed at; probes start at o_max
         const uint32_t y = st + a.popt[p];
-        if ((a.stride == 2 ? y + (y & 1u) : y) >= a.omax) continue;
+        if (y >= a.omax) continue;
         const int len = a.lengths[p];
         if ((uint64_t)st + len > a.n) continue;
         const uint4 mk = a.pmask[p];
@@ -360,15 +358,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
     struct Ent {
         uint32_t code, p, op;
     };
-    // PM_BATCH_STRIDE=2 (experiment; every pattern needs room for two
-    // pieces): every pattern indexed by two consecutive pieces, every other
-    // position probed.  Measured on configs[4]: scan 3.0 -> 2.16 ms, but the
-    // two pieces' expansions raise the candidates and verify 2.08 -> 2.74 ms
-    // (10.6 vs 9.9 ms per step), so every position is probed by default.
-    bi.stride = getenv("PM_BATCH_STRIDE") && atoi(getenv("PM_BATCH_STRIDE")) == 2 ? 2 : 1;
-    for (int p = 0; p < P; ++p)
-        if (lengths[p] < BQ + 1) bi.stride = 1;
-    const int npieces = (int)bi.stride;
+    const int npieces = 1;   // one indexed piece per pattern
     std::vector<Ent> ents;
     std::vector<uint32_t> plen(P, 0);
     bi.popt.assign(P, 0);
@@ -449,8 +439,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
                   hipEvent_t ev_a, hipEvent_t ev_b) {
     // the kernel's own dispatch timestamps (no marker packets)
-    auto kern = va.stride == 1 ? k_batch_scan<1, 0> : (sa.omax & 1u) ? k_batch_scan<2, 1> : k_batch_scan<2, 0>;
-    hipExtLaunchKernelGGL(kern, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
+    hipExtLaunchKernelGGL(k_batch_scan, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_batch_verify, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());

@@ -875,9 +875,7 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     (void)cap_items;   // every acc entry below the list length is written by k_rep_walk (no memset)
     // chunks: REP_G, more for long lists (a big batch's tens of millions of
     // candidates: every block's serial tile scans then stay short)
-    static const int g_env = getenv("PM_REPORT_G") ? std::max(1, atoi(getenv("PM_REPORT_G"))) : 0;
-    const uint32_t G = g_env ? std::min<uint32_t>(REP_G_MAX, (uint32_t)g_env)
-                             : (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
+    const uint32_t G = (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
     if (es && (flags & PM_REPORT_NRGREP)) {
         // nrgrep's esimple engine: its own candidate order and verify
         es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, a.acc, a.bcnt, G, a.tv, s);

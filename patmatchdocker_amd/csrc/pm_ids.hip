@@ -250,16 +250,9 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     std::ostringstream o;
     o << kIdsCommon;
     o << "#define WU " << WU << "\n";
-    // PM_IDS_LDS=1 (experiment): copy each tile into LDS by LDS-DMA first
-    // (one HBM round trip per tile; 2 waves/SIMD for the LDS)
-    const bool lds = env_flag("PM_IDS_LDS", false);
-    sg << (lds ? ":lds" : ":dir");
-    if (lds) o << "#define IDS_LDS 1\n";
-    // workgroups per CU the register budget is cut for (PM_IDS_WG, default 4:
-    // <= 128 VGPRs, 4 waves per SIMD)
-    const int wg = getenv("PM_IDS_WG") ? std::max(1, atoi(getenv("PM_IDS_WG"))) : 4;
-    o << "#define IDS_WG " << wg << "\n";
-    sg << ":wg" << wg;
+    // 4 workgroups per CU: <= 128 VGPRs, 4 waves per SIMD (staging each
+    // tile in LDS by LDS-DMA first measured no faster, round 2)
+    o << "#define IDS_WG 4\n";
     *sig = sg.str();
     o << R"IDS(
 // One wave per tile; lane c owns stream column c (logical words 32c ..
@@ -270,17 +263,10 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
 // lane r < 32 holds row r's 64 flag bits (one load per tile), a step reads
 // its row's with v_readlane.
 extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) {   // IDS_WG workgroups per CU
-#ifdef IDS_LDS
-    __shared__ __attribute__((aligned(1024))) uint4 s_tile[4][(TILE_WORDS / 2 + 63) / 64 * 64];
-#endif
     const u32 col = threadIdx.x & 63;
     const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u64 wave = (u64)blockIdx.x * 4u + wid, nwaves = gridDim.x * 4ull;
     const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
-#ifdef IDS_LDS
-    const uint2* const lt = reinterpret_cast<const uint2*>(s_tile[wid]);
-    const u32 lds_base = (u32)reinterpret_cast<u64>(s_tile[wid]);   // LDS byte address
-#endif
     for (u64 tile = wave; tile < a.ntiles; tile += nwaves) {
         const u64 base = tile * TILE_WORDS;   // a multiple of 32: rows are sbflag word pairs
         const uint2* tb = a.hl + base;
@@ -291,24 +277,6 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
         }
         const u32* hf = a.sbflag + ((base + STREAM) >> 5);
         const u64 halof = (u64)hf[0] | ((u64)hf[1] << 32);   // halo words 2048 .. 2111
-#ifdef IDS_LDS
-        {
-            const unsigned char* tbb = reinterpret_cast<const unsigned char*>(tb);
-            const u32 voff = col * 16u;
-#pragma unroll
-            for (int q = 0; q < (int)((TILE_WORDS * 8 + 1023) / 1024); ++q) {
-                if ((q + 1) * 1024 > (int)(TILE_WORDS * 8) && (int)col * 16 >= (int)(TILE_WORDS * 8) % 1024) continue;
-                const u32 dst = __builtin_amdgcn_readfirstlane(lds_base + q * 1024);
-                const unsigned char* pb = tbb + q * 1024;
-                u32 keep;
-                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                             : "=&s"(keep) : "v"(voff), "s"(pb), "s"(dst) : "memory");
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const uint2* ln = col < 63u ? lt + col + 1 : lt + STREAM;   // the words in LDS
-        const uint2* lm = lt + col;
-#endif
         const uint2* pn = col < 63u ? tb + col + 1 : tb + STREAM;   // warm-up words: t - 32 ..
         const long sn = col < 63u ? 64 : 1;
         const uint2* pm = tb + col;                                  // own words: t * 64
@@ -318,14 +286,13 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
     o << "        uint2 v0, v1;\n";
     o << "        uint2 w0 = make_uint2(0u, 0u), w1 = make_uint2(0u, 0u);\n";
     o << "        const uint2 *p0, *p1, *q0 = tb, *q1 = tb;\n";
-    auto ptr = [](bool own, const std::string& tv, const char* g) {
-        const std::string m = g[0] == 'p' ? "pm" : "lm", n = g[0] == 'p' ? "pn" : "ln";
-        return own ? m + " + (long)(" + tv + ") * 64" : n + " + (long)((" + tv + ") - 32) * sn";
+    auto ptr = [](bool own, const std::string& tv) {
+        return own ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn";
     };
     auto load = [&](const std::string& pv, const std::string& vv, const std::string& ev, bool own,
                     const std::string& tv, const std::string& ind) {
-        o << ind << pv << " = " << ptr(own, tv, "p") << ";\n";
-        o << ind << vv << " = *(" << ptr(own, tv, lds ? "l" : "p") << ");\n";
+        o << ind << pv << " = " << ptr(own, tv) << ";\n";
+        o << ind << vv << " = *(" << ptr(own, tv) << ");\n";
         (void)ev;
     };
     // a phase: `n` steps from t = `t0` down, pointer form `own`; pairs of

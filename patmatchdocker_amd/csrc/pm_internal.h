@@ -448,7 +448,6 @@ constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a q
 
 struct BatchIndex {
     uint32_t omax = 0;     // the largest piece offset: probes start there
-    uint32_t stride = 1;   // 2: every other position probed, two pieces per pattern
     uint64_t expansions = 0;
     std::vector<uint32_t> table;      // [BQ_TABLE_WORDS]: the codes present (bit code & 31 of word code >> 5)
     // [2^(2 BQ)]: first entry << 8 | entries, per code (4 MB, read once per
@@ -489,7 +488,6 @@ struct BatchVerifyArgs {
     const int32_t* lengths;
     uint32_t omax, tiles_per_wave, wpo, nwaves, nout;
     int P;
-    uint32_t stride;
     const uint2 *hl, *bo;
     const uint64_t* lflag;
     uint64_t ntiles, n;

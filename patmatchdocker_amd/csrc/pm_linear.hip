@@ -191,8 +191,6 @@ struct OthersArgs {
     uint32_t nwg, tiles_per_wg;
     int items_per_wave;  // k_linear_others: 1, 2 or 4 (2 * maxlen - 1 <= 64 / items_per_wave)
     int n_classes;       // k_linear_others<true>: classes staged in LDS (<= 256)
-    int direct;          // k_linear_others: iterate the candidate words themselves (selection inline, no
-                         // k_others_select pass)
 };
 
 // Phase 1, one thread per candidate word: the exception bits that can own a
@@ -345,22 +343,11 @@ __device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint
     }
 }
 
-// Phase 2, lane form (patterns of <= 32 positions): one LANE per selected
-// word, bit-parallel over the windows that hold an exception e.  The
-// 2 * maxlen - 1 positions around e (e - maxlen + 1 .. e + maxlen - 1, all
-// in e's stream) are gathered into bit vectors -- bit i = position
-// e - maxlen + 1 + i: the two base planes H / L, breaks, "other" bytes,
-// positions outside the file -- and for each pattern the mismatch count of
-// every window start u at once is a bit-sliced sum of the per-position
-// mismatch vectors shifted by the position (V_j >> j), exception bytes
-// added from their class membership.  A window is evaluated by the first
-// exception it holds (the ones before e own the others), breaks kill it
-// unless the simple engine runs (cross), and windows off the file are dead:
-// the same windows, the same verdicts as the wave form below.
 constexpr int JIT_MAX_P_ = 8;         // = JIT_MAX_P (declared further down)
 constexpr int OTH_CLS_MAX_POS = BATCH_MAX_P * BATCH_MAX_LEN;   // (pattern, position) entries of a q-gram batch
-constexpr int OTH_LANE_MAXLEN = 32;   // 2 * maxlen - 1 <= 63 positions in a 64-bit vector
 
+// bit vectors over a window span: the mismatch of an ACGT subset, and a
+// bit-sliced add into a count (c0, c1; ge4 = count >= 4)
 __device__ inline uint64_t vec_mismatch(uint64_t H, uint64_t L, uint32_t sub) {
     const uint64_t sA = (sub & 1) ? ~0ull : 0ull, sC = (sub & 2) ? ~0ull : 0ull;
     const uint64_t sG = (sub & 4) ? ~0ull : 0ull, sT = (sub & 8) ? ~0ull : 0ull;
@@ -375,136 +362,6 @@ __device__ inline void vec_add(uint64_t x, uint64_t& c0, uint64_t& c1, uint64_t&
     c1 ^= cy0;
     ge4 |= cy1;
 }
-
-__global__ __launch_bounds__(256) void k_others_lane(OthersArgs a) {
-    // per (pattern p, position j) at p * maxlen + j: byte membership of its
-    // class ('.' all ones) and its A/C/G/T subset (+ 16: accepts N)
-    __shared__ uint32_t s_memb[JIT_MAX_P_ * OTH_LANE_MAXLEN][8];
-    __shared__ uint8_t s_sub[JIT_MAX_P_ * OTH_LANE_MAXLEN];
-    for (int i = threadIdx.x; i < a.P * a.maxlen * 8; i += blockDim.x) {
-        const int e = i >> 3, p = e / a.maxlen, j = e % a.maxlen;
-        uint32_t m = 0;
-        if (j < a.lengths[p]) {
-            const int cl = a.pos_class[p * 64 + j];
-            m = a.class_any[cl] ? ~0u : a.class_bytes[cl * 8 + (i & 7)];
-        }
-        s_memb[e][i & 7] = m;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < a.P * a.maxlen; e += blockDim.x) {
-        uint32_t sub = 0;
-        const char* acgt = "ACGT";
-        for (int x = 0; x < 4; ++x) {
-            const uint8_t c = (uint8_t)acgt[x];
-            if ((s_memb[e][c >> 5] >> (c & 31)) & 1) sub |= 1u << x;
-        }
-        if ((s_memb[e]['N' >> 5] >> ('N' & 31)) & 1) sub |= 16;   // accepts N
-        s_sub[e] = (uint8_t)sub;
-    }
-    __syncthreads();
-    const int ML = a.maxlen, span = 2 * ML - 1;
-    const uint32_t nsel = *a.nsel;
-    for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < nsel; it += gridDim.x * blockDim.x) {
-        const OtherSel sv = a.sel[it];
-        const uint64_t tile = sv.word / TILE_WORDS;
-        const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
-        for (uint32_t bits = sv.bits; bits; bits &= bits - 1) {
-            const uint64_t e = pos_of(tile, lw, __builtin_ctz(bits));
-            if (e >= a.n) continue;
-            const int64_t q0 = (int64_t)e - (ML - 1);
-            uint64_t H = 0, L = 0, BR = 0, OT = 0, OUT = 0;
-#pragma unroll 8
-            for (int i = 0; i < span; ++i) {
-                const int64_t q = q0 + i;
-                if (q < 0 || (uint64_t)q >= a.n) {
-                    OUT |= 1ull << i;
-                    continue;
-                }
-                const Loc l = loc_of((uint64_t)q);
-                const uint2 ex = a.nuc.bo[l.word];
-                const uint2 hv = a.nuc.hl[l.word];
-                H |= (uint64_t)((hv.x >> l.bit) & 1) << i;
-                L |= (uint64_t)((hv.y >> l.bit) & 1) << i;
-                BR |= (uint64_t)((ex.x >> l.bit) & 1) << i;
-                OT |= (uint64_t)((ex.y >> l.bit) & 1) << i;
-            }
-            // bytes compared by value (class membership): "other" bytes, and
-            // the breaks too when windows may span lines; kills otherwise.
-            // N (hi plane bit set at an "other" position, NUC_N_MARK) takes
-            // its membership from s_nm; the rest from the side table
-            const uint64_t EX = OT | (a.cross ? BR : 0ull);
-            const uint64_t EXN = OT & ~BR & H;
-            const uint64_t EXL = EX & ~EXN;
-            const uint64_t KILL = OUT | (a.cross ? 0ull : BR);
-            // windows u <= h hold an exception before e: owned by it
-            const uint64_t before = (OT | BR) & ((1ull << (ML - 1)) - 1);
-            const uint64_t owned = before ? ~0ull >> __builtin_clzll(before) : 0ull;
-            // the looked-up bytes (up to 8 kept in registers: their span
-            // index and byte; more -- rare -- are looked up again per pattern)
-            const int nxl = __popcll(EXL);
-            uint64_t xl_pos = 0, xl_byte = 0;
-            if (nxl <= 8) {
-                int q = 0;
-                for (uint64_t x = EXL; x; x &= x - 1, ++q) {
-                    const int i = __builtin_ctzll(x);
-                    const Loc l = loc_of((uint64_t)(q0 + i));
-                    const uint8_t ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
-                    xl_pos |= (uint64_t)i << (8 * q);
-                    xl_byte |= (uint64_t)ch << (8 * q);
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < JIT_MAX_P_; ++p) {
-                if (p >= a.P) break;
-                const int len = a.lengths[p];
-                uint64_t c0 = 0, c1 = 0, ge4 = 0, killw = 0;
-                for (int j = 0; j < len; ++j) {
-                    const uint8_t sub = s_sub[p * ML + j];
-                    const uint64_t nmis = (sub & 16) ? 0ull : EXN;   // N rejected by this class
-                    vec_add(((vec_mismatch(H, L, sub) & ~EX) | nmis) >> j, c0, c1, ge4);
-                    killw |= KILL >> j;
-                }
-                // each looked-up byte is its own addend (two of them may fall
-                // in one window)
-                uint64_t xl = EXL;
-                for (int q = 0; q < nxl; ++q) {
-                    int i;
-                    uint8_t ch;
-                    if (nxl <= 8) {
-                        i = (int)((xl_pos >> (8 * q)) & 255);
-                        ch = (uint8_t)((xl_byte >> (8 * q)) & 255);
-                    } else {
-                        i = __builtin_ctzll(xl);
-                        xl &= xl - 1;
-                        const Loc l = loc_of((uint64_t)(q0 + i));
-                        ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
-                    }
-                    uint64_t mm = 0;
-                    for (int j = 0; j < len && j <= i; ++j)
-                        if (!((s_memb[p * ML + j][ch >> 5] >> (ch & 31)) & 1)) mm |= 1ull << (i - j);
-                    vec_add(mm, c0, c1, ge4);
-                }
-                uint64_t dead;
-                switch (a.k) {
-                    case 0: dead = c0 | c1 | ge4; break;
-                    case 1: dead = c1 | ge4; break;
-                    case 2: dead = (c1 & c0) | ge4; break;
-                    default: dead = ge4; break;
-                }
-                // starts whose window holds e: u in [ML - len, ML - 1]
-                const uint64_t range = ((1ull << len) - 1) << (ML - len);
-                for (uint64_t alive = range & ~dead & ~killw & ~owned; alive; alive &= alive - 1) {
-                    const uint64_t s = (uint64_t)(q0 + __builtin_ctzll(alive));
-                    const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                    const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
-                    const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
-                    if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
-                }
-            }
-        }
-    }
-}
-
 // Phase 2 for large batches (k_batch_scan's exception windows), one WAVE per
 // exception bit e, with the work split per CLASS: a batch of hundreds of
 // IUPAC motifs uses a handful of classes (A, C, G, T, the two-base codes,
@@ -516,7 +373,9 @@ __global__ __launch_bounds__(256) void k_others_lane(OthersArgs a) {
 // Then lane l takes patterns l, l + 64, ...: one LDS read, a 64-bit shift and
 // two ANDs per position give the windows of every start u holding e, alive
 // iff every position accepts its byte (k > 0: mismatches counted
-// bit-sliced).  Ownership, kills and the file end as in k_others_lane.
+// bit-sliced).  A window is evaluated by the first exception it holds,
+// breaks kill it unless the simple engine runs (cross), and windows off the
+// file are dead -- the same verdicts as the wave form below.
 constexpr int OTH_BATCH_THREADS = 256;
 constexpr int OTH_BATCH_MAX_CLASSES = 32;
 
@@ -673,17 +532,10 @@ __global__ __launch_bounds__(256) void k_linear_others(OthersArgs a) {
     // lanes each (an item's window span fits them): more gathers in flight
     const int G = a.items_per_wave, lanes = 64 / G;
     const int lane = (threadIdx.x & 63) % lanes, slice = (threadIdx.x & 63) / lanes;
-    const uint64_t nsel = a.direct ? (a.use_edge ? a.nedge : a.nflag) : *a.nsel;
+    const uint64_t nsel = *a.nsel;
     const uint32_t nitems = gridDim.x * (blockDim.x >> 6) * G;
     for (uint64_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * G + slice; it < nsel; it += nitems) {
-        OtherSel sv;
-        if (a.direct) {   // the item's lanes select its bits themselves (same loads: broadcast)
-            sv.word = 0;
-            sv.bits = select_bits(a, it, &sv.word);
-            if (!sv.bits) continue;
-        } else {
-            sv = a.sel[it];
-        }
+        const OtherSel sv = a.sel[it];
         const uint64_t tile = sv.word / TILE_WORDS;
         const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
         if (CLS)
@@ -735,7 +587,6 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
 constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
-static_assert(JIT_MAX_P == JIT_MAX_P_, "k_others_lane stages a chunk's classes in LDS");
 
 // Hit records of pm_linear_jit -> hit keys.  A record is (tile, lane, step,
 // pattern) and the live mask of that window word, exact for the ACGT fast
@@ -762,7 +613,6 @@ struct ExpandArgs {
     const uint64_t* slot_base;
     const uint32_t* slot_cap;
     uint32_t nwg, nout, group, tiles_per_wg;
-    int accumulate;   // counters zeroed before the scan, k_linear_others appending concurrently:
                       // slots reserved on the global counters
 };
 
@@ -807,18 +657,6 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
             const uint32_t slot = (uint32_t)a.pattern_base + p;
             const uint32_t cap = a.slot_cap[slot];
             uint64_t* dst = a.out + a.slot_base[slot] + (uint64_t)og * cap;
-            if (a.accumulate) {
-                // k_linear_others appends to the same lists concurrently:
-                // reserve each record's slots on the global counter
-                uint32_t v = 0;
-                for (uint32_t t = live; t; t &= t - 1)
-                    if (pos_of(tile, w0, __builtin_ctz(t)) < a.n) v |= t & (0u - t);
-                if (!v) continue;
-                uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nout + og], (uint32_t)__popc(v));
-                for (; v; v &= v - 1, ++o)
-                    if (o < cap) dst[o] = ((uint64_t)slot << 48) | pos_of(tile, w0, __builtin_ctz(v));
-                continue;
-            }
             for (; live; live &= live - 1) {
                 const uint64_t pos = pos_of(tile, w0, __builtin_ctz(live));
                 if (pos >= a.n) continue;
@@ -829,7 +667,7 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
     }
     __syncthreads();
     // k_linear_others (launched after) appends to the same counters
-    if (!a.accumulate && (int)threadIdx.x < a.P)
+    if ((int)threadIdx.x < a.P)
         a.seg_cnt[(uint64_t)(a.pattern_base + threadIdx.x) * a.nout + og] = cnt_p[threadIdx.x];
 }
 
@@ -888,11 +726,8 @@ struct JArgsHost {           // must match JArgs in kJitCommon
     uint32_t rcap, tiles_per_wg;
 };
 constexpr int JIT_REC_LDS = 96;       // hit records staged per wave in LDS (3 workgroups per CU)
-// workgroups resident per CU (PM_JIT_WAVES: experiment override, e.g. 4 with PM_JIT_RING=2)
-int jit_wg_per_cu() {
-    const char* e = getenv("PM_JIT_WAVES");
-    return e ? std::max(1, atoi(e)) : 4;
-}
+// workgroups resident per CU (4: two 16.5 KiB tile slots each fit the LDS)
+constexpr int JIT_WG_PER_CU = 4;
 
 // mismatch of an ACGT subset as an expression of the plane words h, l.
 // Forms with an inverted plane are one explicit v_bitop3 (truth table over
@@ -1031,8 +866,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // LDS tile buffers: 2 (the next tile streams in while this one is
     // scanned) leave room for 4 workgroups per CU, which measured 10 %
     // faster than 3 buffers at 3 workgroups per CU (profiles/r01c_ring_sweep.txt)
-    int RING = 2;
-    if (const char* e = getenv("PM_JIT_RING")) RING = atoi(e);   // experiment: 2 or 3
+    constexpr int RING = 2;
     const int TILE_BYTES = (int)(TILE_WORDS * 8);         // 16896: 16.5 KiB
     const int DMA_PIECES = (TILE_BYTES + 1023) / 1024;   // 1 KiB per glds wave-instruction (last one half)
     const int LDS_TILE = TILE_BYTES;
@@ -1051,20 +885,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     for (int p = 0; p < P; ++p) Lmax = std::max(Lmax, (int)lengths[p]);
     // Class words are pinned in registers (derived once per row); unpinned,
     // the compiler re-derives them per use and keeps the plane words of every
-    // row alive instead, which measured worse for every shape (experiment
-    // knob PM_JIT_PIN_LIMIT: most class words per wave that are pinned).
-    int max_words = 0;
-    for (int part = 0; part < PARTS; ++part) {
-        std::set<std::pair<int, int>> need;
-        for (int t = part * JIT_STEPS; t < (part + 1) * JIT_STEPS; ++t)
-            for (int p = 0; p < P; ++p)
-                for (int j = 0; j < lengths[p]; ++j)
-                    if (!class_is_any[pos_class[64 * p + j]]) need.insert({t + j, class_acgt[pos_class[64 * p + j]] & 15});
-        max_words = std::max(max_words, (int)need.size());
-    }
-    int pin_limit = 1 << 30;
-    if (const char* e = getenv("PM_JIT_PIN_LIMIT")) pin_limit = atoi(e);   // experiment knob
-    const bool pin = max_words <= pin_limit;
+    // row alive instead, which measured worse for every shape (round 1).
     // Shared blocks.  Two patterns whose class sequences agree on a run of
     // positions at some offset -- the strands of a (near-)palindromic motif:
     // TGCTGA[GC]TCAGCA.[AT] and its reverse complement agree on 13 positions
@@ -1094,7 +915,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
                         if (n >= 6 && gain > best) { best = gain; bp = p; bq = q; boff = off; }
                     }
                 }
-            if (bp < 0 || getenv("PM_JIT_NOSHARE")) break;
+            if (bp < 0) break;
             used[bp] = used[bq] = true;
             for (int j = 0; j < lengths[bp]; ++j)
                 if (j - boff >= 0 && j - boff < lengths[bq] && cls(bp, j) >= 0 && cls(bp, j) == cls(bq, j - boff)) {
@@ -1121,7 +942,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
             const std::string nm = "x" + std::to_string(subset) + "_" + std::to_string(i);
             o << "  u32 " << nm << " = "
               << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << ";"
-              << (pin ? " PIN(" + nm + ");" : "") << "\n";
+              << " PIN(" + nm + ");" << "\n";
             cw[key] = nm;
             return nm;
         };
@@ -1160,18 +981,14 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // `waves`: __launch_bounds__ minimum workgroups per CU (4 -> at most
     // 128 VGPRs; jit_function falls back to 3 when that would spill)
     // bytes DMA'd per tile: the 2048 words and only the halo words a window
-    // reads (Lmax - 1 of the 64; PM_JIT_FULL_HALO=1: all) -- ~2 % fewer HBM
-    // lines per tile for a 15-mer
-    const int halo_used = getenv("PM_JIT_FULL_HALO") ? HALO : std::min(HALO, std::max(1, Lmax - 1));
+    // reads (Lmax - 1 of the 64) -- ~2 % fewer HBM lines per tile for a
+    // 15-mer (round 2: 1.036 -> 1.012 x algorithmic traffic)
+    const int halo_used = std::min(HALO, std::max(1, Lmax - 1));
     const int LOAD_BYTES = std::min(TILE_BYTES, (int)(((STREAM + halo_used) * 8 + 15) / 16 * 16));
     const int LOAD_PIECES = (LOAD_BYTES + 1023) / 1024;
     (void)DMA_PIECES;
     o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << LOAD_PIECES
       << "\n#define LOAD_BYTES " << LOAD_BYTES << "\n";
-    // experiment knobs: PM_JIT_NOCOMPUTE=1 only streams the tiles,
-    // PM_JIT_NODMA=1 rescans each workgroup's first tiles (no HBM stream)
-    const bool nocompute = getenv("PM_JIT_NOCOMPUTE") && getenv("PM_JIT_NOCOMPUTE")[0] == '1';
-    if (getenv("PM_JIT_NODMA") && getenv("PM_JIT_NODMA")[0] == '1') o << "#define PM_NODMA 1\n";
     o << R"JIT(// Raw barrier: __syncthreads()'s release fence would wait vmcnt(0) and
 // drain the tile prefetch in flight.  LDS writes are complete at
 // lgkmcnt(0); the empty asm statements keep the compiler from moving memory
@@ -1218,8 +1035,6 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  __shared__ uint2 rst[4][REC_LDS];\n"
          "  const int lane = threadIdx.x & 63;\n"
          "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-         "  // pieces this wave DMAs per tile (its share of DMA_PIECES)\n"
-         "  const u32 mine = (DMA_PIECES - wid + 3) / 4;\n"
          "  // halo word offsets (logical words 32 lane + 32 g + r, r < 32)\n"
          "  const u32 hb1 = lane + 1 < 64 ? lane + 1 : 32u * lane + 32u, hs1 = lane + 1 < 64 ? 64u : 1u;\n"
          "  const u32 hb2 = lane + 2 < 64 ? lane + 2 : 32u * lane + 64u, hs2 = lane + 2 < 64 ? 64u : 1u;\n"
@@ -1235,30 +1050,17 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  stage(a, lds_base + LDS_TILE, t0 + 1, tend, wid, lane);\n"
          "  u32 slot = 0;\n"
          "  for (u64 tile = t0; tile < tend; ++tile) {\n"
-         "    // wait for this tile's pieces (own DMAs; the next tile's stay in\n"
-         "    // flight: vmcnt retires in order), then the barrier makes everyone's\n"
-         "    // pieces visible and frees the previous tile's slot\n"
-         "    if (RING > 2 && tile + 1 < tend) {\n"
-         "      if (mine == 5) asm volatile(\"s_waitcnt vmcnt(5)\" ::: \"memory\");\n"
-         "      else asm volatile(\"s_waitcnt vmcnt(4)\" ::: \"memory\");\n"
-         "    } else {\n"
-         "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
-         "    }\n"
+         "    // wait for this tile's pieces (own DMAs), then the barrier makes\n"
+         "    // everyone's pieces visible and frees the previous tile's slot\n"
+         "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
          "    BARRIER();\n"
-         "#ifndef PM_NODMA   // experiment: keep scanning the workgroup's first tiles (compute only)\n"
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
-         "#endif\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
          "    u32 dd[STEPS][P];   // dead windows per step and pattern (every path writes all of them)\n";
-    if (nocompute) {
-        o << "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) dd[s][p] = ~0u;\n"
-             "    if (sw[lane].x == 0x12345u && lane == 99) dd[0][0] = 0u;   // keeps the tile reads\n";
-    } else {
-        // wid < 4: the last part is the plain else (no ~0 initialization of dd)
-        for (int part = 0; part < PARTS; ++part)
-            o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
-              << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
-    }
+    // wid < 4: the last part is the plain else (no ~0 initialization of dd)
+    for (int part = 0; part < PARTS; ++part)
+        o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
+          << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
     o << "    u32 all = ~0u;\n"
          "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
          "    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {   // wave-uniform, rare\n"
@@ -1343,10 +1145,6 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
         }
         sig += "]";
     }
-    for (const char* knob :
-         {"PM_JIT_WAVES", "PM_JIT_RING", "PM_JIT_NOCOMPUTE", "PM_JIT_NODMA", "PM_JIT_PIN_LIMIT", "PM_JIT_NOSHARE",
-          "PM_JIT_FULL_HALO"})
-        if (const char* e = getenv(knob)) sig += std::string(";") + knob + "=" + e;
     return sig;
 }
 
@@ -1359,7 +1157,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     // 4 workgroups per CU when the kernel fits 128 VGPRs without spilling,
     // else 3 (up to 168 VGPRs)
     JitKernel jk;
-    for (int waves = jit_wg_per_cu(); waves >= 1; --waves) {
+    for (int waves = JIT_WG_PER_CU; waves >= 1; --waves) {
         std::vector<char> code =
             jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves));
         if (jk.module) HIPCHK(hipModuleUnload(jk.module));
@@ -1593,8 +1391,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         std::shared_ptr<const BatchIndex> bip;
         std::string batch_sig;
         if (jit && k == 0 && n_patterns >= batch_min && env_flag("PM_BATCH", true)) {
-            batch_sig = jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any) +
-                        (getenv("PM_BATCH_STRIDE") ? std::string(";stride=") + getenv("PM_BATCH_STRIDE") : "");
+            batch_sig = jit_signature(n_patterns, k, lengths, pos_class, class_acgt, class_is_any);
             bip = batch_index_cached(batch_sig, n_patterns, lengths, pos_class, class_acgt, class_is_any);
         }
         const bool batch = bip != nullptr;
@@ -1623,16 +1420,6 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             chunks.push_back({base, P, fn});
             base += P;
         }
-        // pipelined single-launch scans alternate workspace lanes, so that
-        // this scan's record expansion + sort (on the post stream) overlap
-        // the next scan's kernel; every scan first waits (on the GPU) for the
-        // last reader of its lane
-        // Off by default: measured no faster per step (the chip is at its
-        // power limit either way) and the overlapped expansion slows the
-        // kernel it overlaps.  PM_OFFLOAD=1 turns it on (experiment knob).
-        static const bool want_offload = getenv("PM_OFFLOAD") && getenv("PM_OFFLOAD")[0] == '1';
-        const bool offload = async && jit && chunks.size() == 1 && want_offload;
-        if (offload) switch_lane(db);
         lane_begin(db);
         uint8_t* d_up = up.commit(db);
         const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
@@ -1673,33 +1460,22 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // persistent waves evaluate them
             const bool cls = ch.P * oa.maxlen > OTH_MAX_POS;
             require(!cls || ch.P * oa.maxlen <= OTH_CLS_MAX_POS, "internal: batch too large for the exception pass");
-            static const int others_batch = getenv("PM_OTHERS_BATCH") ? atoi(getenv("PM_OTHERS_BATCH")) : 1;
-            const bool batch_form = (cls ? others_batch >= 1 : others_batch >= 2) && n_classes <= OTH_BATCH_MAX_CLASSES &&
-                                    oa.maxlen <= BATCH_MAX_LEN && ch.P <= BATCH_MAX_P;
-            const bool lane_form = !batch_form && !cls && ch.P <= JIT_MAX_P && oa.maxlen <= OTH_LANE_MAXLEN &&
-                                   env_flag("PM_OTHERS_LANE", false);
-            // a selection pass compacts the words first (PM_OTHERS_DIRECT=1:
-            // the wave form selects inline instead -- measured slower, 0.231
-            // vs 0.138 + 0.046 ms on configs[2]: the persistent waves then
-            // wait on the selection loads of every filtered-out word)
-            oa.direct = !batch_form && !lane_form && env_flag("PM_OTHERS_DIRECT", false) ? 1 : 0;
-            if (!oa.direct) {
-                HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
-                hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
-                HIPCHK(hipGetLastError());
-            }
-            // PM_OTHERS_LANE=1: the lane form (measured 0.20 vs 0.18 ms on
-            // the bench database: both are bound by the random gathers,
-            // ~58 cache lines per exception bit)
-            // the per-class wave form: large batches (class-id staging), or any
-            // chunk with PM_OTHERS_BATCH=2 (experiment)
+            // the per-class wave form for large batches (class-id staging)
+            const bool batch_form = cls && n_classes <= OTH_BATCH_MAX_CLASSES && oa.maxlen <= BATCH_MAX_LEN &&
+                                    ch.P <= BATCH_MAX_P;
+            // a selection pass compacts the words first (an inline selection
+            // in the waves measured slower, 0.231 vs 0.138 + 0.046 ms on
+            // configs[2]: the persistent waves then wait on the selection
+            // loads of every filtered-out word; a lane-per-bit form measured
+            // 0.20 vs 0.18 ms -- both are bound by ~58 gathered cache lines
+            // per exception bit)
+            HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
+            hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
+            HIPCHK(hipGetLastError());
             if (batch_form)
                 hipLaunchKernelGGL(k_others_batch,
                                    dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, OTH_BATCH_THREADS))),
                                    dim3(OTH_BATCH_THREADS), 0, os, oa);
-            else if (lane_form)
-                hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words, 256))),
-                                   dim3(256), 0, os, oa);
             else
                 hipLaunchKernelGGL(cls ? k_linear_others<true> : k_linear_others<false>,
                                    dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, 256))),
@@ -1761,7 +1537,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_pmask),
                                    reinterpret_cast<const uint32_t*>(d_batch + bi.o_popt),
                                    reinterpret_cast<const int32_t*>(d_up + o_len), bi.omax, (uint32_t)tpw,
-                                   (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, bi.stride, db->hl, db->bo,
+                                   (uint32_t)wpo, (uint32_t)nwaves, (uint32_t)nout, n_patterns, db->hl, db->bo,
                                    db->lflag, db->ntiles, db->n, sb.out, sb.cnt, sb.slot_base, sb.slot_cap,
                                    reinterpret_cast<uint64_t*>(rbase + o_x), reinterpret_cast<uint32_t*>(rbase + o_xcnt),
                                    (uint32_t)xcap};
@@ -1796,12 +1572,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         } else if (jit) {
             // one output segment per (pattern, workgroup); workgroups own
             // contiguous tile ranges (3 per CU resident)
-            // more workgroups than resident slots (PM_JIT_SPLIT x): the
-            // dispatcher hands the next one to whichever CU frees a slot, so
-            // an unevenly loaded CU does not hold up the whole launch
-            const char* split_env = getenv("PM_JIT_SPLIT");
-            const uint64_t split = split_env ? std::max(1, atoi(split_env)) : 8;
-            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * jit_wg_per_cu() * split);
+            // 8x more workgroups than resident slots: the dispatcher hands the
+            // next one to whichever CU frees a slot, so an unevenly loaded CU
+            // does not hold up the whole launch (4, 6, 12 within the noise,
+            // 16 and 32 slower: profiles/r02k_bench_spread.txt)
+            const uint64_t split = 8;
+            uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * JIT_WG_PER_CU * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
             const uint64_t nseg = nwg * 4;   // one lane-record segment per wave
@@ -1844,17 +1620,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 uint32_t* d_rcnt = reinterpret_cast<uint32_t*>(rbase + o_rcnt);
                 (void)o_over;
                 // no counter memset: k_linear_expand stores every (pattern,
-                // segment) count, the first launch zeroes the aux counter
-                // the exception pass runs after the expansion on the same
-                // stream; PM_EXC_CONCURRENT=1 runs it on its own stream,
-                // concurrently with the specialized scan (its windows are
-                // independent of the scan, only the hit-list counters are
-                // shared) -- measured no faster: the two contend for the CUs
+                // segment) count, the first launch zeroes the aux counter.
+                // The exception pass runs after the expansion on the same
+                // stream (run concurrently with the scan it measured no
+                // faster: the two contend for the CUs)
                 const bool exc = db->nflag && (db->n_oth_words || cross);
-                const bool exc_conc = exc && env_flag("PM_EXC_CONCURRENT", false);
-                // without the concurrent pass no counter memset: the expansion
-                // stores every (pattern, segment) count
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/exc_conc);
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
                 uint32_t* d_over = sb.cnt + sb.nbins;   // the sink's aux counter
                 // kernel_ms = the scan passes over the database (pm_linear_jit
                 // launches); record expansion and the rest are not included
@@ -1865,18 +1636,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     nospec = g_nospec.count({db, cap_key}) != 0;
                 }
                 const bool spec_async = async && sb.nbins <= 4096 && attempt == 0 && !nospec;
-                // expansion, others and the sort: on the post stream after the
-                // kernel's event when this scan returns pipelined in one launch
-                const hipStream_t xs = spec_async && offload ? post_stream(db) : s;
-                if (exc_conc) {
-                    // forked after the counter memset and the table uploads
-                    // (both on s, behind lane_begin's wait for the lane)
-                    const hipStream_t es = exc_stream(db);
-                    HIPCHK(hipEventRecord(db->exc_fork, s));
-                    HIPCHK(hipStreamWaitEvent(es, db->exc_fork, 0));
-                    for (const Chunk& ch : chunks) launch_others(ch, es, sb, nout, tpw * group);
-                    HIPCHK(hipEventRecord(db->exc_join, es));
-                }
+                // expansion, exception pass and sort run on the scan's stream
+                // (overlapping them with the next scan on a second stream
+                // measured no faster: the chip is at its power limit)
+                const hipStream_t xs = s;
                 for (const Chunk& ch : chunks) {
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
                     void* params[] = {&ja};
@@ -1885,16 +1648,14 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     // (no marker packets around the launch; sizes in threads)
                     HIPCHK(hipExtModuleLaunchKernel(ch.jit, (uint32_t)nwg * 256u, 1, 1, 256, 1, 1, 0, s, params,
                                                     nullptr, jev.back()->a, jev.back()->b, 0));
-                    if (xs != s) HIPCHK(hipStreamWaitEvent(xs, jev.back()->b, 0));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
-                                  (uint32_t)tpw, exc_conc ? 1 : 0};
+                                  (uint32_t)tpw};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
-                    if (exc && !exc_conc) launch_others(ch, xs, sb, nout, tpw * group);
+                    if (exc) launch_others(ch, xs, sb, nout, tpw * group);
                 }
-                if (exc_conc) HIPCHK(hipStreamWaitEvent(xs, db->exc_join, 0));
                 if (spec_async) {
                     // pipelined: the speculative sort also writes the bin
                     // counts into mapped pinned memory (no copy), an event

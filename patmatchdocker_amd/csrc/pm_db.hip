@@ -354,6 +354,7 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
     void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
+    (void)hipGetLastError();   // rocPRIM leaves a stale "stream is capturing" status behind
     uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 16));
     HIPCHK(hipMemcpyAsync(h, db->sbbase + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h + 1, sbcnt + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));

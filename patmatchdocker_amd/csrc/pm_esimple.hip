@@ -249,11 +249,18 @@ void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, u
     s.np = P.npieces;
     s.anchors = (int32_t)(flags & (PM_ANCHOR_START | PM_ANCHOR_END));
     s.pid = pid;
+    // lone starts need no walk (k_es_walk): substitutions only, no
+    // anchors, and every piece test sees its own piece (the 32-bit shift
+    // misses bits 32..63)
+    s.lone = errs == PM_ERR_SUB && !s.anchors;
     for (int i = 0; i < s.np; ++i) {
         s.L[i] = P.L[i];
         if (P.type == 1) {
             const int bit = i * P.piece_len + P.piece_len - 1;
             s.test[i] = (uint64_t)(int64_t)(int32_t)(1u << (bit & 31));
+            if (!((s.test[i] >> bit) & 1)) s.lone = 0;
+        } else {
+            s.test[i] = ~0ull;   // the one window / prefix candidate
         }
     }
     // B | TL[np] | TR[np], each [256][W]: bit r of TL[i][c] = position
@@ -266,6 +273,22 @@ void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, u
     b.tab.resize(b.tab.size() + per * s.np, 0);
     s.o_TR = b.tab.size();
     b.tab.resize(b.tab.size() + per * s.np, 0);
+    // type 1: the pieces packed as BNDM holds them (piece i in bits
+    // [i * len, i * len + len)): bit i * len + j of P[c] = position L_i + j
+    // accepts c.  A forward shift-and over P finds the pieces that match
+    // exactly at a window start (its last bits) -- BNDM's D there.
+    s.o_P = b.tab.size();
+    if (s.type == 1) {
+        require(s.np * s.mpc <= 64, "esimple: pieces exceed a word");
+        b.tab.resize(b.tab.size() + 256, 0);
+        for (int i = 0; i < s.np; ++i) {
+            s.pstart |= 1ull << (i * s.mpc);
+            s.pend |= 1ull << (i * s.mpc + s.mpc - 1);
+            for (int j = 0; j < s.mpc; ++j)
+                for (int c = 0; c < 256; ++c)
+                    if (bit_of(B, W, c, s.L[i] + j)) b.tab[s.o_P + c] |= 1ull << (i * s.mpc + j);
+        }
+    }
     for (int i = 0; i < s.np; ++i) {
         const int L = s.L[i];
         for (int c = 0; c < 256; ++c) {
@@ -283,6 +306,12 @@ void es_upload(const EsBuild& b, Upload& up, EsUpload& u) {
     u.o_tab = up.add(b.tab.data(), b.tab.size() * sizeof(uint64_t));
     u.nslots = (int)b.slots.size();
     u.pid_base = b.slots.empty() ? 0 : b.slots[0].pid;
+    u.wmax = 1;
+    u.kmax = 1;
+    for (const EsSlot& sl : b.slots) {
+        u.wmax = std::max(u.wmax, (int)sl.W);
+        u.kmax = std::max(u.kmax, (int)sl.k);
+    }
 }
 
 EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max) {
@@ -292,6 +321,8 @@ EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max) {
     p.nslots = u.nslots;
     p.pid_base = u.pid_base;
     p.gap_max = gap_max;
+    p.wmax = u.wmax;
+    p.kmax = u.kmax;
     return p;
 }
 
@@ -308,23 +339,112 @@ namespace {
 
 constexpr uint64_t ES_POS_MASK = (1ull << 48) - 1;
 
+constexpr int ES_CHUNK = 8;      // positions staged per refill of a thread's window
+constexpr int ES_THREADS = 64;   // walk threads per block (one wave)
+constexpr int ES_SPAN = 16;      // window starts whose pieces one shift-and pass finds
+
+// A thread's text window: the line-bounded bytes (breaks as '\n') of
+// positions [lo, hi) in an LDS ring of win (a power of two) bytes.  The walk
+// moves forward and every phase reads at most m + k + 1 positions on either
+// side of the candidate; before each candidate the walk tops the ring up to
+// pos + m + k + 2 (EsText::fill), so with win >= gap_max + ES_CHUNK every
+// read hits it; a read outside it (a pattern wider than the ring was sized
+// for) goes to memory.  A refill issues ES_CHUNK independent loads at once
+// instead of one dependent load per step.
+extern __shared__ uint8_t es_lds[];   // k_es_walk: win bytes per thread
+
+struct EsRing {
+    uint32_t base;   // the thread's ring in es_lds
+    uint32_t mask;   // win - 1 (win = 0: no ring)
+    uint64_t lo, hi; // valid positions [lo, hi)
+};
+
 struct EsText {
     TextView tv;
     uint64_t n;
-    // a record break: '\n', a header-line byte, the end of the text
-    __device__ bool brk(uint64_t p) const {
-        if (p >= n) return true;
-        if (tv.nuc_layout) {
-            const Loc l = loc_of(p);
-            return (tv.nuc.bo[l.word].x >> l.bit) & 1;
-        }
-        return tv.bytes[p] == (uint8_t)'\n';
+    EsRing r;
+    // the line-bounded byte from memory: '\n' for breaks and past the end
+    __device__ uint8_t load(uint64_t p) const {
+        if (p >= n) return (uint8_t)'\n';
+        return tv.nuc_layout ? nuc_char_at(tv.nuc, p) : tv.bytes[p];
     }
-    // the (folded) byte inside a record
-    __device__ uint8_t chr(uint64_t p) const { return tv.nuc_layout ? nuc_char_at(tv.nuc, p) : tv.bytes[p]; }
+    __device__ void restart(uint64_t p) { r.lo = r.hi = p; }
+    // extend the ring to cover [.., upto).  A chunk's loads are all
+    // unconditional (addresses clamped into the chunk) so that the chunk
+    // costs one memory round trip plus, only where a lane of the tile holds
+    // an exception (lflag), a second one for the bo words.  Every position
+    // is its own line of hl (the stream layout), so no more positions are
+    // fetched than asked for.
+    __device__ void fill(uint64_t upto) {
+        if (r.mask == ~0u) return;
+        while (r.hi < upto) {
+            const uint64_t b = r.hi;
+            const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
+            if (b >= n) {
+                for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = (uint8_t)'\n';
+            } else if (tv.nuc_layout) {
+                const uint64_t pl = umin64(b + cnt, n) - 1;   // the chunk's last position in the file
+                const uint64_t lf0 = tv.lflag[b / TILE_POS], lf1 = tv.lflag[pl / TILE_POS];
+                uint2 d[ES_CHUNK];
+#pragma unroll
+                for (int q = 0; q < ES_CHUNK; ++q) d[q] = tv.nuc.hl[loc_of(umin64(b + q, pl)).word];
+                uint2 e[ES_CHUNK];
+                const uint64_t w0 = loc_of(b).word;   // a line the first round brought in
+#pragma unroll
+                for (int q = 0; q < ES_CHUNK; ++q) {
+                    const uint64_t p = umin64(b + q, pl);
+                    const uint64_t lf = p / TILE_POS == b / TILE_POS ? lf0 : lf1;
+                    const bool flagged = (lf >> ((uint32_t)(p % STREAM) >> 5)) & 1ull;
+                    e[q] = tv.nuc.bo[flagged ? loc_of(p).word : w0];
+                    if (!flagged) e[q] = make_uint2(0u, 0u);
+                }
+#pragma unroll
+                for (int q = 0; q < ES_CHUNK; ++q) {
+                    if ((uint32_t)q >= cnt) break;
+                    const uint64_t p = b + q;
+                    const uint32_t bit = (uint32_t)((p % TILE_POS) / STREAM);
+                    uint8_t c;
+                    if (p >= n || ((e[q].x >> bit) & 1)) {   // a break or past the end
+                        c = (uint8_t)'\n';
+                    } else if ((e[q].y >> bit) & 1) {
+                        c = nuc_char_at(tv.nuc, p);   // an exception byte: the side tables (rare)
+                    } else {
+                        const uint32_t code = (((d[q].x >> bit) & 1) << 1) | ((d[q].y >> bit) & 1);
+                        c = (uint8_t)((0x54474341u >> (8 * code)) & 0xff);
+                    }
+                    es_lds[r.base + ((uint32_t)p & r.mask)] = c;
+                }
+            } else {
+                uint8_t c[ES_CHUNK];
+#pragma unroll
+                for (int q = 0; q < ES_CHUNK; ++q) c[q] = tv.bytes[umin64(b + q, n)];   // bytes[n..] pad with '\n'
+#pragma unroll
+                for (int q = 0; q < ES_CHUNK; ++q)
+                    if ((uint32_t)q < cnt) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = b + q < n ? c[q] : (uint8_t)'\n';
+            }
+            r.hi = b + cnt;
+            if (r.hi - r.lo > r.mask + 1) r.lo = r.hi - (r.mask + 1);
+        }
+    }
+    // a position known to be in the ring
+    __device__ uint8_t ring(uint64_t p) const {
+        return r.mask == ~0u ? load(p) : es_lds[r.base + ((uint32_t)p & r.mask)];   // (no ring: uniform)
+    }
+    // the line-bounded (folded) byte: '\n' at every break
+    __device__ uint8_t chr(uint64_t p) const {
+        return p - r.lo < r.hi - r.lo ? es_lds[r.base + ((uint32_t)p & r.mask)] : load(p);
+    }
+    // a record break: '\n', a header-line byte, the end of the text
+    __device__ bool brk(uint64_t p) const { return chr(p) == (uint8_t)'\n'; }
     // the file's own (folded) byte, header lines and '\n' included: what
     // the BNDM scanner reads
-    __device__ uint8_t raw(uint64_t p) const { return tv.nuc_layout ? nuc_raw_at(tv.nuc, p) : tv.raw[p]; }
+    __device__ uint8_t raw(uint64_t p) const {
+        const uint8_t c = chr(p);
+        if (c != (uint8_t)'\n' || p >= n) return c;
+        return raw_slow(p);
+    }
+    // the file's byte at a break (a header byte or '\n'), p < n
+    __device__ uint8_t raw_slow(uint64_t p) const { return tv.nuc_layout ? nuc_raw_at(tv.nuc, p) : tv.raw[p]; }
 };
 
 struct EsCtx {
@@ -332,19 +452,23 @@ struct EsCtx {
     const uint64_t* tab;
     EsText t;
     uint64_t R;   // the search region start
+    int errs, W, anchors;   // S's fields read on every step
     // recCheckLeftContext 0x402170 / recCheckRightContext 0x4021e0; p ==
     // recbeg <=> p == R or p starts its line (a record holds no break)
     __device__ bool at_recbeg(uint64_t p) const { return p == R || p == 0 || t.brk(p - 1); }
-    __device__ bool left_ok(uint64_t p) const { return !(S->anchors & PM_ANCHOR_START) || at_recbeg(p); }
-    __device__ bool right_ok(uint64_t q) const { return !(S->anchors & PM_ANCHOR_END) || t.brk(q); }
+    __device__ bool left_ok(uint64_t p) const { return !(anchors & PM_ANCHOR_START) || at_recbeg(p); }
+    __device__ bool right_ok(uint64_t q) const { return !(anchors & PM_ANCHOR_END) || t.brk(q); }
 };
 
 // one phase of checkMatch1 (left: dir < 0, bit r = position L - 1 - r read
 // backward from pos; right: bit r = position L + r read forward from pos).
-// Returns the boundary (start / end) and its error count.
+// Returns the boundary (start / end) and its error count.  WB: position
+// words (len <= 64 WB); the rows are unrolled to PM_MAX_K so that the row
+// vectors stay in registers.
+template <int WB, int KR>
 __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool left, int len, int kmax,
                          uint64_t& bound, int& nerr) {
-    const int errs = x.S->errs;
+    const int errs = x.errs;
     if (len == 0) {   // 0x4141ef / 0x414eae
         for (int e = 0; e <= kmax; ++e) {
             const uint64_t b = left ? pos - e : pos + e;
@@ -358,22 +482,27 @@ __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool l
         }
         return false;
     }
-    const int W = (len + 63) >> 6, lw = W - 1;
+    const int W = WB == 1 ? 1 : (len + 63) >> 6, lw = W - 1;
     const uint64_t fin = 1ull << ((len - 1) & 63), alive_mask = fin * 2 - 1;
-    uint64_t Rw[PM_MAX_K + 1][4];
+    uint64_t Rw[KR + 1][WB];
     int maxk = kmax, best = kmax;
     bool found = false;
     uint64_t fb = 0;
-    for (int j = 0; j <= maxk; ++j) {   // 0x414380: deletions reach the first j positions
-        for (int w = 0; w < W; ++w) {
+#pragma unroll
+    for (int j = 0; j <= KR; ++j) {   // 0x414380: deletions reach the first j positions
+        if (j > maxk) break;
+        uint64_t last = 0;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
             uint64_t v = 0;
             if (errs & PM_ERR_DEL) {
                 if (j >= 64 * (w + 1)) v = ~0ull;
                 else if (j > 64 * w) v = ~(~0ull << (j & 63));
             }
             Rw[j][w] = v;
+            if (w == lw) last = v;
         }
-        if ((Rw[j][lw] & fin) && (left ? x.left_ok(pos) : x.right_ok(pos))) {
+        if ((last & fin) && (left ? x.left_ok(pos) : x.right_ok(pos))) {
             best = j;
             maxk = j - 1;
             found = true;
@@ -382,36 +511,59 @@ __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool l
     }
     if (!(left ? x.at_recbeg(pos) : x.t.brk(pos))) {
         uint64_t inj = 1, p = pos;
+        // a step's mask is loaded one step ahead (its latency overlaps the
+        // step before)
+        uint64_t Mn[WB];
+        {
+            const uint64_t* M = T + (size_t)x.t.chr(left ? p - 1 : p) * x.W;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) Mn[w] = w < W ? M[w] : 0ull;
+        }
         for (;;) {
             uint64_t b;
-            uint8_t c;
             if (left) {
                 --p;
-                c = x.t.chr(p);
                 b = p;
             } else {
-                c = x.t.chr(p);
                 b = ++p;
             }
-            const uint64_t* M = T + (size_t)c * x.S->W;
-            uint64_t t0[4], t1[4];
-            uint64_t carry = inj;
-            for (int w = 0; w < W; ++w) {   // row 0
+            uint64_t Mw[WB], t0[WB], t1[WB];
+#pragma unroll
+            for (int w = 0; w < WB; ++w) Mw[w] = Mn[w];
+            {   // the next step reads p - 1 (left) or p (right)
+                const uint8_t cn = left ? (p > 0 ? x.t.chr(p - 1) : (uint8_t)'\n') : x.t.chr(p);
+                const uint64_t* M = T + (size_t)cn * x.W;
+#pragma unroll
+                for (int w = 0; w < WB; ++w) Mn[w] = w < W ? M[w] : 0ull;
+            }
+            uint64_t carry = inj, last = 0;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) {   // row 0
                 const uint64_t old = Rw[0][w];
-                const uint64_t nv = ((old << 1) | carry) & M[w];
+                const uint64_t nv = ((old << 1) | carry) & Mw[w];
                 t0[w] = old;
                 t1[w] = nv;
                 Rw[0][w] = nv;
                 carry = old >> 63;
+                if (w == lw) last = nv;
             }
-            if ((Rw[0][lw] & fin) && (left ? x.left_ok(b) : x.right_ok(b))) {
+            const bool ok = left ? x.left_ok(b) : x.right_ok(b);
+            if ((last & fin) && ok) {
                 bound = b;
                 nerr = 0;
                 return true;
             }
-            for (int j = 1; j <= maxk; ++j) {   // 0x414640: rows 1..maxk
+            uint64_t top = 0;   // 0x414de3: the highest live row
+#pragma unroll
+            for (int w = 0; w < WB; ++w)
+                if (maxk == 0 && w < W) top |= w == lw ? t1[w] & alive_mask : t1[w];
+#pragma unroll
+            for (int j = 1; j <= KR; ++j) {   // 0x414640: rows 1..maxk
+                if (j > maxk) break;
                 uint64_t dc = 0, sc = inj, mc = inj;
-                for (int w = 0; w < W; ++w) {
+                last = 0;
+#pragma unroll
+                for (int w = 0; w < WB; ++w) {
                     uint64_t r = 0;
                     if (errs & PM_ERR_DEL) {
                         r = (t1[w] << 1) | dc;
@@ -423,39 +575,34 @@ __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool l
                         sc = t0[w] >> 63;
                     }
                     const uint64_t old = Rw[j][w];
-                    const uint64_t nv = (((old << 1) | mc) & M[w]) | r;
+                    const uint64_t nv = (((old << 1) | mc) & Mw[w]) | r;
                     mc = old >> 63;
                     t0[w] = old;
                     t1[w] = nv;
                     Rw[j][w] = nv;
+                    if (w == lw) last = nv;
                 }
-                if ((Rw[j][lw] & fin) && (left ? x.left_ok(b) : x.right_ok(b))) {
-                    // the rows below j do not reach the end here (else they
-                    // had returned first): record, look for fewer errors
-                    int c2 = j;
-                    for (;;) {
-                        const int d = c2 - 1;
-                        if (d < 0) {
-                            bound = b;
-                            nerr = 0;
-                            return true;
-                        }
-                        if (!(Rw[d][lw] & fin)) {
-                            found = true;
-                            fb = b;
-                            best = c2;
-                            maxk = d;
-                            break;
-                        }
-                        c2 = d;
-                    }
+                if ((last & fin) && ok) {
+                    // the rows below j do not reach the end here (they had
+                    // returned or stopped here first): record, look for fewer
+                    // errors with the rows below
+                    found = true;
+                    fb = b;
+                    best = j;
+                    maxk = j - 1;
+                    top = 0;
+#pragma unroll
+                    for (int w = 0; w < WB; ++w)
+                        if (w < W) top |= w == lw ? Rw[j - 1][w] & alive_mask : Rw[j - 1][w];
                     break;
                 }
+                if (j == maxk) {
+#pragma unroll
+                    for (int w = 0; w < WB; ++w)
+                        if (w < W) top |= w == lw ? t1[w] & alive_mask : t1[w];
+                }
             }
-            bool alive = false;   // 0x414de3: the highest live row
-            for (int w = 0; w < lw; ++w) alive |= Rw[maxk][w] != 0;
-            alive |= (Rw[maxk][lw] & alive_mask) != 0;
-            if (!alive) break;
+            if (!top) break;
             if (left ? x.at_recbeg(p) : x.t.brk(p)) break;
             inj = 0;
         }
@@ -467,35 +614,28 @@ __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool l
 }
 
 // checkMatch 0x4151d0 + checkMatch1 0x414190 for candidate (pos, piece i)
-__device__ bool es_verify(const EsCtx& x, uint64_t pos, int i, uint64_t& mb, uint64_t& me) {
+template <int WB, int KR>
+__device__ bool es_verify(EsCtx& x, uint64_t pos, int i, uint64_t& mb, uint64_t& me) {
     const EsSlot& S = *x.S;
     const uint64_t rp = S.type == 3 ? pos - 1 : pos;   // 0x4152dc
+    const int L = S.L[i];
+    // the ring covers what the phases can read: back from pos (a read
+    // before the ring goes to memory) and m - L + k + 1 ahead
+    x.t.fill(pos + (uint64_t)(S.m - L + S.k + 2));
     if (x.t.brk(rp)) return false;                      // the record ends at rp
     const size_t per = (size_t)256 * S.W;
-    const int L = S.L[i];
-    uint64_t start, end;
-    int eL, eR;
-    if (!es_phase(x, x.tab + S.o_TL + per * i, pos, true, L, S.k, start, eL)) return false;
-    if (!es_phase(x, x.tab + S.o_TR + per * i, pos, false, S.m - L, S.k - eL, end, eR)) return false;
-    mb = start;
-    me = end;
-    return true;
-}
-
-// the pieces that match exactly at pos, as BNDM's surviving bits
-__device__ uint64_t es_pieces_at(const EsCtx& x, uint64_t pos) {
-    const EsSlot& S = *x.S;
-    const uint64_t* B = x.tab + S.o_B;
-    uint64_t D = 0;
-    for (int r = 0; r < S.np; ++r) {
-        bool ok = true;
-        for (int j = 0; j < S.mpc && ok; ++j) {
-            const int q = S.L[r] + j;
-            ok = (B[(size_t)x.t.raw(pos + j) * S.W + q / 64] >> (q % 64)) & 1;
-        }
-        if (ok) D |= 1ull << (r * S.mpc + S.mpc - 1);
+    int kmax = S.k;
+#pragma nounroll
+    for (int ph = 0; ph < 2; ++ph) {   // left, then right with what the left left of k
+        uint64_t bound;
+        int e;
+        if (!es_phase<WB, KR>(x, x.tab + (ph ? S.o_TR : S.o_TL) + per * i, pos, ph == 0, ph ? S.m - L : L, kmax, bound,
+                          e))
+            return false;
+        kmax -= e;
+        (ph ? me : mb) = bound;
     }
-    return D;
+    return true;
 }
 
 __global__ void k_es_heads(const uint64_t* __restrict__ keys, const uint64_t* total_d, uint64_t total_h,
@@ -511,7 +651,8 @@ __global__ void k_es_heads(const uint64_t* __restrict__ keys, const uint64_t* to
     }
 }
 
-__global__ void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens, const uint64_t* total_d,
+template <int WB, int KR>
+__global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens, const uint64_t* total_d,
                           uint64_t total_h, uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt, uint32_t G,
                           TextView tv) {
     const uint64_t total = total_d ? *total_d : total_h;
@@ -519,6 +660,8 @@ __global__ void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __res
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
         if (!(acc[i] & 2)) continue;
+        const long long t_start = clock64();   // EXPERIMENT
+        uint64_t n_iter = 0, n_ver = 0;          // EXPERIMENT
         uint64_t j = i + 1;   // the next cluster's head keeps bit 1 set whatever its owner writes
         while (j < total && !(acc[j] & 2)) ++j;
         const uint64_t lo = keys[i] & ES_POS_MASK, hi = keys[j - 1] & ES_POS_MASK;
@@ -526,32 +669,123 @@ __global__ void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __res
         const uint64_t nmax = j - i;
         uint64_t nout = 0;
         const int64_t slot = (int64_t)pid - P.pid_base;
-        if (slot >= 0 && slot < P.nslots) {
+        if (slot >= 0 && slot < P.nslots && P.mode != 1) {
             const EsSlot& S = P.slots[slot];
-            EsCtx x{&S, P.tab, EsText{tv, tv.n}, 0};
+            if (nmax == 1 && S.lone) {
+                // A lone start with substitutions only is what nrgrep prints:
+                // a verification from any candidate returns the window
+                // [pos - L, pos - L + m) (no indels: both phases have fixed
+                // lengths), i.e. one of the cluster's starts, so only s = lo;
+                // and some candidate leads to it (k + 1 pieces, at most k
+                // errors: one piece of the window is exact and its test bit
+                // is right (es_add_slot); the window and prefix scanners stop
+                // at every start of a match).  No text is read.
+                lens[i] = (uint32_t)S.m;
+                acc[i] = 3;
+                atomicAdd(&bcnt[i / C], 1u);
+                continue;
+            }
+            EsCtx x{&S, P.tab, EsText{tv, tv.n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}}, 0, S.errs, S.W,
+                    S.anchors};
             const uint64_t n = tv.n;
-            const uint64_t pmax = umin64(n, hi + (uint64_t)(S.m + S.k));
+            const int type = S.type, m = S.m, k = S.k, mpc = S.mpc, np = S.np;
+            // the ring starts where the left phase of the match at lo can
+            // reach (an earlier read goes to memory); it is filled only as
+            // far as the piece pass and each verification need
+            x.t.restart(lo > (uint64_t)(k + 2) ? lo - (uint64_t)(k + 2) : 0);
+            const uint64_t pmax = umin64(n, hi + (uint64_t)(m + k));
             // type 2: ABNDM windows of wend - wbeg - k characters must fit (0x413a5b)
-            const uint64_t wtail = (uint64_t)(S.wend - S.wbeg - S.k - 1);
-            const uint64_t lim2 = S.type == 2 ? (n > wtail ? n - wtail : 0) : n + 1;
-            uint64_t pos = S.type == 3 ? lo + 1 : lo;
-            uint64_t guard = (pmax - lo + 2) * (uint64_t)(S.np + 2) * 4;
-            while (pos <= pmax && guard--) {
-                bool hit = false;
-                uint64_t mb = 0, me = 0;
-                if (S.type == 1) {
-                    if (pos + (uint64_t)S.mpc <= n) {
-                        const uint64_t D = es_pieces_at(x, pos);
-                        for (int q = 0; q < S.np && !hit; ++q)
-                            if (D & S.test[q]) hit = es_verify(x, pos, q, mb, me);
+            const uint64_t wtail = (uint64_t)(S.wend - S.wbeg - k - 1);
+            const uint64_t lim2 = type == 2 ? (n > wtail ? n - wtail : 0) : n + 1;
+            // type 1: the packed shift-and over the window starts (see
+            // es_add_slot); flags bit d = the pieces' last bits survive at
+            // start fb + d.  Every start < n - mpc + 1 is tested (0x4137f2).
+            const uint64_t* Pt = P.tab + S.o_P;
+            const uint64_t pstart = S.pstart, pend = S.pend;
+            const uint64_t last_start = n >= (uint64_t)mpc ? n - (uint64_t)mpc : 0;   // starts <= this fit
+            uint64_t* dl = reinterpret_cast<uint64_t*>(es_lds + P.dl_off) + threadIdx.x * ES_SPAN;   // D per span start
+            uint64_t fb = 0;
+            uint32_t flags = 0;
+            bool fvalid = false;
+            uint64_t pos = type == 3 ? lo + 1 : lo;
+            uint64_t guard = (pmax - lo + 2) * (uint64_t)(np + 2) * 4;
+            uint32_t cand = 0;   // the pieces still to try at pos, in order
+            // Each round first moves every lane to its next (position, piece)
+            // candidate (the inner loop: cheap, divergent), then verifies them
+            // together, so a wave runs one verification chain per round, not
+            // one per lane or per piece.
+            for (;;) {
+                while (!cand && pos <= pmax && guard) {   // the next candidate position at or after pos
+                    --guard;
+                    ++n_iter;
+                    if (type != 1) {
+                        if (pos < lim2) cand = 1u;   // every start is the window / prefix candidate
+                        else ++pos;
+                        continue;
                     }
-                } else if (pos < lim2) {
-                    hit = es_verify(x, pos, 0, mb, me);
+                    if (!fvalid || pos < fb || pos >= fb + ES_SPAN) {
+                        // the next ES_SPAN starts: feed characters pos ..
+                        // pos + ES_SPAN + mpc - 2 from a fresh state
+                        uint64_t st = 0, tfeed = pos;
+                        fb = pos;
+                        flags = 0;
+                        fvalid = true;
+                        const uint64_t tend = umin64(pos + ES_SPAN, pmax + 1) + (uint64_t)mpc - 1;
+                        x.t.fill(tend);
+                        while (tfeed < tend) {
+                            // 8 characters from the ring, their 8 masks in one
+                            // round trip; a break's mask comes from the file's
+                            // own byte (a header line: rare)
+                            uint8_t cc[8];
+                            uint64_t mk[8];
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) cc[q] = tfeed + q < tend ? x.t.ring(tfeed + q) : (uint8_t)'\n';
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) mk[q] = Pt[cc[q]];
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) {
+                                const uint64_t t = tfeed + q;
+                                if (cc[q] == (uint8_t)'\n' && t < n) mk[q] = Pt[x.t.raw_slow(t)];
+                                if (t >= tend) mk[q] = 0ull;
+                            }
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) {
+                                st = ((st << 1) | pstart) & mk[q];
+                                const uint64_t t = tfeed + q + 1 - (uint64_t)mpc;   // the start whose window ends here
+                                if ((st & pend) && tfeed + q + 1 >= fb + (uint64_t)mpc && t < fb + ES_SPAN) {
+                                    flags |= 1u << (uint32_t)(t - fb);
+                                    dl[t - fb] = st & pend;
+                                }
+                            }
+                            tfeed += 8;
+                        }
+                    }
+                    const uint32_t f = flags >> (uint32_t)(pos - fb);
+                    if (!f) {   // no piece before the span's end
+                        pos = fb + ES_SPAN;
+                        continue;
+                    }
+                    pos += (uint64_t)__builtin_ctz(f);
+                    if (pos > pmax) break;
+                    if (pos <= last_start) {
+                        // BNDM's surviving bits at pos, then the pieces
+                        // checkMatch is called for, in order (0x41384b)
+                        const uint64_t D = dl[pos - fb];
+                        for (int q = 0; q < np; ++q)
+                            if (D & S.test[q]) cand |= 1u << q;
+                    }
+                    if (!cand) ++pos;
                 }
-                if (!hit) {
-                    ++pos;
+                if (!cand) break;
+                const int q = __builtin_ctz(cand);
+                cand &= cand - 1;
+                uint64_t mb = 0, me = 0;
+                ++n_ver;
+                if (P.mode == 2 || !es_verify<WB, KR>(x, pos, q, mb, me)) {
+                    if (!cand) ++pos;
                     continue;
                 }
+                cand = 0;
                 if (nout < nmax) {   // matches start at distinct candidates: never more than the cluster holds
                     keys[i + nout] = (pid << 48) | mb;
                     lens[i + nout] = (uint32_t)(me - mb);
@@ -561,20 +795,46 @@ __global__ void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __res
                 }
                 if (me >= n) break;   // 0x4022eb: a match that ends the region ends the search
                 x.R = me;
-                pos = S.type == 3 ? me + 1 : me;
+                pos = type == 3 ? me + 1 : me;
             }
         }
         for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
+        if (P.mode >= 3) {   // EXPERIMENT: one hit per cluster, its length = the walk's cycles / 16, its size
+            lens[i] = (uint32_t)umin64((uint64_t)(clock64() - t_start) / 16, 0xffffffu) | (uint32_t)(umin64(j - i, 255) << 24);
+            if (P.mode == 4) lens[i] = (uint32_t)(umin64(n_iter, 4095) | (umin64(n_ver, 4095) << 12) | (umin64(j - i, 255) << 24));
+            acc[i] = 3;
+            for (uint64_t q = i + 1; q < j; ++q) acc[q] = 0;
+            for (uint64_t q = 0; q < nout; ++q) atomicSub(&bcnt[(i + q) / C], 1u);
+            atomicAdd(&bcnt[i / C], 1u);
+        }
     }
 }
 
 }  // namespace
 
-void es_launch(const EsPrep& P, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
-               uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
-    const uint32_t blocks = 1024;
-    hipLaunchKernelGGL(k_es_heads, dim3(blocks), dim3(256), 0, s, keys, total_d, total_h, acc, bcnt, G, P.gap_max);
-    hipLaunchKernelGGL(k_es_walk, dim3(blocks), dim3(64), 0, s, P, keys, lens, total_d, total_h, acc, bcnt, G, tv);
+void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint64_t cap, uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
+    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, keys, total_d, total_h, acc, bcnt, G, P0.gap_max);
+    // one thread per list entry (heads walk their cluster, the rest return):
+    // every cluster's walk is a chain of dependent steps, so the grid is as
+    // wide as the list, up to 32 Ki waves
+    EsPrep P = P0;
+    // a candidate's phases reach m + k + 1 back and forth, the piece pass
+    // ES_SPAN + mpc (< 80) ahead, the refills ES_CHUNK more; the ring keeps
+    // the last win positions filled
+    uint32_t win = 64;
+    while (win < (uint32_t)P.gap_max + ES_SPAN + 64 + ES_CHUNK) win <<= 1;
+    P.win = win <= 512 ? win : 0;   // wider patterns read memory directly
+    P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
+    P.mode = getenv("PM_ES_MODE") ? atoi(getenv("PM_ES_MODE")) : 0;   // EXPERIMENT
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(32768, std::max<uint64_t>(1, (cap + ES_THREADS - 1) / ES_THREADS));
+    // WB: position words; KR: the rows unrolled (k <= 3, the common case,
+    // keeps the row vectors in few registers)
+    auto kern = P.kmax <= 3 ? (P.wmax <= 1 ? k_es_walk<1, 3> : P.wmax == 2 ? k_es_walk<2, 3> : k_es_walk<4, 3>)
+                            : (P.wmax <= 1 ? k_es_walk<1, PM_MAX_K> : P.wmax == 2 ? k_es_walk<2, PM_MAX_K>
+                                                                                  : k_es_walk<4, PM_MAX_K>);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), (size_t)P.dl_off + ES_THREADS * ES_SPAN * 8, s, P, keys, lens, total_d,
+                       total_h, acc, bcnt, G, tv);
     HIPCHK(hipGetLastError());
 }
 

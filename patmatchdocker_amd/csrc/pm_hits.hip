@@ -506,6 +506,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             HIPCHK(hipGetLastError());
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
                                                      pack ? (int)(pos_bits + slot_bits) : 64, s));
+            (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
             if (pack) {
                 hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
                                    pos_bits);
@@ -878,7 +879,8 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     const uint32_t G = (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
     if (es && (flags & PM_REPORT_NRGREP)) {
         // nrgrep's esimple engine: its own candidate order and verify
-        es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, a.acc, a.bcnt, G, a.tv, s);
+        es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, total_on_device ? ws.cap : total_h, a.acc, a.bcnt, G,
+                  a.tv, s);
     } else {
         hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
         hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);

@@ -646,10 +646,12 @@ struct EsPlan {               // esimplePreproc 0x415540
 EsPlan es_plan(const uint64_t* B, int W, int m, int k);
 
 struct EsSlot {               // one pattern of a report (device, uploaded as is)
-    int32_t m, k, errs, type, mpc, wbeg, wend, W, np, anchors, pid, pad;
+    int32_t m, k, errs, type, mpc, wbeg, wend, W, np, anchors, pid, lone;
     int32_t L[PM_MAX_K + 1];
     uint64_t test[PM_MAX_K + 1];   // type 1: the piece test mask (0x41384b)
     uint64_t o_B, o_TL, o_TR;      // word offsets of B / TL[np] / TR[np] ([256][W] each) in the table blob
+    uint64_t o_P;                  // type 1: word offset of the packed piece table [256]
+    uint64_t pstart, pend;         // type 1: the pieces' first / last bits in the packed table
 };
 struct EsBuild {
     std::vector<EsSlot> slots;
@@ -659,6 +661,8 @@ struct EsUpload {
     size_t o_slots = 0, o_tab = 0;
     int nslots = 0;
     int32_t pid_base = 0;
+    int wmax = 1;   // position words of the widest pattern
+    int kmax = 1;   // the largest k
 };
 struct EsPrep {
     const EsSlot* slots = nullptr;
@@ -666,6 +670,11 @@ struct EsPrep {
     int nslots = 0;
     int32_t pid_base = 0;   // slot = pattern id - pid_base
     int32_t gap_max = 0;    // candidate starts further apart never interact
+    int wmax = 1;           // position words of the widest pattern (1, 2 or 4)
+    int kmax = 1;           // the largest k (rows of the verify automaton)
+    uint32_t dl_off = 0;    // k_es_walk's piece words in its LDS
+    int mode = 0;           // EXPERIMENT
+    uint32_t win = 0;       // k_es_walk's per-thread text ring (bytes, a power of two; 0: none)
 };
 // slots get pattern ids pid, in increasing order
 void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, uint32_t flags, int32_t pid);
@@ -673,9 +682,10 @@ void es_upload(const EsBuild& b, Upload& up, EsUpload& u);
 int32_t es_gap(const EsBuild& b);
 EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max);
 // k_es_heads + k_es_walk on s: rewrites keys/lens in place and sets acc
-// (bit 0 = reported) and the per-chunk counts bcnt for k_rep_scatter
+// (bit 0 = reported) and the per-chunk counts bcnt for k_rep_scatter; cap:
+// the list's capacity (the grid covers it)
 void es_launch(const EsPrep& P, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
-               uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s);
+               uint64_t cap, uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s);
 
 // es (optional): the list holds a class sequence's candidate starts at
 // k > 0 and the selection is nrgrep's esimple engine (pm_esimple.hip)

@@ -171,3 +171,45 @@ def test_esimple_peptides(engine, oracle_mod):
                 assert _pairs(res[0]) == want, (p, k, types, oracle_mod.nrgrep_plan(prog, k))
     finally:
         db.close()
+
+
+def test_esimple_lone_starts_and_the_shift_quirk(engine, oracle_mod):
+    """Substitution-only lone starts are reported without a walk -- except
+    where a piece's test bit is wrong (bit >= 32 under the 32-bit shift,
+    0x41384b): this 35-mer at k = 2 has pieces of 11 at 1, 12, 23 (end bits
+    10, 21, 32; the last tested as bit 0), so a copy whose two errors sit in
+    the first two pieces is never verified by nrgrep.  Copies of both kinds,
+    far apart, inside lines of random DNA."""
+    rng = random.Random(21)
+    motif = "TCGACCTTTCGCCAGGAACTAGAGACTATTGCTGA"
+    prog = compile_pattern(motif)
+    plan = oracle_mod.nrgrep_plan(prog, 2)
+    assert plan["type"] == 1 and plan["piece_len"] == 11 and plan["L"] == [1, 12, 23], plan
+
+    def edit(copy, j):
+        copy[j] = "ACGT"[("ACGT".index(copy[j]) + 1) % 4]
+
+    recs = []
+    for r in range(30):
+        seq = [rng.choice("ACGT") for _ in range(3000)]
+        for c in range(4):
+            at = 70 * (3 + 10 * c) + 5   # inside one 70-column line
+            copy = list(motif)
+            if c % 2 == 0:
+                edit(copy, 1 + rng.randrange(11))
+                edit(copy, 12 + rng.randrange(11))
+            else:
+                edit(copy, 23 + rng.randrange(12))
+            seq[at:at + len(motif)] = copy
+        s = "".join(seq)
+        recs.append(">c%d\n%s\n" % (r, "\n".join(s[i:i + 70] for i in range(0, len(s), 70))))
+    text = "".join(recs).encode()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        res, _ = engine.scan(db, [prog], k=2, types="s")
+        want = oracle_mod.scan_esimple(text, prog, 2, "s", skip_headers=True)
+        leftmost = oracle_mod.scan_reported(text, prog, 2, "s", skip_headers=True, report="leftmost")
+        assert len(leftmost) >= 120 and len(want) <= len(leftmost) - 55   # the copies nrgrep never verifies
+        assert _pairs(res[0]) == want
+    finally:
+        db.close()

@@ -8,7 +8,7 @@ out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 if [ $# -gt 0 ]; then
-    timeout -k 10 400 python -u -m pytest "$@" -q -rf --timeout 240 --timeout-method thread > "$out/tests.txt" 2>&1
+    timeout -k 10 700 python -u -m pytest "$@" -q -rf --timeout 240 --timeout-method thread > "$out/tests.txt" 2>&1
     rc=$?; echo "tests rc=$rc" >> "$out/status.txt"; tail -3 "$out/tests.txt"
     [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
@@ -16,8 +16,8 @@ timeout -k 10 300 python -u bench.py > "$out/bench.json" 2> "$out/bench.err"
 rc=$?; echo "bench rc=$rc" >> "$out/status.txt"; cat "$out/bench.json"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --types ids > "$out/bench_ids.json" 2> "$out/bench_ids.err"
 rc=$?; echo "bench_ids rc=$rc" >> "$out/status.txt"; cat "$out/bench_ids.json"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --steps 20 --no-cpu-baseline > "$out/prof_bench.json" 2> "$out/prof.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- python3 bench.py --steps 20 --no-cpu-baseline > "$out/prof_bench.json" 2> "$out/prof.err"
 rc=$?; echo "prof rc=$rc" >> "$out/status.txt"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_ids" -o run -- python3 bench.py --types ids --steps 10 --no-cpu-baseline > "$out/prof_ids_bench.json" 2> "$out/prof_ids.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_ids" -o run -- python3 bench.py --types ids --steps 10 --no-cpu-baseline > "$out/prof_ids_bench.json" 2> "$out/prof_ids.err"
 rc=$?; echo "prof_ids rc=$rc" >> "$out/status.txt"
 find "$out" -name "*kernel_stats.csv" | head

@@ -260,6 +260,41 @@ __global__ void k_lane_flags(uint64_t ntiles, const uint2* __restrict__ bo, uint
     if (lane == 0) lflag[t] = bal;
 }
 
+// The position-contiguous copy (lin): lin[p / 32] holds bit p % 32 of the
+// hi, lo, brk and oth planes of positions p..  One block per tile: the
+// tile's 2048 physical words of hl and bo in LDS, then every lin word of the
+// tile is a 32 x 1-bit gather over one lane's column (conflict-free: a wave
+// reads 64 consecutive physical words).  Random access to a few consecutive
+// positions (the report pass's text windows) then costs one line instead of
+// one line per position.
+__global__ __launch_bounds__(256) void k_build_lin(uint64_t ntiles, const uint2* __restrict__ hl,
+                                                   const uint2* __restrict__ bo, uint4* __restrict__ lin) {
+    __shared__ uint2 shl[STREAM], sbo[STREAM];
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        for (uint32_t i = threadIdx.x; i < STREAM; i += blockDim.x) {
+            shl[i] = hl[t * TILE_WORDS + i];
+            sbo[i] = bo[t * TILE_WORDS + i];
+        }
+        __syncthreads();
+        for (uint32_t o = threadIdx.x; o < STREAM; o += blockDim.x) {
+            // lin word o of the tile: stream b = o / 64, logical words
+            // 32 j .. 32 j + 31 (j = o % 64), i.e. physical i * 64 + j
+            const uint32_t b = o >> 6, j = o & 63;
+            uint32_t h = 0, l = 0, k = 0, x = 0;
+#pragma unroll 8
+            for (uint32_t i = 0; i < 32; ++i) {
+                const uint2 d = shl[i * 64 + j], e = sbo[i * 64 + j];
+                h |= ((d.x >> b) & 1u) << i;
+                l |= ((d.y >> b) & 1u) << i;
+                k |= ((e.x >> b) & 1u) << i;
+                x |= ((e.y >> b) & 1u) << i;
+            }
+            lin[t * STREAM + o] = make_uint4(h, l, k, x);
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void k_pack_bytes(const uint8_t* __restrict__ raw, uint64_t n, uint64_t nalloc,
                              uint8_t* __restrict__ out) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -376,6 +411,10 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     hipLaunchKernelGGL(k_lane_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
                        db->lflag);
     HIPCHK(hipGetLastError());
+    db->lin = dalloc<uint4>(db, db->ntiles * STREAM);   // 0.5 byte per position
+    hipLaunchKernelGGL(k_build_lin, dim3((uint32_t)std::min<uint64_t>(db->ntiles, 8192)), dim3(256), 0, s, db->ntiles,
+                       db->hl, db->bo, db->lin);
+    HIPCHK(hipGetLastError());
     require(db->nflag < (1ull << 32), "too many exception words for the run index", PM_E_UNSUPPORTED);
     db->xint = dalloc<uint32_t>(db, db->nflag);
     db->xedge = dalloc<uint32_t>(db, db->nflag);
@@ -432,7 +471,7 @@ void free_db(pm_db* db) {
     }
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
-    void* ptrs[] = {db->hl, db->bo, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
+    void* ptrs[] = {db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)

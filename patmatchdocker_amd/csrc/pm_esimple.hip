@@ -339,7 +339,7 @@ namespace {
 
 constexpr uint64_t ES_POS_MASK = (1ull << 48) - 1;
 
-constexpr int ES_CHUNK = 8;      // positions staged per refill of a thread's window
+constexpr int ES_CHUNK = 16;     // positions staged per refill of a thread's window
 constexpr int ES_THREADS = 64;   // walk threads per block (one wave)
 constexpr int ES_SPAN = 16;      // window starts whose pieces one shift-and pass finds
 
@@ -369,60 +369,45 @@ struct EsText {
         return tv.nuc_layout ? nuc_char_at(tv.nuc, p) : tv.bytes[p];
     }
     __device__ void restart(uint64_t p) { r.lo = r.hi = p; }
-    // extend the ring to cover [.., upto).  A chunk's loads are all
-    // unconditional (addresses clamped into the chunk) so that the chunk
-    // costs one memory round trip plus, only where a lane of the tile holds
-    // an exception (lflag), a second one for the bo words.  Every position
-    // is its own line of hl (the stream layout), so no more positions are
-    // fetched than asked for.
+    // extend the ring to cover [.., upto).  NUC: one 16-byte load of the
+    // position-contiguous planes (pm_db::lin) gives 32 positions; an
+    // "other" byte (N, IUPAC letters) comes from the side tables (rare).
+    // BYTE: ES_CHUNK bytes per round trip.
     __device__ void fill(uint64_t upto) {
         if (r.mask == ~0u) return;
         while (r.hi < upto) {
             const uint64_t b = r.hi;
-            const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
             if (b >= n) {
+                const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
                 for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = (uint8_t)'\n';
+                r.hi = b + cnt;
             } else if (tv.nuc_layout) {
-                const uint64_t pl = umin64(b + cnt, n) - 1;   // the chunk's last position in the file
-                const uint64_t lf0 = tv.lflag[b / TILE_POS], lf1 = tv.lflag[pl / TILE_POS];
-                uint2 d[ES_CHUNK];
-#pragma unroll
-                for (int q = 0; q < ES_CHUNK; ++q) d[q] = tv.nuc.hl[loc_of(umin64(b + q, pl)).word];
-                uint2 e[ES_CHUNK];
-                const uint64_t w0 = loc_of(b).word;   // a line the first round brought in
-#pragma unroll
-                for (int q = 0; q < ES_CHUNK; ++q) {
-                    const uint64_t p = umin64(b + q, pl);
-                    const uint64_t lf = p / TILE_POS == b / TILE_POS ? lf0 : lf1;
-                    const bool flagged = (lf >> ((uint32_t)(p % STREAM) >> 5)) & 1ull;
-                    e[q] = tv.nuc.bo[flagged ? loc_of(p).word : w0];
-                    if (!flagged) e[q] = make_uint2(0u, 0u);
-                }
-#pragma unroll
-                for (int q = 0; q < ES_CHUNK; ++q) {
-                    if ((uint32_t)q >= cnt) break;
-                    const uint64_t p = b + q;
-                    const uint32_t bit = (uint32_t)((p % TILE_POS) / STREAM);
+                const uint4 v = tv.lin[b >> 5];
+                const uint64_t e = umin64(((b >> 5) + 1) << 5, upto);   // through the word's end (or upto)
+                for (uint64_t p = b; p < e; ++p) {
+                    const uint32_t i = (uint32_t)(p & 31);
                     uint8_t c;
-                    if (p >= n || ((e[q].x >> bit) & 1)) {   // a break or past the end
+                    if (p >= n || ((v.z >> i) & 1)) {   // a break or past the end
                         c = (uint8_t)'\n';
-                    } else if ((e[q].y >> bit) & 1) {
-                        c = nuc_char_at(tv.nuc, p);   // an exception byte: the side tables (rare)
+                    } else if ((v.w >> i) & 1) {
+                        c = nuc_char_at(tv.nuc, p);
                     } else {
-                        const uint32_t code = (((d[q].x >> bit) & 1) << 1) | ((d[q].y >> bit) & 1);
+                        const uint32_t code = (((v.x >> i) & 1) << 1) | ((v.y >> i) & 1);
                         c = (uint8_t)((0x54474341u >> (8 * code)) & 0xff);
                     }
                     es_lds[r.base + ((uint32_t)p & r.mask)] = c;
                 }
+                r.hi = e;
             } else {
+                const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
                 uint8_t c[ES_CHUNK];
 #pragma unroll
                 for (int q = 0; q < ES_CHUNK; ++q) c[q] = tv.bytes[umin64(b + q, n)];   // bytes[n..] pad with '\n'
 #pragma unroll
                 for (int q = 0; q < ES_CHUNK; ++q)
                     if ((uint32_t)q < cnt) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = b + q < n ? c[q] : (uint8_t)'\n';
+                r.hi = b + cnt;
             }
-            r.hi = b + cnt;
             if (r.hi - r.lo > r.mask + 1) r.lo = r.hi - (r.mask + 1);
         }
     }
@@ -820,10 +805,10 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
     // wide as the list, up to 32 Ki waves
     EsPrep P = P0;
     // a candidate's phases reach m + k + 1 back and forth, the piece pass
-    // ES_SPAN + mpc (< 80) ahead, the refills ES_CHUNK more; the ring keeps
-    // the last win positions filled
+    // ES_SPAN + mpc ahead, a refill to the end of a 32-position word; the
+    // ring keeps the last win positions (a read before them goes to memory)
     uint32_t win = 64;
-    while (win < (uint32_t)P.gap_max + ES_SPAN + 64 + ES_CHUNK) win <<= 1;
+    while (win < (uint32_t)P.gap_max + ES_SPAN + 32) win <<= 1;
     P.win = win <= 512 ? win : 0;   // wider patterns read memory directly
     P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
     P.mode = getenv("PM_ES_MODE") ? atoi(getenv("PM_ES_MODE")) : 0;   // EXPERIMENT

@@ -826,7 +826,8 @@ void retire_buffers(pm_hits* h, hipStream_t s) {
 }  // namespace
 
 TextView text_view(const pm_db* db) {
-    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag};
+    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag,
+                    db->lin};
 }
 
 bool report_needed(uint32_t flags, bool cross) {

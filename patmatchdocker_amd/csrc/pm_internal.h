@@ -313,6 +313,7 @@ struct pm_db : pm_lane {
     uint8_t* xbytes = nullptr;
     uint64_t* xword = nullptr;   // NUC: physical word of each flagged word
     uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
+    uint4* lin = nullptr;        // NUC: {hi, lo, brk, oth} bits of positions 32 q .. 32 q + 31 (k_build_lin)
     // NUC, runs of N: per flagged word, the bits whose position is preceded
     // by an exception and followed by RUN_SKIP more "other" bytes (xint);
     // the flagged words with a bit outside that mask (xedge, nedge of them;
@@ -602,6 +603,7 @@ struct TextView {
     uint64_t n;
     int nuc_layout;
     const uint64_t* lflag;  // NUC: per tile, the lanes with an exception (a clean lane holds no header byte)
+    const uint4* lin;       // NUC: the position-contiguous planes (pm_db::lin)
 };
 TextView text_view(const pm_db* db);
 // true when the pass changes anything for `flags` (cross: candidates may

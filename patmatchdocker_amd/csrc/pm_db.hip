@@ -573,7 +573,7 @@ uint8_t* Upload::commit(pm_db* db) {
 }
 
 NucView nuc_view(const pm_db* db) {
-    return NucView{db->hl, db->bo, db->sbflag, db->sbbase, db->xbytes};
+    return NucView{db->hl, db->bo, db->sbflag, db->sbbase, db->xbytes, db->lin};
 }
 
 }  // namespace pm

@@ -382,7 +382,7 @@ struct EsText {
                 for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = (uint8_t)'\n';
                 r.hi = b + cnt;
             } else if (tv.nuc_layout) {
-                const uint4 v = tv.lin[b >> 5];
+                const uint4 v = tv.nuc.lin[b >> 5];
                 const uint64_t e = umin64(((b >> 5) + 1) << 5, upto);   // through the word's end (or upto)
                 for (uint64_t p = b; p < e; ++p) {
                     const uint32_t i = (uint32_t)(p & 31);
@@ -623,17 +623,37 @@ __device__ bool es_verify(EsCtx& x, uint64_t pos, int i, uint64_t& mb, uint64_t&
     return true;
 }
 
+// a record break before p (p > 0): '\n', a header byte
+__device__ inline bool es_brk_before(const TextView& tv, uint64_t p) {
+    if (tv.nuc_layout) {
+        const uint4 v = tv.nuc.lin[(p - 1) >> 5];
+        return (v.z >> ((uint32_t)(p - 1) & 31)) & 1;
+    }
+    return tv.bytes[p - 1] == (uint8_t)'\n';
+}
+
 __global__ void k_es_heads(const uint64_t* __restrict__ keys, const uint64_t* total_d, uint64_t total_h,
-                           uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt, uint32_t G, int32_t gap) {
+                           uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt, uint32_t G, int32_t gap, int lines,
+                           TextView tv) {
     const uint64_t total = total_d ? *total_d : total_h;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t b = tid; b < G; b += stride) bcnt[b] = 0u;
     for (uint64_t i = tid; i < total; i += stride) {
-        // a new pattern (high key bits) or a gap wider than any phase reads
-        const bool head = i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap;
+        // a new pattern (high key bits) or a gap wider than any phase reads;
+        // lines: also every start of a line (records never interact)
+        bool head = i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap;
+        if (lines && !head) {
+            const uint64_t p = keys[i] & ES_POS_MASK;
+            head = p > 0 && es_brk_before(tv, p);
+        }
         acc[i] = head ? 2 : 0;
     }
+}
+
+__global__ void k_es_iota(uint64_t* __restrict__ keys, uint64_t n, uint64_t pid) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = (pid << 48) | i;
 }
 
 template <int WB, int KR>
@@ -678,7 +698,9 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
             // reach (an earlier read goes to memory); it is filled only as
             // far as the piece pass and each verification need
             x.t.restart(lo > (uint64_t)(k + 2) ? lo - (uint64_t)(k + 2) : 0);
-            const uint64_t pmax = umin64(n, hi + (uint64_t)(m + k));
+            // lines (every position is a key): the cluster is one line and
+            // its break, the next line is another cluster's
+            const uint64_t pmax = P.lines ? hi : umin64(n, hi + (uint64_t)(m + k));
             // type 2: ABNDM windows of wend - wbeg - k characters must fit (0x413a5b)
             const uint64_t wtail = (uint64_t)(S.wend - S.wbeg - k - 1);
             const uint64_t lim2 = type == 2 ? (n > wtail ? n - wtail : 0) : n + 1;
@@ -799,7 +821,8 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
 
 void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint64_t cap, uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
-    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, keys, total_d, total_h, acc, bcnt, G, P0.gap_max);
+    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, keys, total_d, total_h, acc, bcnt, G, P0.gap_max,
+                       P0.lines, tv);
     // one thread per list entry (heads walk their cluster, the rest return):
     // every cluster's walk is a chain of dependent steps, so the grid is as
     // wide as the list, up to 32 Ki waves
@@ -826,6 +849,33 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
 }  // namespace pm
 
 using namespace pm;
+
+namespace pm {
+
+pm_hits* es_all_positions(pm_db* db, int32_t pattern_id) {
+    require(db->n <= ES_ALL_MAX, "deletions with k >= the pattern length: the file is too large for the GPU walk",
+            PM_E_UNSUPPORTED);
+    pm_hits* h = new pm_hits();
+    h->device = db->device;
+    h->count = db->n;
+    try {
+        h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(db->n, 1) * 8, &h->keys_cap));
+        h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(db->n, 1) * 4, &h->lens_cap));
+        if (db->n) {
+            hipLaunchKernelGGL(k_es_iota, dim3(blocks_for(db->n, 256)), dim3(256), 0, db->stream, h->keys, db->n,
+                               (uint64_t)pattern_id);
+            HIPCHK(hipGetLastError());
+        }
+    } catch (...) {
+        pool_put(h->device, h->keys, h->keys_cap);
+        pool_put(h->device, h->lens, h->lens_cap);
+        delete h;
+        throw;
+    }
+    return h;
+}
+
+}  // namespace pm
 
 extern "C" int pm_esimple_plan(int m, int words, const uint64_t* byte_mask, int k, int32_t* out) {
     return guarded([&] {

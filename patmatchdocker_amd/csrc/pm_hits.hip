@@ -826,8 +826,7 @@ void retire_buffers(pm_hits* h, hipStream_t s) {
 }  // namespace
 
 TextView text_view(const pm_db* db) {
-    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag,
-                    db->lin};
+    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag};
 }
 
 bool report_needed(uint32_t flags, bool cross) {

@@ -157,6 +157,7 @@ struct NucView {
     const uint2 *hl, *bo;
     const uint32_t *sbflag, *sbbase;
     const uint8_t* xbytes;
+    const uint4* lin;   // the position-contiguous planes (pm_db::lin)
 };
 
 // index of flagged physical word w in the compacted side tables
@@ -603,7 +604,6 @@ struct TextView {
     uint64_t n;
     int nuc_layout;
     const uint64_t* lflag;  // NUC: per tile, the lanes with an exception (a clean lane holds no header byte)
-    const uint4* lin;       // NUC: the position-contiguous planes (pm_db::lin)
 };
 TextView text_view(const pm_db* db);
 // true when the pass changes anything for `flags` (cross: candidates may
@@ -675,9 +675,15 @@ struct EsPrep {
     int wmax = 1;           // position words of the widest pattern (1, 2 or 4)
     int kmax = 1;           // the largest k (rows of the verify automaton)
     uint32_t dl_off = 0;    // k_es_walk's piece words in its LDS
+    int lines = 0;          // every position is a key (es_all_positions): clusters are lines
     int mode = 0;           // EXPERIMENT
     uint32_t win = 0;       // k_es_walk's per-thread text ring (bytes, a power of two; 0: none)
 };
+// Deletions with k >= m (the whole pattern may be deleted): every position
+// can be reported, so the walk takes every position as a key and each line
+// as a cluster (EsPrep::lines).  At most ES_ALL_MAX positions.
+constexpr uint64_t ES_ALL_MAX = 1ull << 28;
+pm_hits* es_all_positions(pm_db* db, int32_t pattern_id);
 // slots get pattern ids pid, in increasing order
 void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, uint32_t flags, int32_t pid);
 void es_upload(const EsBuild& b, Upload& up, EsUpload& u);

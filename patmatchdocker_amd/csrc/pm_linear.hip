@@ -291,24 +291,19 @@ __device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint
             const int64_t q = q0 + i;
             uint8_t c = 0, f = 0;
             if (q >= 0 && (uint64_t)q < a.n) {
-                const Loc l = loc_of((uint64_t)q);
-                // the exception plane only for words that hold an exception
-                // (sbflag: 1 bit per word, 1/64 of the plane, cache-resident):
-                // most of a window's words are clean, so about half the HBM
-                // lines of a gather
-                const uint32_t sf = a.nuc.sbflag[l.word >> 5];
-                const uint2 hv = a.nuc.hl[l.word];
-                uint32_t brk = 0, oth = 0;
-                if ((sf >> (l.word & 31)) & 1) {
-                    const uint2 ex = a.nuc.bo[l.word];
-                    brk = (ex.x >> l.bit) & 1;
-                    oth = (ex.y >> l.bit) & 1;
-                }
+                // the span is 1-2 words of the position-contiguous planes
+                // (the lanes share their lines); an exception's byte comes
+                // from the side tables
+                const uint4 v = a.nuc.lin[(uint64_t)q >> 5];
+                const uint32_t i5 = (uint32_t)q & 31;
+                const uint32_t brk = (v.z >> i5) & 1, oth = (v.w >> i5) & 1;
                 f = (uint8_t)((brk | oth) | (brk << 1));
-                if (brk | oth)
+                if (brk | oth) {
+                    const Loc l = loc_of((uint64_t)q);
                     c = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, l.word) * 32 + l.bit];
-                else
-                    c = (uint8_t)((0x54474341u >> (8 * ((((hv.x >> l.bit) & 1) << 1) | ((hv.y >> l.bit) & 1)))) & 0xff);
+                } else {
+                    c = (uint8_t)((0x54474341u >> (8 * ((((v.x >> i5) & 1) << 1) | ((v.y >> i5) & 1)))) & 0xff);
+                }
             }
             wch[i] = c;
             wfl[i] = f;
@@ -421,18 +416,13 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
             const int64_t q = q0 + lane;
             const bool in_span = lane < span, in_file = in_span && q >= 0 && (uint64_t)q < a.n;
             uint32_t h = 0, l = 0, br = 0, ot = 0;
-            Loc lc{0, 0};
-            if (in_file) {
-                lc = loc_of((uint64_t)q);
-                const uint32_t sf = a.nuc.sbflag[lc.word >> 5];   // the exception plane only for flagged words
-                const uint2 hv = a.nuc.hl[lc.word];
-                h = (hv.x >> lc.bit) & 1;
-                l = (hv.y >> lc.bit) & 1;
-                if ((sf >> (lc.word & 31)) & 1) {
-                    const uint2 ex = a.nuc.bo[lc.word];
-                    br = (ex.x >> lc.bit) & 1;
-                    ot = (ex.y >> lc.bit) & 1;
-                }
+            if (in_file) {   // 1-2 words of the position-contiguous planes for the whole span
+                const uint4 v = a.nuc.lin[(uint64_t)q >> 5];
+                const uint32_t i5 = (uint32_t)q & 31;
+                h = (v.x >> i5) & 1;
+                l = (v.y >> i5) & 1;
+                br = (v.z >> i5) & 1;
+                ot = (v.w >> i5) & 1;
             }
             const uint64_t H = __builtin_amdgcn_ballot_w64(h != 0), L = __builtin_amdgcn_ballot_w64(l != 0);
             const uint64_t BR = __builtin_amdgcn_ballot_w64(br != 0), OT = __builtin_amdgcn_ballot_w64(ot != 0);
@@ -446,8 +436,10 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
             // the lane's byte when it is compared by value (N: its mark)
             uint8_t ch = 'N';
             const bool byval = ((EXN | EXL) >> lane) & 1;
-            if ((EXL >> lane) & 1)
+            if ((EXL >> lane) & 1) {
+                const Loc lc = loc_of((uint64_t)q);
                 ch = a.nuc.xbytes[(uint64_t)exception_index(a.nuc.sbflag, a.nuc.sbbase, lc.word) * 32 + lc.bit];
+            }
             for (int c = 0; c < nc; ++c) {
                 const uint64_t vb = __builtin_amdgcn_ballot_w64(byval && ((s_cm[c][ch >> 5] >> (ch & 31)) & 1));
                 if (lane == c) mv[c] = (~vec_mismatch(H, L, s_csub[c]) & ~EX) | vb;

@@ -476,8 +476,11 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // engine does (pm_esimple.hip); its walk computes the ends itself
     const bool esimple = (flags & PM_ESIMPLE) && k > 0 && (flags & PM_REPORT_NRGREP);
     // a match must consume a pattern position (pm_oracle.c reports
-    // non-empty matches only): with deletions that needs min_len > k
-    require(!(errs & PM_ERR_DEL) || min_len > k,
+    // non-empty matches only): with deletions that needs min_len > k --
+    // except for nrgrep's esimple report, whose walk takes every position
+    // of every line (es_all_positions; nrgrep then prints empty matches too)
+    const bool all_pos = esimple && (errs & PM_ERR_DEL) && min_len <= k;
+    require(!(errs & PM_ERR_DEL) || min_len > k || all_pos,
             "deletions with k >= the shortest match length are not supported by the GPU scan", PM_E_UNSUPPORTED);
     const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
     require((uint64_t)max_len + ins_extra < (1ull << 31), "max_len out of range");
@@ -546,7 +549,8 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         es_upload(esb, up, esu);
     }
     uint8_t* d_up = up.commit(db);
-    const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
+    EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
+    esp.lines = all_pos ? 1 : 0;
 
     NfaArgs a{};
     a.nuc = nuc_view(db);
@@ -632,7 +636,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // a class sequence on the nucleotide planes: the bit-sliced start pass
     // (pm_ids.hip), 32 streams per lane instead of one
     const bool ids = nuc && W == 1 && a.shift_only && !cross && !unbounded && use_ids_kernel(db);
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    for (int attempt = 0; attempt < 2 && !all_pos; ++attempt) {
         sb = make_sink(db, 1, db->n, expected);
         a.sink = sb.sink();
         bool launched = false;
@@ -657,8 +661,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         require(attempt == 0, "internal: hit bins overflowed twice");
         expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
     }
-    double kms = ev.ms() + carry_ms;
-    pm_hits* h = sink_to_hits(db, sb, counts, total);
+    double kms = all_pos ? 0.0 : ev.ms() + carry_ms;
+    if (all_pos) total = db->n;
+    pm_hits* h = all_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
     if (total && !esimple) {
         a.starts = h->keys;
         a.nstarts = total;

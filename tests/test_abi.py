@@ -104,7 +104,8 @@ def test_specialized_kernel_shares_strand_blocks(tmp_path, monkeypatch):
 
 def test_route_indels():
     """-k with insertions/deletions routes to the Glushkov kernels; deletions
-    with k >= the shortest match are refused loudly (no CPU fallback)."""
+    with k >= the shortest match of a non-simple pattern are refused loudly
+    (no CPU fallback)."""
     from patmatchdocker_amd import engine
     from patmatchdocker_amd._lib import UnsupportedOnGPU
     from patmatchdocker_amd.regex import compile_pattern
@@ -115,6 +116,9 @@ def test_route_indels():
     assert engine.route(lin, engine.NUC, 0, "") == "linear"
     assert engine.parse_error_types(2, "") == "ids"
     assert engine.error_mask("ids") == 7 and engine.error_mask("d") == 2
+    # deletions with k >= the shortest match: class sequences only (the
+    # esimple walk over every line), other patterns are refused loudly
+    assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 3, "d") == "nfa"
     with pytest.raises(UnsupportedOnGPU):
-        engine.route(compile_pattern("(RGD)"), engine.BYTE, 3, "d")
+        engine.route(compile_pattern("(RG?D)"), engine.BYTE, 2, "d")
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 2, "d") == "nfa"

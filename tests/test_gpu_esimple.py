@@ -213,3 +213,32 @@ def test_esimple_lone_starts_and_the_shift_quirk(engine, oracle_mod):
         assert _pairs(res[0]) == want
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("layout", ["nuc", "byte"])
+def test_deletions_reaching_the_pattern_length(engine, oracle_mod, layout):
+    """-k 3ids on a 3-residue pattern (patmatch.py:308-314 passes it through):
+    every position of every line is a candidate and nrgrep prints empty
+    matches too; the walk takes each line as a cluster
+    (pm_esimple.hip, es_all_positions)."""
+    rng = random.Random(31)
+    if layout == "nuc":
+        text = dense_fasta(33, "TACGATT", n_records=4, rec_len=3000, width=61)
+        cases = [("ACG", 3, "ids"), ("GAT", 4, "d"), ("[AC]GT", 3, "ds"), ("AT", 2, "id")]
+    else:
+        recs = []
+        for r in range(20):
+            seq = "".join(rng.choice(AMINO) for _ in range(rng.randint(50, 400)))
+            recs.append(">p%d\n%s\n" % (r, "\n".join(seq[i:i + 60] for i in range(0, len(seq), 60))))
+        text = "".join(recs).encode()
+        cases = [("CWK", 3, "ids"), ("LL", 2, "d"), ("[ST]P", 2, "ids")]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC if layout == "nuc" else engine.BYTE)
+    try:
+        for pat, k, types in cases:
+            prog = compile_pattern(pat)
+            res, _ = engine.scan(db, [prog], k=k, types=types)
+            want = oracle_mod.scan_esimple(text, prog, k, types, skip_headers=True)
+            assert len(want) > 100
+            assert _pairs(res[0]) == want, (pat, k, types)
+    finally:
+        db.close()

@@ -216,3 +216,22 @@ def test_ids_reports_differ_from_shortest_end(oracle_mod):
     got = oracle_mod.scan_esimple(text, prog, 1, "ids")
     assert got == esimple_model.report(text, prog, 1, "ids", oracle_mod.nrgrep_plan(prog, 1))
     assert got != oracle_mod.scan_reported(text, prog, 1, "ids", report="leftmost")
+
+
+@pytest.mark.parametrize("case", [("ACG", 3, "ids"), ("ACG", 4, "d"), ("AT", 2, "id"), ("GAT", 3, "ds"),
+                                  ("[AC]GT", 3, "ids")])
+def test_deletions_reaching_the_pattern_length(oracle_mod, case):
+    """k >= m with deletions (the whole pattern may be deleted; the web form
+    lets a 3-residue pattern run at -k 3ids, patmatch.py:308-314): the plan
+    falls back to the forward prefix scanner (simpleFindBest finds no window,
+    no pieces fit), every position is a candidate, and empty matches are
+    printed -- the replay and the model agree."""
+    from tests.fastagen import dna_fasta
+    pat, k, types = case
+    prog = compile_pattern(pat)
+    plan = oracle_mod.nrgrep_plan(prog, k)
+    assert plan["type"] == 3
+    text = dna_fasta(5, n_records=3, max_len=200, width=30)
+    got = oracle_mod.scan_esimple(text, prog, k, types)
+    assert got == esimple_model.report(text, prog, k, types, plan)
+    assert any(b == e for b, e in got) and any(e > b for b, e in got)

@@ -32,8 +32,11 @@ def test_refusals_left():
         engine.route(prog("A" * 200), engine.NUC, 8, "s")
     with pytest.raises(_lib.UnsupportedOnGPU):
         engine.route(prog("ACG"), engine.NUC, 16, "s")
+    # every position deletable: class sequences run the esimple walk over
+    # every line (pm_esimple.hip), other patterns are refused
+    assert engine.route(prog("ACG"), engine.NUC, 3, "ids") == "nfa"
     with pytest.raises(_lib.UnsupportedOnGPU):
-        engine.route(prog("ACG"), engine.NUC, 3, "ids")   # every position deletable
+        engine.route(prog("AC?G"), engine.NUC, 2, "ids")
 
 
 def test_nfa_words():

@@ -226,8 +226,8 @@ def main():
             engine.destroy_hits(h)
         keys = shards.to_global(keys, offset)
         # substitutions only: every hit of pattern p is prog.m long, so only
-        # the keys travel (to rank 0)
-        out = shards.gather_hits(keys, None, fixed_len=[p.m for p in progs])
+        # the keys travel (to rank 0, which rebuilds the lengths)
+        out = shards.gather_hits(keys, lens, fixed_len=[p.m for p in progs])
         return out, ms
 
     def ids_step():

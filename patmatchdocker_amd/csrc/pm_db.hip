@@ -237,6 +237,40 @@ __global__ void k_run_interior(uint64_t nflag, const uint64_t* __restrict__ xwor
     if (xoth[idx] & ~m) xedge_oth[atomicAdd(&nedge[1], 1ull)] = (uint32_t)idx;
 }
 
+// The "other"-position list (pm_db::xlist): one thread per edge word of
+// xedge_oth; every "other" bit outside the run interiors becomes one entry
+// e | ahead << 48 | prev << 56, read from the position-contiguous planes.
+// fill = false: count only.
+__global__ void k_build_xlist(uint64_t nedge, const uint32_t* __restrict__ xedge_oth,
+                              const uint64_t* __restrict__ xword, const uint32_t* __restrict__ xoth,
+                              const uint32_t* __restrict__ xint, const uint4* __restrict__ lin, uint64_t nlin,
+                              uint64_t* __restrict__ out, unsigned long long* __restrict__ cnt, int fill) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nedge) return;
+    const uint32_t idx = xedge_oth[t];
+    const uint64_t w = xword[idx];
+    const uint64_t tile = w / TILE_WORDS;
+    const uint32_t lw = logical_word((uint32_t)(w % TILE_WORDS));
+    if (lw >= STREAM) return;   // a halo copy of a main word
+    uint32_t bits = xoth[idx] & ~xint[idx];
+    if (!fill) {
+        if (bits) atomicAdd(cnt, (unsigned long long)__popc(bits));
+        return;
+    }
+    const auto exc = [&](uint64_t p) {   // brk | oth at position p (past the planes: a break)
+        if ((p >> 5) >= nlin) return true;
+        const uint4 v = lin[p >> 5];
+        return (((v.z | v.w) >> (uint32_t)(p & 31)) & 1u) != 0;
+    };
+    for (; bits; bits &= bits - 1) {
+        const uint64_t e = pos_of(tile, lw, (uint32_t)__builtin_ctz(bits));
+        const uint64_t prev = e > 0 && exc(e - 1) ? 1 : 0;
+        uint64_t ahead = 0;
+        while (ahead < 255 && exc(e + ahead)) ++ahead;
+        out[atomicAdd(cnt, 1ull)] = e | ahead << XL_AHEAD_SHIFT | prev << XL_PREV_SHIFT;
+    }
+}
+
 // oth = oth & ~brk everywhere (a header byte is a break, not an "other")
 __global__ void k_clean_oth(uint64_t nwords, uint2* __restrict__ bo) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -430,6 +464,21 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipStreamSynchronize(s));
     db->nedge = reinterpret_cast<uint64_t*>(h)[0];
     db->nedge_oth = reinterpret_cast<uint64_t*>(h)[1];
+    // the "other"-position list: count, allocate, fill
+    for (int fill = 0; fill < 2; ++fill) {
+        HIPCHK(hipMemsetAsync(d_nedge, 0, sizeof(uint64_t), s));
+        if (db->nedge_oth)
+            hipLaunchKernelGGL(k_build_xlist, dim3(blocks_for(db->nedge_oth, 256)), dim3(256), 0, s, db->nedge_oth,
+                               db->xedge_oth, db->xword, db->xoth, db->xint, db->lin, db->ntiles * STREAM, db->xlist,
+                               d_nedge, fill);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(h, d_nedge, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (!fill) {
+            db->nxlist = reinterpret_cast<uint64_t*>(h)[0];
+            db->xlist = dalloc<uint64_t>(db, db->nxlist);
+        }
+    }
     if (env_flag("PM_DEBUG_DB", false))
         fprintf(stderr, "pm_db: n=%llu tiles=%llu flagged words=%llu other words=%llu edge words=%llu (other %llu)\n",
                 (unsigned long long)db->n, (unsigned long long)db->ntiles, (unsigned long long)db->nflag,
@@ -472,7 +521,7 @@ void free_db(pm_db* db) {
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
     void* ptrs[] = {db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->bytes, db->bytes_raw, db->ws_post.p,
+                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

@@ -632,22 +632,65 @@ __device__ inline bool es_brk_before(const TextView& tv, uint64_t p) {
     return tv.bytes[p - 1] == (uint8_t)'\n';
 }
 
-__global__ void k_es_heads(const uint64_t* __restrict__ keys, const uint64_t* total_d, uint64_t total_h,
-                           uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt, uint32_t G, int32_t gap, int lines,
-                           TextView tv) {
+// Cluster heads: a new pattern (high key bits) or a gap wider than any phase
+// reads; with `lines` also every start of a line (records never interact).
+__device__ inline bool es_head(const uint64_t* keys, uint64_t i, int32_t gap, int lines, const TextView& tv) {
+    if (i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap) return true;
+    if (!lines) return false;
+    const uint64_t p = keys[i] & ES_POS_MASK;
+    return p > 0 && es_brk_before(tv, p);
+}
+
+// One thread per list entry: acc = 2 at a cluster head, else 0.  A lone
+// start of a slot whose lone starts need no walk (EsSlot::lone) is settled
+// here (acc = 3, its length m); every other head goes to the walk list
+// (one atomic per wave).
+__global__ __launch_bounds__(256) void k_es_heads(EsPrep P, const uint64_t* __restrict__ keys,
+                                                  uint32_t* __restrict__ lens, const uint64_t* total_d,
+                                                  uint64_t total_h, uint8_t* __restrict__ acc,
+                                                  uint32_t* __restrict__ wlist, uint32_t* __restrict__ wcount,
+                                                  TextView tv) {
     const uint64_t total = total_d ? *total_d : total_h;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t b = tid; b < G; b += stride) bcnt[b] = 0u;
-    for (uint64_t i = tid; i < total; i += stride) {
-        // a new pattern (high key bits) or a gap wider than any phase reads;
-        // lines: also every start of a line (records never interact)
-        bool head = i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap;
-        if (lines && !head) {
-            const uint64_t p = keys[i] & ES_POS_MASK;
-            head = p > 0 && es_brk_before(tv, p);
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x - lane; i0 < total; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        bool walk = false;
+        if (i < total) {
+            uint8_t a = 0;
+            if (es_head(keys, i, P.gap_max, P.lines, tv)) {
+                a = 2;
+                walk = true;
+                const int64_t slot = (int64_t)(keys[i] >> 48) - P.pid_base;
+                if (!P.lines && slot >= 0 && slot < P.nslots && (i + 1 == total || es_head(keys, i + 1, P.gap_max, 0, tv))) {
+                    const EsSlot& S = P.slots[slot];
+                    if (S.lone) {
+                        // A lone start with substitutions only is what nrgrep
+                        // prints: a verification from any candidate returns
+                        // the window [pos - L, pos - L + m) (no indels: both
+                        // phases have fixed lengths), i.e. one of the
+                        // cluster's starts, so only this one; and some
+                        // candidate leads to it (k + 1 pieces, at most k
+                        // errors: one piece of the window is exact and its
+                        // test bit is right (es_add_slot); the window and
+                        // prefix scanners stop at every start of a match).
+                        // No text is read.
+                        lens[i] = (uint32_t)S.m;
+                        a = 3;
+                        walk = false;
+                    }
+                }
+            }
+            acc[i] = a;
         }
-        acc[i] = head ? 2 : 0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(walk);
+        if (m) {
+            uint32_t base = 0;
+            const uint32_t first = (uint32_t)__builtin_ctzll(m);
+            if (lane == first) base = atomicAdd(wcount, (uint32_t)__builtin_popcountll(m));
+            base = __shfl(base, (int)first, 64);
+            if (walk) wlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)i;
+        }
     }
 }
 
@@ -656,17 +699,19 @@ __global__ void k_es_iota(uint64_t* __restrict__ keys, uint64_t n, uint64_t pid)
     if (i < n) keys[i] = (pid << 48) | i;
 }
 
+// One thread per cluster of the walk list (grid-stride): nrgrep's candidate
+// order over the cluster's text; the printed matches are written in place
+// from the head on (acc bit 0), every other entry of the cluster is cleared.
 template <int WB, int KR>
-__global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens, const uint64_t* total_d,
-                          uint64_t total_h, uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt, uint32_t G,
-                          TextView tv) {
+__global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                        const uint64_t* total_d, uint64_t total_h,
+                                                        uint8_t* __restrict__ acc, const uint32_t* __restrict__ wlist,
+                                                        const uint32_t* __restrict__ wcount, TextView tv) {
     const uint64_t total = total_d ? *total_d : total_h;
-    const uint64_t C = (total + G - 1) / G;   // the scatter's chunk
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-        if (!(acc[i] & 2)) continue;
-        const long long t_start = clock64();   // EXPERIMENT
-        uint64_t n_iter = 0, n_ver = 0;          // EXPERIMENT
+    const uint32_t nw = *wcount;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nw; t += stride) {
+        const uint64_t i = wlist[t];
         uint64_t j = i + 1;   // the next cluster's head keeps bit 1 set whatever its owner writes
         while (j < total && !(acc[j] & 2)) ++j;
         const uint64_t lo = keys[i] & ES_POS_MASK, hi = keys[j - 1] & ES_POS_MASK;
@@ -674,22 +719,8 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         const uint64_t nmax = j - i;
         uint64_t nout = 0;
         const int64_t slot = (int64_t)pid - P.pid_base;
-        if (slot >= 0 && slot < P.nslots && P.mode != 1) {
+        if (slot >= 0 && slot < P.nslots) {
             const EsSlot& S = P.slots[slot];
-            if (nmax == 1 && S.lone) {
-                // A lone start with substitutions only is what nrgrep prints:
-                // a verification from any candidate returns the window
-                // [pos - L, pos - L + m) (no indels: both phases have fixed
-                // lengths), i.e. one of the cluster's starts, so only s = lo;
-                // and some candidate leads to it (k + 1 pieces, at most k
-                // errors: one piece of the window is exact and its test bit
-                // is right (es_add_slot); the window and prefix scanners stop
-                // at every start of a match).  No text is read.
-                lens[i] = (uint32_t)S.m;
-                acc[i] = 3;
-                atomicAdd(&bcnt[i / C], 1u);
-                continue;
-            }
             EsCtx x{&S, P.tab, EsText{tv, tv.n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}}, 0, S.errs, S.W,
                     S.anchors};
             const uint64_t n = tv.n;
@@ -724,7 +755,6 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
             for (;;) {
                 while (!cand && pos <= pmax && guard) {   // the next candidate position at or after pos
                     --guard;
-                    ++n_iter;
                     if (type != 1) {
                         if (pos < lim2) cand = 1u;   // every start is the window / prefix candidate
                         else ++pos;
@@ -787,8 +817,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                 const int q = __builtin_ctz(cand);
                 cand &= cand - 1;
                 uint64_t mb = 0, me = 0;
-                ++n_ver;
-                if (P.mode == 2 || !es_verify<WB, KR>(x, pos, q, mb, me)) {
+                if (!es_verify<WB, KR>(x, pos, q, mb, me)) {
                     if (!cand) ++pos;
                     continue;
                 }
@@ -797,7 +826,6 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                     keys[i + nout] = (pid << 48) | mb;
                     lens[i + nout] = (uint32_t)(me - mb);
                     acc[i + nout] = (nout == 0 ? 2 : 0) | 1;
-                    atomicAdd(&bcnt[(i + nout) / C], 1u);
                     ++nout;
                 }
                 if (me >= n) break;   // 0x4022eb: a match that ends the region ends the search
@@ -806,26 +834,33 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
             }
         }
         for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
-        if (P.mode >= 3) {   // EXPERIMENT: one hit per cluster, its length = the walk's cycles / 16, its size
-            lens[i] = (uint32_t)umin64((uint64_t)(clock64() - t_start) / 16, 0xffffffu) | (uint32_t)(umin64(j - i, 255) << 24);
-            if (P.mode == 4) lens[i] = (uint32_t)(umin64(n_iter, 4095) | (umin64(n_ver, 4095) << 12) | (umin64(j - i, 255) << 24));
-            acc[i] = 3;
-            for (uint64_t q = i + 1; q < j; ++q) acc[q] = 0;
-            for (uint64_t q = 0; q < nout; ++q) atomicSub(&bcnt[(i + q) / C], 1u);
-            atomicAdd(&bcnt[i / C], 1u);
-        }
     }
+}
+
+// kept entries (acc bit 0) per chunk of C = ceil(total / G) entries, for
+// k_rep_scatter
+__global__ __launch_bounds__(256) void k_es_count(const uint64_t* total_d, uint64_t total_h,
+                                                  const uint8_t* __restrict__ acc, uint32_t* __restrict__ bcnt) {
+    __shared__ uint32_t red[4];
+    const uint64_t total = total_d ? *total_d : total_h;
+    const uint64_t C = (total + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
+    uint32_t c = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) c += acc[i] & 1;
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 }  // namespace
 
 void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
-               uint64_t cap, uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
-    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, keys, total_d, total_h, acc, bcnt, G, P0.gap_max,
-                       P0.lines, tv);
-    // one thread per list entry (heads walk their cluster, the rest return):
-    // every cluster's walk is a chain of dependent steps, so the grid is as
-    // wide as the list, up to 32 Ki waves
+               uint8_t* acc, uint32_t* wlist, uint32_t* wcount, uint32_t* bcnt, uint32_t G, const TextView& tv,
+               hipStream_t s) {
+    HIPCHK(hipMemsetAsync(wcount, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, P0, keys, lens, total_d, total_h, acc, wlist, wcount,
+                       tv);
     EsPrep P = P0;
     // a candidate's phases reach m + k + 1 back and forth, the piece pass
     // ES_SPAN + mpc ahead, a refill to the end of a 32-position word; the
@@ -834,15 +869,21 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
     while (win < (uint32_t)P.gap_max + ES_SPAN + 32) win <<= 1;
     P.win = win <= 512 ? win : 0;   // wider patterns read memory directly
     P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
-    P.mode = getenv("PM_ES_MODE") ? atoi(getenv("PM_ES_MODE")) : 0;   // EXPERIMENT
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(32768, std::max<uint64_t>(1, (cap + ES_THREADS - 1) / ES_THREADS));
+    // one wave per block (a cluster's walk is a chain of dependent steps,
+    // and the ring takes LDS): 8 per CU, all resident, striding over the
+    // walk list (its length is on the device)
+    int dev = 0, ncu = 0;
+    HIPCHK(hipGetDevice(&dev));
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const uint32_t blocks = (uint32_t)std::max(1, ncu) * 8;
     // WB: position words; KR: the rows unrolled (k <= 3, the common case,
     // keeps the row vectors in few registers)
     auto kern = P.kmax <= 3 ? (P.wmax <= 1 ? k_es_walk<1, 3> : P.wmax == 2 ? k_es_walk<2, 3> : k_es_walk<4, 3>)
                             : (P.wmax <= 1 ? k_es_walk<1, PM_MAX_K> : P.wmax == 2 ? k_es_walk<2, PM_MAX_K>
                                                                                   : k_es_walk<4, PM_MAX_K>);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), (size_t)P.dl_off + ES_THREADS * ES_SPAN * 8, s, P, keys, lens, total_d,
-                       total_h, acc, bcnt, G, tv);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), (size_t)P.dl_off + ES_THREADS * ES_SPAN * 8, s, P, keys,
+                       lens, total_d, total_h, acc, wlist, wcount, tv);
+    hipLaunchKernelGGL(k_es_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);
     HIPCHK(hipGetLastError());
 }
 

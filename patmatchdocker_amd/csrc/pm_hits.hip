@@ -836,6 +836,7 @@ bool report_needed(uint32_t flags, bool cross) {
 ReportWs report_ws(pm_db* db, uint64_t cap_items) {
     Carve c;
     const size_t o_t = c.take(8), o_c = c.take(8), o_m = c.take(REP_G_MAX * 8), o_b = c.take(REP_G_MAX * 4),
+                 o_wc = c.take(8), o_w = c.take(std::max<uint64_t>(cap_items, 1) * 4),
                  o_a = c.take(std::max<uint64_t>(cap_items, 1));
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_rep, c.off));
     ReportWs ws;
@@ -844,6 +845,8 @@ ReportWs report_ws(pm_db* db, uint64_t cap_items) {
     ws.bmax = reinterpret_cast<uint64_t*>(d + o_m);
     ws.bcnt = reinterpret_cast<uint32_t*>(d + o_b);
     ws.acc = d + o_a;
+    ws.wlist = reinterpret_cast<uint32_t*>(d + o_w);
+    ws.wcount = reinterpret_cast<uint32_t*>(d + o_wc);
     ws.cap = std::max<uint64_t>(cap_items, 1);
     return ws;
 }
@@ -879,8 +882,7 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     const uint32_t G = (uint32_t)std::min<uint64_t>(REP_G_MAX, std::max<uint64_t>(REP_G, ws.cap / 16384));
     if (es && (flags & PM_REPORT_NRGREP)) {
         // nrgrep's esimple engine: its own candidate order and verify
-        es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, total_on_device ? ws.cap : total_h, a.acc, a.bcnt, G,
-                  a.tv, s);
+        es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, a.acc, ws.wlist, ws.wcount, a.bcnt, G, a.tv, s);
     } else {
         hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
         hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);

@@ -160,6 +160,11 @@ struct NucView {
     const uint4* lin;   // the position-contiguous planes (pm_db::lin)
 };
 
+// the "other"-position list (pm_db::xlist)
+constexpr uint64_t XL_POS_MASK = (1ull << 48) - 1;
+constexpr int XL_AHEAD_SHIFT = 48;
+constexpr int XL_PREV_SHIFT = 56;
+
 // index of flagged physical word w in the compacted side tables
 __device__ inline uint32_t exception_index(const uint32_t* sbflag, const uint32_t* sbbase, uint64_t w) {
     const uint32_t f = sbflag[w >> 5];
@@ -324,6 +329,12 @@ struct pm_db : pm_lane {
     uint64_t nedge = 0;
     uint32_t* xedge_oth = nullptr;
     uint64_t nedge_oth = 0;
+    // NUC: every "other" position outside the run interiors, as
+    // e | ahead << 48 | prev << 56 (XL_*): ahead = consecutive exception
+    // positions from e on (at most 255), prev = e - 1 is an exception
+    // (k_others_lane's work list, built once per database)
+    uint64_t* xlist = nullptr;
+    uint64_t nxlist = 0;
     uint8_t* bytes = nullptr;    // BYTE alphabet: folded bytes, header lines stored as '\n'
     uint8_t* bytes_raw = nullptr;   // BYTE alphabet: folded bytes as in the file (headers kept)
     hipStream_t stream = nullptr;
@@ -628,6 +639,8 @@ struct ReportWs {
     uint64_t* bmax = nullptr;
     uint32_t* bcnt = nullptr;
     uint8_t* acc = nullptr;
+    uint32_t* wlist = nullptr;   // esimple: the clusters to walk
+    uint32_t* wcount = nullptr;
     uint64_t cap = 0;
 };
 ReportWs report_ws(pm_db* db, uint64_t cap_items);
@@ -676,7 +689,6 @@ struct EsPrep {
     int kmax = 1;           // the largest k (rows of the verify automaton)
     uint32_t dl_off = 0;    // k_es_walk's piece words in its LDS
     int lines = 0;          // every position is a key (es_all_positions): clusters are lines
-    int mode = 0;           // EXPERIMENT
     uint32_t win = 0;       // k_es_walk's per-thread text ring (bytes, a power of two; 0: none)
 };
 // Deletions with k >= m (the whole pattern may be deleted): every position
@@ -689,11 +701,12 @@ void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, u
 void es_upload(const EsBuild& b, Upload& up, EsUpload& u);
 int32_t es_gap(const EsBuild& b);
 EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max);
-// k_es_heads + k_es_walk on s: rewrites keys/lens in place and sets acc
-// (bit 0 = reported) and the per-chunk counts bcnt for k_rep_scatter; cap:
-// the list's capacity (the grid covers it)
+// k_es_heads + k_es_walk + k_es_count on s: rewrites keys/lens in place and
+// sets acc (bit 0 = reported) and the per-chunk counts bcnt (G chunks) for
+// k_rep_scatter; wlist / wcount: the walk list (one entry per list item)
 void es_launch(const EsPrep& P, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
-               uint64_t cap, uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s);
+               uint8_t* acc, uint32_t* wlist, uint32_t* wcount, uint32_t* bcnt, uint32_t G, const TextView& tv,
+               hipStream_t s);
 
 // es (optional): the list holds a class sequence's candidate starts at
 // k > 0 and the selection is nrgrep's esimple engine (pm_esimple.hip)

@@ -357,6 +357,90 @@ __device__ inline void vec_add(uint64_t x, uint64_t& c0, uint64_t& c1, uint64_t&
     c1 ^= cy0;
     ge4 |= cy1;
 }
+// The lane form of the exception pass (line-bounded scans whose classes are
+// all A/C/G/T-only or '.'): one LANE per entry of the database's
+// "other"-position list (pm_db::xlist, built at load time), so no selection
+// pass and no byte gathers.  An "other" byte then mismatches every A/C/G/T
+// class and matches '.', and a break kills, so the planes decide every
+// window: the lane loads the position-contiguous planes (pm_db::lin) of the
+// 2 maxlen - 1 positions around e as 64-bit vectors (three 16-byte loads)
+// and tests the windows owned by e (no exception between their start and e)
+// bit-parallel over their starts, the count bit-sliced.  A run tail whose
+// window at e starts with `jdead` exception bytes (k + 1 mismatches for
+// every pattern) is skipped from the list entry alone.
+struct LaneArgs {
+    const uint64_t* list;
+    uint64_t nlist;
+    const uint4* lin;
+    uint64_t nlin, n;
+    const uint8_t* csub;      // chunk: [P][64] A/C/G/T subset of each position's class, | 16 for '.'
+    const int32_t* lengths;   // chunk
+    int P, k, pattern_base, maxlen, jdead;
+    uint64_t* out;
+    uint32_t* seg_cnt;
+    const uint64_t* slot_base;
+    const uint32_t* slot_cap;
+    uint32_t nout, tiles_per_out;
+};
+
+__device__ inline uint4 lin_word(const LaneArgs& a, int64_t w) {
+    return (w < 0 || (uint64_t)w >= a.nlin) ? make_uint4(0u, 0u, ~0u, 0u) : a.lin[w];   // outside: breaks
+}
+__device__ inline uint64_t span64(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t off) {
+    const uint64_t lo = ((uint64_t)v1 << 32) | v0;
+    return off ? (lo >> off) | ((uint64_t)v2 << (64 - off)) : lo;
+}
+
+__global__ __launch_bounds__(256) void k_others_lane(LaneArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < a.nlist; t += stride) {
+        const uint64_t it = a.list[t];
+        const uint64_t e = it & XL_POS_MASK;
+        const int ahead = (int)((it >> XL_AHEAD_SHIFT) & 255), prev = (int)((it >> XL_PREV_SHIFT) & 1);
+        // e - 1 an exception: e owns only the window starting at e
+        if ((prev && ahead >= a.jdead) || e >= a.n) continue;
+        const int c = a.maxlen - 1;                 // span index of e
+        const int64_t q0 = (int64_t)e - c;          // span: positions q0 .. q0 + 63
+        const int64_t w0 = q0 >> 5;                 // (floor)
+        const uint32_t off = (uint32_t)(q0 & 31);
+        const uint4 v0 = lin_word(a, w0), v1 = lin_word(a, w0 + 1), v2 = lin_word(a, w0 + 2);
+        const uint64_t H = span64(v0.x, v1.x, v2.x, off), L = span64(v0.y, v1.y, v2.y, off);
+        const uint64_t B = span64(v0.z, v1.z, v2.z, off), O = span64(v0.w, v1.w, v2.w, off);
+        // windows starting after the last exception before e (those before
+        // are owned by it, or killed)
+        const uint64_t Eb = (B | O) & ((1ull << c) - 1);
+        const int own = Eb ? 64 - __builtin_clzll(Eb) : 0;
+        for (int p = 0; p < a.P; ++p) {
+            const int len = a.lengths[p];
+            const int ulo = own > c - len + 1 ? own : c - len + 1;
+            if (ulo > c) continue;
+            const uint8_t* cs = a.csub + p * 64;
+            uint64_t c0 = 0, c1 = 0, ge4 = 0, kill = 0;
+            for (int j = 0; j < len; ++j) {
+                kill |= B >> j;
+                const uint32_t sub = cs[j];
+                if (sub & 16) continue;   // '.': every byte
+                vec_add((vec_mismatch(H, L, sub) | O) >> j, c0, c1, ge4);
+            }
+            uint64_t dead = ge4 | kill;
+            switch (a.k) {
+                case 0: dead |= c0 | c1; break;
+                case 1: dead |= c1; break;
+                case 2: dead |= c1 & c0; break;
+                default: break;
+            }
+            uint64_t live = ~dead & (((2ull << c) - 1) & ~((1ull << ulo) - 1));
+            for (; live; live &= live - 1) {
+                const uint64_t s = (uint64_t)(q0 + __builtin_ctzll(live));
+                const uint32_t slot = (uint32_t)(a.pattern_base + p);
+                const uint64_t og = (s / TILE_POS) / a.tiles_per_out;
+                const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nout + og], 1u);
+                if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
+            }
+        }
+    }
+}
+
 // Phase 2 for large batches (k_batch_scan's exception windows), one WAVE per
 // exception bit e, with the work split per CLASS: a batch of hundreds of
 // IUPAC motifs uses a handful of classes (A, C, G, T, the two-base codes,
@@ -1371,6 +1455,25 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         const size_t o_acgt = up.add(class_acgt, (size_t)n_classes);
         const size_t o_any = up.add(class_is_any, (size_t)n_classes);
         const size_t o_jsel = up.add(jsel.data(), jsel.size());
+        // k_others_lane: per (pattern, position) the class's A/C/G/T subset,
+        // | 16 for '.'; lane_cls[p]: every class of pattern p is A/C/G/T-only
+        // or '.' (an "other" byte is then a mismatch or a match without
+        // looking at its value)
+        std::vector<uint8_t> csub((size_t)n_patterns * 64, 0), lane_cls(n_patterns, 1);
+        for (int p = 0; p < n_patterns; ++p)
+            for (int j = 0; j < lengths[p]; ++j) {
+                const int c = pos_class[64 * p + j];
+                const uint32_t* cb = class_bytes + 8 * c;
+                bool acgt_only = true;
+                for (int w = 0; w < 8 && acgt_only; ++w) {
+                    uint32_t bits = cb[w];
+                    if (w == 2) bits &= ~((1u << ('A' - 64)) | (1u << ('C' - 64)) | (1u << ('G' - 64)) | (1u << ('T' - 64)));
+                    acgt_only = bits == 0;
+                }
+                if (!acgt_only && !class_is_any[c]) lane_cls[p] = 0;
+                csub[(size_t)64 * p + j] = (uint8_t)((class_acgt[c] & 15) | (class_is_any[c] ? 16 : 0));
+            }
+        const size_t o_csub = up.add(csub.data(), csub.size());
         // k > 0: nrgrep's esimple engine decides which overlapping window
         // is printed (pm_esimple.hip)
         EsBuild esb;
@@ -1430,6 +1533,22 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         auto launch_others = [&](const Chunk& ch, hipStream_t os, const SinkBuffers& sb, uint64_t nout,
                                  uint64_t tiles_per_out) {
             const bool use_edge = edge_ok(ch.base, ch.P);
+            const int maxlen = *std::max_element(lengths + ch.base, lengths + ch.base + ch.P);
+            bool lane = !cross && use_edge && 2 * maxlen - 1 <= 64;
+            for (int p = ch.base; p < ch.base + ch.P && lane; ++p) lane = lane_cls[p] != 0;
+            if (lane) {
+                // the lane form over the database's "other"-position list
+                if (!db->nxlist) return;
+                int jdead = 0;   // a run tail's window at e with this many exceptions first is dead
+                for (int p = ch.base; p < ch.base + ch.P; ++p) jdead = std::max(jdead, (int)jsel[(size_t)p * 4 + k] + 1);
+                LaneArgs la{db->xlist, db->nxlist, db->lin, db->ntiles * STREAM, db->n, d_up + o_csub + 64 * ch.base,
+                            reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, k, ch.base, maxlen, jdead,
+                            sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)tiles_per_out};
+                hipLaunchKernelGGL(k_others_lane, dim3((uint32_t)std::min<uint64_t>(8192, blocks_for(db->nxlist, 256))),
+                                   dim3(256), 0, os, la);
+                HIPCHK(hipGetLastError());
+                return;
+            }
             // line-bounded: only words with an "other" byte can own a window
             const uint32_t* edge = cross ? db->xedge : db->xedge_oth;
             const uint64_t nedge = cross ? db->nedge : db->nedge_oth;

@@ -36,6 +36,7 @@
 #include "pm_internal.h"
 
 #include <cmath>
+#include <map>
 
 namespace pm {
 
@@ -301,9 +302,64 @@ void es_add_slot(EsBuild& b, const uint64_t* B, int W, int m, int k, int errs, u
     b.slots.push_back(s);
 }
 
+// The walk's tables over a compact alphabet: bytes whose rows agree in every
+// table of every slot share a code (a DNA query: A, C, G, T, '\n' and "the
+// rest"), code 0 is '\n' alone (a break).  The tables then shrink from 256
+// rows to a few and k_es_walk keeps them, and the byte -> code map, in LDS:
+// its per-step lookups are LDS reads instead of a chain of global loads.
 void es_upload(const EsBuild& b, Upload& up, EsUpload& u) {
-    u.o_slots = up.add(b.slots.data(), b.slots.size() * sizeof(EsSlot));
-    u.o_tab = up.add(b.tab.data(), b.tab.size() * sizeof(uint64_t));
+    std::vector<std::vector<uint64_t>> sig(256);
+    for (int c = 0; c < 256; ++c)
+        for (const EsSlot& sl : b.slots) {
+            const size_t W = sl.W, per = 256 * W;
+            for (size_t w = 0; w < W; ++w) {
+                sig[c].push_back(b.tab[sl.o_B + c * W + w]);
+                for (int i = 0; i < sl.np; ++i) {
+                    sig[c].push_back(b.tab[sl.o_TL + per * i + c * W + w]);
+                    sig[c].push_back(b.tab[sl.o_TR + per * i + c * W + w]);
+                }
+            }
+            if (sl.type == 1) sig[c].push_back(b.tab[sl.o_P + c]);
+        }
+    std::vector<uint8_t> cmap(256, 0);
+    std::vector<int> rep{'\n'};   // the byte whose rows a code takes
+    {
+        std::map<std::vector<uint64_t>, int> code;
+        for (int c = 0; c < 256; ++c) {
+            if (c == '\n') continue;
+            auto it = code.find(sig[c]);
+            if (it == code.end()) {
+                it = code.emplace(sig[c], (int)rep.size()).first;
+                rep.push_back(c);
+            }
+            cmap[c] = (uint8_t)it->second;
+        }
+    }
+    const int nc = (int)rep.size();
+    std::vector<EsSlot> slots = b.slots;
+    std::vector<uint64_t> ctab;
+    auto rows = [&](uint64_t o, size_t W) {   // [nc][W] from [256][W] at o
+        const uint64_t at = ctab.size();
+        for (int q = 0; q < nc; ++q)
+            for (size_t w = 0; w < W; ++w) ctab.push_back(b.tab[o + rep[q] * W + w]);
+        return at;
+    };
+    for (size_t j = 0; j < slots.size(); ++j) {
+        EsSlot& sl = slots[j];
+        const EsSlot& src = b.slots[j];
+        const size_t W = sl.W, per = 256 * W;
+        sl.o_B = rows(src.o_B, W);
+        sl.o_TL = ctab.size();
+        for (int i = 0; i < sl.np; ++i) rows(src.o_TL + per * i, W);
+        sl.o_TR = ctab.size();
+        for (int i = 0; i < sl.np; ++i) rows(src.o_TR + per * i, W);
+        sl.o_P = sl.type == 1 ? rows(src.o_P, 1) : 0;
+    }
+    u.o_slots = up.add(slots.data(), slots.size() * sizeof(EsSlot));
+    u.o_tab = up.add(ctab.data(), ctab.size() * sizeof(uint64_t));
+    u.o_map = up.add(cmap.data(), cmap.size());
+    u.tab_words = (uint32_t)ctab.size();
+    u.ncodes = nc;
     u.nslots = (int)b.slots.size();
     u.pid_base = b.slots.empty() ? 0 : b.slots[0].pid;
     u.wmax = 1;
@@ -318,6 +374,9 @@ EsPrep es_bind(const EsUpload& u, const uint8_t* d_up, int32_t gap_max) {
     EsPrep p;
     p.slots = reinterpret_cast<const EsSlot*>(d_up + u.o_slots);
     p.tab = reinterpret_cast<const uint64_t*>(d_up + u.o_tab);
+    p.cmap = d_up + u.o_map;
+    p.tab_words = u.tab_words;
+    p.ncodes = u.ncodes;
     p.nslots = u.nslots;
     p.pid_base = u.pid_base;
     p.gap_max = gap_max;
@@ -342,8 +401,9 @@ constexpr uint64_t ES_POS_MASK = (1ull << 48) - 1;
 constexpr int ES_CHUNK = 16;     // positions staged per refill of a thread's window
 constexpr int ES_THREADS = 64;   // walk threads per block (one wave)
 constexpr int ES_SPAN = 16;      // window starts whose pieces one shift-and pass finds
+constexpr size_t ES_TAB_LDS = 16 << 10;   // compact tables kept in LDS up to this size
 
-// A thread's text window: the line-bounded bytes (breaks as '\n') of
+// A thread's text window: the codes (es_upload) of the line-bounded bytes of
 // positions [lo, hi) in an LDS ring of win (a power of two) bytes.  The walk
 // moves forward and every phase reads at most m + k + 1 positions on either
 // side of the candidate; before each candidate the walk tops the ring up to
@@ -363,10 +423,11 @@ struct EsText {
     TextView tv;
     uint64_t n;
     EsRing r;
-    // the line-bounded byte from memory: '\n' for breaks and past the end
+    const uint8_t* cmap;   // byte -> code (LDS); code 0 = a break
+    // the line-bounded byte's code from memory: 0 for breaks and past the end
     __device__ uint8_t load(uint64_t p) const {
-        if (p >= n) return (uint8_t)'\n';
-        return tv.nuc_layout ? nuc_char_at(tv.nuc, p) : tv.bytes[p];
+        if (p >= n) return 0;
+        return cmap[tv.nuc_layout ? nuc_char_at(tv.nuc, p) : tv.bytes[p]];
     }
     __device__ void restart(uint64_t p) { r.lo = r.hi = p; }
     // extend the ring to cover [.., upto).  NUC: one 16-byte load of the
@@ -379,7 +440,7 @@ struct EsText {
             const uint64_t b = r.hi;
             if (b >= n) {
                 const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
-                for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = (uint8_t)'\n';
+                for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = 0;
                 r.hi = b + cnt;
             } else if (tv.nuc_layout) {
                 const uint4 v = tv.nuc.lin[b >> 5];
@@ -388,12 +449,12 @@ struct EsText {
                     const uint32_t i = (uint32_t)(p & 31);
                     uint8_t c;
                     if (p >= n || ((v.z >> i) & 1)) {   // a break or past the end
-                        c = (uint8_t)'\n';
+                        c = 0;
                     } else if ((v.w >> i) & 1) {
-                        c = nuc_char_at(tv.nuc, p);
+                        c = cmap[nuc_char_at(tv.nuc, p)];
                     } else {
                         const uint32_t code = (((v.x >> i) & 1) << 1) | ((v.y >> i) & 1);
-                        c = (uint8_t)((0x54474341u >> (8 * code)) & 0xff);
+                        c = cmap[(0x54474341u >> (8 * code)) & 0xff];
                     }
                     es_lds[r.base + ((uint32_t)p & r.mask)] = c;
                 }
@@ -405,7 +466,7 @@ struct EsText {
                 for (int q = 0; q < ES_CHUNK; ++q) c[q] = tv.bytes[umin64(b + q, n)];   // bytes[n..] pad with '\n'
 #pragma unroll
                 for (int q = 0; q < ES_CHUNK; ++q)
-                    if ((uint32_t)q < cnt) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = b + q < n ? c[q] : (uint8_t)'\n';
+                    if ((uint32_t)q < cnt) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = b + q < n ? cmap[c[q]] : 0;
                 r.hi = b + cnt;
             }
             if (r.hi - r.lo > r.mask + 1) r.lo = r.hi - (r.mask + 1);
@@ -415,21 +476,15 @@ struct EsText {
     __device__ uint8_t ring(uint64_t p) const {
         return r.mask == ~0u ? load(p) : es_lds[r.base + ((uint32_t)p & r.mask)];   // (no ring: uniform)
     }
-    // the line-bounded (folded) byte: '\n' at every break
+    // the line-bounded (folded) byte's code: 0 at every break
     __device__ uint8_t chr(uint64_t p) const {
         return p - r.lo < r.hi - r.lo ? es_lds[r.base + ((uint32_t)p & r.mask)] : load(p);
     }
     // a record break: '\n', a header-line byte, the end of the text
-    __device__ bool brk(uint64_t p) const { return chr(p) == (uint8_t)'\n'; }
-    // the file's own (folded) byte, header lines and '\n' included: what
-    // the BNDM scanner reads
-    __device__ uint8_t raw(uint64_t p) const {
-        const uint8_t c = chr(p);
-        if (c != (uint8_t)'\n' || p >= n) return c;
-        return raw_slow(p);
-    }
-    // the file's byte at a break (a header byte or '\n'), p < n
-    __device__ uint8_t raw_slow(uint64_t p) const { return tv.nuc_layout ? nuc_raw_at(tv.nuc, p) : tv.raw[p]; }
+    __device__ bool brk(uint64_t p) const { return chr(p) == 0; }
+    // the code of the file's byte at a break (a header byte or '\n'), p < n:
+    // what the BNDM scanner reads there
+    __device__ uint8_t raw_code(uint64_t p) const { return cmap[tv.nuc_layout ? nuc_raw_at(tv.nuc, p) : tv.raw[p]]; }
 };
 
 struct EsCtx {
@@ -438,6 +493,7 @@ struct EsCtx {
     EsText t;
     uint64_t R;   // the search region start
     int errs, W, anchors;   // S's fields read on every step
+    int nc;                 // codes of the compact alphabet (rows per table)
     // recCheckLeftContext 0x402170 / recCheckRightContext 0x4021e0; p ==
     // recbeg <=> p == R or p starts its line (a record holds no break)
     __device__ bool at_recbeg(uint64_t p) const { return p == R || p == 0 || t.brk(p - 1); }
@@ -516,7 +572,7 @@ __device__ bool es_phase(const EsCtx& x, const uint64_t* T, uint64_t pos, bool l
 #pragma unroll
             for (int w = 0; w < WB; ++w) Mw[w] = Mn[w];
             {   // the next step reads p - 1 (left) or p (right)
-                const uint8_t cn = left ? (p > 0 ? x.t.chr(p - 1) : (uint8_t)'\n') : x.t.chr(p);
+                const uint8_t cn = left ? (p > 0 ? x.t.chr(p - 1) : (uint8_t)0) : x.t.chr(p);
                 const uint64_t* M = T + (size_t)cn * x.W;
 #pragma unroll
                 for (int w = 0; w < WB; ++w) Mn[w] = w < W ? M[w] : 0ull;
@@ -608,7 +664,7 @@ __device__ bool es_verify(EsCtx& x, uint64_t pos, int i, uint64_t& mb, uint64_t&
     // before the ring goes to memory) and m - L + k + 1 ahead
     x.t.fill(pos + (uint64_t)(S.m - L + S.k + 2));
     if (x.t.brk(rp)) return false;                      // the record ends at rp
-    const size_t per = (size_t)256 * S.W;
+    const size_t per = (size_t)x.nc * S.W;
     int kmax = S.k;
 #pragma nounroll
     for (int ph = 0; ph < 2; ++ph) {   // left, then right with what the left left of k
@@ -710,7 +766,21 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
     const uint64_t total = total_d ? *total_d : total_h;
     const uint32_t nw = *wcount;
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nw; t += stride) {
+    // list entry t goes to lane t / gridDim.x of block t % gridDim.x: a short
+    // list is spread one cluster per wave (a wave runs its lanes' divergent
+    // walks one after the other)
+    if (blockIdx.x >= nw) return;   // (block-uniform) nothing to walk
+    // the compact tables (when they fit) and the byte -> code map in LDS
+    uint8_t* cmap = es_lds + P.map_off;
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) cmap[c] = P.cmap[c];
+    const uint64_t* tab = P.tab;
+    if (P.tab_lds) {
+        uint64_t* lt = reinterpret_cast<uint64_t*>(es_lds + P.tab_off);
+        for (uint32_t q = threadIdx.x; q < P.tab_words; q += blockDim.x) lt[q] = P.tab[q];
+        tab = lt;
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x * gridDim.x + blockIdx.x; t < nw; t += stride) {
         const uint64_t i = wlist[t];
         uint64_t j = i + 1;   // the next cluster's head keeps bit 1 set whatever its owner writes
         while (j < total && !(acc[j] & 2)) ++j;
@@ -721,14 +791,77 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         const int64_t slot = (int64_t)pid - P.pid_base;
         if (slot >= 0 && slot < P.nslots) {
             const EsSlot& S = P.slots[slot];
-            EsCtx x{&S, P.tab, EsText{tv, tv.n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}}, 0, S.errs, S.W,
-                    S.anchors};
+            EsCtx x{&S, tab, EsText{tv, tv.n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}, cmap}, 0, S.errs, S.W,
+                    S.anchors, P.ncodes};
             const uint64_t n = tv.n;
             const int type = S.type, m = S.m, k = S.k, mpc = S.mpc, np = S.np;
-            // the ring starts where the left phase of the match at lo can
-            // reach (an earlier read goes to memory); it is filled only as
-            // far as the piece pass and each verification need
-            x.t.restart(lo > (uint64_t)(k + 2) ? lo - (uint64_t)(k + 2) : 0);
+            if (S.lone) {
+                // Substitutions only, no anchors: a verification from (pos,
+                // piece q) succeeds exactly when the window pos - L_q is one
+                // of the cluster's starts (both phases have fixed lengths)
+                // and it returns that window.  So nrgrep prints, from R on,
+                // the start s >= R discovered first: type 1 at its smallest
+                // (s + L_q, q) with piece q exact there (every test bit is
+                // right, es_add_slot), types 2 and 3 at s itself; R = s + m.
+                // The walk needs only the cluster's starts and their pieces:
+                // a start s is discovered at or before s + L_max (one of its
+                // k + 1 pieces is exact), so none after the first start
+                // s_f >= R plus L_max can come first -- each round looks at
+                // the starts in [s_f, s_f + L_max] only.
+                x.t.restart(lo);
+                const uint64_t lim = type == 2 ? (n > (uint64_t)(S.wend - S.wbeg - k - 1) ? n - (uint64_t)(S.wend - S.wbeg - k - 1) : 0) : n + 1;
+                const uint64_t last = n >= (uint64_t)mpc ? n - (uint64_t)mpc : 0;
+                const uint64_t lmax = (uint64_t)S.L[np - 1];
+                const size_t W = (size_t)S.W;
+                uint64_t R = 0, f = i;
+                for (;;) {
+                    while (f < j && (keys[f] & ES_POS_MASK) < R) ++f;
+                    if (f == j) break;
+                    const uint64_t sf = keys[f] & ES_POS_MASK;
+                    uint64_t best = ~0ull, bs = 0;
+                    if (type != 1) {
+                        if (sf + (uint64_t)S.L[0] >= lim) break;   // (and every later start)
+                        best = bs = sf;
+                    }
+                    for (uint64_t q2 = f; type == 1 && q2 < j; ++q2) {
+                        const uint64_t sj = keys[q2] & ES_POS_MASK;
+                        if (sj > sf + lmax) break;
+                        x.t.fill(umin64(sj + (uint64_t)m, n) + 1);
+                        for (int q = 0; q < np; ++q) {   // L_q increases with q: the first exact piece
+                            const uint64_t pp = sj + (uint64_t)S.L[q];
+                            bool exact = pp <= last;
+                            for (int t = 0; t < mpc && exact; ++t) {
+                                const int bpos = S.L[q] + t;
+                                exact = (tab[S.o_B + (size_t)x.t.chr(pp + t) * W + (bpos >> 6)] >> (bpos & 63)) & 1;
+                            }
+                            if (exact) {
+                                if (pp * 64 + (uint64_t)q < best) {
+                                    best = pp * 64 + (uint64_t)q;
+                                    bs = sj;
+                                }
+                                break;
+                            }
+                        }
+                    }
+                    if (best == ~0ull) break;
+                    // the entries below f are < R: overwriting them is safe
+                    keys[i + nout] = (pid << 48) | bs;
+                    lens[i + nout] = (uint32_t)m;
+                    acc[i + nout] = (nout == 0 ? 2 : 0) | 1;
+                    ++nout;
+                    R = bs + (uint64_t)m;
+                }
+                for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
+                continue;
+            }
+            // A verification from (pos, piece q) returns a start within k of
+            // pos - L_q, and every start nrgrep can print is one of the
+            // cluster's, so candidates with pos + k < lo + L_q cannot print
+            // (skipped: a failed verification changes nothing).  The left
+            // phase of the others reads back to lo - 2k - 2: the ring starts
+            // there (an earlier read goes to memory) and is filled only as
+            // far as the piece pass and each verification need.
+            x.t.restart(lo > (uint64_t)(2 * k + 3) ? lo - (uint64_t)(2 * k + 3) : 0);
             // lines (every position is a key): the cluster is one line and
             // its break, the next line is another cluster's
             const uint64_t pmax = P.lines ? hi : umin64(n, hi + (uint64_t)(m + k));
@@ -738,7 +871,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
             // type 1: the packed shift-and over the window starts (see
             // es_add_slot); flags bit d = the pieces' last bits survive at
             // start fb + d.  Every start < n - mpc + 1 is tested (0x4137f2).
-            const uint64_t* Pt = P.tab + S.o_P;
+            const uint64_t* Pt = tab + S.o_P;
             const uint64_t pstart = S.pstart, pend = S.pend;
             const uint64_t last_start = n >= (uint64_t)mpc ? n - (uint64_t)mpc : 0;   // starts <= this fit
             uint64_t* dl = reinterpret_cast<uint64_t*>(es_lds + P.dl_off) + threadIdx.x * ES_SPAN;   // D per span start
@@ -756,7 +889,8 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                 while (!cand && pos <= pmax && guard) {   // the next candidate position at or after pos
                     --guard;
                     if (type != 1) {
-                        if (pos < lim2) cand = 1u;   // every start is the window / prefix candidate
+                        // every start is the window / prefix candidate
+                        if (pos < lim2 && pos + (uint64_t)k >= lo + (uint64_t)S.L[0]) cand = 1u;
                         else ++pos;
                         continue;
                     }
@@ -776,13 +910,13 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                             uint8_t cc[8];
                             uint64_t mk[8];
 #pragma unroll
-                            for (int q = 0; q < 8; ++q) cc[q] = tfeed + q < tend ? x.t.ring(tfeed + q) : (uint8_t)'\n';
+                            for (int q = 0; q < 8; ++q) cc[q] = tfeed + q < tend ? x.t.ring(tfeed + q) : (uint8_t)0;
 #pragma unroll
                             for (int q = 0; q < 8; ++q) mk[q] = Pt[cc[q]];
 #pragma unroll
                             for (int q = 0; q < 8; ++q) {
                                 const uint64_t t = tfeed + q;
-                                if (cc[q] == (uint8_t)'\n' && t < n) mk[q] = Pt[x.t.raw_slow(t)];
+                                if (cc[q] == 0 && t < n) mk[q] = Pt[x.t.raw_code(t)];
                                 if (t >= tend) mk[q] = 0ull;
                             }
 #pragma unroll
@@ -809,7 +943,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                         // checkMatch is called for, in order (0x41384b)
                         const uint64_t D = dl[pos - fb];
                         for (int q = 0; q < np; ++q)
-                            if (D & S.test[q]) cand |= 1u << q;
+                            if ((D & S.test[q]) && pos + (uint64_t)k >= lo + (uint64_t)S.L[q]) cand |= 1u << q;
                     }
                     if (!cand) ++pos;
                 }
@@ -869,19 +1003,25 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
     while (win < (uint32_t)P.gap_max + ES_SPAN + 32) win <<= 1;
     P.win = win <= 512 ? win : 0;   // wider patterns read memory directly
     P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
+    // then the compact tables (up to ES_TAB_LDS bytes) and the code map
+    P.tab_off = P.dl_off + ES_THREADS * ES_SPAN * 8;
+    P.tab_lds = (size_t)P.tab_words * 8 <= ES_TAB_LDS ? 1 : 0;
+    P.map_off = P.tab_off + (P.tab_lds ? P.tab_words * 8 : 0);
+    const size_t lds = P.map_off + 256;
     // one wave per block (a cluster's walk is a chain of dependent steps,
     // and the ring takes LDS): 8 per CU, all resident, striding over the
     // walk list (its length is on the device)
     int dev = 0, ncu = 0;
     HIPCHK(hipGetDevice(&dev));
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const uint32_t blocks = (uint32_t)std::max(1, ncu) * 8;
+    const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160u << 10) / lds));
+    const uint32_t blocks = (uint32_t)std::max(1, ncu) * per_cu;
     // WB: position words; KR: the rows unrolled (k <= 3, the common case,
     // keeps the row vectors in few registers)
     auto kern = P.kmax <= 3 ? (P.wmax <= 1 ? k_es_walk<1, 3> : P.wmax == 2 ? k_es_walk<2, 3> : k_es_walk<4, 3>)
                             : (P.wmax <= 1 ? k_es_walk<1, PM_MAX_K> : P.wmax == 2 ? k_es_walk<2, PM_MAX_K>
                                                                                   : k_es_walk<4, PM_MAX_K>);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), (size_t)P.dl_off + ES_THREADS * ES_SPAN * 8, s, P, keys,
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), lds, s, P, keys,
                        lens, total_d, total_h, acc, wlist, wcount, tv);
     hipLaunchKernelGGL(k_es_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);
     HIPCHK(hipGetLastError());

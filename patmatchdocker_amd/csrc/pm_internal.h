@@ -673,7 +673,9 @@ struct EsBuild {
     std::vector<uint64_t> tab;
 };
 struct EsUpload {
-    size_t o_slots = 0, o_tab = 0;
+    size_t o_slots = 0, o_tab = 0, o_map = 0;
+    uint32_t tab_words = 0;   // the compact tables ([codes][W] rows per table)
+    int ncodes = 0;
     int nslots = 0;
     int32_t pid_base = 0;
     int wmax = 1;   // position words of the widest pattern
@@ -681,7 +683,10 @@ struct EsUpload {
 };
 struct EsPrep {
     const EsSlot* slots = nullptr;
-    const uint64_t* tab = nullptr;
+    const uint64_t* tab = nullptr;   // compact tables: [ncodes][W] rows (es_upload)
+    const uint8_t* cmap = nullptr;   // byte -> code (code 0: '\n', a break)
+    uint32_t tab_words = 0;
+    int ncodes = 0;
     int nslots = 0;
     int32_t pid_base = 0;   // slot = pattern id - pid_base
     int32_t gap_max = 0;    // candidate starts further apart never interact
@@ -690,6 +695,8 @@ struct EsPrep {
     uint32_t dl_off = 0;    // k_es_walk's piece words in its LDS
     int lines = 0;          // every position is a key (es_all_positions): clusters are lines
     uint32_t win = 0;       // k_es_walk's per-thread text ring (bytes, a power of two; 0: none)
+    uint32_t tab_off = 0, map_off = 0;   // k_es_walk's LDS: the compact tables, the code map
+    int tab_lds = 0;        // the tables are read from LDS
 };
 // Deletions with k >= m (the whole pattern may be deleted): every position
 // can be reported, so the walk takes every position as a key and each line

@@ -61,6 +61,24 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device,
  * scans exercise the exception path as on a real genome.               */
 int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed,
                            int device, void* stream, pm_db** out);
+/* nrgrep reads '<datafile>' in buffers of -b BYTES (patmatch.py:733-743
+ * passes -b 1600000; main() stores atoi(optarg) in OptBufSize, 0x401162, and
+ * bufCreate allocates that many bytes, 0x41bb6b -- the help text's "Kb"
+ * is not applied).  Each buffer that is not the file's last is searched up
+ * to and including its last '
+', and the next buffer starts at that '
+'
+ * (recSearchFile 0x402450-0x402497, bufLoad 0x41bbf0); a buffer without one
+ * is searched whole.  These search regions matter to what is printed: no
+ * match spans a region end, the report rule restarts at each region start,
+ * and '^' passes there.  pm_db_create* set the regions of the loaded text
+ * read with PM_NRGREP_BUFFER; pm_db_set_regions replaces them (a piece of a
+ * larger file takes the file's regions, shifted; `count` = 1, [0, n): none).
+ * Region r = [starts[r], ends[r]), starts increasing from 0.             */
+#define PM_NRGREP_BUFFER 1600000ull
+int pm_db_set_regions(pm_db* db, uint64_t count, const uint64_t* starts, const uint64_t* ends);
+/* The current regions: *count of them, the first `cap` copied out.       */
+int pm_db_regions(const pm_db* db, uint64_t cap, uint64_t* starts, uint64_t* ends, uint64_t* count);
 int pm_db_destroy(pm_db* db);
 int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet,
                uint64_t* n_exception_words, uint64_t* device_bytes);

@@ -98,6 +98,57 @@ def drop_header_hits(text: bytes, hits):
 
 PMO_NRGREP, PMO_START, PMO_END, PMO_SIMPLE = 1, 2, 4, 8
 
+# nrgrep_coords -b 1600000 (patmatch.py:733-743): buffers of 1,600,000 bytes
+# (main() stores atoi(optarg), 0x401162; bufCreate mallocs that, 0x41bb6b)
+NRGREP_BUFFER = 1600000
+
+
+def regions(text: bytes, bufsize: int = NRGREP_BUFFER):
+    """The regions recSearchFile (0x402250) searches: a full buffer up to and
+    including its last '\n' (simpleRevSearch 0x402475), the next buffer
+    loaded from that '\n' (bufLoad 0x4023e6 with r13 = its start); with no
+    '\n' in it (or only at its start) the whole buffer, the next one after
+    it (0x4024a0 -> 0x4022ba); the last buffer (not full: bufEof 0x41bfc0)
+    to the end of the file.  [(beg, end)]."""
+    out, at, n = [], 0, len(text)
+    while True:
+        if not bufsize or at + bufsize > n:
+            out.append((at, n))
+            return out
+        d = text.rfind(b"\n", at, at + bufsize)
+        if d > at:
+            out.append((at, d + 1))
+            at = d
+        else:
+            out.append((at, at + bufsize))
+            at += bufsize
+        if at >= n:
+            return out
+
+
+def by_region(text: bytes, scan_one, skip_headers: bool, bufsize: int = NRGREP_BUFFER, threads: int = 1,
+              regs=None):
+    """recSearchFile's loop: every region searched as a text of its own (its
+    start is R, its end the end of the text), the printed matches in file
+    order -- a match over a region's last '\n' is found in both regions and
+    printed twice, as the binary does.  Header-line starts are dropped with
+    the whole file as context."""
+    regs = regions(text, bufsize) if regs is None else [(int(a), int(b)) for a, b in regs]
+    if len(regs) == 1:
+        hits = scan_one(text)
+    else:
+        def one(r):
+            a, b = r
+            return [(x + a, y + a) for x, y in scan_one(text[a:b])]
+        if threads > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=threads) as ex:
+                parts = list(ex.map(one, regs))
+        else:
+            parts = [one(r) for r in regs]
+        hits = [h for part in parts for h in part]
+    return drop_header_hits(text, hits) if skip_headers else hits
+
 
 def mode_of(prog, k: int, report: str = "nrgrep", simple=None) -> int:
     """pmo_scan2 mode bits for a compiled program: nrgrep's engine choice
@@ -113,16 +164,16 @@ def mode_of(prog, k: int, report: str = "nrgrep", simple=None) -> int:
     return m
 
 
-def scan_candidates(text: bytes, prog, k: int = 0, types: str = "ids"):
+def scan_candidates(text: bytes, prog, k: int = 0, types: str = "ids", bufsize: int = NRGREP_BUFFER, regs=None):
     """Every start with a match under nrgrep's engine choice (shortest end;
-    '$' applied, '^' not, header-line starts kept): what the sharded scan
-    re-chains when a report crosses into the next piece."""
+    '$' applied, '^' not, header-line starts kept), region by region: what
+    the sharded scan re-chains when a report crosses into the next piece."""
     m = mode_of(prog, k, "all") & ~PMO_START
-    return scan_reported(text, prog, k, types, mode=m)
+    return scan_reported(text, prog, k, types, mode=m, bufsize=bufsize, regs=regs)
 
 
 def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers: bool = False,
-                  report: str = "nrgrep", simple=None, mode=None):
+                  report: str = "nrgrep", simple=None, mode=None, bufsize: int = NRGREP_BUFFER, regs=None):
     """What ``nrgrep_coords`` prints for ``prog``.  A class sequence at
     k > 0 runs nrgrep's esimple engine (``scan_esimple``, pm_nrgrep.c: its
     own candidate order and verify).  Everything else (pmo_scan2): the
@@ -132,9 +183,13 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
     being the leftmost start (``report="leftmost"`` forces that rule for a
     class sequence too).  ``skip_headers`` then drops the header-line hits
     process_output throws away.  ``simple`` overrides the engine choice
-    (False: line-bounded windows even at k = 0)."""
+    (False: line-bounded windows even at k = 0).  The file is searched in
+    nrgrep's regions (``regions``: buffers of ``bufsize`` bytes; 0 = one)."""
     if report == "nrgrep" and simple is None and mode is None and k > 0 and is_esimple(prog):
-        return scan_esimple(text, prog, k, types, skip_headers)
+        return scan_esimple(text, prog, k, types, skip_headers, bufsize, regs)
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, simple, mode, 0),
+                         skip_headers, bufsize, regs=regs)
     L = lib()
     B = np.array(prog.byte_masks(), dtype=np.uint64)
     F = np.array(prog.follow + [0], dtype=np.uint64)
@@ -192,6 +247,10 @@ def scan_threads(text: bytes, prog, k: int = 0, types: str = "ids", skip_headers
         if report is None:
             return scan(t, prog, k, types, skip_headers)
         return scan_reported(t, prog, k, types, skip_headers, report)
+    if report is not None and len(text) >= NRGREP_BUFFER:
+        # nrgrep's regions are independent searches: one per task
+        return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, bufsize=0),
+                         skip_headers, NRGREP_BUFFER, threads)
     # the simple engine's windows may span a line break: no cut is safe
     cross = report is not None and k == 0 and prog.linear and any(10 in c for c in prog.classes)
     if threads <= 1 or len(text) < (1 << 20) or cross or prog.anchor_start:
@@ -267,11 +326,16 @@ def nrgrep_plan(prog, k: int):
             "L": [out[4 + i] for i in range(n)]}
 
 
-def scan_esimple(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False):
+def scan_esimple(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False,
+                 bufsize: int = NRGREP_BUFFER, regs=None):
     """What nrgrep_coords prints for a class sequence at k > 0 (pmn_esimple:
-    nrgrep's own scanners, record lookup, two-phase verify and report rule)."""
+    nrgrep's own scanners, record lookup, two-phase verify and report rule),
+    region by region (``regions``)."""
     if not prog.linear or k < 1:
         raise ValueError("scan_esimple needs a class sequence and k > 0")
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_esimple(t, prog, k, types, False, 0), skip_headers, bufsize,
+                         regs=regs)
     B = wide_masks(prog)
     mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
     cap = 1 << 16

@@ -32,8 +32,9 @@ EXPORTED = (
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
-    "pm_ids_jit_compile", "pm_esimple_plan",
+    "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
 )
+PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
 
 class EngineUnavailable(RuntimeError):
@@ -67,6 +68,8 @@ def _declare(lib):
     lib.pm_db_destroy.argtypes = [P]
     lib.pm_db_info.argtypes = [P, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
     lib.pm_db_decode.argtypes = [P, u64, ctypes.c_uint32, ctypes.c_char_p]
+    lib.pm_db_set_regions.argtypes = [P, u64, P, P]
+    lib.pm_db_regions.argtypes = [P, u64, P, P, pu64]
     lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_scan_linear_async.argtypes = lib.pm_scan_linear.argtypes
     lib.pm_scan_nfa.argtypes = [P, ctypes.c_int, P, P, u64, u64, ctypes.c_int, ctypes.c_int,

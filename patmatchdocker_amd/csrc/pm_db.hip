@@ -520,7 +520,7 @@ void free_db(pm_db* db) {
     }
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
-    void* ptrs[] = {db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
+    void* ptrs[] = {db->reg_t, db->reg_e, db->reg_lut, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
@@ -625,6 +625,33 @@ NucView nuc_view(const pm_db* db) {
     return NucView{db->hl, db->bo, db->sbflag, db->sbbase, db->xbytes, db->lin};
 }
 
+// the region table on the device: starts, ends, and the bucket lookup
+void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<uint64_t>& e) {
+    require(t.size() == e.size() && !t.empty() && t.size() < (1ull << 31), "bad region table");
+    for (size_t r = 0; r < t.size(); ++r) {
+        require(t[r] <= e[r] && e[r] <= db->n, "region outside the database");
+        require(r == 0 ? t[r] == 0 : t[r] > t[r - 1], "region starts must increase from 0");
+    }
+    const uint64_t nlut = (db->n >> REG_LUT_SHIFT) + 1;
+    std::vector<uint32_t> lut(nlut);
+    for (uint64_t b = 0, r = 0; b < nlut; ++b) {
+        while (r + 1 < t.size() && t[r + 1] <= (b << REG_LUT_SHIFT)) ++r;
+        lut[b] = (uint32_t)r;
+    }
+    HIPCHK(hipStreamSynchronize(db->stream));   // queued scans may still read the old table
+    for (void* p : {(void*)db->reg_t, (void*)db->reg_e, (void*)db->reg_lut})
+        if (p) HIPCHK(hipFree(p));
+    db->reg_t = db->reg_e = nullptr;
+    db->reg_lut = nullptr;
+    HIPCHK(hipMalloc(&db->reg_t, t.size() * 8));
+    HIPCHK(hipMalloc(&db->reg_e, e.size() * 8));
+    HIPCHK(hipMalloc(&db->reg_lut, nlut * 4));
+    HIPCHK(hipMemcpy(db->reg_t, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db->reg_e, e.data(), e.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db->reg_lut, lut.data(), nlut * 4, hipMemcpyHostToDevice));
+    db->nreg = (uint32_t)t.size();
+}
+
 }  // namespace pm
 
 using namespace pm;
@@ -690,6 +717,12 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
             }
         }
         free_all(db, owned);
+        std::vector<uint64_t> rt, re;
+        nrgrep_regions(n, PM_NRGREP_BUFFER, [&](uint64_t lo, uint64_t hi) {
+            const void* p = memrchr(fasta + lo, '\n', hi - lo);
+            return p ? (uint64_t)(static_cast<const uint8_t*>(p) - fasta) : ~0ull;
+        }, rt, re);
+        set_regions(db, rt, re);
         *out = db;
     });
     if (rc != PM_OK) {
@@ -720,6 +753,17 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         HIPCHK(hipGetLastError());
         finish_nuc(db, owned, nullptr, rec_len, seed);
         free_all(db, owned);
+        // the layout's line breaks: after each header and each record
+        const uint64_t rb = SYN_HDR + 1 + rec_len + 1;
+        std::vector<uint64_t> rt, re;
+        nrgrep_regions(db->n, PM_NRGREP_BUFFER, [&](uint64_t lo, uint64_t hi) {
+            if (hi == 0) return ~0ull;
+            const uint64_t q = hi - 1, r = q / rb, o = q % rb;
+            const uint64_t d = o >= rb - 1 ? r * rb + rb - 1 : o >= SYN_HDR ? r * rb + SYN_HDR
+                             : r ? (r - 1) * rb + rb - 1 : ~0ull;
+            return d != ~0ull && d >= lo ? d : ~0ull;
+        }, rt, re);
+        set_regions(db, rt, re);
         *out = db;
     });
     if (rc != PM_OK) {
@@ -728,6 +772,28 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         free_db(db);
     }
     return rc;
+}
+
+int pm_db_set_regions(pm_db* db, uint64_t count, const uint64_t* starts, const uint64_t* ends) {
+    return guarded([&] {
+        require(db != nullptr && starts != nullptr && ends != nullptr && count >= 1, "null argument");
+        std::lock_guard<std::recursive_mutex> lk(db->mu);
+        DeviceGuard g(db->device);
+        set_regions(db, std::vector<uint64_t>(starts, starts + count), std::vector<uint64_t>(ends, ends + count));
+    });
+}
+
+int pm_db_regions(const pm_db* db, uint64_t cap, uint64_t* starts, uint64_t* ends, uint64_t* count) {
+    return guarded([&] {
+        require(db != nullptr && count != nullptr && (cap == 0 || (starts && ends)), "null argument");
+        *count = db->nreg;
+        const uint64_t n = std::min<uint64_t>(cap, db->nreg);
+        if (n) {
+            DeviceGuard g(db->device);
+            HIPCHK(hipMemcpy(starts, db->reg_t, n * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ends, db->reg_e, n * 8, hipMemcpyDeviceToHost));
+        }
+    });
 }
 
 int pm_db_destroy(pm_db* db) {

@@ -690,10 +690,13 @@ __device__ inline bool es_brk_before(const TextView& tv, uint64_t p) {
 
 // Cluster heads: a new pattern (high key bits) or a gap wider than any phase
 // reads; with `lines` also every start of a line (records never interact).
+// The search restarts at every region start (recSearchFile), so a cluster
+// never spans one.
 __device__ inline bool es_head(const uint64_t* keys, uint64_t i, int32_t gap, int lines, const TextView& tv) {
     if (i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap) return true;
-    if (!lines) return false;
     const uint64_t p = keys[i] & ES_POS_MASK;
+    if (tv.reg.n > 1 && region_of(tv.reg, p) != region_of(tv.reg, keys[i - 1] & ES_POS_MASK)) return true;
+    if (!lines) return false;
     return p > 0 && es_brk_before(tv, p);
 }
 
@@ -720,7 +723,8 @@ __global__ __launch_bounds__(256) void k_es_heads(EsPrep P, const uint64_t* __re
                 const int64_t slot = (int64_t)(keys[i] >> 48) - P.pid_base;
                 if (!P.lines && slot >= 0 && slot < P.nslots && (i + 1 == total || es_head(keys, i + 1, P.gap_max, 0, tv))) {
                     const EsSlot& S = P.slots[slot];
-                    if (S.lone) {
+                    if (S.lone && (tv.reg.n <= 1 || (keys[i] & ES_POS_MASK) + (uint64_t)S.m <=
+                                                         tv.reg.e[region_of(tv.reg, keys[i] & ES_POS_MASK)])) {
                         // A lone start with substitutions only is what nrgrep
                         // prints: a verification from any candidate returns
                         // the window [pos - L, pos - L + m) (no indels: both
@@ -791,9 +795,16 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         const int64_t slot = (int64_t)pid - P.pid_base;
         if (slot >= 0 && slot < P.nslots) {
             const EsSlot& S = P.slots[slot];
-            EsCtx x{&S, tab, EsText{tv, tv.n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}, cmap}, 0, S.errs, S.W,
+            // the cluster's region [R0, n): its search starts at R0 and the
+            // text ends at n for it (reads past it see a break)
+            uint64_t R0 = 0, n = tv.n;
+            if (tv.reg.n > 1) {
+                const uint32_t r = region_of(tv.reg, lo);
+                R0 = tv.reg.t[r];
+                n = tv.reg.e[r];
+            }
+            EsCtx x{&S, tab, EsText{tv, n, EsRing{threadIdx.x * P.win, P.win - 1u, 0, 0}, cmap}, R0, S.errs, S.W,
                     S.anchors, P.ncodes};
-            const uint64_t n = tv.n;
             const int type = S.type, m = S.m, k = S.k, mpc = S.mpc, np = S.np;
             if (S.lone) {
                 // Substitutions only, no anchors: a verification from (pos,
@@ -818,6 +829,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                     while (f < j && (keys[f] & ES_POS_MASK) < R) ++f;
                     if (f == j) break;
                     const uint64_t sf = keys[f] & ES_POS_MASK;
+                    if (sf + (uint64_t)m > n) break;   // (and every later start): past the region end
                     uint64_t best = ~0ull, bs = 0;
                     if (type != 1) {
                         if (sf + (uint64_t)S.L[0] >= lim) break;   // (and every later start)
@@ -825,7 +837,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
                     }
                     for (uint64_t q2 = f; type == 1 && q2 < j; ++q2) {
                         const uint64_t sj = keys[q2] & ES_POS_MASK;
-                        if (sj > sf + lmax) break;
+                        if (sj > sf + lmax || sj + (uint64_t)m > n) break;
                         x.t.fill(umin64(sj + (uint64_t)m, n) + 1);
                         for (int q = 0; q < np; ++q) {   // L_q increases with q: the first exact piece
                             const uint64_t pp = sj + (uint64_t)S.L[q];

@@ -582,11 +582,30 @@ __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
     // holds stale keys: never read the text at a position outside it
     const uint64_t s = key & POS_MASK;
     if (s >= a.tv.n || len > a.tv.n - s) return false;
-    if (!(a.flags & PM_ANCHOR_END)) return true;
     const uint64_t e = s + len;
-    return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n';
+    // inside the region it is found in (only a simple-engine window over a
+    // region's last '\n', or a cut without one, can stick out)
+    if (a.tv.reg.n > 1 && e > a.tv.reg.e[region_of(a.tv.reg, s)]) return false;
+    if (!(a.flags & PM_ANCHOR_END)) return true;
+    // '$': a line end or the region end (recCheckRightContext 0x4021e0)
+    return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n' ||
+           (a.tv.reg.n > 1 && e == a.tv.reg.e[region_of(a.tv.reg, s)]);
 }
-__device__ inline uint64_t rep_val(uint64_t key, uint32_t len) { return key + len; }   // (pattern, end)
+// (pattern, end), the running maximum the heads are found with; the report
+// rule restarts at every region start, so an end past the next region's
+// start (the '\n' both regions hold) counts as that start
+__device__ inline uint64_t rep_val(const RepArgs& a, uint64_t key, uint32_t len) {
+    uint64_t v = key + len;
+    if (a.tv.reg.n > 1) {
+        const uint32_t r = region_of(a.tv.reg, key & POS_MASK);
+        if (r + 1 < a.tv.reg.n) v = umin64(v, (key & ~POS_MASK) | a.tv.reg.t[r + 1]);
+    }
+    return v;
+}
+// s starts a region (the search restarts there: R = s)
+__device__ inline bool rep_region_start(const RepArgs& a, uint64_t s) {
+    return a.tv.reg.n > 1 && a.tv.reg.t[region_of(a.tv.reg, s)] == s;
+}
 
 // a start on a header line or on the '\n' that ends it maps to the '>name'
 // record in process_output (get_name_offset) and is discarded
@@ -606,8 +625,10 @@ __device__ inline bool rep_keep(const RepArgs& a, uint64_t key) {
     return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
 }
 
+// '^' passes at a line start or at R (recCheckLeftContext 0x402170): the
+// region start is R when a region's search begins
 __device__ inline bool rep_line_start(const RepArgs& a, uint64_t s) {
-    return s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n';
+    return s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n' || rep_region_start(a, s);
 }
 
 // 64-bit wave shuffle as two 32-bit halves (a (pattern, end) key does not
@@ -646,7 +667,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
         for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint32_t len = a.lens[i];
-            if (rep_valid(a, key, len)) m = umax64(m, rep_val(key, len));
+            if (rep_valid(a, key, len)) m = umax64(m, rep_val(a, key, len));
         }
         m = block_max(m, red);
     }
@@ -668,7 +689,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             const uint64_t key = a.keys[i];
             const uint64_t s = key & POS_MASK;
             bool ok = rep_valid(a, key, a.lens[i]);
-            if (ok && (a.flags & PM_ANCHOR_START)) ok = s == 0 || tv_raw(a.tv, s - 1) == (uint8_t)'\n';
+            if (ok && (a.flags & PM_ANCHOR_START)) ok = rep_line_start(a, s);
             ok = ok && rep_keep(a, key);
             a.acc[i] = ok ? 1 : 0;
             own += ok;
@@ -687,7 +708,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         for (uint64_t i = threadIdx.x; i < b0; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint32_t len = a.lens[i];
-            if (rep_valid(a, key, len)) c2 = umax64(c2, rep_val(key, len));
+            if (rep_valid(a, key, len)) c2 = umax64(c2, rep_val(a, key, len));
         }
         c2 = block_max(c2, red);
         if (threadIdx.x == 0 && c2 != carry)
@@ -704,7 +725,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             key = a.keys[i];
             len = a.lens[i];
             valid = rep_valid(a, key, len);
-            if (valid) val = rep_val(key, len);
+            if (valid) val = rep_val(a, key, len);
             else a.acc[i] = 0;
         }
         scan[threadIdx.x] = val;
@@ -722,7 +743,9 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         // '^': a start is reported only at a line start or exactly at the
         // resume point R (recCheckLeftContext 0x402170), so a candidate that
         // touches the previous cluster's end belongs to that cluster
-        if (!valid || (anch ? key <= excl : key < excl)) continue;   // not a head: its head's walk writes it
+        // (with '^' a candidate at a region start is a head: R restarts there)
+        if (!valid || (anch ? key < excl || (key == excl && !rep_region_start(a, key & POS_MASK)) : key < excl))
+            continue;   // not a head: its head's walk writes it
         // head: every earlier report ends before it (R < its start)
         const uint64_t s0 = key & POS_MASK;
         const bool first = !anch || rep_line_start(a, s0);
@@ -732,7 +755,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         uint64_t R = first ? s0 + len : s0 - 1, run = val;   // s0 - 1: below every start of the cluster
         for (uint64_t j = i + 1; j < total; ++j) {
             const uint64_t kj = a.keys[j];
-            if (anch ? kj > run : kj >= run) break;  // the next head
+            if (anch ? kj > run || (kj == run && rep_region_start(a, kj & POS_MASK)) : kj >= run) break;  // the next head
             const uint32_t lj = a.lens[j];
             kept = 0;
             if (rep_valid(a, kj, lj)) {
@@ -741,7 +764,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
                     R = sj + lj;
                     kept = rep_keep(a, kj) ? 1 : 0;
                 }
-                run = umax64(run, rep_val(kj, lj));
+                run = umax64(run, rep_val(a, kj, lj));
             }
             a.acc[j] = kept;
             if (kept) {
@@ -826,11 +849,13 @@ void retire_buffers(pm_hits* h, hipStream_t s) {
 }  // namespace
 
 TextView text_view(const pm_db* db) {
-    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag};
+    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag,
+                    Regions{db->reg_t, db->reg_e, db->reg_lut, db->nreg}};
 }
 
-bool report_needed(uint32_t flags, bool cross) {
-    return (flags & (PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) || cross;
+bool report_needed(const pm_db* db, uint32_t flags, bool cross) {
+    // several search regions: windows over a region end are dropped
+    return (flags & (PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END)) || cross || db->nreg > 1;
 }
 
 ReportWs report_ws(pm_db* db, uint64_t cap_items) {

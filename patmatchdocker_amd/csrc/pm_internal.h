@@ -358,6 +358,11 @@ struct pm_db : pm_lane {
     hipEvent_t exc_fork = nullptr, exc_join = nullptr;
     std::set<pm_hits*> pending;       // pipelined scans not yet resolved
     uint64_t device_bytes = 0;
+    // nrgrep's search regions (Regions; set by pm_db_create* for the file
+    // itself, or by pm_db_set_regions)
+    uint64_t *reg_t = nullptr, *reg_e = nullptr;
+    uint32_t* reg_lut = nullptr;
+    uint32_t nreg = 0;
 };
 
 // A pipelined scan (pm_scan_linear_async) between launch and resolution: the
@@ -430,6 +435,36 @@ void* pool_get(int device, size_t bytes, size_t* cap);
 void pool_put(int device, void* p, size_t cap);
 void* reserve_host(pm_db* db, pm_hostbuf& b, size_t bytes);
 NucView nuc_view(const pm_db* db);
+// nrgrep's regions of a text read in buffers of `bufsize` bytes
+// (recSearchFile 0x402250): last_nl(lo, hi) = the last '\n' in [lo, hi), or
+// ~0.  Region r = [t[r], e[r]).  bufsize 0: one region.
+template <class LastNl>
+void nrgrep_regions(uint64_t n, uint64_t bufsize, LastNl last_nl, std::vector<uint64_t>& t, std::vector<uint64_t>& e) {
+    t.clear();
+    e.clear();
+    for (uint64_t at = 0;;) {
+        if (bufsize == 0 || at + bufsize > n) {   // bufEof (0x41bfc0): the buffer is not full
+            t.push_back(at);
+            e.push_back(n);
+            return;
+        }
+        t.push_back(at);
+        // simpleRevSearch (0x402475) for the record delimiter; the region ends
+        // after it and the next buffer starts AT it (bufLoad 0x4023e6 from its
+        // start); none, or only at the buffer start: the whole buffer, and the
+        // next one starts after it (0x4024a0 -> 0x4022ba)
+        const uint64_t d = last_nl(at, at + bufsize);
+        if (d != ~0ull && d != at) {
+            e.push_back(d + 1);
+            at = d;
+        } else {
+            e.push_back(at + bufsize);
+            at += bufsize;
+        }
+        if (at >= n) return;   // bufEmpty after the load
+    }
+}
+void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<uint64_t>& e);
 
 // hipRTC: compiles generated kernel source for gfx950 (pm_linear.hip)
 std::vector<char> hiprtc_compile(const std::string& src);
@@ -608,6 +643,23 @@ void pinned_put(void* p, size_t cap);
 // the region start R and the line ends.  Hits whose start lies on a header
 // line (incl. its '\n') are dropped afterwards (process_output discards them,
 // patmatch.py:548).
+// nrgrep's search regions (pm_db::reg_*, DESIGN.md §1 "Regions"): region r
+// is [reg_t[r], reg_e[r]); a match is found in the region whose start is the
+// last one at or before its start, must lie inside it, and the report rule
+// restarts at every region start.
+struct Regions {
+    const uint64_t* t = nullptr;    // starts (increasing)
+    const uint64_t* e = nullptr;    // ends
+    const uint32_t* lut = nullptr;  // [p >> REG_LUT_SHIFT]: the last region starting at or before that bucket
+    uint32_t n = 0;                 // <= 1: one region, the whole text (nothing to check)
+};
+constexpr int REG_LUT_SHIFT = 20;
+__device__ inline uint32_t region_of(const Regions& g, uint64_t s) {
+    uint32_t r = g.lut[s >> REG_LUT_SHIFT];
+    while (r + 1 < g.n && g.t[r + 1] <= s) ++r;
+    return r;
+}
+
 struct TextView {
     NucView nuc;
     const uint8_t* bytes;   // BYTE layout (header bytes stored as '\n')
@@ -615,11 +667,12 @@ struct TextView {
     uint64_t n;
     int nuc_layout;
     const uint64_t* lflag;  // NUC: per tile, the lanes with an exception (a clean lane holds no header byte)
+    Regions reg;
 };
 TextView text_view(const pm_db* db);
 // true when the pass changes anything for `flags` (cross: candidates may
 // start on header lines)
-bool report_needed(uint32_t flags, bool cross);
+bool report_needed(const pm_db* db, uint32_t flags, bool cross);
 // report_enqueue_ws (below) enqueues the pass on s: h's keys/lens are
 // replaced by the reported subset (the old buffers are recycled once the pass
 // has read them).  The input count is *ws.total (device; the speculative

@@ -1379,7 +1379,7 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
                            reinterpret_cast<const int32_t*>(d_up + o_len), h->lens);
         HIPCHK(hipGetLastError());
     }
-    if (report_needed(flags, cross)) report_sync(db, h, flags, total, cross, esimple ? &esp : nullptr);
+    if (report_needed(db, flags, cross)) report_sync(db, h, flags, total, cross, esimple ? &esp : nullptr);
     hits_ready(db, h);
     *out = h;
 }
@@ -1411,7 +1411,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
         bool cross = false;
         if (k == 0)
             for (int c = 0; c < n_classes; ++c) cross |= ((class_bytes[8 * c] >> '\n') & 1) != 0;
-        const bool report = report_needed(flags, cross);
+        const bool report = report_needed(db, flags, cross);
         // k_linear_others' run skip: per pattern, the first k+1 positions
         // whose class accepts only A/C/G/T (an "other" byte there is a
         // mismatch); jsel_ok[p]: the pattern has k+1 of them

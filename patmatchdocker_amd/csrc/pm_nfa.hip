@@ -686,7 +686,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (esimple) {
         // the walk replaces the lengths; until it runs they are unset
         report_sync(db, h, (uint32_t)flags, total, false, &esp);
-    } else if (report_needed((uint32_t)flags, cross)) {
+    } else if (report_needed(db, (uint32_t)flags, cross)) {
         report_sync(db, h, (uint32_t)flags, total, cross);
     }
     HIPCHK(hipStreamSynchronize(s));

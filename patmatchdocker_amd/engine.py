@@ -83,6 +83,38 @@ def choose_alphabet(data: bytes, sample: int = 1 << 22) -> str:
     return NUC if good >= 0.9 else BYTE
 
 
+def nrgrep_regions(data, bufsize: int = _lib.PM_NRGREP_BUFFER):
+    """nrgrep's search regions of a file read in buffers of ``bufsize`` bytes:
+    (starts, ends) int64 arrays, region r = [starts[r], ends[r]).
+
+    ``nrgrep_coords -b 1600000`` (patmatch.py:733-743) reads the file in
+    buffers of 1,600,000 BYTES (OptBufSize = atoi(optarg), 0x401162; bufCreate
+    allocates it, 0x41bb6b).  recSearchFile (0x402250) searches a full buffer
+    up to and including its last '\n' (simpleRevSearch, 0x402475) and loads
+    the next buffer from that '\n' on (bufLoad, 0x4023e6); a buffer with no
+    '\n' but at its start is searched whole and the next starts after it
+    (0x4024a0 -> 0x4022ba); the last buffer (bufEof 0x41bfc0: not full)
+    reaches the end of the file.  ``data``: bytes or an mmap (rfind)."""
+    n = len(data)
+    starts, ends = [], []
+    at = 0
+    while True:
+        starts.append(at)
+        if bufsize <= 0 or at + bufsize > n:
+            ends.append(n)
+            break
+        d = data.rfind(b"\n", at, at + bufsize)
+        if d > at:
+            ends.append(d + 1)
+            at = d
+        else:
+            ends.append(at + bufsize)
+            at += bufsize
+        if at >= n:
+            break
+    return np.array(starts, dtype=np.int64), np.array(ends, dtype=np.int64)
+
+
 class SequenceDatabase:
     """A FASTA file resident in the HBM of one GPU (``pm_db``)."""
 
@@ -130,6 +162,27 @@ class SequenceDatabase:
 
     def __len__(self):
         return self.info()["positions"]
+
+    def regions(self):
+        """nrgrep's search regions of the loaded text (nrgrep_regions):
+        (starts, ends) int64 arrays."""
+        lib = _lib.load()
+        cnt = ctypes.c_uint64()
+        check(lib.pm_db_regions(self.handle, 0, None, None, ctypes.byref(cnt)))
+        t = np.empty(cnt.value, dtype=np.uint64)
+        e = np.empty(cnt.value, dtype=np.uint64)
+        check(lib.pm_db_regions(self.handle, cnt.value, t.ctypes.data, e.ctypes.data, ctypes.byref(cnt)))
+        return t.astype(np.int64), e.astype(np.int64)
+
+    def set_regions(self, starts, ends):
+        """Replace the search regions (a piece of a larger file takes the
+        file's regions shifted into its coordinates; one region [0, n): no
+        cuts)."""
+        t = np.ascontiguousarray(starts, dtype=np.uint64)
+        e = np.ascontiguousarray(ends, dtype=np.uint64)
+        if t.shape != e.shape or t.size == 0:
+            raise ValueError("starts and ends: equal non-empty lengths")
+        check(_lib.load().pm_db_set_regions(self.handle, t.size, t.ctypes.data, e.ctypes.data))
 
     def decode(self, beg: int, length: int) -> bytes:
         buf = ctypes.create_string_buffer(max(length, 1))

@@ -256,6 +256,11 @@ def drop_header_starts(beg: np.ndarray, end: np.ndarray, hs: np.ndarray, he: np.
     return beg[~on], end[~on]
 
 
+def _lib_bufsize() -> int:
+    from . import _lib
+    return _lib.PM_NRGREP_BUFFER
+
+
 class ShardedDatabase:
     """Rank ``rank``'s piece of a FASTA file (``split_fasta``) in HBM, with
     ``HALO`` bytes of the next piece so windows that start in the piece are
@@ -265,7 +270,7 @@ class ShardedDatabase:
     piece is sliced from the map on demand.  Hit offsets are file offsets."""
 
     def __init__(self, data, world: int, rank: int, device: int = 0, alphabet: Optional[str] = None,
-                 halo: int = HALO, open_db: bool = True):
+                 halo: int = HALO, open_db: bool = True, bufsize: Optional[int] = None):
         self.raw = data
         self.world, self.rank = world, rank
         self.ranges = split_fasta(data, world)
@@ -274,10 +279,22 @@ class ShardedDatabase:
         local = bytes(data[self.beg:self.stop])
         hs, he = header_lines(local[:self.end - self.beg])
         self.headers = (hs, he)
+        # nrgrep's search regions are the whole file's (buffers of -b bytes
+        # from offset 0): the piece takes those over [beg, stop), shifted to
+        # its offsets (the first clipped to 0)
+        from . import engine
+        gt, ge = engine.nrgrep_regions(data, _lib_bufsize() if bufsize is None else bufsize)
+        sel = (gt < self.stop) & (ge > self.beg)
+        if self.stop > self.beg and sel.any():
+            lt = np.maximum(gt[sel], self.beg) - self.beg
+            le = np.minimum(ge[sel], self.stop) - self.beg
+        else:
+            lt, le = np.zeros(1, dtype=np.int64), np.full(1, self.stop - self.beg, dtype=np.int64)
+        self.regions = (lt, le)
         self.db = None
         if open_db and self.stop > self.beg:
-            from . import engine
             self.db = engine.SequenceDatabase.from_bytes(local, alphabet or engine.choose_alphabet(local), device)
+            self.db.set_regions(lt, le)
 
     @classmethod
     def from_file(cls, path: str, world: int, rank: int, device: int = 0, open_db: bool = True) -> "ShardedDatabase":
@@ -329,16 +346,33 @@ def _rechain(piece: ShardedDatabase, prog, cand, chain, R: int):
     """The piece's report chain for one program when the scan enters it at
     local offset ``R`` > 0 instead of 0: the report rule replayed over the
     candidates from R until it takes a candidate the original chain took
-    (from there on the two chains agree)."""
+    (from there on the two chains agree).  The rule restarts at every
+    search region's start (R = that start, recSearchFile); the incoming
+    report lies in the piece's first region."""
     cb, ce = (np.asarray(x, dtype=np.int64) for x in cand)
     keep = cb < len(piece)
     cb, ce = cb[keep], ce[keep]
     ob, oe = chain
     text, base = piece.raw, piece.beg
+    lt = piece.regions[0]
     out_b, out_e = [], []
-    i = int(np.searchsorted(cb, R))
+    cur = 0   # the region of the last report
+
+    def first_from(R, cur):
+        # the next candidate at or after R -- or at the next region's start,
+        # which may lie before R (the '\n' two regions share)
+        lim = min(R, int(lt[cur + 1])) if cur + 1 < lt.size else R
+        return int(np.searchsorted(cb, lim))
+
+    i = first_from(R, cur)
     while i < cb.size:
         s = int(cb[i])
+        reg = int(np.searchsorted(lt, s, side="right")) - 1
+        if reg > cur:   # a new region: its search starts at its first byte
+            cur, R = reg, int(lt[reg])
+        if s < R:
+            i += 1
+            continue
         if prog.anchor_start and not (s == R or s == 0 or text[base + s - 1] == 10):
             i += 1
             continue
@@ -349,7 +383,7 @@ def _rechain(piece: ShardedDatabase, prog, cand, chain, R: int):
         out_b.append(s)
         out_e.append(int(ce[i]))
         R = int(ce[i])
-        i = int(np.searchsorted(cb, R))
+        i = first_from(R, cur)
     return np.array(out_b, dtype=np.int64), np.array(out_e, dtype=np.int64)
 
 

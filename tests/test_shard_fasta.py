@@ -45,18 +45,19 @@ class OracleScanner:
 
     def __init__(self, piece):
         self.text = piece.raw[piece.beg:piece.stop]
+        self.regs = list(zip(*piece.regions))   # the file's search regions over the piece
 
     def reported(self, progs, k, types):
         from oracle import oracle
         out = []
         for p in progs:
-            hits = oracle.scan_reported(self.text, p, k, types)
+            hits = oracle.scan_reported(self.text, p, k, types, regs=self.regs)
             out.append((np.array([b for b, _ in hits], dtype=np.int64), np.array([e for _, e in hits], dtype=np.int64)))
         return out
 
     def candidates(self, prog, k, types):
         from oracle import oracle
-        hits = oracle.scan_candidates(self.text, prog, k, types)
+        hits = oracle.scan_candidates(self.text, prog, k, types, regs=self.regs)
         return (np.array([b for b, _ in hits], dtype=np.int64), np.array([e for _, e in hits], dtype=np.int64))
 
 
@@ -68,13 +69,13 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, data, q):
+def _worker(rank, world, port, data, q, bufsize=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from patmatchdocker_amd.regex import compile_pattern
-        piece = shards.ShardedDatabase(data, world, rank, open_db=False)
+        piece = shards.ShardedDatabase(data, world, rank, open_db=False, bufsize=bufsize)
         res = []
         for pat, k in CASES:
             prog = compile_pattern(pat, ignore_case=True)
@@ -104,15 +105,17 @@ def test_header_lines_follow_the_index_script():
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_scan_equals_whole_file(world):
+@pytest.mark.parametrize("world,bufsize", [(2, None), (3, None), (2, 301), (3, 173)])
+def test_sharded_scan_equals_whole_file(world, bufsize):
+    """bufsize: nrgrep's search regions (-b) small enough that the file holds
+    many, the report chain restarting at each region start across cuts."""
     from oracle import oracle
     from patmatchdocker_amd.regex import compile_pattern
     data = make_fasta()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q, bufsize)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=200) for _ in range(world))
@@ -121,7 +124,8 @@ def test_sharded_scan_equals_whole_file(world):
         assert p.exitcode == 0
     crossed = 0
     for i, (pat, k) in enumerate(CASES):
-        want = oracle.scan_reported(data, compile_pattern(pat, ignore_case=True), k, "s", skip_headers=True)
+        want = oracle.scan_reported(data, compile_pattern(pat, ignore_case=True), k, "s", skip_headers=True,
+                                    bufsize=bufsize or oracle.NRGREP_BUFFER)
         for r in range(world):
             assert got[r][i] == want, (pat, k, r)
         cuts = [b for b, _ in shards.split_fasta(data, world)[1:]]

@@ -520,7 +520,7 @@ void free_db(pm_db* db) {
     }
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
-    void* ptrs[] = {db->reg_t, db->reg_e, db->reg_lut, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
+    void* ptrs[] = {db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
@@ -638,18 +638,29 @@ void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<ui
         while (r + 1 < t.size() && t[r + 1] <= (b << REG_LUT_SHIFT)) ++r;
         lut[b] = (uint32_t)r;
     }
+    // blocks with a region start (> 0) within REG_NEAR_SPAN on either side
+    const uint64_t nblk = (db->n >> REG_NEAR_SHIFT) + 1;
+    std::vector<uint32_t> near((nblk + 31) / 32, 0u);
+    for (size_t r = 1; r < t.size(); ++r) {
+        const uint64_t lo = t[r] > REG_NEAR_SPAN ? t[r] - REG_NEAR_SPAN : 0, hi = t[r] + REG_NEAR_SPAN;
+        for (uint64_t b = lo >> REG_NEAR_SHIFT; b <= (hi >> REG_NEAR_SHIFT) && b < nblk; ++b) near[b >> 5] |= 1u << (b & 31);
+    }
     HIPCHK(hipStreamSynchronize(db->stream));   // queued scans may still read the old table
-    for (void* p : {(void*)db->reg_t, (void*)db->reg_e, (void*)db->reg_lut})
+    for (void* p : {(void*)db->reg_t, (void*)db->reg_e, (void*)db->reg_lut, (void*)db->reg_near})
         if (p) HIPCHK(hipFree(p));
     db->reg_t = db->reg_e = nullptr;
-    db->reg_lut = nullptr;
+    db->reg_lut = db->reg_near = nullptr;
     HIPCHK(hipMalloc(&db->reg_t, t.size() * 8));
     HIPCHK(hipMalloc(&db->reg_e, e.size() * 8));
     HIPCHK(hipMalloc(&db->reg_lut, nlut * 4));
+    HIPCHK(hipMalloc(&db->reg_near, near.size() * 4));
     HIPCHK(hipMemcpy(db->reg_t, t.data(), t.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(db->reg_e, e.data(), e.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(db->reg_lut, lut.data(), nlut * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db->reg_near, near.data(), near.size() * 4, hipMemcpyHostToDevice));
     db->nreg = (uint32_t)t.size();
+    db->reg_blind = false;
+    for (size_t r = 0; r + 1 < t.size(); ++r) db->reg_blind |= e[r] != t[r + 1] + 1;
 }
 
 }  // namespace pm

@@ -695,7 +695,7 @@ __device__ inline bool es_brk_before(const TextView& tv, uint64_t p) {
 __device__ inline bool es_head(const uint64_t* keys, uint64_t i, int32_t gap, int lines, const TextView& tv) {
     if (i == 0 || keys[i] - keys[i - 1] > (uint64_t)gap) return true;
     const uint64_t p = keys[i] & ES_POS_MASK;
-    if (tv.reg.n > 1 && region_of(tv.reg, p) != region_of(tv.reg, keys[i - 1] & ES_POS_MASK)) return true;
+    if (region_near(tv.reg, p) && region_of(tv.reg, p) != region_of(tv.reg, keys[i - 1] & ES_POS_MASK)) return true;
     if (!lines) return false;
     return p > 0 && es_brk_before(tv, p);
 }
@@ -723,8 +723,8 @@ __global__ __launch_bounds__(256) void k_es_heads(EsPrep P, const uint64_t* __re
                 const int64_t slot = (int64_t)(keys[i] >> 48) - P.pid_base;
                 if (!P.lines && slot >= 0 && slot < P.nslots && (i + 1 == total || es_head(keys, i + 1, P.gap_max, 0, tv))) {
                     const EsSlot& S = P.slots[slot];
-                    if (S.lone && (tv.reg.n <= 1 || (keys[i] & ES_POS_MASK) + (uint64_t)S.m <=
-                                                         tv.reg.e[region_of(tv.reg, keys[i] & ES_POS_MASK)])) {
+                    if (S.lone && (!region_near(tv.reg, keys[i] & ES_POS_MASK) ||
+                                   (keys[i] & ES_POS_MASK) + (uint64_t)S.m <= tv.reg.e[region_of(tv.reg, keys[i] & ES_POS_MASK)])) {
                         // A lone start with substitutions only is what nrgrep
                         // prints: a verification from any candidate returns
                         // the window [pos - L, pos - L + m) (no indels: both

@@ -585,18 +585,18 @@ __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
     const uint64_t e = s + len;
     // inside the region it is found in (only a simple-engine window over a
     // region's last '\n', or a cut without one, can stick out)
-    if (a.tv.reg.n > 1 && e > a.tv.reg.e[region_of(a.tv.reg, s)]) return false;
+    const bool near = region_near(a.tv.reg, s);
+    if (near && e > a.tv.reg.e[region_of(a.tv.reg, s)]) return false;
     if (!(a.flags & PM_ANCHOR_END)) return true;
     // '$': a line end or the region end (recCheckRightContext 0x4021e0)
-    return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n' ||
-           (a.tv.reg.n > 1 && e == a.tv.reg.e[region_of(a.tv.reg, s)]);
+    return e >= a.tv.n || tv_raw(a.tv, e) == (uint8_t)'\n' || (near && e == a.tv.reg.e[region_of(a.tv.reg, s)]);
 }
 // (pattern, end), the running maximum the heads are found with; the report
 // rule restarts at every region start, so an end past the next region's
 // start (the '\n' both regions hold) counts as that start
 __device__ inline uint64_t rep_val(const RepArgs& a, uint64_t key, uint32_t len) {
     uint64_t v = key + len;
-    if (a.tv.reg.n > 1) {
+    if (region_near(a.tv.reg, key & POS_MASK)) {
         const uint32_t r = region_of(a.tv.reg, key & POS_MASK);
         if (r + 1 < a.tv.reg.n) v = umin64(v, (key & ~POS_MASK) | a.tv.reg.t[r + 1]);
     }
@@ -604,7 +604,7 @@ __device__ inline uint64_t rep_val(const RepArgs& a, uint64_t key, uint32_t len)
 }
 // s starts a region (the search restarts there: R = s)
 __device__ inline bool rep_region_start(const RepArgs& a, uint64_t s) {
-    return a.tv.reg.n > 1 && a.tv.reg.t[region_of(a.tv.reg, s)] == s;
+    return region_near(a.tv.reg, s) && a.tv.reg.t[region_of(a.tv.reg, s)] == s;
 }
 
 // a start on a header line or on the '\n' that ends it maps to the '>name'
@@ -637,6 +637,10 @@ __device__ inline uint64_t shfl_xor64(uint64_t v, int d) {
     const uint32_t lo = __shfl_xor((uint32_t)v, d, 64), hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
     return ((uint64_t)hi << 32) | lo;
 }
+__device__ inline uint64_t shfl_up64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_up((uint32_t)v, d, 64), hi = __shfl_up((uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline uint64_t block_max(uint64_t v, uint64_t* red) {
     for (int d = 32; d > 0; d >>= 1) v = umax64(v, shfl_xor64(v, d));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -664,10 +668,21 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     uint64_t m = 0;
     if (a.flags & PM_REPORT_NRGREP) {
-        for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
-            const uint64_t key = a.keys[i];
-            const uint32_t len = a.lens[i];
-            if (rep_valid(a, key, len)) m = umax64(m, rep_val(a, key, len));
+        // 4 candidates per round: their loads (and the region lookups that
+        // depend on them) are in flight together
+        constexpr int U = 4;
+        for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += U * REP_T) {
+            uint64_t key[U];
+            uint32_t len[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = i0 + (uint64_t)u * REP_T;
+                key[u] = i < b1 ? a.keys[i] : 0ull;
+                len[u] = i < b1 ? a.lens[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (rep_valid(a, key[u], len[u])) m = umax64(m, rep_val(a, key[u], len[u]));
         }
         m = block_max(m, red);
     }
@@ -680,7 +695,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
 // acc[] and the kept count of every chunk
 __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     __shared__ uint64_t red[REP_T / 64];
-    __shared__ uint64_t scan[REP_T];
+    __shared__ uint64_t wmax[REP_T / 64];
     const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     if (!(a.flags & PM_REPORT_NRGREP)) {   // every candidate: only the anchors filter
@@ -728,17 +743,26 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             if (valid) val = rep_val(a, key, len);
             else a.acc[i] = 0;
         }
-        scan[threadIdx.x] = val;
-        __syncthreads();
-        for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive max-scan
-            const uint64_t o = threadIdx.x >= d ? scan[threadIdx.x - d] : 0;
-            __syncthreads();
-            scan[threadIdx.x] = umax64(scan[threadIdx.x], o);
-            __syncthreads();
+        // exclusive max-scan over the tile: within each wave by shuffles,
+        // then the maxima of the waves before it (one LDS exchange)
+        const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint64_t incl = val;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o = shfl_up64(incl, d);
+            if (lane >= (uint32_t)d) incl = umax64(incl, o);
         }
-        const uint64_t excl = umax64(carry, threadIdx.x ? scan[threadIdx.x - 1] : 0ull);
-        const uint64_t tile_max = scan[REP_T - 1];
+        if (lane == 63) wmax[w] = incl;
         __syncthreads();
+        uint64_t pre = 0, tile_max = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < REP_T / 64; ++q) {
+            if (q < w) pre = umax64(pre, wmax[q]);
+            tile_max = umax64(tile_max, wmax[q]);
+        }
+        __syncthreads();   // wmax is rewritten by the next tile
+        const uint64_t below = shfl_up64(incl, 1);
+        const uint64_t excl = umax64(carry, lane ? umax64(below, pre) : pre);
         carry = umax64(carry, tile_max);
         // '^': a start is reported only at a line start or exactly at the
         // resume point R (recCheckLeftContext 0x402170), so a candidate that
@@ -795,7 +819,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_check(RepArgs a) {   // PM_REPORT
 
 __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
     __shared__ uint64_t red[REP_T / 64];
-    __shared__ uint32_t scan[REP_T];
+    __shared__ uint32_t scan[REP_T / 64];
     const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
     uint64_t base_out = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) base_out += a.bcnt[b];
@@ -809,24 +833,27 @@ __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
         }
     }
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
-        const uint32_t keep = (i < b1 && (a.acc[i] & 1)) ? 1u : 0u;   // bit 1: a cluster head (k_es_walk)
-        scan[threadIdx.x] = keep;
+        const bool keep = i < b1 && (a.acc[i] & 1);   // bit 1: a cluster head (k_es_walk)
+        // the kept entries before this one: a wave ballot, then the counts
+        // of the waves before it (one LDS exchange)
+        const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+        if (lane == 0) scan[w] = (uint32_t)__builtin_popcountll(m);
         __syncthreads();
-        for (uint32_t d = 1; d < REP_T; d <<= 1) {   // inclusive sum-scan
-            const uint32_t o = threadIdx.x >= d ? scan[threadIdx.x - d] : 0u;
-            __syncthreads();
-            scan[threadIdx.x] += o;
-            __syncthreads();
+        uint32_t pre = 0, tile = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < REP_T / 64; ++q) {
+            if (q < w) pre += scan[q];
+            tile += scan[q];
         }
+        __syncthreads();
         if (keep) {
-            const uint64_t o = base_out + scan[threadIdx.x] - 1;
+            const uint64_t o = base_out + pre + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             a.okeys[o] = a.keys[i];
             a.olens[o] = a.lens[i];
         }
-        const uint32_t tile = scan[REP_T - 1];
-        __syncthreads();
         base_out += tile;
     }
 }
@@ -850,7 +877,7 @@ void retire_buffers(pm_hits* h, hipStream_t s) {
 
 TextView text_view(const pm_db* db) {
     return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag,
-                    Regions{db->reg_t, db->reg_e, db->reg_lut, db->nreg}};
+                    Regions{db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->nreg}};
 }
 
 bool report_needed(const pm_db* db, uint32_t flags, bool cross) {
@@ -896,6 +923,10 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     a.count = ws.count;
     a.host_count = host_count;
     a.tv = text_view(db);
+    // Regions cut after a '\n': a line-bounded match never reaches one, and
+    // '^' never starts on the '\n' a region starts at -- only the simple
+    // engine's windows (hdr) and blind cuts need the region checks
+    if (!hdr && !db->reg_blind) a.tv.reg.n = 0;
     a.flags = flags;
     // PM_REPORT_KEEP_HEADERS=1 (debugging): keep header-line starts
     static const bool keep_hdr = getenv("PM_REPORT_KEEP_HEADERS") && getenv("PM_REPORT_KEEP_HEADERS")[0] == '1';

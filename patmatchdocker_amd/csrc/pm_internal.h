@@ -361,8 +361,9 @@ struct pm_db : pm_lane {
     // nrgrep's search regions (Regions; set by pm_db_create* for the file
     // itself, or by pm_db_set_regions)
     uint64_t *reg_t = nullptr, *reg_e = nullptr;
-    uint32_t* reg_lut = nullptr;
+    uint32_t *reg_lut = nullptr, *reg_near = nullptr;
     uint32_t nreg = 0;
+    bool reg_blind = false;   // some region ends without a '\n' (a buffer holding none)
 };
 
 // A pipelined scan (pm_scan_linear_async) between launch and resolution: the
@@ -651,13 +652,24 @@ struct Regions {
     const uint64_t* t = nullptr;    // starts (increasing)
     const uint64_t* e = nullptr;    // ends
     const uint32_t* lut = nullptr;  // [p >> REG_LUT_SHIFT]: the last region starting at or before that bucket
+    const uint32_t* near = nullptr; // bit per REG_NEAR_SHIFT block: a region start within REG_NEAR_SPAN
     uint32_t n = 0;                 // <= 1: one region, the whole text (nothing to check)
 };
 constexpr int REG_LUT_SHIFT = 20;
+constexpr int REG_NEAR_SHIFT = 12;
+constexpr uint64_t REG_NEAR_SPAN = 512;   // > the longest window (PM_MAX_POSITIONS + PM_MAX_K + 1)
 __device__ inline uint32_t region_of(const Regions& g, uint64_t s) {
     uint32_t r = g.lut[s >> REG_LUT_SHIFT];
     while (r + 1 < g.n && g.t[r + 1] <= s) ++r;
     return r;
+}
+// a region start (other than 0) lies within REG_NEAR_SPAN of s: only then
+// can the regions change anything about a window starting at s (one cached
+// load; regions are ~1.6 MB apart)
+__device__ inline bool region_near(const Regions& g, uint64_t s) {
+    if (g.n <= 1) return false;
+    const uint64_t b = s >> REG_NEAR_SHIFT;
+    return (g.near[b >> 5] >> (b & 31)) & 1u;
 }
 
 struct TextView {

@@ -576,7 +576,8 @@ __device__ inline uint64_t rep_chunk(uint64_t total, uint32_t G) { return (total
 
 // '$': the match must end at a line end or at the end of the text (the
 // region end, recCheckRightContext 0x4021e0)
-__device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
+// near: region_near(key's start), computed once per candidate by the caller
+__device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len, bool near) {
     if (len == 0) return false;   // a start whose verify found no (anchored) end
     // a speculative list that will be discarded (a bin the LDS sort skipped)
     // holds stale keys: never read the text at a position outside it
@@ -585,7 +586,6 @@ __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
     const uint64_t e = s + len;
     // inside the region it is found in (only a simple-engine window over a
     // region's last '\n', or a cut without one, can stick out)
-    const bool near = region_near(a.tv.reg, s);
     if (near && e > a.tv.reg.e[region_of(a.tv.reg, s)]) return false;
     if (!(a.flags & PM_ANCHOR_END)) return true;
     // '$': a line end or the region end (recCheckRightContext 0x4021e0)
@@ -594,9 +594,9 @@ __device__ inline bool rep_valid(const RepArgs& a, uint64_t key, uint32_t len) {
 // (pattern, end), the running maximum the heads are found with; the report
 // rule restarts at every region start, so an end past the next region's
 // start (the '\n' both regions hold) counts as that start
-__device__ inline uint64_t rep_val(const RepArgs& a, uint64_t key, uint32_t len) {
+__device__ inline uint64_t rep_val(const RepArgs& a, uint64_t key, uint32_t len, bool near) {
     uint64_t v = key + len;
-    if (region_near(a.tv.reg, key & POS_MASK)) {
+    if (near) {
         const uint32_t r = region_of(a.tv.reg, key & POS_MASK);
         if (r + 1 < a.tv.reg.n) v = umin64(v, (key & ~POS_MASK) | a.tv.reg.t[r + 1]);
     }
@@ -682,7 +682,10 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (rep_valid(a, key[u], len[u])) m = umax64(m, rep_val(a, key[u], len[u]));
+                if (len[u]) {
+                    const bool nr = region_near(a.tv.reg, key[u] & POS_MASK);
+                    if (rep_valid(a, key[u], len[u], nr)) m = umax64(m, rep_val(a, key[u], len[u], nr));
+                }
         }
         m = block_max(m, red);
     }
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint64_t s = key & POS_MASK;
-            bool ok = rep_valid(a, key, a.lens[i]);
+            bool ok = rep_valid(a, key, a.lens[i], region_near(a.tv.reg, s));
             if (ok && (a.flags & PM_ANCHOR_START)) ok = rep_line_start(a, s);
             ok = ok && rep_keep(a, key);
             a.acc[i] = ok ? 1 : 0;
@@ -723,7 +726,8 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         for (uint64_t i = threadIdx.x; i < b0; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint32_t len = a.lens[i];
-            if (rep_valid(a, key, len)) c2 = umax64(c2, rep_val(a, key, len));
+            const bool nr = region_near(a.tv.reg, key & POS_MASK);
+            if (rep_valid(a, key, len, nr)) c2 = umax64(c2, rep_val(a, key, len, nr));
         }
         c2 = block_max(c2, red);
         if (threadIdx.x == 0 && c2 != carry)
@@ -739,8 +743,9 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         if (i < b1) {
             key = a.keys[i];
             len = a.lens[i];
-            valid = rep_valid(a, key, len);
-            if (valid) val = rep_val(a, key, len);
+            const bool nr = region_near(a.tv.reg, key & POS_MASK);
+            valid = rep_valid(a, key, len, nr);
+            if (valid) val = rep_val(a, key, len, nr);
             else a.acc[i] = 0;
         }
         // exclusive max-scan over the tile: within each wave by shuffles,
@@ -782,13 +787,14 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             if (anch ? kj > run || (kj == run && rep_region_start(a, kj & POS_MASK)) : kj >= run) break;  // the next head
             const uint32_t lj = a.lens[j];
             kept = 0;
-            if (rep_valid(a, kj, lj)) {
+            const bool nj = region_near(a.tv.reg, kj & POS_MASK);
+            if (rep_valid(a, kj, lj, nj)) {
                 const uint64_t sj = kj & POS_MASK;
                 if (sj >= R && (!anch || sj == R || rep_line_start(a, sj))) {
                     R = sj + lj;
                     kept = rep_keep(a, kj) ? 1 : 0;
                 }
-                run = umax64(run, rep_val(a, kj, lj));
+                run = umax64(run, rep_val(a, kj, lj, nj));
             }
             a.acc[j] = kept;
             if (kept) {

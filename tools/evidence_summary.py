@@ -47,6 +47,7 @@ copy(os.path.join(root, "prof", "run_kernel_trace.csv"), "%s_prof_kernel_trace.c
 
 lin = pmc(["p1", "p2", "p3", "p4"], "pm_linear_jit")
 ids = pmc(["q1", "q2", "q3", "q4"], "pm_ids_rev")
+batch = pmc(["c1", "c2"], "k_batch_scan")
 cal = pmc(["cal"], "k_read")
 bench = json.load(open(os.path.join(root, "bench.json")))
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]
@@ -65,6 +66,7 @@ json.dump({"workload": bench["config"]["workload"], "kernel": "pm_linear_jit",
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu_evidence.sh)"},
           open(os.path.join(prof, "%s_traffic.json" % rnd), "w"), indent=1)
 json.dump({"pm_linear_jit (configs[2], k=2 substitutions)": lin, "pm_ids_rev (configs[2], -k 2ids)": ids,
+           "k_batch_scan (configs[4], 256 patterns k=0)": batch,
            "note": "medians per dispatch; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles "
                    "(MI355X_MICROARCH.md); one counter group per rocprofv3 run"},
           open(os.path.join(prof, "%s_pmc.json" % rnd), "w"), indent=1)

@@ -30,6 +30,12 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
   timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$out/p$i" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$out/p$i.json" 2> "$out/p$i.err" || die "pmc pass $i" "$out/p$i.err"
   timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$out/q$i" -o run -- python3 bench.py --types ids --steps 2 --warmup 1 --no-cpu-baseline > "$out/q$i.json" 2> "$out/q$i.err" || die "ids pmc pass $i" "$out/q$i.err"
 done
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$out/c$i" -o run -- python3 bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c$i.json" 2> "$out/c$i.err" || die "batch pmc pass $i" "$out/c$i.err"
+done
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/cal" -o run -- ./tools/micro/calib_read 4096 > "$out/cal.json" 2> "$out/cal.err" || die calibration "$out/cal.err"
 timeout -k 10 300 python tools/config_times.py > "$out/configs.json" 2> "$out/configs.err" || die configs "$out/configs.err"
 echo evidence-done

@@ -100,6 +100,29 @@ def load_traffic(workload):
     return None
 
 
+def load_issue(kernel_key):
+    """VALU-issue occupancy of a kernel from the committed PMC run
+    (profiles/<ROUND>_pmc.json): SQ_INSTS_VALU wave-instructions x 4 cycles
+    over the 1024 SIMDs, divided by the dispatch's cycles at its measured
+    clock (MI355X_MICROARCH.md) -- how close an integer kernel that does not
+    saturate HBM sits to its own (VALU) bound."""
+    path = os.path.join(ROOT, "profiles", "%s_pmc.json" % ROUND)
+    try:
+        with open(path) as fh:
+            data = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for name, c in data.items():
+        if name.startswith(kernel_key) and isinstance(c, dict):
+            try:
+                busy = c["SQ_INSTS_VALU"] * 4 / 1024 / (c["effective_clock_ghz"] * 1e9) / (c["median_dispatch_ms"] * 1e-3)
+            except (KeyError, TypeError, ZeroDivisionError):
+                return None
+            return {"valu_issue_frac": round(busy, 3), "dispatch_ms": round(c["median_dispatch_ms"], 4),
+                    "source": "profiles/%s_pmc.json (rocprofv3 --pmc, median dispatch)" % ROUND}
+    return None
+
+
 def cpu_threads_default():
     """The box's CPU share: OMP_NUM_THREADS (16 on the GPU box), else the
     affinity mask, capped at 16."""
@@ -332,6 +355,7 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "note": "VALU-issue bound (see DESIGN.md §4)"},
         }
+        line["roofline"]["issue"] = load_issue("pm_linear_jit") if jit else None
         if args.config == 4:
             # per-pattern throughput beside the scanned-bases metric
             line["pattern_gbases_per_s"] = round(value * len(progs), 1)
@@ -346,17 +370,19 @@ def main():
                 # one k_batch_scan launch reads the planes once (0.25 B/base)
                 # and probes a 10-mer table in LDS per position (pm_batch.hip)
                 line["roofline"]["kernel"] = "k_batch_scan (q-gram filter: register transpose + LDS table probe per position)"
-                line["roofline"]["note"] = ("one database read per query in one launch; VALU/LDS-issue bound "
+                line["roofline"]["note"] = ("one database read per query in one launch; VALU-issue bound "
                                             "(~5 VALU + 1 ds_read per position), see DESIGN.md §3")
+                line["roofline"]["issue"] = load_issue("k_batch_scan")
             else:
                 line["roofline"]["note"] = ("one database read per query; kernel_ms = the sum of the query's "
                                             "specialized launches (<= 8 patterns each); VALU-bound, see DESIGN.md §4")
             line["roofline"]["traffic"] = None
         if indel:
             line["roofline"].update({
-                "kernel": "pm_ids_rev (hipRTC, bit-sliced over the 32 streams of a tile) + k_nfa_verify",
-                "note": "per strand launch: start pass + verify of its candidates; one read of the planes "
-                        "(0.25 B/base) per launch; VALU-bound (DESIGN.md §4)"})
+                "kernel": "pm_ids_rev (hipRTC, bit-sliced over the 32 streams of a tile) + k_es_walk",
+                "note": "per strand launch: start pass + nrgrep's esimple walk over its candidates; one read of "
+                        "the planes (0.25 B/base) per launch; issue / latency bound (DESIGN.md §4)",
+                "issue": load_issue("pm_ids_rev")})
             line["roofline"]["traffic"] = None
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
             thr = args.cpu_threads or cpu_threads_default()

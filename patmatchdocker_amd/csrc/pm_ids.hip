@@ -34,6 +34,11 @@ namespace pm {
 namespace {
 
 constexpr int IDS_MAX_REGS = 64;   // m * (k + 1) state registers at most
+// Words in flight per wave: a step's plane word is DMA'd into a per-wave LDS
+// ring IDS_DEPTH steps before it is used (the step itself is ~100 dependent
+// VALU ops, too short to cover an HBM miss, and the compiler's waits drained
+// register prefetches right after issuing them)
+constexpr int IDS_DEPTH = 4;
 
 const char* kIdsCommon = R"IDS(
 typedef unsigned int u32;
@@ -58,6 +63,24 @@ struct IArgs {
 };
 __device__ inline u64 phys(u64 tile, u32 w) {
     return tile * TILE_WORDS + (w < STREAM ? (u64)((w & 31u) * 64u + (w >> 5)) : (u64)w);
+}
+// LDS-DMA of one plane word per lane: the hi plane's dword lands at
+// lds + 4 lane, the lo plane's at lds + 256 + 4 lane (no VGPR destination;
+// waited for with vmcnt).  Inline asm, so that the compiler's own wait
+// bookkeeping does not drain the loads in flight.
+__device__ __forceinline__ void dma_dword(u64 ga, u32 lds) {
+    u32 keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(ga), "s"(lds) : "memory");
+}
+// a step's word of both planes: {hi, lo} at lds, lds + 256 and the
+// exception plane's {brk, oth} at lds + 512, lds + 768 (4 lane-linear dwords)
+__device__ __forceinline__ void dma_word(const uint2* p, long dbo, u32 lds) {
+    const u64 ga = (u64)p, ge = (u64)(p + dbo);
+    dma_dword(ga, lds);
+    dma_dword(ga + 4ull, lds + 256u);
+    dma_dword(ge, lds + 512u);
+    dma_dword(ge + 4ull, lds + 768u);
 }
 __device__ inline void push(const IArgs& a, u64 pos) {
     const u32 bin = (u32)(pos >> a.pos_shift);
@@ -128,7 +151,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    sg << "ids5:" << m << ":" << k << ":" << sp.errs << ":";
+    sg << "ids8:" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
     for (int j = 0; j <= k; ++j) sg << ":" << sp.rev_pre[j] << "," << sp.rev_ins[j];
 
@@ -200,8 +223,21 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     auto step = [&](std::ostringstream& o, char src, char dst, const std::string& tv, const std::string& vv,
                     const std::string& pv, bool emit) {
         const std::string in = "            ";
+        (void)vv;
         o << in << "{\n";
-        o << in << "    const uint2 v = " << vv << ";\n";
+        // this step's word landed (the DEPTH - 1 later steps' DMAs may
+        // still be in flight), then the DMA DEPTH steps ahead goes into the
+        // slot the previous step read
+        o << in << "    asm volatile(\"s_waitcnt vmcnt(" << 4 * (IDS_DEPTH - 1) << ")\" ::: \"memory\");\n";
+        o << in << "    const uint2 v = make_uint2(ring[sl * 256u + col], ring[sl * 256u + 64u + col]);\n";
+        o << in << "    {\n";
+        o << in << "        const int q2 = qs + IDS_DEPTH, t2 = 31 + WU - q2;\n";
+        o << in << "        dma_word(q2 < WU ? pn + (long)(t2 - 32) * sn : q2 < WU + 32 ? pm + (long)t2 * 64 : tb, dbo, "
+                   "rbase + snx * 1024u);\n";
+        o << in << "    }\n";
+        o << in << "    const uint2* " << pv << " = " << (emit ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn") << ";\n";
+        o << in << "    const u32 sl_ = sl;\n";
+        o << in << "    ++qs; sl = sl + 1u == IDS_SLOTS ? 0u : sl + 1u; snx = snx + 1u == IDS_SLOTS ? 0u : snx + 1u;\n";
         for (size_t c = 0; c < rep.size(); ++c) {
             const PosClass& p = pc[rep[c]];
             if (p.any) o << in << "    u32 M" << c << " = 0xffffffffu;\n";
@@ -215,14 +251,20 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         o << in << "    const u32 rf = (u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr) | "
                    "(u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr);\n";
         o << in << "    if (rf != 0u" << (emit ? "" : " || ((halof >> rr) & 1ull)") << ") {   // wave-uniform, rare\n";
-        o << in << "        const uint2 e = " << pv << "[dbo];\n";
+        o << in << "        const uint2 e = make_uint2(ring[sl_ * 256u + 128u + col], ring[sl_ * 256u + 192u + col]);\n";
         o << in << "        const u32 nb = ~e.x;\n";
-        // "other" bytes: the byte's own class membership
-        o << in << "        if (e.y) {\n";
+        // "other" bytes: an N (NUC_N_MARK: its hi bit) matches '.' only;
+        // any other byte takes its own class membership from the side tables
+        o << in << "        const u32 en = e.y & v.x, eo = e.y & ~v.x;\n";
+        for (size_t c = 0; c < rep.size(); ++c) {
+            const bool n_in = (sp.byte_mask[(uint8_t)'N'] >> rep[c]) & 1;   // the class takes N ('.', [ACGTN] ...)
+            o << in << "        M" << c << (n_in ? " |= en;\n" : " &= ~en;\n");
+        }
+        o << in << "        if (eo) {\n";
         o << in << "            const u64 pw = (u64)(" << pv << " - a.hl);\n";
         o << in << "            const u32 f = a.sbflag[pw >> 5];\n";
         o << in << "            const u32 xi = a.sbbase[pw >> 5] + __popc(f & ((1u << (u32)(pw & 31)) - 1u));\n";
-        o << in << "            for (u32 ob = e.y; ob; ob &= ob - 1) {\n";
+        o << in << "            for (u32 ob = eo; ob; ob &= ob - 1) {\n";
         o << in << "                const u32 b = __builtin_ctz(ob);\n";
         o << in << "                const u64 mk = a.bmask[a.xbytes[(u64)xi * 32 + b]];\n";
         for (size_t c = 0; c < rep.size(); ++c)
@@ -252,7 +294,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     o << "#define WU " << WU << "\n";
     // 4 workgroups per CU: <= 128 VGPRs, 4 waves per SIMD (staging each
     // tile in LDS by LDS-DMA first measured no faster, round 2)
-    o << "#define IDS_WG 4\n";
+    o << "#define IDS_WG 4\n#define IDS_DEPTH " << IDS_DEPTH << "\n#define IDS_SLOTS " << IDS_DEPTH + 1 << "\n";
     *sig = sg.str();
     o << R"IDS(
 // One wave per tile; lane c owns stream column c (logical words 32c ..
@@ -263,8 +305,11 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
 // lane r < 32 holds row r's 64 flag bits (one load per tile), a step reads
 // its row's with v_readlane.
 extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) {   // IDS_WG workgroups per CU
+    __shared__ __attribute__((aligned(16))) u32 ids_ring[4][IDS_SLOTS * 256];   // per wave: {hi, lo, brk, oth} x 64 lanes per slot
     const u32 col = threadIdx.x & 63;
     const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    u32* const ring = ids_ring[wid];
+    const u32 rbase = __builtin_amdgcn_readfirstlane((u32)reinterpret_cast<u64>(ring));   // its LDS byte address
     const u64 wave = (u64)blockIdx.x * 4u + wid, nwaves = gridDim.x * 4ull;
     const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
     for (u64 tile = wave; tile < a.ntiles; tile += nwaves) {
@@ -280,59 +325,46 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
         const uint2* pn = col < 63u ? tb + col + 1 : tb + STREAM;   // warm-up words: t - 32 ..
         const long sn = col < 63u ? 64 : 1;
         const uint2* pm = tb + col;                                  // own words: t * 64
+        // step q (0 .. WU + 31) reads word t = 31 + WU - q; the first
+        // IDS_DEPTH words go in flight now (the previous tile's DMAs have all
+        // landed: the slots are free)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int qs = 0;
+        u32 sl = 0, snx = IDS_DEPTH;
+        for (int q = 0; q < IDS_DEPTH; ++q) {
+            const int t2 = 31 + WU - q;
+            dma_word(q < WU ? pn + (long)(t2 - 32) * sn : q < WU + 32 ? pm + (long)t2 * 64 : tb, dbo, rbase + (u32)q * 1024u);
+        }
 )IDS";
     for (int j = 0; j <= k; ++j)
         for (int i = 0; i < m; ++i) o << "        u32 " << V('r', j, i) << " = 0, " << V('s', j, i) << " = 0;\n";
-    o << "        uint2 v0, v1;\n";
-    o << "        uint2 w0 = make_uint2(0u, 0u), w1 = make_uint2(0u, 0u);\n";
-    o << "        const uint2 *p0, *p1, *q0 = tb, *q1 = tb;\n";
-    auto ptr = [](bool own, const std::string& tv) {
-        return own ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn";
-    };
-    auto load = [&](const std::string& pv, const std::string& vv, const std::string& ev, bool own,
-                    const std::string& tv, const std::string& ind) {
-        o << ind << pv << " = " << ptr(own, tv) << ";\n";
-        o << ind << vv << " = *(" << ptr(own, tv) << ");\n";
-        (void)ev;
-    };
     // a phase: `n` steps from t = `t0` down, pointer form `own`; pairs of
-    // steps alternate the register banks and the word buffers (each step's
-    // successor word is loaded before the step runs)
+    // steps alternate the register banks (each step's word comes from the
+    // LDS ring)
     char b0 = 'r', b1 = 's';
     auto phase = [&](int t0, int n, bool own) {
         int t = t0;
         if (n % 2) {   // a single step first
             o << "        {\n";
-            load("p0", "v0", "e0", own, std::to_string(t), "            ");
-            step(o, b0, b1, std::to_string(t), "v0", "p0", own);
+            step(o, b0, b1, std::to_string(t), "", "p0", own);
             o << "        }\n";
             std::swap(b0, b1);
             --t;
             --n;
         }
         if (!n) return;
-        // the words of steps t and t - 1 are in v0 / v1 when an iteration
-        // starts; it issues the loads of t - 2 and t - 3 first (two steps
-        // ahead of their use)
         const std::string ind = "            ";
         const int last = t - n + 1;
-        o << "        {\n";
-        load("p0", "v0", "e0", own, std::to_string(t), ind);
-        load("p1", "v1", "e1", own, std::to_string(t - 1), ind);
-        o << "        }\n";
         o << "        for (int t = " << t << "; t >= " << last + 1 << "; t -= 2) {\n";
-        o << ind << "if (t - 2 >= " << last << ") {\n";
-        load("q0", "w0", "e0", own, "t - 2", ind + "    ");
-        load("q1", "w1", "e1", own, "t - 3", ind + "    ");
-        o << ind << "}\n";
-        step(o, b0, b1, "t", "v0", "p0", own);
-        step(o, b1, b0, "t - 1", "v1", "p1", own);
-        o << ind << "v0 = w0; v1 = w1; p0 = q0; p1 = q1;\n";
+        step(o, b0, b1, "t", "", "p0", own);
+        step(o, b1, b0, "t - 1", "", "p1", own);
         o << "        }\n";
     };
     phase(31 + WU, WU, false);   // warm-up: t = 32 + WU - 1 .. 32
     phase(31, 32, true);         // own column: t = 31 .. 0
-    o << "    }\n}\n";
+    // the last tile's look-ahead DMAs land before the wave ends (its LDS is
+    // released with the workgroup)
+    o << "    }\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}\n";
     return o.str();
 }
 

@@ -134,6 +134,29 @@ def test_anchors_on_gpu(engine, oracle_mod):
         db.close()
 
 
+def test_anchored_patterns_on_a_large_database(engine, oracle_mod):
+    """'^' on a 256 Mbp database (the converter turns every '<' pattern into
+    '^(...)'): the report pass handles anchored candidates in parallel (no
+    serial walk over the list), dense cross-line '^' windows included, within
+    a time bound, and equals the oracle over the whole text (256 records,
+    a few hundred search regions)."""
+    import time
+    # (records, pattern, k): '^(..)' chains a report from every line start to
+    # the end of its region (p == R passes '^'), the densest anchored case
+    for recs, pat, k in ((256, "^(A.)", 0), (256, "^(TA.?A)", 0), (256, "^(TAT[AT]A[AT]A[AG])", 1), (4, "^(..)", 0)):
+        db = engine.SequenceDatabase.synthetic(recs, 1_000_000, seed=77)
+        try:
+            text = db.decode(0, len(db))
+            prog = compile_pattern(pat)
+            t0 = time.perf_counter()
+            res, _ = engine.scan(db, [prog], k=k, types="s")
+            assert time.perf_counter() - t0 < 30.0, pat
+            want = oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True)
+            assert _pairs(res[0]) == want, (pat, k)
+        finally:
+            db.close()
+
+
 @pytest.mark.parametrize("alpha", ["nuc", "byte"])
 def test_nfa_reported_vs_oracle(engine, oracle_mod, alpha):
     """Variable-length patterns and indels: candidates (leftmost start,

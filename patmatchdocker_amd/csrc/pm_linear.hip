@@ -241,10 +241,18 @@ __device__ inline uint32_t select_bits(const OthersArgs& a, uint64_t t, uint64_t
 
 __global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
     const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= (a.use_edge ? a.nedge : a.nflag)) return;
     uint64_t w = 0;
-    const uint32_t ot = select_bits(a, t, &w);
-    if (ot) a.sel[atomicAdd(a.nsel, 1u)] = OtherSel{w, ot, 0u};
+    const uint32_t ot = t < (a.use_edge ? a.nedge : a.nflag) ? select_bits(a, t, &w) : 0u;
+    // one atomic per wave on the list length (a single counter: per-lane
+    // atomics serialize on it)
+    const uint64_t m = __builtin_amdgcn_ballot_w64(ot != 0u);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(a.nsel, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, (int)first, 64);
+    if (ot) a.sel[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+        OtherSel{w, ot, 0u};
 }
 
 constexpr int OTH_MAX_POS = 8 * 64;   // (pattern, position) entries of a chunk (JIT_MAX_P x 64)

@@ -421,6 +421,7 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipGetLastError());
     size_t tmp_bytes = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
+    (void)hipGetLastError();   // (rocPRIM's stale capture status, as below)
     void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
     (void)hipGetLastError();   // rocPRIM leaves a stale "stream is capturing" status behind

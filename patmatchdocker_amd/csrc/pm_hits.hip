@@ -438,6 +438,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                                                      (int)total, 0, 64, s));
         if (!inline_off)
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)sb.nbins, s));
+        (void)hipGetLastError();   // rocPRIM's stale capture status, size queries too (see the scan below)
         Carve c;
         const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
         const size_t o_uns = lds ? 0 : c.take(total * sizeof(uint64_t));
@@ -772,8 +773,12 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         // '^': a start is reported only at a line start or exactly at the
         // resume point R (recCheckLeftContext 0x402170), so a candidate that
         // touches the previous cluster's end belongs to that cluster
-        // (with '^' a candidate at a region start is a head: R restarts there)
-        if (!valid || (anch ? key < excl || (key == excl && !rep_region_start(a, key & POS_MASK)) : key < excl))
+        // (with '^' a candidate at a region start is a head: R restarts
+        // there -- the file's first position included, R = 0 before any
+        // report, key == excl == 0 for pattern 0)
+        if (!valid ||
+            (anch ? key < excl || (key == excl && (key & POS_MASK) != 0 && !rep_region_start(a, key & POS_MASK))
+                  : key < excl))
             continue;   // not a head: its head's walk writes it
         // head: every earlier report ends before it (R < its start)
         const uint64_t s0 = key & POS_MASK;

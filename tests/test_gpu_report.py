@@ -221,6 +221,30 @@ def test_config4_batch_of_256_patterns(engine, oracle_mod, monkeypatch, k, mbp):
     assert total > 1000
 
 
+def test_config4_batch_at_scale_on_the_synthetic_database(engine, oracle_mod, monkeypatch):
+    """configs[4]'s batch on the bench's own synthetic database (N runs,
+    IUPAC letters, ~70 search regions) at 70 Mbp: the q-gram filter, the
+    per-class exception pass over cross-line windows and the report rule
+    restarting at every region start, every pattern vs the oracle on the
+    decoded text."""
+    import bench
+    monkeypatch.setenv("PM_JIT", "1")
+    progs = [compile_pattern(convert("-n", m)) for m in bench.batch_patterns(256)]
+    db = engine.SequenceDatabase.synthetic(70, 1_000_000, seed=321)
+    try:
+        text = db.decode(0, len(db))
+        assert len(db.regions()[0]) > 40
+        res, _ = engine.scan(db, progs, k=0, types="")
+    finally:
+        db.close()
+    total = 0
+    for prog, r in list(zip(progs, res))[::4]:   # every 4th pattern: the oracle takes ~0.4 s each
+        want = oracle_mod.scan_threads(text, prog, 0, "", skip_headers=True, threads=16, report="nrgrep")
+        assert _pairs(r) == want, prog.source
+        total += len(want)
+    assert total > 10000
+
+
 def _exception_rich_fasta(seed, mbp, width, headless):
     """Multi-line records with N runs, IUPAC letters and lower case: windows
     over breaks (the simple engine's cross windows) and over "other" bytes

@@ -569,7 +569,6 @@ struct RepArgs {
     TextView tv;
     uint32_t flags;
     int hdr;                // candidates may start on a header line (simple engine, cross windows)
-    int debug;
 };
 
 __device__ inline uint64_t rep_total(const RepArgs& a) { return a.total_d ? *a.total_d : a.total_h; }
@@ -722,19 +721,6 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     uint64_t carry = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
     carry = block_max(carry, red);
-    if (a.debug) {   // PM_REPORT_DEBUG=1: brute-force check of the chunk carry
-        uint64_t c2 = 0;
-        for (uint64_t i = threadIdx.x; i < b0; i += REP_T) {
-            const uint64_t key = a.keys[i];
-            const uint32_t len = a.lens[i];
-            const bool nr = region_near(a.tv.reg, key & POS_MASK);
-            if (rep_valid(a, key, len, nr)) c2 = umax64(c2, rep_val(a, key, len, nr));
-        }
-        c2 = block_max(c2, red);
-        if (threadIdx.x == 0 && c2 != carry)
-            printf("rep carry mismatch block %u: bmax-carry %llx brute %llx\n", blockIdx.x, (unsigned long long)carry,
-                   (unsigned long long)c2);
-    }
     uint64_t own = 0;   // kept candidates of this chunk found by this thread's walks
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
@@ -810,22 +796,6 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     }
     own = block_sum(own, red);
     if (threadIdx.x == 0 && own) atomicAdd(&a.bcnt[blockIdx.x], (uint32_t)own);
-}
-
-__global__ __launch_bounds__(REP_T) void k_rep_check(RepArgs a) {   // PM_REPORT_DEBUG: acc sums vs counts
-    __shared__ uint64_t red[REP_T / 64];
-    const uint64_t total = rep_total(a), C = rep_chunk(total, gridDim.x);
-    const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
-    uint64_t c = 0, bad = 0;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
-        c += a.acc[i] & 1;
-        bad += a.acc[i] > 3;
-    }
-    c = block_sum(c, red);
-    bad = block_sum(bad, red);
-    if (threadIdx.x == 0 && (c != a.bcnt[blockIdx.x] || bad))
-        printf("rep check block %u: acc sum %llu bcnt %u bad %llu (C %llu)\n", blockIdx.x, (unsigned long long)c,
-               a.bcnt[blockIdx.x], (unsigned long long)bad, (unsigned long long)C);
 }
 
 __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
@@ -939,10 +909,7 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     // engine's windows (hdr) and blind cuts need the region checks
     if (!hdr && !db->reg_blind) a.tv.reg.n = 0;
     a.flags = flags;
-    // PM_REPORT_KEEP_HEADERS=1 (debugging): keep header-line starts
-    static const bool keep_hdr = getenv("PM_REPORT_KEEP_HEADERS") && getenv("PM_REPORT_KEEP_HEADERS")[0] == '1';
-    a.hdr = hdr && !keep_hdr && !(flags & PM_KEEP_HEADERS) ? 1 : 0;
-    a.debug = getenv("PM_REPORT_DEBUG") ? 1 : 0;
+    a.hdr = hdr && !(flags & PM_KEEP_HEADERS) ? 1 : 0;
     (void)cap_items;   // every acc entry below the list length is written by k_rep_walk (no memset)
     // chunks: REP_G, more for long lists (a big batch's tens of millions of
     // candidates: every block's serial tile scans then stay short)
@@ -954,7 +921,6 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
         hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
         hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
     }
-    if (a.debug) hipLaunchKernelGGL(k_rep_check, dim3(G), dim3(REP_T), 0, s, a);
     if (done)
         hipExtLaunchKernelGGL(k_rep_scatter, dim3(G), dim3(REP_T), 0, s, nullptr, done, 0u, a);
     else

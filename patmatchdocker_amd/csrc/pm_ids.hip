@@ -25,6 +25,7 @@
 // (L = the longest match, m + k) read from the next column or the halo.
 #include <map>
 #include <sstream>
+#include <tuple>
 
 #include <hip/hip_ext.h>
 
@@ -131,18 +132,22 @@ int subset_table(int s) {
     return t;
 }
 
-std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
+// The kernel's source and its cache signature (everything the source
+// depends on); with want_source false only the signature (a query's cache
+// lookup: generating the source cost ~0.1 ms per query).
+std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source = true) {
     const int m = sp.m, k = sp.k;
     const bool SUB = sp.errs & PM_ERR_SUB, INS = sp.errs & PM_ERR_INS, DEL = sp.errs & PM_ERR_DEL;
     const int L = m + (INS ? k : 0);   // the longest match
     const int WU = L - 1;              // warm-up words
     std::vector<PosClass> pc(m);
-    std::map<std::pair<int, bool>, int> cls;   // distinct classes -> register index
+    std::map<std::tuple<int, bool, bool>, int> cls;   // distinct classes (ACGT subset, any, takes N) -> register
     std::vector<int> rep;                       // a position of each class
     std::vector<int> ci(m);
     for (int i = 0; i < m; ++i) {
         pc[i] = pos_class_of(sp.byte_mask, i);
-        auto key = std::make_pair(pc[i].any ? 15 : pc[i].acgt, pc[i].any);
+        auto key = std::make_tuple(pc[i].any ? 15 : pc[i].acgt, pc[i].any,
+                                   !pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1));
         auto it = cls.find(key);
         if (it == cls.end()) {
             it = cls.emplace(key, (int)rep.size()).first;
@@ -151,9 +156,14 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    sg << "ids8:" << m << ":" << k << ":" << sp.errs << ":";
-    for (int i = 0; i < m; ++i) sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
+    sg << "ids9:" << m << ":" << k << ":" << sp.errs << ":";
+    for (int i = 0; i < m; ++i) {
+        sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
+        if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
+    }
     for (int j = 0; j <= k; ++j) sg << ":" << sp.rev_pre[j] << "," << sp.rev_ins[j];
+    *sig = sg.str();
+    if (!want_source) return std::string();
 
     // two register banks, r and s: a step reads one and writes the other,
     // and the loop body is two steps (r -> s, s -> r), so no state moves
@@ -295,7 +305,6 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig) {
     // 4 workgroups per CU: <= 128 VGPRs, 4 waves per SIMD (staging each
     // tile in LDS by LDS-DMA first measured no faster, round 2)
     o << "#define IDS_WG 4\n#define IDS_DEPTH " << IDS_DEPTH << "\n#define IDS_SLOTS " << IDS_DEPTH + 1 << "\n";
-    *sig = sg.str();
     o << R"IDS(
 // One wave per tile; lane c owns stream column c (logical words 32c ..
 // 32c + 31, physical word t * 64 + c at step t): it scans the next column's
@@ -382,14 +391,14 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     const int WU = sp.m + ((sp.errs & PM_ERR_INS) ? sp.k : 0) - 1;
     if (WU > HALO - 1) return false;   // the warm-up must fit the next lane column or the halo
     std::string sig;
-    const std::string src = gen_ids_source(sp, &sig);
+    gen_ids_source(sp, &sig, false);
     hipFunction_t fn;
     {
         std::lock_guard<std::mutex> lk(g_ids_mu);
         auto key = std::make_pair(db->device, sig);
         auto it = g_ids_cache.find(key);
         if (it == g_ids_cache.end()) {
-            std::vector<char> code = hiprtc_compile(src);
+            std::vector<char> code = hiprtc_compile(gen_ids_source(sp, &sig));
             IdsKernel kk;
             HIPCHK(hipModuleLoadData(&kk.module, code.data()));
             HIPCHK(hipModuleGetFunction(&kk.fn, kk.module, "pm_ids_rev"));

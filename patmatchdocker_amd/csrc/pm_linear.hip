@@ -1613,10 +1613,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // scan waves per output segment: segments of ~750 tiles (~49 Mbp;
             // configs[4] at 12.5 Gbp: 16 waves, 256 segments -- one round of
             // verify blocks and 64 Ki (pattern, segment) bins; measured 9.25,
-            // 8.73, 10.6 ms per step at 8, 16, 32 waves); PM_BATCH_WPO overrides
-            static const int wpo_env = getenv("PM_BATCH_WPO") ? std::max(1, atoi(getenv("PM_BATCH_WPO"))) : 0;
-            const uint64_t wpo = std::min<uint64_t>(
-                BATCH_MAX_WPO, wpo_env ? (uint64_t)wpo_env : std::max<uint64_t>(1, (752 + tpw / 2) / tpw));
+            // 8.73, 10.6 ms per step at 8, 16, 32 waves)
+            const uint64_t wpo = std::min<uint64_t>(BATCH_MAX_WPO, std::max<uint64_t>(1, (752 + tpw / 2) / tpw));
             const uint64_t nout = (nwaves + wpo - 1) / wpo;
             std::vector<uint32_t> slot_caps(n_patterns, 64);
             // candidates per wave: ~1 % of the positions at configs[4]

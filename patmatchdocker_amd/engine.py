@@ -374,15 +374,25 @@ def _words(x: int, w: int) -> List[int]:
     return [(x >> (64 * q)) & 0xFFFFFFFFFFFFFFFF for q in range(w)]
 
 
+def _nfa_tables(prog: Program):
+    """The automaton's tables as pm_scan_nfa_wide takes them, built once per
+    program (a compiled Program is not modified; building them costs a few
+    hundred microseconds of Python per query)."""
+    t = prog.__dict__.get("_nfa_tables")
+    if t is None:
+        w = nfa_words(prog.m)
+        t = (w, np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64),
+             np.array([_words(x, w) for x in prog.follow], dtype=np.uint64),
+             np.array(_words(prog.first, w), dtype=np.uint64), np.array(_words(prog.last, w), dtype=np.uint64))
+        prog.__dict__["_nfa_tables"] = t
+    return t
+
+
 def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
                flags: int = None):
     """pm_scan_nfa_wide; returns the raw pm_hits handle (caller destroys),
     keys ``pattern_id << 48 | beg`` -- see :func:`scan_nfa`."""
-    w = nfa_words(prog.m)
-    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
-    fol = np.array([_words(x, w) for x in prog.follow], dtype=np.uint64)
-    first = np.array(_words(prog.first, w), dtype=np.uint64)
-    last = np.array(_words(prog.last, w), dtype=np.uint64)
+    w, bm, fol, first, last = _nfa_tables(prog)
     errs = error_mask(types) if k else _lib.PM_ERR_SUB
     flags = report_flags(prog) if flags is None else flags
     if k == 0 and prog.linear and any(10 in c for c in prog.classes):

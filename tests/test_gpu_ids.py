@@ -87,3 +87,21 @@ def test_ids_pass_through_engine_scan(engine, oracle_mod, monkeypatch):
             assert _pairs(r) == oracle_mod.scan_reported(text, prog, 2, "ids", skip_headers=True)
     finally:
         db.close()
+
+
+def test_ids_pass_classes_that_take_n(engine, oracle_mod, monkeypatch):
+    """Two classes with the same A/C/G/T subset, one taking N and one not
+    ([ACGN] / [ACG]): they need their own match registers (an N takes its
+    membership from the plane mark), and kernels for the two cache apart."""
+    monkeypatch.setenv("PM_IDS_JIT", "1")
+    text = TEXTS["dna"]()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for src, k in [("A[ACGN]GT[ACG]TTAC", 1), ("A[ACG]GT[ACG]TTAC", 1), ("A[ACGN]GT[ACGN]TTAC", 1),
+                       ("[ACGN][ACGN]A[ACG]", 1)]:
+            prog = compile_pattern(src, ignore_case=True)
+            r = engine.scan_nfa(db, prog, k, 0, "ids", engine.report_flags(prog, "all"))
+            want = oracle_mod.scan_reported(text, prog, k, "ids", skip_headers=True, report="all")
+            assert list(zip(r.beg.tolist(), r.end.tolist())) == want, src
+    finally:
+        db.close()

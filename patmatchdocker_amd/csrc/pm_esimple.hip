@@ -703,17 +703,21 @@ __device__ inline bool es_head(const uint64_t* keys, uint64_t i, int32_t gap, in
 // One thread per list entry: acc = 2 at a cluster head, else 0.  A lone
 // start of a slot whose lone starts need no walk (EsSlot::lone) is settled
 // here (acc = 3, its length m); every other head goes to the walk list
-// (one atomic per wave).
-__global__ __launch_bounds__(256) void k_es_heads(EsPrep P, const uint64_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ lens, const uint64_t* total_d,
-                                                  uint64_t total_h, uint8_t* __restrict__ acc,
-                                                  uint32_t* __restrict__ wlist, uint32_t* __restrict__ wcount,
-                                                  TextView tv) {
+// (one atomic per block and pass: the list length is one counter, and
+// thousands of waves' atomics on it serialize -- ~0.1 ms with one per wave).
+constexpr uint32_t ES_HEADS_T = 1024;
+__global__ __launch_bounds__(ES_HEADS_T) void k_es_heads(EsPrep P, const uint64_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ lens, const uint64_t* total_d,
+                                                         uint64_t total_h, uint8_t* __restrict__ acc,
+                                                         uint32_t* __restrict__ wlist, uint32_t* __restrict__ wcount,
+                                                         TextView tv) {
+    __shared__ uint32_t s_wc[ES_HEADS_T / 64];
+    __shared__ uint32_t s_base;
     const uint64_t total = total_d ? *total_d : total_h;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x - lane; i0 < total; i0 += stride) {
-        const uint64_t i = i0 + lane;
+    const uint64_t stride = (uint64_t)gridDim.x * ES_HEADS_T;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * ES_HEADS_T; b0 < total; b0 += stride) {   // block-uniform
+        const uint64_t i = b0 + threadIdx.x;
         bool walk = false;
         if (i < total) {
             uint8_t a = 0;
@@ -744,13 +748,22 @@ __global__ __launch_bounds__(256) void k_es_heads(EsPrep P, const uint64_t* __re
             acc[i] = a;
         }
         const uint64_t m = __builtin_amdgcn_ballot_w64(walk);
-        if (m) {
-            uint32_t base = 0;
-            const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            if (lane == first) base = atomicAdd(wcount, (uint32_t)__builtin_popcountll(m));
-            base = __shfl(base, (int)first, 64);
-            if (walk) wlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)i;
+        if (lane == 0) s_wc[wv] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {   // the waves' offsets, then one reservation for the block
+            uint32_t run = 0;
+            for (uint32_t w = 0; w < ES_HEADS_T / 64; ++w) {
+                const uint32_t c = s_wc[w];
+                s_wc[w] = run;
+                run += c;
+            }
+            s_base = run ? atomicAdd(wcount, run) : 0u;
         }
+        __syncthreads();
+        if (walk)
+            wlist[s_base + s_wc[wv] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                (uint32_t)i;
+        __syncthreads();   // s_wc / s_base are rewritten by the next pass
     }
 }
 
@@ -1005,7 +1018,7 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
                uint8_t* acc, uint32_t* wlist, uint32_t* wcount, uint32_t* bcnt, uint32_t G, const TextView& tv,
                hipStream_t s) {
     HIPCHK(hipMemsetAsync(wcount, 0, sizeof(uint32_t), s));
-    hipLaunchKernelGGL(k_es_heads, dim3(1024), dim3(256), 0, s, P0, keys, lens, total_d, total_h, acc, wlist, wcount,
+    hipLaunchKernelGGL(k_es_heads, dim3(256), dim3(ES_HEADS_T), 0, s, P0, keys, lens, total_d, total_h, acc, wlist, wcount,
                        tv);
     EsPrep P = P0;
     // a candidate's phases reach m + k + 1 back and forth, the piece pass

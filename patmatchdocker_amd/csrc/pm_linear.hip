@@ -239,20 +239,32 @@ __device__ inline uint32_t select_bits(const OthersArgs& a, uint64_t t, uint64_t
     return ot;
 }
 
-__global__ __launch_bounds__(256) void k_others_select(OthersArgs a) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+constexpr uint32_t OTH_SELECT_T = 1024;
+__global__ __launch_bounds__(OTH_SELECT_T) void k_others_select(OthersArgs a) {
+    __shared__ uint32_t s_wc[OTH_SELECT_T / 64];
+    __shared__ uint32_t s_base;
+    const uint64_t t = blockIdx.x * (uint64_t)OTH_SELECT_T + threadIdx.x;
     uint64_t w = 0;
     const uint32_t ot = t < (a.use_edge ? a.nedge : a.nflag) ? select_bits(a, t, &w) : 0u;
-    // one atomic per wave on the list length (a single counter: per-lane
-    // atomics serialize on it)
+    // one atomic per block on the list length (a single counter: the
+    // atomics of many waves serialize on it)
     const uint64_t m = __builtin_amdgcn_ballot_w64(ot != 0u);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63, first = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(a.nsel, (uint32_t)__builtin_popcountll(m));
-    base = __shfl(base, (int)first, 64);
-    if (ot) a.sel[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-        OtherSel{w, ot, 0u};
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) s_wc[wv] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t q = 0; q < OTH_SELECT_T / 64; ++q) {
+            const uint32_t c = s_wc[q];
+            s_wc[q] = run;
+            run += c;
+        }
+        s_base = run ? atomicAdd(a.nsel, run) : 0u;
+    }
+    __syncthreads();
+    if (ot)
+        a.sel[s_base + s_wc[wv] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+            OtherSel{w, ot, 0u};
 }
 
 constexpr int OTH_MAX_POS = 8 * 64;   // (pattern, position) entries of a chunk (JIT_MAX_P x 64)
@@ -1589,7 +1601,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // 0.20 vs 0.18 ms -- both are bound by ~58 gathered cache lines
             // per exception bit)
             HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
-            hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, 256)), dim3(256), 0, os, oa);
+            hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, OTH_SELECT_T)), dim3(OTH_SELECT_T), 0, os, oa);
             HIPCHK(hipGetLastError());
             if (batch_form)
                 hipLaunchKernelGGL(k_others_batch,

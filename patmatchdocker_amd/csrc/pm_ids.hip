@@ -411,12 +411,14 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
                 sink.out, sink.bin_cnt, sink.cap, sink.bins_per_pattern, sink.pos_shift, (uint32_t)sp.pattern_id};
     void* params[] = {&a};
     // one wave per tile, waves loop over tiles (every wave reaches the end);
-    // as many waves as are resident at once (4 per SIMD at <= 128 VGPRs):
-    // a second round of waves would start only as the first drains (PMC:
-    // ~2.9 of 4 waves resident on average with 2 rounds)
-    int ncu = 0;
+    // four rounds of the resident waves (the kernel needs 120 VGPRs: 4 per
+    // SIMD): later rounds' workgroups start wherever earlier ones finish,
+    // which evens out CUs that run slower (per strand: one round 1.80 ms,
+    // two 1.71, four 1.68; r03z, r03i2, r03i4)
+    int ncu = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, db->device));
-    const uint64_t resident = (uint64_t)std::max(ncu, 1) * 4;   // blocks of 4 waves: 16 waves per CU
+    HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0));
+    const uint64_t resident = (uint64_t)std::max(ncu, 1) * (uint64_t)std::max(per_cu, 1) * 4;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((db->ntiles + 3) / 4, resident));
     HIPCHK(hipExtModuleLaunchKernel(fn, blocks * 256u, 1, 1, 256, 1, 1, 0, s, params, nullptr, ev_a, ev_b, 0));
     return true;

@@ -65,10 +65,8 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed,
  * passes -b 1600000; main() stores atoi(optarg) in OptBufSize, 0x401162, and
  * bufCreate allocates that many bytes, 0x41bb6b -- the help text's "Kb"
  * is not applied).  Each buffer that is not the file's last is searched up
- * to and including its last '
-', and the next buffer starts at that '
-'
- * (recSearchFile 0x402450-0x402497, bufLoad 0x41bbf0); a buffer without one
+ * to and including its last line break, and the next buffer starts at that
+ * line break (recSearchFile 0x402450-0x402497, bufLoad 0x41bbf0); a buffer without one
  * is searched whole.  These search regions matter to what is printed: no
  * match spans a region end, the report rule restarts at each region start,
  * and '^' passes there.  pm_db_create* set the regions of the loaded text
@@ -124,6 +122,23 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
  * byte's positions; classes hold both cases, as `-i` builds them).  Host
  * only, no GPU needed.  out must hold 5 + k + 1 ints.                    */
 int pm_esimple_plan(int m, int words, const uint64_t* byte_mask, int k, int32_t* out);
+/* The pattern is a sequence of classes each with an optional '?', '*' or '+'
+ * (nrgrep's detClass() == 2) searched with k = 0: nrgrep_coords runs its
+ * "extended" engine (searchPreproc 0x4026b7), whose scanner and
+ * nearest-boundary verification decide which overlapping match is printed
+ * (DESIGN.md §1).  pm_scan_nfa_wide only; the optional / repeatable
+ * positions are read off first / follow / last (PM_E_ARG if the automaton
+ * has another shape).  Ignored at k > 0.                                 */
+#define PM_EXTENDED 128
+/* The scan plan nrgrep's extendedPreproc (0x413260) derives for such a
+ * pattern: out[0] = 2 (a window scanned backward) or 3 (the prefix scanned
+ * forward); out[1] = the window's non-optional positions (0: no window);
+ * out[2..3] = the window / prefix [beg, end); out[4] = pattern positions
+ * left of the candidate; out[5] = 1 when the window holds no '?*+'.
+ * opt_mask / rep_mask: `words` words of optional / repeatable positions.
+ * Host only, no GPU needed.  out must hold 6 ints.                       */
+int pm_extended_plan(int m, int words, const uint64_t* byte_mask, const uint64_t* opt_mask,
+                     const uint64_t* rep_mask, int32_t* out);
 
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched
@@ -183,7 +198,8 @@ int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* fol
 /* pm_scan_nfa with an explicit error-type mask `errs` (PM_ERR_*) -- the
  * general `nrgrep_coords -k <k><ids>` scan.  min_len = the shortest match
  * length of the pattern (regex.py); with PM_ERR_DEL it must exceed k
- * (otherwise PM_E_UNSUPPORTED).  Insertions let a match run to
+ * (otherwise PM_E_UNSUPPORTED) unless the pattern is a class sequence
+ * reported with PM_ESIMPLE.  Insertions let a match run to
  * max_len + k characters.  pm_scan_nfa(...) == pm_scan_nfa_errs(..., 0, k,
  * PM_ERR_SUB, ...). */
 int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,

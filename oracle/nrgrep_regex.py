@@ -124,7 +124,80 @@ def parse(pattern: str, icase: bool = True):
     tree = alt()
     if pos[0] != len(p):
         raise PatternError("unbalanced ')'")
-    return tree, a_start, a_end
+    return simplify(tree), a_start, a_end
+
+
+def _nullable(node) -> bool:
+    k = node[0]
+    if k in ("eps", "opt", "star"):
+        return True
+    if k == "sym":
+        return False
+    if k == "plus":
+        return _nullable(node[1])
+    if k == "cat":
+        return all(_nullable(c) for c in node[1])
+    return any(_nullable(c) for c in node[1])
+
+
+def simplify(tree):
+    """nrgrep's simplify pass (the binary's 0x41a170, called by parse with
+    both edges set), restated on this module's n-ary tree: a nullable
+    subexpression touching an edge of the pattern is dropped -- at the left
+    edge only the first element of a concatenation sees it, at the right
+    edge the whole nullable tail goes; a '+' touching an edge keeps one
+    copy of its operand; a postfix operator over '*', '+' or '?' merges
+    into '*' or '?'; a '|' of two single classes is one class, a '|' with an
+    empty side is '?' of the other.  Nested concatenations and alternations
+    are right-deep binary nodes in the binary, which fixes who sees an edge."""
+
+    def simp(node, left, right):
+        k = node[0]
+        if _nullable(node) and (left or right):
+            return ("eps",)
+        if k in ("sym", "eps"):
+            return node
+        if k in ("cat", "alt") and len(node[1]) > 2:
+            node = (k, [node[1][0], (k, node[1][1:])])
+        if k in ("cat", "alt") and len(node[1]) == 1:
+            return simp(node[1][0], left, right)
+        if k == "cat":
+            a, b = simp(node[1][0], left, False), simp(node[1][1], False, right)
+            if a[0] == "eps":
+                return b
+            if b[0] == "eps":
+                return a
+            return ("cat", [a, b])
+        if k == "alt":
+            a, b = simp(node[1][0], left, False), simp(node[1][1], False, right)
+            leafy = lambda x: x[0] in ("sym", "eps")
+            if leafy(a) and leafy(b):
+                if a[0] == b[0] == "sym":
+                    return ("sym", frozenset(a[1] | b[1]))
+                if a[0] == b[0] == "eps":
+                    return a
+                return ("opt", b if a[0] == "eps" else a)
+            return ("alt", [a, b])
+        if k == "plus" and not _nullable(node):
+            c = simp(node[1], left, right)
+            if left or right:
+                return c
+        else:
+            c = simp(node[1], False, False) if k == "plus" else simp(node[1], left, right)
+        if c[0] == "eps":
+            return c
+        if k == "star":
+            return ("star", c[1]) if c[0] in ("star", "opt", "plus") else ("star", c)
+        if k == "opt":
+            if c[0] in ("star", "plus"):
+                return ("star", c[1])
+            return c if c[0] == "opt" else ("opt", c)
+        # plus
+        if c[0] in ("star", "opt"):
+            return ("star", c[1])
+        return c if c[0] == "plus" else ("plus", c)
+
+    return simp(tree, True, True)
 
 
 Rel = Dict[Tuple[int, bool], int]

@@ -25,7 +25,8 @@ ERR_INS, ERR_DEL, ERR_SUB = 1, 2, 4
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "pm_nrgrep.c", "Makefile")]
+    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "pm_nrgrep.c", "pm_nrgrep_ext.c",
+                                              "Makefile")]
     if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return path
@@ -57,6 +58,11 @@ def lib():
         _LIB.pmn_esimple.restype = ctypes.c_int64
         _LIB.pmn_esimple.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmx_plan.restype = ctypes.c_int
+        _LIB.pmx_plan.argtypes = [pu64, ctypes.c_int, pu64, pu64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        _LIB.pmx_extended.restype = ctypes.c_int64
+        _LIB.pmx_extended.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, pu64, pu64, ctypes.c_int,
+                                      ctypes.c_int, p64, p64, ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -187,6 +193,8 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
     nrgrep's regions (``regions``: buffers of ``bufsize`` bytes; 0 = one)."""
     if report == "nrgrep" and simple is None and mode is None and k > 0 and is_esimple(prog):
         return scan_esimple(text, prog, k, types, skip_headers, bufsize, regs)
+    if report == "nrgrep" and simple is None and mode is None and k == 0 and prog.kind == "extended":
+        return scan_extended(text, prog, skip_headers, bufsize, regs)
     if regs is not None or (bufsize and len(text) >= bufsize):
         return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, simple, mode, 0),
                          skip_headers, bufsize, regs=regs)
@@ -348,6 +356,60 @@ def scan_esimple(text: bytes, prog, k: int, types: str = "ids", skip_headers: bo
                               end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
         if n < 0:
             raise ValueError("pmn_esimple rejected m=%d k=%d" % (prog.m, k))
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+# ---------------------------------------------------------------------------
+# nrgrep's extended engine at k = 0 (pm_nrgrep_ext.c): classes with '?*+',
+# restated from the binary's disassembly
+# ---------------------------------------------------------------------------
+
+def _mask_words(x: int) -> np.ndarray:
+    return np.array([(x >> (64 * q)) & 0xFFFFFFFFFFFFFFFF for q in range(4)], dtype=np.uint64)
+
+
+def extended_plan(prog):
+    """nrgrep's extendedPreproc plan for ``prog`` (pmx_plan): ``type`` 2 = a
+    window scanned backward, 3 = the prefix scanned forward; ``window``
+    [beg, end); ``L`` = the left part's length; ``simple`` = the window holds
+    no '?*+' (simpleScan)."""
+    if prog.kind != "extended":
+        raise ValueError("not an extended pattern: %s" % prog.source)
+    B = wide_masks(prog)
+    out = (ctypes.c_int * 8)()
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    opt, rep = _mask_words(prog.opt_mask), _mask_words(prog.rep_mask)
+    if lib().pmx_plan(B.ctypes.data_as(pu64), prog.m, opt.ctypes.data_as(pu64), rep.ctypes.data_as(pu64),
+                      1 if prog.ignore_case else 0, out) < 0:
+        raise ValueError("no extended plan for %s" % prog.source)
+    return {"type": out[0], "fwd": out[1], "window": (out[2], out[3]), "L": out[4], "simple": bool(out[5])}
+
+
+def scan_extended(text: bytes, prog, skip_headers: bool = False, bufsize: int = NRGREP_BUFFER, regs=None):
+    """What nrgrep_coords prints for a class-2 pattern at k = 0 (pmx_extended:
+    nrgrep's plan, scanners, two-phase verify and report rule), region by
+    region (``regions``)."""
+    if prog.kind != "extended":
+        raise ValueError("scan_extended needs an extended pattern")
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_extended(t, prog, False, 0), skip_headers, bufsize, regs=regs)
+    B = wide_masks(prog)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    opt, rep = _mask_words(prog.opt_mask), _mask_words(prog.rep_mask)
+    mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = lib().pmx_extended(text, len(text), B.ctypes.data_as(pu64), prog.m, opt.ctypes.data_as(pu64),
+                               rep.ctypes.data_as(pu64), 1 if prog.ignore_case else 0, mode,
+                               beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                               end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pmx_extended rejected %s" % prog.source)
         if n <= cap:
             hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
             return drop_header_hits(text, hits) if skip_headers else hits

@@ -54,8 +54,8 @@
 #define PMN_START 2         /* '^' (OptStartLine) */
 #define PMN_END 4           /* '$' (OptEndLine) */
 
-/* letterProb, .data 0x621120 (256 doubles) */
-static const double letterProb[256] = {
+/* letterProb, .data 0x621120 (256 doubles); pm_nrgrep_ext.c shares it */
+const double pmn_letter_prob[256] = {
     0, 0, 0, 0, 0, 0, 0, 0,
     0, 0.000344, 0.020793, 0, 0, 0, 0, 0,
     0, 0, 0, 0, 0, 0, 0, 0,
@@ -89,6 +89,8 @@ static const double letterProb[256] = {
     0, 9e-06, 0, 4e-05, 0, 0, 0, 0,
     0, 0, 2.7e-05, 0, 0, 0, 0, 0,
 };
+
+#define letterProb pmn_letter_prob
 
 static inline uint8_t fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 

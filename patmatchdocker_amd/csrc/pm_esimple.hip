@@ -129,6 +129,11 @@ double find_best(const std::vector<double>& pr, int m, int K, int* fwd, int* beg
 
 }  // namespace
 
+void letter_probs(double out[256]) {
+    for (int c = 0; c < 256; ++c) out[c] = 0.0;
+    for (const LP& e : kLetterProb) out[e.c] = e.p;
+}
+
 EsPlan es_plan(const uint64_t* B, int W, int m, int k) {
     require(m >= 1 && m <= PM_MAX_POSITIONS && k >= 1 && k <= PM_MAX_K, "esimple plan: m or k out of range");
     // class probabilities, bytes in increasing order (0x4156b8); B holds the

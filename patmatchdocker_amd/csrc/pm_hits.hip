@@ -886,7 +886,7 @@ ReportWs report_ws(pm_db* db, uint64_t cap_items) {
 
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
                        uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr,
-                       const EsPrep* es) {
+                       const EsPrep* es, const XtPrep* xt) {
     // acc is indexed below the list length, which never exceeds the
     // capacity the workspace was sized for (the sort's slot capacities)
     const uint64_t cap_items = std::min<uint64_t>(h->keys_cap / 8, ws.cap);
@@ -917,6 +917,10 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     if (es && (flags & PM_REPORT_NRGREP)) {
         // nrgrep's esimple engine: its own candidate order and verify
         es_launch(*es, h->keys, h->lens, a.total_d, a.total_h, a.acc, ws.wlist, ws.wcount, a.bcnt, G, a.tv, s);
+    } else if (xt && (flags & PM_REPORT_NRGREP)) {
+        // nrgrep's extended engine (k = 0): its scanners and checkMatch; it
+        // reads the file's own bytes, regions included
+        xt_launch(*xt, h->keys, h->lens, a.total_d, a.total_h, a.acc, a.bcnt, G, text_view(db), s);
     } else {
         hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
         hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
@@ -933,13 +937,14 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     h->lens_cap = lc;
 }
 
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es) {
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es,
+                 const XtPrep* xt) {
     if (total == 0) {
         h->count = 0;
         return;
     }
     const ReportWs ws = report_ws(db, h->keys_cap / 8);
-    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr, hdr, es);
+    report_enqueue_ws(db, h, flags, ws, false, total, nullptr, db->stream, nullptr, hdr, es, xt);
     uint32_t* hc = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 8));
     HIPCHK(hipMemcpyAsync(hc, ws.count, 4, hipMemcpyDeviceToHost, db->stream));
     HIPCHK(hipStreamSynchronize(db->stream));

@@ -695,7 +695,9 @@ bool report_needed(const pm_db* db, uint32_t flags, bool cross);
 // hdr: candidates may start on a header line (the simple engine's cross
 // windows) -- only then is every start checked against the header bytes.
 struct EsPrep;
-void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es = nullptr);
+struct XtPrep;
+void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr, const EsPrep* es = nullptr,
+                 const XtPrep* xt = nullptr);
 // Workspace of one pass (db's current lane), sized for `cap_items` keys;
 // reserve it BEFORE enqueueing the producer of *total (reserve() may move it).
 struct ReportWs {
@@ -780,10 +782,52 @@ void es_launch(const EsPrep& P, uint64_t* keys, uint32_t* lens, const uint64_t* 
                uint8_t* acc, uint32_t* wlist, uint32_t* wcount, uint32_t* bcnt, uint32_t G, const TextView& tv,
                hipStream_t s);
 
+// letterProb (.data 0x621120), 256 entries (pm_esimple.hip)
+void letter_probs(double out[256]);
+
+// ---------------------------------------------------------------------------
+// nrgrep's extended engine at k = 0 (pm_extended.hip): the report of a class
+// sequence with '?', '*', '+' (detClass() == 2, PM_EXTENDED) -- extendedFindBest's
+// plan, the window / prefix scanners and checkMatch replayed per cluster of
+// candidate starts
+// ---------------------------------------------------------------------------
+struct XtPlan {                // extendedPreproc 0x413260
+    int type = 0;              // 2: a window scanned backward, 3: the prefix scanned forward
+    int fwd = 0;               // extendedFindBest's count: the window's non-optional positions
+    int beg = 0, end = 0;      // the window / prefix [beg, end)
+    int L = 0;                 // pattern positions left of the candidate (beg, or end for type 3)
+    int simple = 0;            // no '?*+' in [beg, end): simpleScan instead of extendedScan
+};
+// B: [256][W] position sets of the folded bytes; opt / rep: [W] masks
+XtPlan xt_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep);
+
+struct XtSlot {                // one pattern (device, uploaded as is)
+    int32_t m, type, fwd, len, simple, L, anchors, pid;
+    int32_t plen[2], pw[2];    // verify parts: [0] left (reversed), [1] right; positions, words
+    int64_t max_len;           // the longest match, -1: unbounded
+    uint64_t fI, fF, fS;       // scanner: optional-block masks (extendedLoadFast)
+    uint64_t vI[2][4], vF[2][4], vS[2][4], vX[2][4];
+    uint64_t o_T, o_TA, o_vB[2], o_vA[2];   // word offsets of [256] / [256][pw] tables in the blob
+};
+struct XtPrep {
+    const XtSlot* slot = nullptr;
+    const uint64_t* tab = nullptr;
+    int32_t pid = 0;
+};
+// builds the plan and tables of one pattern into `up`; returns the slot's
+// and the table blob's offsets
+void xt_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int64_t max_len,
+              uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab);
+// heads + walk + per-chunk counts on s (keys/lens rewritten in place, acc
+// bit 0 = reported), like es_launch
+void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s);
+
 // es (optional): the list holds a class sequence's candidate starts at
-// k > 0 and the selection is nrgrep's esimple engine (pm_esimple.hip)
+// k > 0 and the selection is nrgrep's esimple engine (pm_esimple.hip); xt
+// (optional): an extended pattern's starts at k = 0 (pm_extended.hip)
 void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws, bool total_on_device,
                        uint64_t total_h, uint32_t* host_count, hipStream_t s, hipEvent_t done, bool hdr,
-                       const EsPrep* es = nullptr);
+                       const EsPrep* es = nullptr, const XtPrep* xt = nullptr);
 
 }  // namespace pm

@@ -680,7 +680,12 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
     }
 }
 
-constexpr int JIT_STEPS = 8;   // window words per lane per wave and tile (4 waves x 8 = 32)
+// waves per workgroup = parts of a lane's 32 window words; each wave scans
+// 32 / parts consecutive words of every lane column of the tile
+int jit_parts() {
+    static const int p = getenv("PM_JIT_PARTS") ? atoi(getenv("PM_JIT_PARTS")) : 4;
+    return (p == 2 || p == 4) ? p : 4;
+}
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
 
@@ -709,7 +714,7 @@ struct ExpandArgs {
     const uint64_t* slot_base;
     const uint32_t* slot_cap;
     uint32_t nwg, nout, group, tiles_per_wg;
-                      // slots reserved on the global counters
+    uint32_t parts;   // waves per pm_linear_jit workgroup (32 / parts words each)
 };
 
 // One block per output segment (`group` workgroups x 4 wave segments); each
@@ -725,10 +730,11 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
     const uint32_t og = blockIdx.x, sub = threadIdx.x / SEG_LANES, lane_t = threadIdx.x % SEG_LANES;
     if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * 4;
+    const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * a.parts;
+    const uint32_t steps = LANE_WORDS / a.parts;
     for (uint32_t q = sub; q < pairs; q += EXPAND_THREADS / SEG_LANES) {
-        const uint32_t wg = wg0 + q / 4, part = q % 4;
-        const uint32_t seg = wg * 4 + part;
+        const uint32_t wg = wg0 + q / a.parts, part = q % a.parts;
+        const uint32_t seg = wg * a.parts + part;
         uint32_t cnt = a.rec_cnt[seg];
         if (cnt > a.rcap) {
             if (lane_t == 0) atomicMax(a.rec_over, cnt);
@@ -736,10 +742,10 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
         }
         for (uint32_t i = lane_t; i < cnt; i += SEG_LANES) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 12);
-            const uint32_t lane = (r.x >> 6) & 63, s = (r.x >> 3) & 7, p = r.x & 7;
+            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 13);
+            const uint32_t lane = (r.x >> 7) & 63, s = (r.x >> 3) & 15, p = r.x & 7;
             if (tile >= a.ntiles) continue;
-            const uint32_t w0 = 32u * lane + part * JIT_STEPS + s;
+            const uint32_t w0 = 32u * lane + part * steps + s;
             uint32_t live = r.y;
             if ((a.lflag[tile] >> lane) & 1) {
                 uint32_t kill = 0;
@@ -782,14 +788,14 @@ typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
 // Hit records: one uint2 per (tile, lane, step, pattern) with a live window:
-// x = (tile - first tile of the workgroup) << 12 | lane << 6 | step << 3 |
+// x = (tile - first tile of the workgroup) << 13 | lane << 7 | step << 3 |
 // pattern, y = the live mask (bit b = the window of stream b).  Staged per
 // wave in LDS and flushed to the wave's global segment, so the scan loop
 // never waits on a global store; k_linear_expand turns records into keys.
 struct JArgs {
     const uint2* hl;
-    uint2* rec;             // [nwg * 4][rcap]
-    u32* rec_cnt;           // [nwg * 4]
+    uint2* rec;             // [nwg * NW][rcap]
+    u32* rec_cnt;           // [nwg * NW]
     u32* aux_zero;          // the sink's record-overflow counter, zeroed by the first launch of a scan (or null)
     u64 ntiles;
     u32 rcap, tiles_per_wg;
@@ -957,8 +963,9 @@ std::string net_dead(std::ostringstream& o, const CountNet& n, int K, int& uid, 
 // record with its live mask (wave ballot + mbcnt into an LDS stage, flushed
 // rarely); k_linear_expand turns records into hit keys.
 std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
-                              const uint8_t* class_acgt, const uint8_t* class_is_any, int waves) {
-    constexpr int PARTS = LANE_WORDS / JIT_STEPS;   // == 4 waves
+                              const uint8_t* class_acgt, const uint8_t* class_is_any, int waves, int parts) {
+    const int PARTS = parts;                     // waves per workgroup
+    const int JIT_STEPS = LANE_WORDS / parts;    // window words per lane and wave
     // LDS tile buffers: 2 (the next tile streams in while this one is
     // scanned) leave room for 4 workgroups per CU, which measured 10 %
     // faster than 3 buffers at 3 workgroups per CU (profiles/r01c_ring_sweep.txt)
@@ -969,7 +976,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     std::ostringstream o;
     o << kJitCommon;
     o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define STEPS "
-      << JIT_STEPS << "\n";
+      << JIT_STEPS << "\n#define NW " << PARTS << "\n";
     auto word_off = [&](int i) {   // physical word of logical word 32 lane + i, relative to the tile
         std::ostringstream s;
         if (i < LANE_WORDS) s << (i * 64) << " + lane";
@@ -1096,7 +1103,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     asm volatile("" ::: "memory");                                  \
   } while (0)
 // DMA tile t into the ring slot at LDS byte address `dst0`: DMA_PIECES 1-KiB
-// pieces, piece q issued by wave q % 4 (lane-linear LDS image of the tile).
+// pieces, piece q issued by wave q % NW (lane-linear LDS image of the tile).
 // Inline asm so that the compiler's wait bookkeeping does not drain it
 // before the ds_reads of the slot being computed; waited for explicitly.
 __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 tend, u32 wid, int lane) {
@@ -1106,7 +1113,7 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
   const unsigned char* tb = reinterpret_cast<const unsigned char*>(a.hl + tile * TILE_WORDS);
   const u32 voff = (u32)lane * 16u;
 #pragma unroll
-  for (int q = 0; q < DMA_PIECES; q += 4) {
+  for (int q = 0; q < DMA_PIECES; q += NW) {
     if (q + (int)wid >= DMA_PIECES) break;
     if ((q + (int)wid + 1) * 1024 > LOAD_BYTES && lane * 16 >= LOAD_BYTES % 1024) continue;   // partial last piece
     const u32 dst = __builtin_amdgcn_readfirstlane(dst0 + (q + wid) * 1024);
@@ -1126,9 +1133,10 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 )JIT";
-    o << "extern \"C\" __global__ __launch_bounds__(256, " << waves << ") void pm_linear_jit(JArgs a) {\n"
+    o << "extern \"C\" __global__ __launch_bounds__(" << 64 * PARTS << ", " << std::max(1, waves * PARTS / 4)
+      << ") void pm_linear_jit(JArgs a) {\n"
          "  __shared__ __attribute__((aligned(1024))) unsigned char lds[RING * LDS_TILE];\n"
-         "  __shared__ uint2 rst[4][REC_LDS];\n"
+         "  __shared__ uint2 rst[NW][REC_LDS];\n"
          "  const int lane = threadIdx.x & 63;\n"
          "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
          "  // halo word offsets (logical words 32 lane + 32 g + r, r < 32)\n"
@@ -1138,7 +1146,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  // this workgroup's contiguous tile range\n"
          "  const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
          "  const u64 tend = t0 + a.tiles_per_wg < a.ntiles ? t0 + a.tiles_per_wg : a.ntiles;\n"
-         "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * 4 + wid) * a.rcap);\n"
+         "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * NW + wid) * a.rcap);\n"
          "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
          "  u32 scnt = 0, gcnt = 0;   // staged / flushed records (wave-uniform)\n"
          "  if (a.aux_zero && blockIdx.x == 0 && threadIdx.x == 0) *a.aux_zero = 0u;   // read by k_linear_expand (after)\n"
@@ -1168,7 +1176,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);\n"
          "          if (m) {\n"
          "            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));\n"
-         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 12 | (u32)lane << 6 | (u32)s << 3 | (u32)p, lv);\n"
+         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 13 | (u32)lane << 7 | (u32)s << 3 | (u32)p, lv);\n"
          "            scnt += (u32)__builtin_popcountll(m);\n"
          "            if (scnt > REC_LDS - 64) {\n"
          "              flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
@@ -1181,7 +1189,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    }\n"
          "    slot = slot == RING - 1 ? 0 : slot + 1;\n  }\n"
          "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
-         "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * 4 + wid] = gcnt + scnt;\n"
+         "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * NW + wid] = gcnt + scnt;\n"
          "}\n";
     return o.str();
 }
@@ -1246,7 +1254,9 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
 
 hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
-    const auto key = std::make_pair(device, jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
+    const int parts = jit_parts();
+    const auto key = std::make_pair(device, std::to_string(parts) + "/" +
+                                                jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);
     if (it != g_jit_cache.end()) return it->second.fn;
@@ -1255,7 +1265,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     JitKernel jk;
     for (int waves = JIT_WG_PER_CU; waves >= 1; --waves) {
         std::vector<char> code =
-            jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves));
+            jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves, parts));
         if (jk.module) HIPCHK(hipModuleUnload(jk.module));
         HIPCHK(hipModuleLoadData(&jk.module, code.data()));
         HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
@@ -1709,7 +1719,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * JIT_WG_PER_CU * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
-            const uint64_t nseg = nwg * 4;   // one lane-record segment per wave
+            require(tpw < (1ull << 19), "database too large for the record encoding", PM_E_UNSUPPORTED);
+            const uint64_t parts = (uint64_t)jit_parts();
+            const uint64_t nseg = nwg * parts;   // one lane-record segment per wave
             // segment capacities scale with the tiles a workgroup owns (a
             // random 15-mer at k = 2 leaves ~1.4 hits per tile and strand);
             // an overflow re-runs with the counts seen
@@ -1723,8 +1735,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // per-pattern capacities: a dense pattern (many hits) gets its own
             // larger segments on the retry, the others keep theirs
             std::vector<uint32_t> slot_caps(n_patterns, cap);
-            // records per wave: at most tiles_per_wg * 64 lanes * 8 steps * 4 patterns
-            const uint64_t rec_max = tpw * 64 * JIT_STEPS * JIT_MAX_P;
+            // records per wave: at most tiles_per_wg * 64 lanes * steps * patterns
+            const uint64_t rec_max = tpw * 64 * (LANE_WORDS / parts) * JIT_MAX_P;
             uint32_t rcap = (uint32_t)std::min<uint64_t>(rec_max, std::max<uint64_t>(128, 8 * tpw));
             // capacities that sufficed for the same batch on this database
             // last time (a repeated query does not pay the overflow retry)
@@ -1775,12 +1787,12 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     jev.emplace_back(new EventPair());
                     // the events take the dispatch's own start/end timestamps
                     // (no marker packets around the launch; sizes in threads)
-                    HIPCHK(hipExtModuleLaunchKernel(ch.jit, (uint32_t)nwg * 256u, 1, 1, 256, 1, 1, 0, s, params,
+                    HIPCHK(hipExtModuleLaunchKernel(ch.jit, (uint32_t)(nwg * 64 * parts), 1, 1, (uint32_t)(64 * parts), 1, 1, 0, s, params,
                                                     nullptr, jev.back()->a, jev.back()->b, 0));
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
-                                  (uint32_t)tpw};
+                                  (uint32_t)tpw, (uint32_t)parts};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
                     if (exc) launch_others(ch, xs, sb, nout, tpw * group);
@@ -2023,7 +2035,8 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
         require(k >= 0 && k <= PM_MAX_LINEAR_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
-        const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4);
+        const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4,
+                                                  jit_parts());
         const std::vector<char> code = jit_compile(src);
         if (code_bytes) *code_bytes = code.size();
     });

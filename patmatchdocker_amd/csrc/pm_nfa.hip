@@ -445,13 +445,53 @@ bool a_shift_only(int m, int W, const uint64_t* first, const uint64_t* last, con
     return ok;
 }
 
+// PM_EXTENDED: the automaton of a sequence of classes each with an optional
+// '?', '*' or '+' (nrgrep's detClass() == 2).  Its optional / repeatable
+// positions are read off the automaton (position i is optional iff the
+// position before it -- or the start -- may skip to i + 1; repeatable iff it
+// follows itself) and the automaton is rebuilt from them to check the shape.
+bool extended_shape(int m, int W, const uint64_t* first, const uint64_t* last, const uint64_t* follow,
+                    uint64_t* opt, uint64_t* rep) {
+    auto bit = [&](const uint64_t* set, int i) { return ((set[i >> 6] >> (i & 63)) & 1) != 0; };
+    for (int q = 0; q < 4; ++q) opt[q] = rep[q] = 0;
+    for (int i = 0; i < m; ++i) {
+        if (bit(follow + (size_t)i * W, i)) rep[i >> 6] |= 1ull << (i & 63);
+        const bool o = i + 1 < m ? (i == 0 ? bit(first, 1) : bit(follow + (size_t)(i - 1) * W, i + 1))
+                                 : (m > 1 && bit(last, m - 2));
+        if (o) opt[i >> 6] |= 1ull << (i & 63);
+    }
+    auto is_opt = [&](int i) { return bit(opt, i); };
+    std::vector<uint64_t> f2(W, 0), l2(W, 0), fo2((size_t)m * W, 0);
+    auto put = [&](uint64_t* set, int i) { set[i >> 6] |= 1ull << (i & 63); };
+    for (int j = 0; j < m; ++j) {
+        put(f2.data(), j);
+        if (!is_opt(j)) break;
+    }
+    for (int j = m - 1; j >= 0; --j) {
+        put(l2.data(), j);
+        if (!is_opt(j)) break;
+    }
+    for (int i = 0; i < m; ++i) {
+        if (bit(rep, i)) put(fo2.data() + (size_t)i * W, i);
+        for (int j = i + 1; j < m; ++j) {
+            put(fo2.data() + (size_t)i * W, j);
+            if (!is_opt(j)) break;
+        }
+    }
+    for (int q = 0; q < W; ++q)
+        if (f2[q] != first[q] || l2[q] != last[q]) return false;
+    for (size_t q = 0; q < (size_t)m * W; ++q)
+        if (fo2[q] != follow[q]) return false;
+    return true;
+}
+
 // The scan behind pm_scan_nfa_errs / pm_scan_nfa_wide: position sets of W
 // words (W = ceil(m / 64)).
 void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t* follow, const uint64_t* first,
               const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
               pm_hits** out) {
     require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES |
-                       PM_ESIMPLE)) == 0,
+                       PM_ESIMPLE | PM_EXTENDED)) == 0,
             "bad flags");
     require(db != nullptr, "db is NULL");
     std::lock_guard<std::recursive_mutex> lk(db->mu);
@@ -475,6 +515,12 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // PM_ESIMPLE: a class sequence at k > 0 reported as nrgrep's esimple
     // engine does (pm_esimple.hip); its walk computes the ends itself
     const bool esimple = (flags & PM_ESIMPLE) && k > 0 && (flags & PM_REPORT_NRGREP);
+    // PM_EXTENDED: an extended pattern at k = 0 reported as nrgrep's
+    // extended engine does (pm_extended.hip); its walk computes the ends
+    const bool extended = (flags & PM_EXTENDED) && k == 0 && (flags & PM_REPORT_NRGREP);
+    uint64_t xopt[4] = {}, xrep[4] = {};
+    require(!(flags & PM_EXTENDED) || extended_shape(m, W, first, last, follow, xopt, xrep),
+            "PM_EXTENDED needs a sequence of classes with '?', '*', '+'");
     // a match must consume a pattern position (pm_oracle.c reports
     // non-empty matches only): with deletions that needs min_len > k --
     // except for nrgrep's esimple report, whose walk takes every position
@@ -548,8 +594,18 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         es_add_slot(esb, byte_mask, W, m, k, errs, (uint32_t)flags, pattern_id);
         es_upload(esb, up, esu);
     }
+    size_t o_xslot = 0, o_xtab = 0;
+    if (extended)
+        xt_build(byte_mask, W, m, xopt, xrep, max_len == 0 ? -1 : (int64_t)max_len, (uint32_t)flags, pattern_id, up,
+                 o_xslot, o_xtab);
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
+    XtPrep xtp;
+    if (extended) {
+        xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
+        xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
+        xtp.pid = pattern_id;
+    }
     esp.lines = all_pos ? 1 : 0;
 
     NfaArgs a{};
@@ -664,7 +720,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     double kms = all_pos ? 0.0 : ev.ms() + carry_ms;
     if (all_pos) total = db->n;
     pm_hits* h = all_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
-    if (total && !esimple) {
+    if (total && !esimple && !extended) {
         a.starts = h->keys;
         a.nstarts = total;
         a.lens = h->lens;
@@ -686,6 +742,8 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (esimple) {
         // the walk replaces the lengths; until it runs they are unset
         report_sync(db, h, (uint32_t)flags, total, false, &esp);
+    } else if (extended) {
+        report_sync(db, h, (uint32_t)flags, total, false, nullptr, &xtp);
     } else if (report_needed(db, (uint32_t)flags, cross)) {
         report_sync(db, h, (uint32_t)flags, total, cross);
     }

@@ -350,6 +350,21 @@ def esimple_plan(prog: Program, k: int) -> dict:
             "L": [out[5 + i] for i in range(out[4])]}
 
 
+def extended_plan(prog: Program) -> dict:
+    """The scan plan nrgrep's extendedPreproc derives for an extended
+    pattern (pm_extended_plan, host only): ``type`` 2 = the ``window``
+    scanned backward, 3 = the prefix scanned forward; ``fwd`` = the window's
+    non-optional positions; ``L`` = pattern positions left of a candidate;
+    ``simple`` = the window holds no '?*+'."""
+    w = nfa_words(prog.m)
+    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
+    opt = np.array(_words(prog.opt_mask, w), dtype=np.uint64)
+    rep = np.array(_words(prog.rep_mask, w), dtype=np.uint64)
+    out = (ctypes.c_int32 * 6)()
+    check(_lib.load().pm_extended_plan(prog.m, w, bm.ctypes.data, opt.ctypes.data, rep.ctypes.data, out))
+    return {"type": out[0], "fwd": out[1], "window": (out[2], out[3]), "L": out[4], "simple": bool(out[5])}
+
+
 def kernel_ms(handle) -> float:
     ms = ctypes.c_double()
     check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))
@@ -399,6 +414,8 @@ def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0,
         flags |= _lib.PM_CROSS_LINES
     if k > 0 and prog.linear and prog.kind == "simple":
         flags |= _lib.PM_ESIMPLE   # nrgrep's esimple engine decides the report
+    if k == 0 and prog.kind == "extended":
+        flags |= _lib.PM_EXTENDED  # nrgrep's extended engine decides the report
     out = ctypes.c_void_p()
     check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                        last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,

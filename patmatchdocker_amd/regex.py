@@ -62,9 +62,30 @@ SEPARATORS = frozenset(b for b in range(256) if not _isalnum(b))
 
 
 # --------------------------------------------------------------------------
-# parser: recursive descent over the byte string -> small AST
-#   ('sym', frozenset) | ('cat', [..]) | ('alt', [..]) | ('opt'|'star'|'plus', node)
+# parser: nrgrep's own tree (parse 0x41ae90 / parseOr 0x41a530 / parseConc
+# 0x41a760), then its simplify pass (0x41a170), then a small AST
+#   ('sym', frozenset) | ('eps',) | ('cat', [..]) | ('alt', [..])
+#   | ('opt'|'star'|'plus', node)
 # --------------------------------------------------------------------------
+
+# node types of nrgrep's tree (the jump tables at 0x41d4c0 / 0x41d4f0)
+_LEAF, _STAR, _OR, _CAT, _OPT, _PLUS = 0, 1, 2, 3, 4, 5
+
+
+class _Node:
+    """A node of nrgrep's parse tree: ``type`` (above), ``nullable`` (the
+    parse-time flag at +0x8: an empty leaf, '?', '*', a nullable '+' / '|' /
+    concatenation), ``cls`` (a leaf's byte set; None = an empty leaf) and the
+    children ``a`` / ``b`` (+0x10 / +0x18)."""
+
+    __slots__ = ("type", "nullable", "cls", "a", "b")
+
+    def __init__(self, type_, nullable, cls=None, a=None, b=None):
+        self.type, self.nullable, self.cls, self.a, self.b = type_, nullable, cls, a, b
+
+
+_EMPTY_AT = (None, ord(")"), ord("*"), ord("+"), ord("?"), ord("|"))
+
 
 class _Parser:
     def __init__(self, text: bytes, ignore_case: bool):
@@ -100,13 +121,11 @@ class _Parser:
             return value
         return b
 
-    def sym(self, members) -> tuple:
+    def sym(self, members) -> frozenset:
         members = frozenset(members)
-        if self.icase:
-            members = _fold_set(members)
-        return ("sym", members)
+        return _fold_set(members) if self.icase else members
 
-    def klass(self) -> tuple:
+    def klass(self) -> frozenset:
         negate = self.peek() == ord("^")
         if negate:
             self.i += 1
@@ -129,13 +148,8 @@ class _Parser:
             members = set(ALL_BYTES) - members
         return self.sym(members)
 
-    def atom(self) -> tuple:
+    def leaf(self) -> frozenset:
         b = self.take()
-        if b == ord("("):
-            node = self.alternation()
-            if self.take() != ord(")"):
-                raise RegexSyntaxError("missing ')'")
-            return node
         if b == ord("["):
             return self.klass()
         if b == ord("."):
@@ -144,31 +158,214 @@ class _Parser:
             return self.sym(SEPARATORS)
         if b == ord("\\"):
             return self.sym({self.escape()})
-        if b in (ord("?"), ord("*"), ord("+"), ord(")"), ord("|")):
-            raise RegexSyntaxError("operator %r without operand" % chr(b))
+        if b == ord("("):   # (parseConc handles a group before the leaf)
+            raise RegexSyntaxError("unexpected '('")
         return self.sym({b})
 
-    def factor(self) -> tuple:
-        node = self.atom()
-        while self.peek() in (ord("?"), ord("*"), ord("+")):
-            op = {ord("?"): "opt", ord("*"): "star", ord("+"): "plus"}[self.take()]
-            node = (op, node)
-        return node
-
-    def concatenation(self) -> tuple:
-        items = []
-        while self.peek() is not None and self.peek() not in (ord("|"), ord(")")):
-            items.append(self.factor())
-        if not items:
-            raise RegexSyntaxError("empty expression")
-        return items[0] if len(items) == 1 else ("cat", items)
-
-    def alternation(self) -> tuple:
-        branches = [self.concatenation()]
+    def alternatives(self) -> _Node:
+        """parse / parseOr: c1 | c2 | ... as right-deep '|' nodes, each
+        nullable when either side is."""
+        items = [self.conc()]
         while self.peek() == ord("|"):
             self.i += 1
-            branches.append(self.concatenation())
-        return branches[0] if len(branches) == 1 else ("alt", branches)
+            items.append(self.conc())
+        node = items[-1]
+        for it in reversed(items[:-1]):
+            node = _Node(_OR, it.nullable or node.nullable, a=it, b=node)
+        return node
+
+    def conc(self) -> _Node:
+        """parseConc: one atom -- a group, an empty leaf (at end, ')', '|'
+        or a postfix operator, nothing consumed: 0x41a830) or a class --, its
+        postfix operators, then the rest of the concatenation (right-deep;
+        built here from a list, the binary recurses)."""
+        items = []
+        while True:
+            c = self.peek()
+            if c == ord("("):
+                self.i += 1
+                node = self.alternatives()
+                if self.peek() != ord(")"):
+                    raise RegexSyntaxError("missing ')'")
+                self.i += 1
+            elif c in _EMPTY_AT:
+                node = _Node(_LEAF, True)
+            else:
+                node = _Node(_LEAF, False, cls=self.leaf())
+            while self.peek() in (ord("+"), ord("?"), ord("*")):
+                op = self.take()
+                if op == ord("+"):
+                    node = _Node(_PLUS, node.nullable, a=node)
+                else:
+                    node = _Node(_OPT if op == ord("?") else _STAR, True, a=node)
+            items.append(node)
+            if self.peek() in (None, ord(")"), ord("|")):
+                break
+            if len(items) > MAX_POSITIONS:
+                raise RegexSyntaxError("pattern longer than %d positions" % MAX_POSITIONS)
+        node = items[-1]
+        for it in reversed(items[:-1]):
+            node = _Node(_CAT, it.nullable and node.nullable, a=it, b=node)
+        return node
+
+
+def _empty_leaf() -> _Node:
+    return _Node(_LEAF, True)
+
+
+def _simplify(n: _Node, left: bool, right: bool) -> _Node:
+    """nrgrep's simplify (0x41a170), applied by parse() with both edge flags
+    set (no -w / -x, 0x41aec3): a nullable subexpression at the left or
+    right edge of the pattern becomes an empty leaf and drops out, a '+' at
+    an edge loses its repetition, nested postfix operators merge, and a '|'
+    of two single classes becomes one class.  Only the first element of a
+    concatenation sees the left edge, the last the right edge (0x41a1c8,
+    0x41a2f8); a '|' passes (left, 0) / (0, right) to its two sides."""
+    if n.nullable and (left or right):                 # 0x41a190 -> 0x41a260
+        return _empty_leaf()
+    t = n.type
+    if t == _LEAF:
+        return n
+    if t == _STAR:                                     # 0x41a378
+        c = _simplify(n.a, left, right)
+        if c.type in (_STAR, _OPT, _PLUS):
+            return _Node(_STAR, True, a=c.a)           # 0x41a480: the child becomes '*'
+        if c.type == _LEAF and c.nullable:
+            return c
+        n.a = c
+        return n
+    if t == _OPT:                                      # 0x41a2a0
+        c = _simplify(n.a, left, right)
+        if c.type in (_STAR, _PLUS):
+            return _Node(_STAR, True, a=c.a)           # 0x41a458
+        if c.type == _OPT or (c.type == _LEAF and c.nullable):
+            return c
+        n.a = c
+        return n
+    if t == _PLUS:                                     # 0x41a3d8 / 0x41a410
+        if n.nullable:
+            c = _simplify(n.a, False, False)
+        else:
+            c = _simplify(n.a, left, right)
+            if left or right:
+                return c                               # a '+' at an edge: its operand once
+        if c.type in (_STAR, _OPT):
+            return _Node(_STAR, True, a=c.a)
+        if c.type == _PLUS or (c.type == _LEAF and c.nullable):
+            return c
+        n.a = c
+        return n
+    if t == _CAT:
+        return _simplify_chain(n, left, right)
+    a = _simplify(n.a, left, False)
+    b = _simplify(n.b, False, right)
+    if t == _OR:                                       # 0x41a1c8
+        n.a, n.b = a, b
+        if a.type != _LEAF or b.type != _LEAF:
+            return n
+        if a.nullable == b.nullable:                   # 0x41a498: one class
+            cls = None if a.nullable else frozenset(a.cls | b.cls)
+            return _Node(_LEAF, a.nullable, cls=cls)
+        return _Node(_OPT, True, a=b if a.nullable else a)   # 0x41a501 / 0x41a51f
+    raise AssertionError("node type %d" % t)
+
+
+def _simplify_chain(n: _Node, left: bool, right: bool) -> _Node:
+    """simplify of a right-deep concatenation a1 (a2 (.. an)) (0x41a2f8),
+    without recursing along it: a1 gets (left, 0), each suffix node
+    (a_i .. a_n) gets (0, right) -- the first nullable one touching the right
+    edge becomes an empty leaf --, the elements before it (0, 0) and a_n
+    (0, right); an empty leaf on either side of a node drops out."""
+    items, suffix = [], []
+    x = n
+    while x.type == _CAT:
+        items.append(x.a)
+        suffix.append(x)
+        x = x.b
+    items.append(x)
+    suffix.append(x)
+    out = [_simplify(items[0], left, False)]
+    for i in range(1, len(items)):
+        s_node = suffix[i]
+        if right and s_node.nullable:                   # the suffix node's own check
+            break
+        last = i == len(items) - 1
+        out.append(_simplify(items[i], False, right if last else False))
+    # rebuild right-deep, dropping empty leaves (0x41a32d / 0x41a342)
+    node = None
+    for it in reversed(out):
+        if it.type == _LEAF and it.nullable:
+            if node is None:
+                node = it
+            continue
+        if node is None or (node.type == _LEAF and node.nullable):
+            node = it
+        else:
+            node = _Node(_CAT, it.nullable and node.nullable, a=it, b=node)
+    return node
+
+
+def _det_class(n: _Node) -> int:
+    """detClass (0x41ac90): 1 a class sequence, 2 classes each with an
+    optional '? * +', 3 anything else."""
+    best = 1
+    stack = [n]
+    while stack:
+        x = stack.pop()
+        if x.type == _LEAF:
+            continue
+        if x.type == _OR:
+            return 3
+        if x.type == _CAT:
+            stack += [x.a, x.b]
+        elif x.a.type == _LEAF:                        # 0x41acf8
+            best = max(best, 2)
+        else:
+            return 3
+    return best
+
+
+def _to_ast(n: _Node):
+    if n.type == _LEAF:
+        return ("eps",) if n.cls is None else ("sym", n.cls)
+    if n.type in (_OR, _CAT):
+        kind = "alt" if n.type == _OR else "cat"
+        items = []
+        x = n
+        while x.type == n.type:      # a right-deep chain, flattened
+            sub = _to_ast(x.a)
+            items.extend(sub[1] if sub[0] == kind else [sub])
+            x = x.b
+        sub = _to_ast(x)
+        items.extend(sub[1] if sub[0] == kind else [sub])
+        return (kind, items)
+    return ({_STAR: "star", _OPT: "opt", _PLUS: "plus"}[n.type], _to_ast(n.a))
+
+
+def _extended_flags(n: _Node):
+    """(opt, rep) position masks of a class-2 tree (extendedTreeLoad
+    0x411970): '?' optional, '+' repeatable, '*' both."""
+    opt = rep = 0
+    pos = 0
+    stack = [n]
+    order = []
+    while stack:
+        x = stack.pop()
+        if x.type == _CAT:
+            stack.append(x.b)
+            stack.append(x.a)
+        else:
+            order.append(x)
+    for x in order:
+        leaf = x if x.type == _LEAF else x.a
+        if leaf.cls is None:
+            continue
+        if x.type in (_OPT, _STAR):
+            opt |= 1 << pos
+        if x.type in (_PLUS, _STAR):
+            rep |= 1 << pos
+        pos += 1
+    return opt, rep
 
 
 # --------------------------------------------------------------------------
@@ -205,6 +402,8 @@ class Program:
     anchor_start: bool = False   # leading '^' (OptStartLine)
     anchor_end: bool = False     # trailing '$' (OptEndLine)
     kind: str = "simple"         # nrgrep engine class: simple / extended / regular
+    opt_mask: int = 0            # extended: optional positions ('?', '*')
+    rep_mask: int = 0            # extended: repeatable positions ('+', '*')
 
     @property
     def m(self) -> int:
@@ -222,6 +421,8 @@ class Program:
 def _glushkov(node, classes: list):
     """Returns (first, last, nullable, follow-pairs) for ``node``."""
     kind = node[0]
+    if kind == "eps":
+        return 0, 0, True, []
     if kind == "sym":
         i = len(classes)
         if i >= MAX_POSITIONS:
@@ -253,6 +454,8 @@ def _glushkov(node, classes: list):
 
 def _length_bounds(node) -> Tuple[int, Optional[int]]:
     kind = node[0]
+    if kind == "eps":
+        return 0, 0
     if kind == "sym":
         return 1, 1
     if kind == "cat":
@@ -274,16 +477,7 @@ def _length_bounds(node) -> Tuple[int, Optional[int]]:
     return a, (0 if b == 0 else None)
 
 
-def _kind(node) -> str:
-    """nrgrep's engine class (detClass, called by searchPreproc 0x4025b5):
-    "simple" = a sequence of classes, "extended" = a sequence of classes
-    each optionally followed by ``? * +``, "regular" = anything else."""
-    items = node[1] if node[0] == "cat" else [node]
-    if all(c[0] == "sym" for c in items):
-        return "simple"
-    if all(c[0] == "sym" or (c[0] in ("opt", "star", "plus") and c[1][0] == "sym") for c in items):
-        return "extended"
-    return "regular"
+_KINDS = {1: "simple", 2: "extended", 3: "regular"}
 
 
 # the line searchPreproc puts() before scanning (0x402654 .. 0x40275d):
@@ -314,15 +508,25 @@ def split_anchors(text: bytes):
 
 
 def compile_pattern(pattern, ignore_case: bool = True) -> Program:
-    """Compile an nrgrep-syntax pattern (e.g. ``(GAA[CT]TC)``)."""
+    """Compile an nrgrep-syntax pattern (e.g. ``(GAA[CT]TC)``) as nrgrep_coords
+    does: anchors stripped (main), parsed into nrgrep's tree and simplified
+    (parse 0x41ae90, simplify 0x41a170: e.g. ``(GAATTC.?.?)`` becomes the class
+    sequence ``GAATTC``), its engine class from detClass (0x41ac90), then the
+    position automaton of what is left."""
     source = pattern.encode("latin-1") if isinstance(pattern, str) else bytes(pattern)
     text, a_start, a_end = split_anchors(source)
     parser = _Parser(text, ignore_case)
     if not text:
         raise RegexSyntaxError("empty pattern")
-    ast = parser.alternation()
+    tree = parser.alternatives()
     if parser.i != len(text):
+        # parse() stops at a top-level ')' (0x41af3a) -- the converter never
+        # emits one; a user pattern that nrgrep would cut there is refused
         raise RegexSyntaxError("unbalanced ')' in pattern")
+    tree = _simplify(tree, True, True)
+    ast = _to_ast(tree)
+    if ast[0] == "eps":
+        raise RegexSyntaxError("the pattern matches only the empty string")
     classes: list = []
     first, last, nullable, pairs = _glushkov(ast, classes)
     follow = [0] * len(classes)
@@ -336,7 +540,10 @@ def compile_pattern(pattern, ignore_case: bool = True) -> Program:
             if f >> j & 1:
                 precede[j] |= 1 << i
     lo, hi = _length_bounds(ast)
+    kind = _KINDS[_det_class(tree)]
+    opt, rep = _extended_flags(tree) if kind == "extended" else (0, 0)
     return Program(source=source.decode("latin-1"), classes=classes, first=first,
                    last=last, follow=follow, nullable=nullable, min_len=lo,
                    max_len=hi, linear=_is_linear(ast), ignore_case=ignore_case,
-                   precede=precede, anchor_start=a_start, anchor_end=a_end, kind=_kind(ast))
+                   precede=precede, anchor_start=a_start, anchor_end=a_end, kind=kind,
+                   opt_mask=opt, rep_mask=rep)

@@ -10,8 +10,10 @@ from patmatchdocker_amd.convert import convert
 from patmatchdocker_amd.regex import compile_pattern
 from tests.fastagen import dna_fasta, pep_fasta
 
+# no '?', '*', '+' at a pattern edge: nrgrep's simplify (regex.py) drops or
+# shortens those, Python's re does not
 PATTERNS = ["(GAATTC)", "(TATA[AT]A[AT][AG])", "(C..?.?C...[LIVMFYWC])", "(A(CG)*T)", "(AC|GT.)", "(A[^C]G)",
-            "((GA)?TTC)", "(C?.?.TG)", "(A+C)", "(#A)"]
+            "(C(GA)?TTC)", "(GC?.?.TG)", "(GA+C)", "(#A)"]
 
 
 def _to_python_re(source):

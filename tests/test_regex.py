@@ -48,10 +48,20 @@ def test_anchor_characters():
     assert q.m == 5 and q.classes[1] == frozenset(b"$") and q.classes[3] == frozenset(b"^")
 
 
-@pytest.mark.parametrize("bad", ["", "()", "(?A)", "(A", "A)", "(*)", "[AC", "(A|)"])
+@pytest.mark.parametrize("bad", ["", "()", "(A", "A)", "(*)", "[AC", "(A|)"])
 def test_syntax_errors(bad):
     with pytest.raises(RegexSyntaxError):
         compile_pattern(bad)
+
+
+@pytest.mark.parametrize("pat, want", [("(?A)", "A"), ("(*AC)", "AC"), ("(GAATTC.?.?)", "GAATTC"), ("(A+CG)", "ACG"),
+                                       ("(CGA+)", "CGA"), ("(A|C|G)", "[ACG]"), ("(AT(AT)?)", "AT")])
+def test_nrgrep_simplify(pat, want):
+    """parseConc makes an empty leaf where an operand is missing (0x41a830),
+    and simplify (0x41a170) drops nullable edges, a '+' at an edge and merges
+    a '|' of single classes: what nrgrep searches is the simpler pattern."""
+    assert compile_pattern(pat).classes == compile_pattern("(" + want + ")").classes
+    assert compile_pattern(pat).kind == "simple"
 
 
 def test_long_patterns_compile():

@@ -681,11 +681,11 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
 }
 
 // waves per workgroup = parts of a lane's 32 window words; each wave scans
-// 32 / parts consecutive words of every lane column of the tile
-int jit_parts() {
-    static const int p = getenv("PM_JIT_PARTS") ? atoi(getenv("PM_JIT_PARTS")) : 4;
-    return (p == 2 || p == 4) ? p : 4;
-}
+// 32 / parts consecutive words of every lane column of the tile.  Two waves
+// of 16 words (12 % fewer VALU instructions per tile: the Lmax - 1 halo words
+// and the strands' shared blocks are paid per wave) measured slower, 0.500 vs
+// 0.464 ms: the LDS ring then allows only 2 waves per SIMD (r04b A/B).
+int jit_parts() { return 4; }
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
 

@@ -731,7 +731,6 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
     if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * a.parts;
-    const uint32_t steps = LANE_WORDS / a.parts;
     for (uint32_t q = sub; q < pairs; q += EXPAND_THREADS / SEG_LANES) {
         const uint32_t wg = wg0 + q / a.parts, part = q % a.parts;
         const uint32_t seg = wg * a.parts + part;
@@ -742,10 +741,10 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
         }
         for (uint32_t i = lane_t; i < cnt; i += SEG_LANES) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 13);
-            const uint32_t lane = (r.x >> 7) & 63, s = (r.x >> 3) & 15, p = r.x & 7;
+            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 14);
+            const uint32_t lane = (r.x >> 8) & 63, s = (r.x >> 3) & 31, p = r.x & 7;
             if (tile >= a.ntiles) continue;
-            const uint32_t w0 = 32u * lane + part * steps + s;
+            const uint32_t w0 = 32u * lane + s;
             uint32_t live = r.y;
             if ((a.lflag[tile] >> lane) & 1) {
                 uint32_t kill = 0;
@@ -788,7 +787,7 @@ typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
 // Hit records: one uint2 per (tile, lane, step, pattern) with a live window:
-// x = (tile - first tile of the workgroup) << 13 | lane << 7 | step << 3 |
+// x = (tile - first tile of the workgroup) << 14 | lane << 8 | word << 3 |
 // pattern, y = the live mask (bit b = the window of stream b).  Staged per
 // wave in LDS and flushed to the wave's global segment, so the scan loop
 // never waits on a global store; k_linear_expand turns records into keys.
@@ -946,6 +945,50 @@ std::string net_dead(std::ostringstream& o, const CountNet& n, int K, int& uid, 
     return emit_or(o, terms, uid, ind);
 }
 
+// Shared blocks.  Two patterns whose class sequences agree on a run of
+// positions at some offset -- the strands of a (near-)palindromic motif:
+// TGCTGA[GC]TCAGCA.[AT] and its reverse complement agree on 13 positions
+// at offset 2, restriction sites on all of them -- read the same
+// (row, class) words for those positions at steps `off` apart, so the
+// carry-save count of the block is built once per row and both windows
+// only add their own positions (a 13-position block at k = 2: 17 ops
+// once, then 3 per window, instead of 19 per window).  Greedy pairing,
+// each pattern in at most one pair; a pair pays when the block is large
+// and the offset small against the wave's `steps` window words.
+std::vector<std::vector<int>> shared_blocks(int P, const int32_t* lengths, const uint8_t* pos_class,
+                                            const uint8_t* class_acgt, const uint8_t* class_is_any, int steps) {
+    const int JIT_STEPS = steps;
+    std::vector<std::vector<int>> block(P);   // positions of pattern p in its shared block
+    {
+        std::vector<bool> used(P, false);
+        auto cls = [&](int p, int j) { return class_is_any[pos_class[64 * p + j]] ? -1 : class_acgt[pos_class[64 * p + j]] & 15; };
+        for (;;) {
+            int bp = -1, bq = -1, boff = 0, best = 0;
+            for (int p = 0; p < P; ++p)
+                for (int q = p + 1; q < P; ++q) {
+                    if (used[p] || used[q]) continue;
+                    for (int off = -(JIT_STEPS / 2); off <= JIT_STEPS / 2; ++off) {
+                        // position j of p meets position j - off of q
+                        int n = 0;
+                        for (int j = 0; j < lengths[p]; ++j)
+                            n += j - off >= 0 && j - off < lengths[q] && cls(p, j) >= 0 && cls(p, j) == cls(q, j - off);
+                        // ops saved ~ 1.3 per shared input and shared step, a block per extra step
+                        const int gain = n * (JIT_STEPS - 2 * std::abs(off));
+                        if (n >= 6 && gain > best) { best = gain; bp = p; bq = q; boff = off; }
+                    }
+                }
+            if (bp < 0) break;
+            used[bp] = used[bq] = true;
+            for (int j = 0; j < lengths[bp]; ++j)
+                if (j - boff >= 0 && j - boff < lengths[bq] && cls(bp, j) >= 0 && cls(bp, j) == cls(bq, j - boff)) {
+                    block[bp].push_back(j);
+                    block[bq].push_back(j - boff);
+                }
+        }
+    }
+    return block;
+}
+
 // Source of the specialized kernel for a batch of P <= 8 patterns.
 //
 // Workgroup = 4 waves = one tile at a time: wave w scans steps
@@ -999,34 +1042,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // once, then 3 per window, instead of 19 per window).  Greedy pairing,
     // each pattern in at most one pair; a pair pays when the block is large
     // and the offset small against the wave's 8 steps.
-    std::vector<std::vector<int>> block(P);   // positions of pattern p in its shared block
-    {
-        std::vector<bool> used(P, false);
-        auto cls = [&](int p, int j) { return class_is_any[pos_class[64 * p + j]] ? -1 : class_acgt[pos_class[64 * p + j]] & 15; };
-        for (;;) {
-            int bp = -1, bq = -1, boff = 0, best = 0;
-            for (int p = 0; p < P; ++p)
-                for (int q = p + 1; q < P; ++q) {
-                    if (used[p] || used[q]) continue;
-                    for (int off = -(JIT_STEPS / 2); off <= JIT_STEPS / 2; ++off) {
-                        // position j of p meets position j - off of q
-                        int n = 0;
-                        for (int j = 0; j < lengths[p]; ++j)
-                            n += j - off >= 0 && j - off < lengths[q] && cls(p, j) >= 0 && cls(p, j) == cls(q, j - off);
-                        // ops saved ~ 1.3 per shared input and shared step, a block per extra step
-                        const int gain = n * (JIT_STEPS - 2 * std::abs(off));
-                        if (n >= 6 && gain > best) { best = gain; bp = p; bq = q; boff = off; }
-                    }
-                }
-            if (bp < 0) break;
-            used[bp] = used[bq] = true;
-            for (int j = 0; j < lengths[bp]; ++j)
-                if (j - boff >= 0 && j - boff < lengths[bq] && cls(bp, j) >= 0 && cls(bp, j) == cls(bq, j - boff)) {
-                    block[bp].push_back(j);
-                    block[bq].push_back(j - boff);
-                }
-        }
-    }
+    const std::vector<std::vector<int>> block = shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, JIT_STEPS);
     for (int part = 0; part < PARTS; ++part) {
         const int t0 = part * JIT_STEPS, t1 = t0 + JIT_STEPS;
         const int wend = t1 + Lmax - 1;   // words [t0, wend)
@@ -1165,7 +1181,8 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
     for (int part = 0; part < PARTS; ++part)
         o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
           << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
-    o << "    u32 all = ~0u;\n"
+    o << "    const u32 S0 = wid * STEPS;   // the wave's first window word\n"
+         "    u32 all = ~0u;\n"
          "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
          "    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {   // wave-uniform, rare\n"
          "#pragma unroll\n"
@@ -1176,7 +1193,7 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);\n"
          "          if (m) {\n"
          "            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));\n"
-         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 13 | (u32)lane << 7 | (u32)s << 3 | (u32)p, lv);\n"
+         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 14 | (u32)lane << 8 | (u32)(S0 + s) << 3 | (u32)p, lv);\n"
          "            scnt += (u32)__builtin_popcountll(m);\n"
          "            if (scnt > REC_LDS - 64) {\n"
          "              flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
@@ -1190,6 +1207,133 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    slot = slot == RING - 1 ? 0 : slot + 1;\n  }\n"
          "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
          "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * NW + wid] = gcnt + scnt;\n"
+         "}\n";
+    return o.str();
+}
+
+// The whole-tile variant: each wave of a workgroup scans its own tiles
+// (every 4th of the workgroup's range), all 32 window words of every lane,
+// reading the plane words straight from global memory (coalesced rows of
+// 64 words), so the Lmax - 1 halo rows and the strands' shared blocks are
+// paid once per tile instead of once per 8-word part, and no LDS ring
+// limits the occupancy.  The 32 words are emitted as 4 chunks of 8 whose
+// live windows are checked (and recorded) after each chunk; class words and
+// blocks carry over between chunks.
+std::string gen_linear_wave_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
+                                   const uint8_t* class_acgt, const uint8_t* class_is_any, int waves) {
+    constexpr int CH = 8;
+    std::ostringstream o;
+    o << kJitCommon;
+    o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define CH " << CH
+      << "\n";
+    auto word_off = [&](int i) {
+        std::ostringstream w;
+        if (i < LANE_WORDS) w << (i * 64) << " + lane";
+        else if (i < 2 * LANE_WORDS) w << "hb1 + " << (i - 32) << " * hs1";
+        else w << "hb2 + " << (i - 64) << " * hs2";
+        return w.str();
+    };
+    int Lmax = 0;
+    for (int p = 0; p < P; ++p) Lmax = std::max(Lmax, (int)lengths[p]);
+    const std::vector<std::vector<int>> block = shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, LANE_WORDS);
+    o << R"JIT(__device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2* g,
+                                           u32 gcnt, u32 rcap, int lane) {
+  for (u32 r = lane; r < n; r += 64)
+    if (gcnt + r < rcap) g[gcnt + r] = st[r];
+}
+// the live windows of a chunk's CH words: one 8-byte record per (word,
+// pattern) with a live lane, staged per wave in LDS
+#define CHUNK_CHECK(S0)                                                                                   \
+  {                                                                                                       \
+    u32 all = ~0u;                                                                                        \
+    _Pragma("unroll") for (int s = 0; s < CH; ++s) _Pragma("unroll") for (int p = 0; p < P; ++p) all &= dd[s][p]; \
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {                              \
+      _Pragma("unroll") for (int s = 0; s < CH; ++s) {                                                    \
+        _Pragma("unroll") for (int p = 0; p < P; ++p) {                                                   \
+          const u32 lv = ~dd[s][p];                                                                       \
+          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);                                            \
+          if (m) {                                                                                        \
+            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)); \
+            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 14 | (u32)lane << 8 | (u32)((S0) + s) << 3 | (u32)p, lv); \
+            scnt += (u32)__builtin_popcountll(m);                                                         \
+            if (scnt > REC_LDS - 64) {                                                                    \
+              flush_records(st, scnt, grec, gcnt, a.rcap, lane);                                          \
+              gcnt += scnt;                                                                               \
+              scnt = 0;                                                                                   \
+            }                                                                                             \
+          }                                                                                               \
+        }                                                                                                 \
+      }                                                                                                   \
+    }                                                                                                     \
+  }
+)JIT";
+    o << "extern \"C\" __global__ __launch_bounds__(256, " << waves << ") void pm_linear_jit(JArgs a) {\n"
+         "  __shared__ uint2 rst[4][REC_LDS];\n"
+         "  const int lane = threadIdx.x & 63;\n"
+         "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+         "  const u32 hb1 = lane + 1 < 64 ? lane + 1 : 32u * lane + 32u, hs1 = lane + 1 < 64 ? 64u : 1u;\n"
+         "  const u32 hb2 = lane + 2 < 64 ? lane + 2 : 32u * lane + 64u, hs2 = lane + 2 < 64 ? 64u : 1u;\n"
+         "  const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
+         "  const u64 tend = t0 + a.tiles_per_wg < a.ntiles ? t0 + a.tiles_per_wg : a.ntiles;\n"
+         "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * 4 + wid) * a.rcap);\n"
+         "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
+         "  u32 scnt = 0, gcnt = 0;\n"
+         "  if (a.aux_zero && blockIdx.x == 0 && threadIdx.x == 0) *a.aux_zero = 0u;\n"
+         "  for (u64 tile = t0 + wid; tile < tend; tile += 4) {\n"
+         "    const glb_uint2* __restrict__ sw = (const glb_uint2*)(a.hl + tile * TILE_WORDS);\n"
+         "    u32 dd[CH][P];\n";
+    std::vector<bool> loaded(LANE_WORDS + Lmax + 1, false);
+    std::map<std::pair<int, int>, std::string> cw;
+    auto class_word = [&](int i, int subset) {
+        const auto key = std::make_pair(i, subset);
+        auto it = cw.find(key);
+        if (it != cw.end()) return it->second;
+        if (!loaded[i]) {
+            loaded[i] = true;
+            o << "    const uint2 v" << i << " = sw[" << word_off(i) << "];\n";
+        }
+        const std::string nm = "x" + std::to_string(subset) + "_" + std::to_string(i);
+        o << "    u32 " << nm << " = "
+          << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << "; PIN(" << nm
+          << ");\n";
+        cw[key] = nm;
+        return nm;
+    };
+    int uid = 0;
+    std::map<std::vector<std::string>, CountNet> blocks;
+    for (int c = 0; c < LANE_WORDS / CH; ++c) {
+        for (int t = c * CH; t < (c + 1) * CH; ++t) {
+            for (int p = 0; p < P; ++p) {
+                const uint8_t* pc = pos_class + 64 * p;
+                std::vector<std::string> in, bin;
+                for (int j = 0, b = 0; j < lengths[p]; ++j) {
+                    if (class_is_any[pc[j]]) continue;
+                    const bool sh = b < (int)block[p].size() && block[p][b] == j;
+                    b += sh;
+                    (sh ? bin : in).push_back(class_word(t + j, class_acgt[pc[j]] & 15));
+                }
+                CountNet n;
+                if (!bin.empty()) {
+                    auto it = blocks.find(bin);
+                    if (it == blocks.end()) {
+                        CountNet bn;
+                        net_add(o, bn, bin, K, uid, "    ");
+                        if (bn.dead.size() > 1) bn.dead = {emit_or(o, bn.dead, uid, "    ")};
+                        it = blocks.emplace(bin, bn).first;
+                    }
+                    n = it->second;
+                }
+                o << "    {  // word " << t << ", pattern " << p << "\n";
+                net_add(o, n, in, K, uid, "      ");
+                const std::string d = net_dead(o, n, K, uid, "      ");
+                o << "      dd[" << (t - c * CH) << "][" << p << "] = " << d << ";\n    }\n";
+            }
+        }
+        o << "    CHUNK_CHECK(" << c * CH << ");\n";
+    }
+    o << "  }\n"
+         "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
+         "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * 4 + wid] = gcnt + scnt;\n"
          "}\n";
     return o.str();
 }
@@ -1255,7 +1399,8 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
 hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
-    const auto key = std::make_pair(device, std::to_string(parts) + "/" +
+    const bool wave = getenv("PM_JIT_WAVE") && getenv("PM_JIT_WAVE")[0] == '1';
+    const auto key = std::make_pair(device, std::to_string(parts) + (wave ? "w/" : "/") +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);
@@ -1265,7 +1410,8 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     JitKernel jk;
     for (int waves = JIT_WG_PER_CU; waves >= 1; --waves) {
         std::vector<char> code =
-            jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves, parts));
+            jit_compile(wave ? gen_linear_wave_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves)
+                             : gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves, parts));
         if (jk.module) HIPCHK(hipModuleUnload(jk.module));
         HIPCHK(hipModuleLoadData(&jk.module, code.data()));
         HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
@@ -1719,7 +1865,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * JIT_WG_PER_CU * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
-            require(tpw < (1ull << 19), "database too large for the record encoding", PM_E_UNSUPPORTED);
+            require(tpw < (1ull << 18), "database too large for the record encoding", PM_E_UNSUPPORTED);
             const uint64_t parts = (uint64_t)jit_parts();
             const uint64_t nseg = nwg * parts;   // one lane-record segment per wave
             // segment capacities scale with the tiles a workgroup owns (a
@@ -2035,8 +2181,10 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
         require(k >= 0 && k <= PM_MAX_LINEAR_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
-        const std::string src = gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4,
-                                                  jit_parts());
+        const bool wave = getenv("PM_JIT_WAVE") && getenv("PM_JIT_WAVE")[0] == '1';
+        const std::string src =
+            wave ? gen_linear_wave_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4)
+                 : gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4, jit_parts());
         const std::vector<char> code = jit_compile(src);
         if (code_bytes) *code_bytes = code.size();
     });

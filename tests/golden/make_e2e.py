@@ -45,6 +45,12 @@ QUERIES = [
     # unbounded repeats ({m,} -> nrgrep '*')
     ("GA{2,}TC", "dna", None, None, None, None, None, 500),
     ("CX{3,}C", "pep", None, None, None, "substitution", "1", 300),
+    # the extended engine's window away from the pattern start (nearest
+    # start from the window) and nrgrep's simplify at the pattern edges
+    ("AN{0,3}GAATTC", "dna", "Both strands", None, None, None, None, 500),
+    ("TTN{0,3}NNNAA", "dna", None, None, None, None, None, 500),
+    ("N{0,3}GAATTCN{0,3}", "dna", None, None, None, None, None, 500),
+    ("CX{1,3}CX{2}C", "pep", None, None, None, None, None, 500),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]

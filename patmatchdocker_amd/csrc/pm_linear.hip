@@ -684,7 +684,10 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
 // 32 / parts consecutive words of every lane column of the tile.  Two waves
 // of 16 words (12 % fewer VALU instructions per tile: the Lmax - 1 halo words
 // and the strands' shared blocks are paid per wave) measured slower, 0.500 vs
-// 0.464 ms: the LDS ring then allows only 2 waves per SIMD (r04b A/B).
+// 0.464 ms: the LDS ring then allows only 2 waves per SIMD (r04b A/B).  A
+// wave per whole tile reading the rows straight from global memory (19 %
+// fewer VALU instructions, no LDS) measured slower still, 0.546 vs 0.473 ms:
+// each row load's latency is exposed at 3 waves per SIMD (r04w A/B).
 int jit_parts() { return 4; }
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
@@ -1211,133 +1214,6 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
     return o.str();
 }
 
-// The whole-tile variant: each wave of a workgroup scans its own tiles
-// (every 4th of the workgroup's range), all 32 window words of every lane,
-// reading the plane words straight from global memory (coalesced rows of
-// 64 words), so the Lmax - 1 halo rows and the strands' shared blocks are
-// paid once per tile instead of once per 8-word part, and no LDS ring
-// limits the occupancy.  The 32 words are emitted as 4 chunks of 8 whose
-// live windows are checked (and recorded) after each chunk; class words and
-// blocks carry over between chunks.
-std::string gen_linear_wave_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
-                                   const uint8_t* class_acgt, const uint8_t* class_is_any, int waves) {
-    constexpr int CH = 8;
-    std::ostringstream o;
-    o << kJitCommon;
-    o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define CH " << CH
-      << "\n";
-    auto word_off = [&](int i) {
-        std::ostringstream w;
-        if (i < LANE_WORDS) w << (i * 64) << " + lane";
-        else if (i < 2 * LANE_WORDS) w << "hb1 + " << (i - 32) << " * hs1";
-        else w << "hb2 + " << (i - 64) << " * hs2";
-        return w.str();
-    };
-    int Lmax = 0;
-    for (int p = 0; p < P; ++p) Lmax = std::max(Lmax, (int)lengths[p]);
-    const std::vector<std::vector<int>> block = shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, LANE_WORDS);
-    o << R"JIT(__device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2* g,
-                                           u32 gcnt, u32 rcap, int lane) {
-  for (u32 r = lane; r < n; r += 64)
-    if (gcnt + r < rcap) g[gcnt + r] = st[r];
-}
-// the live windows of a chunk's CH words: one 8-byte record per (word,
-// pattern) with a live lane, staged per wave in LDS
-#define CHUNK_CHECK(S0)                                                                                   \
-  {                                                                                                       \
-    u32 all = ~0u;                                                                                        \
-    _Pragma("unroll") for (int s = 0; s < CH; ++s) _Pragma("unroll") for (int p = 0; p < P; ++p) all &= dd[s][p]; \
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {                              \
-      _Pragma("unroll") for (int s = 0; s < CH; ++s) {                                                    \
-        _Pragma("unroll") for (int p = 0; p < P; ++p) {                                                   \
-          const u32 lv = ~dd[s][p];                                                                       \
-          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);                                            \
-          if (m) {                                                                                        \
-            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)); \
-            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 14 | (u32)lane << 8 | (u32)((S0) + s) << 3 | (u32)p, lv); \
-            scnt += (u32)__builtin_popcountll(m);                                                         \
-            if (scnt > REC_LDS - 64) {                                                                    \
-              flush_records(st, scnt, grec, gcnt, a.rcap, lane);                                          \
-              gcnt += scnt;                                                                               \
-              scnt = 0;                                                                                   \
-            }                                                                                             \
-          }                                                                                               \
-        }                                                                                                 \
-      }                                                                                                   \
-    }                                                                                                     \
-  }
-)JIT";
-    o << "extern \"C\" __global__ __launch_bounds__(256, " << waves << ") void pm_linear_jit(JArgs a) {\n"
-         "  __shared__ uint2 rst[4][REC_LDS];\n"
-         "  const int lane = threadIdx.x & 63;\n"
-         "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-         "  const u32 hb1 = lane + 1 < 64 ? lane + 1 : 32u * lane + 32u, hs1 = lane + 1 < 64 ? 64u : 1u;\n"
-         "  const u32 hb2 = lane + 2 < 64 ? lane + 2 : 32u * lane + 64u, hs2 = lane + 2 < 64 ? 64u : 1u;\n"
-         "  const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
-         "  const u64 tend = t0 + a.tiles_per_wg < a.ntiles ? t0 + a.tiles_per_wg : a.ntiles;\n"
-         "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * 4 + wid) * a.rcap);\n"
-         "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
-         "  u32 scnt = 0, gcnt = 0;\n"
-         "  if (a.aux_zero && blockIdx.x == 0 && threadIdx.x == 0) *a.aux_zero = 0u;\n"
-         "  for (u64 tile = t0 + wid; tile < tend; tile += 4) {\n"
-         "    const glb_uint2* __restrict__ sw = (const glb_uint2*)(a.hl + tile * TILE_WORDS);\n"
-         "    u32 dd[CH][P];\n";
-    std::vector<bool> loaded(LANE_WORDS + Lmax + 1, false);
-    std::map<std::pair<int, int>, std::string> cw;
-    auto class_word = [&](int i, int subset) {
-        const auto key = std::make_pair(i, subset);
-        auto it = cw.find(key);
-        if (it != cw.end()) return it->second;
-        if (!loaded[i]) {
-            loaded[i] = true;
-            o << "    const uint2 v" << i << " = sw[" << word_off(i) << "];\n";
-        }
-        const std::string nm = "x" + std::to_string(subset) + "_" + std::to_string(i);
-        o << "    u32 " << nm << " = "
-          << subset_expr(subset, "v" + std::to_string(i) + ".x", "v" + std::to_string(i) + ".y") << "; PIN(" << nm
-          << ");\n";
-        cw[key] = nm;
-        return nm;
-    };
-    int uid = 0;
-    std::map<std::vector<std::string>, CountNet> blocks;
-    for (int c = 0; c < LANE_WORDS / CH; ++c) {
-        for (int t = c * CH; t < (c + 1) * CH; ++t) {
-            for (int p = 0; p < P; ++p) {
-                const uint8_t* pc = pos_class + 64 * p;
-                std::vector<std::string> in, bin;
-                for (int j = 0, b = 0; j < lengths[p]; ++j) {
-                    if (class_is_any[pc[j]]) continue;
-                    const bool sh = b < (int)block[p].size() && block[p][b] == j;
-                    b += sh;
-                    (sh ? bin : in).push_back(class_word(t + j, class_acgt[pc[j]] & 15));
-                }
-                CountNet n;
-                if (!bin.empty()) {
-                    auto it = blocks.find(bin);
-                    if (it == blocks.end()) {
-                        CountNet bn;
-                        net_add(o, bn, bin, K, uid, "    ");
-                        if (bn.dead.size() > 1) bn.dead = {emit_or(o, bn.dead, uid, "    ")};
-                        it = blocks.emplace(bin, bn).first;
-                    }
-                    n = it->second;
-                }
-                o << "    {  // word " << t << ", pattern " << p << "\n";
-                net_add(o, n, in, K, uid, "      ");
-                const std::string d = net_dead(o, n, K, uid, "      ");
-                o << "      dd[" << (t - c * CH) << "][" << p << "] = " << d << ";\n    }\n";
-            }
-        }
-        o << "    CHUNK_CHECK(" << c * CH << ");\n";
-    }
-    o << "  }\n"
-         "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
-         "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * 4 + wid] = gcnt + scnt;\n"
-         "}\n";
-    return o.str();
-}
-
 #define RTCCHK(expr)                                                                      \
     do {                                                                                  \
         hiprtcResult r_ = (expr);                                                         \
@@ -1399,8 +1275,7 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
 hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
-    const bool wave = getenv("PM_JIT_WAVE") && getenv("PM_JIT_WAVE")[0] == '1';
-    const auto key = std::make_pair(device, std::to_string(parts) + (wave ? "w/" : "/") +
+    const auto key = std::make_pair(device, std::to_string(parts) + "/" +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);
@@ -1410,8 +1285,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
     JitKernel jk;
     for (int waves = JIT_WG_PER_CU; waves >= 1; --waves) {
         std::vector<char> code =
-            jit_compile(wave ? gen_linear_wave_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves)
-                             : gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves, parts));
+            jit_compile(gen_linear_source(P, K, lengths, pos_class, class_acgt, class_is_any, waves, parts));
         if (jk.module) HIPCHK(hipModuleUnload(jk.module));
         HIPCHK(hipModuleLoadData(&jk.module, code.data()));
         HIPCHK(hipModuleGetFunction(&jk.fn, jk.module, "pm_linear_jit"));
@@ -2181,10 +2055,8 @@ int pm_linear_jit_compile(int n_patterns, const int32_t* lengths, const uint8_t*
         require(k >= 0 && k <= PM_MAX_LINEAR_K, "k out of range", PM_E_UNSUPPORTED);
         for (int p = 0; p < n_patterns; ++p)
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
-        const bool wave = getenv("PM_JIT_WAVE") && getenv("PM_JIT_WAVE")[0] == '1';
         const std::string src =
-            wave ? gen_linear_wave_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4)
-                 : gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4, jit_parts());
+            gen_linear_source(n_patterns, k, lengths, pos_class, class_acgt, class_is_any, 4, jit_parts());
         const std::vector<char> code = jit_compile(src);
         if (code_bytes) *code_bytes = code.size();
     });

@@ -75,9 +75,14 @@ __device__ __forceinline__ void dma_dword(u64 ga, u32 lds) {
                  : "=&s"(keep) : "v"(ga), "s"(lds) : "memory");
 }
 // a step's word of both planes: {hi, lo} at lds, lds + 256 and the
-// exception plane's {brk, oth} at lds + 512, lds + 768 (4 lane-linear dwords)
-__device__ __forceinline__ void dma_word(const uint2* p, long dbo, u32 lds) {
-    const u64 ga = (u64)p, ge = (u64)(p + dbo);
+// exception plane's {brk, oth} at lds + 512, lds + 768 (4 lane-linear dwords).
+// A row with no break or "other" byte in any lane (`ex` false, wave-uniform)
+// never reads its exception slots: they get the plane word again, a hit on
+// the line just fetched, so the exception plane costs HBM bytes only for
+// flagged rows while every step still issues 4 DMAs (the vmcnt waits count
+// them).
+__device__ __forceinline__ void dma_word(const uint2* p, long dbo, u32 lds, bool ex) {
+    const u64 ga = (u64)p, ge = ex ? (u64)(p + dbo) : ga;
     dma_dword(ga, lds);
     dma_dword(ga + 4ull, lds + 256u);
     dma_dword(ge, lds + 512u);
@@ -156,7 +161,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    sg << "ids9:" << m << ":" << k << ":" << sp.errs << ":";
+    sg << "ids10:" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) {
         sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
         if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
@@ -242,8 +247,14 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
         o << in << "    const uint2 v = make_uint2(ring[sl * 256u + col], ring[sl * 256u + 64u + col]);\n";
         o << in << "    {\n";
         o << in << "        const int q2 = qs + IDS_DEPTH, t2 = 31 + WU - q2;\n";
+        // the DMA'd row's exception flags (warm-up: row t2 - 32 of the next
+        // column, or the halo word for lane 63)
+        o << in << "        const u32 rr2 = (u32)(q2 < WU ? t2 - 32 : q2 < WU + 32 ? t2 : 0);\n";
+        o << in << "        const bool ex2 = q2 < WU + 32 && (((u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr2) | "
+                   "(u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr2)) != 0u || "
+                   "(q2 < WU && ((halof >> rr2) & 1ull)));\n";
         o << in << "        dma_word(q2 < WU ? pn + (long)(t2 - 32) * sn : q2 < WU + 32 ? pm + (long)t2 * 64 : tb, dbo, "
-                   "rbase + snx * 1024u);\n";
+                   "rbase + snx * 1024u, ex2);\n";
         o << in << "    }\n";
         o << in << "    const uint2* " << pv << " = " << (emit ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn") << ";\n";
         o << in << "    const u32 sl_ = sl;\n";
@@ -342,7 +353,12 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
         u32 sl = 0, snx = IDS_DEPTH;
         for (int q = 0; q < IDS_DEPTH; ++q) {
             const int t2 = 31 + WU - q;
-            dma_word(q < WU ? pn + (long)(t2 - 32) * sn : q < WU + 32 ? pm + (long)t2 * 64 : tb, dbo, rbase + (u32)q * 1024u);
+            const u32 rr2 = (u32)(q < WU ? t2 - 32 : q < WU + 32 ? t2 : 0);
+            const bool ex2 = q < WU + 32 && (((u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr2) |
+                                              (u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr2)) != 0u ||
+                                             (q < WU && ((halof >> rr2) & 1ull)));
+            dma_word(q < WU ? pn + (long)(t2 - 32) * sn : q < WU + 32 ? pm + (long)t2 * 64 : tb, dbo,
+                     rbase + (u32)q * 1024u, ex2);
         }
 )IDS";
     for (int j = 0; j <= k; ++j)

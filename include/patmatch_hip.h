@@ -123,12 +123,12 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
  * only, no GPU needed.  out must hold 5 + k + 1 ints.                    */
 int pm_esimple_plan(int m, int words, const uint64_t* byte_mask, int k, int32_t* out);
 /* The pattern is a sequence of classes each with an optional '?', '*' or '+'
- * (nrgrep's detClass() == 2) searched with k = 0: nrgrep_coords runs its
- * "extended" engine (searchPreproc 0x4026b7), whose scanner and
- * nearest-boundary verification decide which overlapping match is printed
- * (DESIGN.md §1).  pm_scan_nfa_wide only; the optional / repeatable
- * positions are read off first / follow / last (PM_E_ARG if the automaton
- * has another shape).  Ignored at k > 0.                                 */
+ * (nrgrep's detClass() == 2): nrgrep_coords runs its "extended" engine at
+ * k = 0 (searchPreproc 0x4026b7) and its "eextended" engine at k > 0
+ * (0x402710), whose scanners and nearest-boundary verification decide which
+ * overlapping match is printed.  pm_scan_nfa_wide only; the
+ * optional / repeatable positions are read off first / follow / last
+ * (PM_E_ARG if the automaton has another shape).                          */
 #define PM_EXTENDED 128
 /* The scan plan nrgrep's extendedPreproc (0x413260) derives for such a
  * pattern: out[0] = 2 (a window scanned backward) or 3 (the prefix scanned
@@ -139,6 +139,18 @@ int pm_esimple_plan(int m, int words, const uint64_t* byte_mask, int k, int32_t*
  * Host only, no GPU needed.  out must hold 6 ints.                       */
 int pm_extended_plan(int m, int words, const uint64_t* byte_mask, const uint64_t* opt_mask,
                      const uint64_t* rep_mask, int32_t* out);
+/* The plan nrgrep's eextendedPreproc (0x40fe30) derives for such a pattern
+ * at k errors (1..PM_MAX_K): out[0] = 1 (k + 1 pieces searched exactly), 2
+ * (a window backward with k errors) or 3 (the prefix forward with k
+ * errors); out[1] = 1 when the scanned positions hold no '?*+' (nrgrep then
+ * runs its esimple scanners); out[2] = P, the pieces (1 for types 2 and 3);
+ * out[3] = the pieces' length in characters (type 1) or the window's
+ * non-optional positions; out[4..5] = extendedFindBest's window [beg, end);
+ * out[6 + 2i], out[7 + 2i] = piece i's [off, end) (the window / prefix for
+ * types 2 and 3).  Host only, no GPU needed.  out must hold 6 + 2 (k + 1)
+ * ints.                                                                   */
+int pm_eextended_plan(int m, int words, const uint64_t* byte_mask, const uint64_t* opt_mask,
+                      const uint64_t* rep_mask, int k, int32_t* out);
 
 /* --- fixed-length patterns: bit-sliced Hamming scan (nucleotide DB) -----
  * A batch of P linear patterns (sequences of classes, no ? * + |), matched

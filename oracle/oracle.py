@@ -63,6 +63,13 @@ def lib():
         _LIB.pmx_extended.restype = ctypes.c_int64
         _LIB.pmx_extended.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, pu64, pu64, ctypes.c_int,
                                       ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmx_eplan.restype = ctypes.c_int
+        _LIB.pmx_eplan.argtypes = [pu64, ctypes.c_int, ctypes.c_int, pu64, pu64, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_int)]
+        _LIB.pmx_eextended.restype = ctypes.c_int64
+        _LIB.pmx_eextended.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, pu64, pu64, ctypes.c_int, ctypes.c_int, p64, p64,
+                                       ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -88,6 +95,7 @@ def drop_header_hits(text: bytes, hits):
     """Remove hits starting on a header line, its terminating '\n' included:
     process_output maps such a start to the '>name' record offset
     (get_name_offset, patmatch.py:214-238) and discards it (:548-550)."""
+    hits = [h for h in hits if h[0] >= 0]   # eextended: a start before the file (its first byte read, pm_nrgrep_ext.c)
     spans = header_spans(text)
     if not spans:
         return hits
@@ -195,6 +203,8 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
         return scan_esimple(text, prog, k, types, skip_headers, bufsize, regs)
     if report == "nrgrep" and simple is None and mode is None and k == 0 and prog.kind == "extended":
         return scan_extended(text, prog, skip_headers, bufsize, regs)
+    if report == "nrgrep" and simple is None and mode is None and k > 0 and prog.kind == "extended":
+        return scan_eextended(text, prog, k, types, skip_headers, bufsize, regs)
     if regs is not None or (bufsize and len(text) >= bufsize):
         return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, simple, mode, 0),
                          skip_headers, bufsize, regs=regs)
@@ -410,6 +420,58 @@ def scan_extended(text: bytes, prog, skip_headers: bool = False, bufsize: int = 
                                end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
         if n < 0:
             raise ValueError("pmx_extended rejected %s" % prog.source)
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+def eextended_plan(prog, k: int):
+    """nrgrep's eextendedPreproc plan for ``prog`` at k errors (pmx_eplan):
+    ``type`` 1 = k + 1 pieces, 2 = a window scanned backward, 3 = the prefix
+    scanned forward; ``simple`` = the scanned positions hold no '?*+' (the
+    esimple scanners); ``pieces`` = [(off, end)] (the window / prefix for
+    types 2 and 3); ``plen`` = the pieces' length in characters (type 1),
+    ``fwd`` = the window's (type 2); ``window`` = extendedFindBest's."""
+    if prog.kind != "extended":
+        raise ValueError("not an extended pattern: %s" % prog.source)
+    B = wide_masks(prog)
+    out = (ctypes.c_int * (6 + 2 * 17))()
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    opt, rep = _mask_words(prog.opt_mask), _mask_words(prog.rep_mask)
+    if lib().pmx_eplan(B.ctypes.data_as(pu64), prog.m, k, opt.ctypes.data_as(pu64), rep.ctypes.data_as(pu64),
+                       1 if prog.ignore_case else 0, out) < 0:
+        raise ValueError("no eextended plan for %s at k=%d" % (prog.source, k))
+    np_ = out[2]
+    return {"type": out[0], "simple": bool(out[1]), "plen": out[3] if out[0] == 1 else 0,
+            "fwd": out[3] if out[0] != 1 else 0, "window": (out[4], out[5]),
+            "pieces": [(out[6 + 2 * i], out[7 + 2 * i]) for i in range(np_)]}
+
+
+def scan_eextended(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False,
+                   bufsize: int = NRGREP_BUFFER, regs=None):
+    """What nrgrep_coords prints for a class-2 pattern at k > 0 (pmx_eextended:
+    nrgrep's eextended plan, scanners, checkMatch1 and report rule), region
+    by region (``regions``)."""
+    if prog.kind != "extended" or k < 1:
+        raise ValueError("scan_eextended needs an extended pattern and k > 0")
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_eextended(t, prog, k, types, False, 0), skip_headers, bufsize,
+                         regs=regs)
+    B = wide_masks(prog)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    opt, rep = _mask_words(prog.opt_mask), _mask_words(prog.rep_mask)
+    mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = lib().pmx_eextended(text, len(text), B.ctypes.data_as(pu64), prog.m, k, err_flags(types),
+                                opt.ctypes.data_as(pu64), rep.ctypes.data_as(pu64), 1 if prog.ignore_case else 0,
+                                mode, beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pmx_eextended rejected %s at k=%d" % (prog.source, k))
         if n <= cap:
             hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
             return drop_header_hits(text, hits) if skip_headers else hits

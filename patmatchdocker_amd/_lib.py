@@ -24,7 +24,7 @@ PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
 PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END, PM_KEEP_HEADERS = 0, 1, 2, 4, 8
 PM_CROSS_LINES = 16
 PM_ESIMPLE = 64               # a class sequence at k > 0: nrgrep's esimple report
-PM_EXTENDED = 128             # classes with '?*+' at k = 0: nrgrep's extended report
+PM_EXTENDED = 128             # classes with '?*+': nrgrep's extended / eextended report
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -34,7 +34,7 @@ EXPORTED = (
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
-    "pm_extended_plan",
+    "pm_extended_plan", "pm_eextended_plan",
 )
 PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
@@ -82,6 +82,7 @@ def _declare(lib):
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_ids_jit_compile.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, pu64]
     lib.pm_extended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+    lib.pm_eextended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P]
     lib.pm_hits_count.argtypes = [P, pu64]
     lib.pm_hits_copy.argtypes = [P, P, P, P, u64]
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]

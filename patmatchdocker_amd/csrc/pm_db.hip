@@ -391,6 +391,14 @@ std::vector<uint64_t> header_ranges(const uint8_t* t, uint64_t n) {
     return r;
 }
 
+// the header line starts, kept on the device for the eextended walk
+void set_headers(pm_db* db, const std::vector<uint64_t>& starts) {
+    db->nhdr = starts.size();
+    if (!db->nhdr) return;
+    db->hdr = dalloc<uint64_t>(db, db->nhdr);
+    HIPCHK(hipMemcpy(db->hdr, starts.data(), db->nhdr * 8, hipMemcpyHostToDevice));
+}
+
 // Tiles cover the file plus room for the longest NFA halo after the last
 // chunk; every position >= n is a break.
 uint64_t tiles_for(uint64_t n) { return (n + MAX_NFA_CHUNK + 2048 + TILE_POS - 1) / TILE_POS; }
@@ -521,7 +529,7 @@ void free_db(pm_db* db) {
     }
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
-    void* ptrs[] = {db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
+    void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
@@ -699,6 +707,11 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
         hipStream_t s = db->stream;
         const std::vector<uint64_t> ranges = header_ranges(fasta, n);
         const uint64_t nr = ranges.size() / 2;
+        {
+            std::vector<uint64_t> hs(nr);
+            for (uint64_t i = 0; i < nr; ++i) hs[i] = ranges[2 * i];
+            set_headers(db, hs);
+        }
         uint64_t* d_ranges = tmp_alloc<uint64_t>(owned, ranges.size());
         if (nr) HIPCHK(hipMemcpy(d_ranges, ranges.data(), ranges.size() * 8, hipMemcpyHostToDevice));
         uint8_t* d_raw = tmp_alloc<uint8_t>(owned, n + 64);
@@ -767,6 +780,11 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         free_all(db, owned);
         // the layout's line breaks: after each header and each record
         const uint64_t rb = SYN_HDR + 1 + rec_len + 1;
+        {
+            std::vector<uint64_t> hs(n_records);
+            for (uint64_t r = 0; r < n_records; ++r) hs[r] = r * rb;
+            set_headers(db, hs);
+        }
         std::vector<uint64_t> rt, re;
         nrgrep_regions(db->n, PM_NRGREP_BUFFER, [&](uint64_t lo, uint64_t hi) {
             if (hi == 0) return ~0ull;

@@ -1,0 +1,1077 @@
+// pm_eextended.hip -- what nrgrep_coords reports for an extended pattern at
+// k > 0 (nrgrep's "eextended" engine), on the GPU.
+//
+// The web form's default `-k <k>ids` (www/FlaskApp/FlaskApp/patmatch.py
+// :299-314) on any PatMatch range X{m,n} (patmatch_to_nrgrep.pl:476-486:
+// X..?.?) selects it: searchPreproc 0x402710, OptErrors != 0 and detClass
+// == 2 -> eextendedPreproc 0x40fe30.  The binary's code (disassembled, never
+// run; DESIGN.md §1, oracle/pm_nrgrep_ext.c which replays it literally):
+//
+//  * plan: extendedFindBest with K = k prices a window; a DP prices k + 1
+//    pieces of L "units" (optional* mandatory) with a cost table built from
+//    extendedFindBest's recurrence; pieces below 0.95 (and below k + 1 times
+//    the window's cost) are searched exactly, else the window backward with
+//    k errors, else the prefix forward with k errors.  Scanned positions
+//    without '?*+' run esimpleScan's loops instead;
+//  * verify (checkMatch1 0x40e340): the left part read back from the
+//    candidate, the right part forward, each keeping the nearest boundary
+//    with the fewest errors -- and, after reading a character, recording it
+//    one position further out (the left phase the look-ahead pointer, the
+//    right phase one past the end), so such a match prints as [s - 1, e + 1)
+//    around its alignment;
+//  * report (recSearchFile 0x402250): the first verified candidate is
+//    printed, R = its end, the scan restarts at R.
+//
+// GPU form.  The automaton kernels (pm_nfa.hip, k errors) produce every start
+// of an alignment.  A printed match comes from a candidate in [s, e] of an
+// alignment [s, e) of at most max_len characters, so starts further apart
+// than 2 max_len + 2k + 8 (bounded patterns) or on different lines
+// (unbounded) fall into independent clusters (the gap keeps the previous
+// cluster's last resume point, its reads and its scanner state out of the
+// next cluster's walk).  One thread per cluster replays the scanner and
+// checkMatch1 over the cluster's text, the printed matches are written in
+// place and compacted by the report pass's scatter.
+#include "pm_internal.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace pm {
+
+namespace {
+
+#pragma clang fp contract(off)
+
+inline bool hb(const uint64_t* w, int i) { return (w[i >> 6] >> (i & 63)) & 1; }
+inline void sb(uint64_t* w, int i) { w[i >> 6] |= 1ull << (i & 63); }
+
+}  // namespace
+
+// eextendedPreproc 0x40fe30 (no transpositions: PatMatch never asks for them)
+EePlan ee_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k) {
+    require(W >= 1 && W <= 4 && m >= 1 && m <= 64 * W, "eextended plan: m / words out of range");
+    require(k >= 1 && k <= PM_MAX_K, "eextended plan: k out of range");
+    double lp[256];
+    letter_probs(lp);
+    auto cls = [&](int c, int p) { return ((B[(size_t)fold((uint8_t)c) * W + (p >> 6)] >> (p & 63)) & 1) != 0; };
+    std::vector<double> pr(m, 0.0), apr(m, 0.0);
+    for (int i = 0; i < m; ++i)                           // 0x41000f, bytes in increasing order
+        for (int c = 0; c < 256; ++c)
+            if (cls(c, i)) {
+                pr[i] += lp[c];
+                if (hb(rep, i)) apr[i] += lp[c];
+            }
+    EePlan P{};
+    int fwd = 0, beg = 0, end = 0;
+    const double prob = find_best_ext(pr, apr, opt, m, k, &fwd, &beg, &end);   // 0x40ff33
+    P.fwd = fwd;
+    P.wbeg = beg;
+    P.wend = end;
+    const int mp = std::min(m, 64) / (k + 1);            // 0x40ffda
+    double best = 0.95;                                  // .rodata 0x41d2a0
+    int bestL = 0, offs[PM_MAX_K + 1] = {}, ends[PM_MAX_K + 1] = {};
+    if (mp > 1 && !(1.0 / (double)mp > 0.95)) {
+        // tab[t][i]: the end after t units (optional* mandatory) from i (0x4100fb)
+        std::vector<int> tab((size_t)(mp + 1) * m);
+        for (int i = 0; i < m; ++i) {
+            int r = i;
+            for (int t = 0;; ++t) {
+                if (r > m) {
+                    r = m;
+                } else if (r > 0 && r < m) {
+                    while (hb(opt, r - 1)) {
+                        ++r;
+                        if (r == m) break;
+                    }
+                }
+                tab[(size_t)t * m + i] = r;
+                if (t + 1 > mp) break;
+                ++r;
+            }
+        }
+        // cost[i * mp + e]: rows overlap as in the binary (stride mp, column
+        // e < m); a span over 64 / (k + 1) positions writes 1.0 at i m + 1 + e
+        // (0x4102cd .. 0x4106a0); never-written cells read 0.0
+        const int cap = 64 / (k + 1);
+        const int tc = std::min(cap, m);
+        const size_t T1 = (size_t)tc + 1, EM = (size_t)m * T1;
+        auto pidx = [&](int l, int e, int t) { return (size_t)l * EM + (size_t)e * T1 + (size_t)t; };
+        std::vector<double> P1(((size_t)m + 1) * EM), P2(((size_t)m + 1) * EM);
+        std::vector<int> pos(m, 0);
+        for (int i = 0; i < m; ++i)                       // 0x4101de
+            for (int t = 0; t <= i + 1; ++t) P1[pidx(t, i, 0)] = P2[pidx(t, i, 0)] = 1.0;
+        std::vector<double> C((size_t)m * m + 2, 0.0);
+        for (int i = 0; i < m; ++i)
+            for (int e = i; e < m; ++e) {
+                const int j = e - i + 1;
+                if (j > cap) {
+                    C[(size_t)i * m + 1 + e] = 1.0;
+                    continue;
+                }
+                double sum = 1.0;
+                for (int t = 1; t <= j; ++t) {
+                    if (pos[e] < t) {                     // 0x410470
+                        P2[pidx(e + 1, e, t)] = 0.0;
+                        P1[pidx(e + 1, e, t)] = 0.0;
+                        for (int l = e; l >= 0; --l) {
+                            double v = pr[l] * P1[pidx(l + 1, e, t - 1)] + apr[l] * P1[pidx(l, e, t - 1)];
+                            v = hb(opt, l) ? P1[pidx(l + 1, e, t)] + v : 0.0 + v;
+                            double r;
+                            if (v > 1.0) {
+                                P1[pidx(l, e, t)] = 1.0;
+                                r = 0.0;
+                            } else {
+                                P1[pidx(l, e, t)] = v;
+                                r = 1.0 - v;
+                            }
+                            P2[pidx(l, e, t)] = 1.0 - (1.0 - P2[pidx(l + 1, e, t)]) * r;
+                        }
+                        pos[e] = t;
+                    }
+                    sum = sum + P2[pidx(i, e, t)];
+                }
+                C[(size_t)i * mp + e] = sum;
+            }
+        // the piece DP (0x410929)
+        const int K2 = k + 2;
+        std::vector<double> D((size_t)(m + 1) * K2);
+        std::vector<int> Wc((size_t)(m + 1) * K2, 0);
+        for (int L = mp;;) {
+            for (int q = 0; q <= m; ++q) D[(size_t)q * K2] = 0.0;
+            for (int c = 1; c <= k + 1; ++c) D[(size_t)m * K2 + c] = 1.0;
+            for (int c = 1; c <= k + 1; ++c)
+                for (int p = m - 1; p >= 0; --p) {
+                    const int en = tab[(size_t)L * m + p];
+                    const int len = en - p;
+                    const double x1 = C[(size_t)p * mp + en - 1];
+                    double q = 0.0;
+                    if ((double)(len + 1) > x1) {
+                        const double xx = x1 / (((double)len - x1) + 1.0);
+                        q = xx <= 1.0 ? 1.0 - xx : 0.0;
+                    }
+                    double val = 1.0 - q * (1.0 - D[(size_t)en * K2 + c - 1]);
+                    Wc[(size_t)p * K2 + c] = p;
+                    if (val > D[(size_t)(p + 1) * K2 + c]) {
+                        val = D[(size_t)(p + 1) * K2 + c];
+                        Wc[(size_t)p * K2 + c] = Wc[(size_t)(p + 1) * K2 + c];
+                    }
+                    D[(size_t)p * K2 + c] = val;
+                }
+            const double v = D[k + 1];                    // 0x410bbe
+            if (best > v) {
+                int p = 0;
+                for (int c = k + 1, idx = 0; c >= 1; --c, ++idx) {
+                    const int o = Wc[(size_t)p * K2 + c];
+                    offs[idx] = o;
+                    ends[idx] = tab[(size_t)L * m + o];
+                    p = tab[(size_t)L * m + o];
+                }
+                best = v;
+                bestL = L;
+            }
+            --L;                                          // 0x410c44
+            if (L == 1) break;
+            if (1.0 / (double)L > best) break;
+        }
+    }
+    bool split = false;
+    if (!(best >= 0.95) && bestL != 0) {                 // 0x410cbd
+        split = true;
+        for (int i = 0; i <= k && split; ++i) {          // 0x410cc7: optional ends trimmed
+            while (offs[i] < ends[i] && hb(opt, offs[i])) ++offs[i];
+            while (ends[i] > offs[i] && hb(opt, ends[i] - 1)) --ends[i];
+            if (offs[i] == ends[i]) split = false;
+        }
+        if (split && best >= (double)(k + 1) * prob) split = false;   // 0x410d95
+    }
+    uint64_t scanned[4] = {};
+    if (split) {
+        P.type = 1;
+        P.np = k + 1;
+        P.plen = bestL;
+        for (int i = 0; i <= k; ++i) {
+            P.off[i] = offs[i];
+            P.pend[i] = ends[i];
+            P.L[i] = offs[i];
+            for (int p = offs[i]; p < ends[i]; ++p) sb(scanned, p);
+        }
+    } else {
+        P.type = fwd >= 1 ? 2 : 3;                       // 0x411087
+        P.np = 1;
+        P.off[0] = beg;
+        P.pend[0] = end;
+        P.L[0] = fwd ? beg : end;
+        require(end - beg >= 1 && end - beg <= 64, "eextended plan: window out of range");
+        for (int p = beg; p < end; ++p) sb(scanned, p);
+    }
+    P.simple = 1;                                        // detClass over them (0x4110d9 / 0x4112e5)
+    for (int p = 0; p < m; ++p)
+        if (hb(scanned, p) && (hb(opt, p) || hb(rep, p))) P.simple = 0;
+    return P;
+}
+
+void ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
+              int64_t max_len, uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab) {
+    const EePlan P = ee_plan(B, W, m, opt, rep, k);
+    auto cls = [&](int c, int p) { return ((B[(size_t)fold((uint8_t)c) * W + (p >> 6)] >> (p & 63)) & 1) != 0; };
+    auto rp = [&](int c, int p) { return hb(rep, p) && cls(c, p); };
+    EeSlot S{};
+    S.m = m;
+    S.k = k;
+    S.errs = errs;
+    S.type = P.type;
+    S.simple = P.simple;
+    S.np = P.np;
+    S.plen = P.plen;
+    S.wbeg = P.wbeg;
+    S.wend = P.wend;
+    S.anchors = (int32_t)(flags & (PM_ANCHOR_START | PM_ANCHOR_END));
+    S.pid = pid;
+    S.max_len = max_len;
+    std::vector<uint64_t> tab;
+    auto grab = [&](size_t words) {
+        const size_t at = tab.size();
+        tab.resize(at + words, 0);
+        return at;
+    };
+    S.o_T = grab(256);
+    S.o_TA = grab(256);
+    S.o_T2 = grab(256);
+    uint64_t* T = tab.data() + S.o_T;
+    uint64_t* TA = tab.data() + S.o_TA;
+    uint64_t* T2 = tab.data() + S.o_T2;
+    const int beg = P.wbeg, end = P.wend, span = end - beg;
+    if (P.simple && P.type == 1) {                       // esimpleLoadFast 0x4153fa
+        for (int r = 0; r < P.np; ++r)
+            for (int pp = 0; pp < P.plen; ++pp)
+                for (int c = 0; c < 256; ++c)
+                    if (P.off[r] + P.plen - 1 - pp < m && cls(c, P.off[r] + P.plen - 1 - pp)) {
+                        const uint64_t bit = 1ull << (r * P.plen + pp);
+                        T[c] |= bit;
+                        if (pp > 0) T2[c] |= bit;
+                    }
+    } else if (P.simple && P.type == 2) {                // simpleLoadFast 0x417561 (backward)
+        for (int r = 0; r < span; ++r)
+            for (int c = 0; c < 256; ++c)
+                if (cls(c, end - 1 - r)) T[c] |= 1ull << (64 - span + r);
+    } else if (P.simple) {                               // simpleLoadFast 0x417615 (forward shift-or)
+        const uint64_t full = span == 64 ? ~0ull : (1ull << span) - 1;
+        for (int c = 0; c < 256; ++c) T[c] = full;
+        for (int r = 0; r < span; ++r)
+            for (int c = 0; c < 256; ++c)
+                if (cls(c, beg + r)) T[c] &= ~(1ull << r);
+    } else if (P.type == 1) {                            // eextendedLoadFast 0x40fb79
+        S.flen = P.plen;
+        int b = 0;
+        for (int q = 0; q <= k; ++q) {
+            const int plen = P.pend[q] - P.off[q];
+            for (int r = 0; r < plen; ++r, ++b) {
+                const int p = P.pend[q] - 1 - r;
+                const uint64_t bit = 1ull << (b & 63);
+                for (int c = 0; c < 256; ++c) {
+                    if (cls(c, p)) {
+                        T[c] |= bit;
+                        if (r > 0) T2[c] |= bit;
+                    }
+                    if (rp(c, p)) TA[c] |= bit;
+                }
+                if (hb(opt, p)) {
+                    const uint64_t pbit = 1ull << ((b - 1) & 63);
+                    S.fS |= bit;
+                    if (S.fF & pbit) {
+                        S.fF = (S.fF & ~pbit) | bit;
+                    } else {
+                        S.fI |= pbit;
+                        S.fF |= bit;
+                    }
+                }
+            }
+            S.top[q] = 1ull << ((b - 1) & 63);
+        }
+    } else {                                             // extendedLoadFast 0x413060 (fwd, beg, end)
+        S.flen = P.fwd;
+        S.fspan = span;
+        int b = P.fwd ? 64 - span : 0, p = P.fwd ? end - 1 : beg;
+        for (int r = 0; r < span; ++r, ++b, p += P.fwd ? -1 : 1) {
+            const uint64_t bit = 1ull << b;
+            for (int c = 0; c < 256; ++c) {
+                if (cls(c, p)) T[c] |= bit;
+                if (rp(c, p)) TA[c] |= bit;
+            }
+            if (hb(opt, p)) {
+                const uint64_t pbit = 1ull << ((b - 1) & 63);
+                S.fS |= bit;
+                if (S.fF & pbit) {
+                    S.fF = (S.fF & ~pbit) | bit;
+                } else {
+                    S.fI |= pbit;
+                    S.fF |= bit;
+                }
+            }
+        }
+    }
+    if (P.simple) S.fspan = span;
+    // verify parts (extendedLoadVerif 0x412c60): piece q's left [0, L) from
+    // L - 1 down, its right [L, m) up
+    for (int q = 0; q < P.np; ++q)
+        for (int side = 0; side < 2; ++side) {
+            EePart& V = side == 0 ? S.lv[q] : S.rv[q];
+            const int L = P.L[q];
+            const int plen = side == 0 ? L : m - L, p0 = side == 0 ? L - 1 : L, dir = side == 0 ? -1 : 1;
+            const int pw = std::max(1, (plen + 63) >> 6);
+            V.len = plen;
+            V.pw = pw;
+            V.o_B = grab((size_t)256 * pw);
+            V.o_A = grab((size_t)256 * pw);
+            bool opened = false;
+            for (int r = 0; r < plen; ++r) {
+                const int p = p0 + r * dir;
+                for (int c = 0; c < 256; ++c) {
+                    if (cls(c, p)) sb(tab.data() + V.o_B + (size_t)c * pw, r);
+                    if (rp(c, p)) sb(tab.data() + V.o_A + (size_t)c * pw, r);
+                }
+                if (!hb(opt, p)) continue;
+                if (r > 0) {
+                    if (hb(V.F, r - 1)) {                // 0x412ff1: the block goes on
+                        V.F[(r - 1) >> 6] &= ~(1ull << ((r - 1) & 63));
+                        sb(V.F, r);
+                    } else {
+                        sb(V.I, r - 1);
+                        sb(V.F, r);
+                        sb(V.S, r);
+                        opened = true;
+                        continue;
+                    }
+                }
+                if (opened) sb(V.S, r);                  // 0x413015
+                else sb(V.X, r);
+            }
+        }
+    o_slot = up.add(&S, sizeof(S));
+    o_tab = up.add(tab.data(), tab.size() * 8);
+}
+
+#pragma clang fp contract(on)
+
+// ---------------------------------------------------------------------------
+// device: the per-cluster replay of eextendedScan / esimpleScan and
+// checkMatch1 (oracle/pm_nrgrep_ext.c holds the same loops, addresses cited)
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t EE_POS_MASK = (1ull << 48) - 1;
+constexpr uint64_t EE_SCAN = 1ull << 16;   // unbounded: how far a head looks back for a line break
+constexpr uint32_t EE_T = 256;
+
+struct EeWalk {
+    const EeSlot* S;
+    const uint64_t* tab;
+    TextView tv;
+    int64_t n;         // the region end
+    int64_t R;
+    int64_t nl_lo;     // the last '\n' below the record cursor (-1: none since the walk began)
+    int64_t nl_hi;     // the first '\n' at or after it (n: none)
+
+    __device__ uint8_t at(int64_t p) const { return xt_byte(tv, (uint64_t)p); }
+    __device__ bool is_nl(int64_t p) const { return xt_brk(tv, (uint64_t)p) && at(p) == (uint8_t)'\n'; }
+    __device__ int64_t next_nl(int64_t p) const {
+        if (tv.nuc_layout) {
+            while (p < n) {
+                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
+                if (!z) {
+                    p = ((p >> 5) + 1) << 5;
+                    continue;
+                }
+                p += (int64_t)__builtin_ctz(z);
+                if (p >= n) break;
+                if (at(p) == (uint8_t)'\n') return p;
+                ++p;
+            }
+            return n;
+        }
+        for (; p < n; ++p)
+            if (tv.raw[p] == (uint8_t)'\n') return p;
+        return n;
+    }
+    // recGetRecord 0x402030 for rp (non-decreasing over a walk)
+    __device__ void record(int64_t rp, int64_t& recbeg, int64_t& recend) {
+        while (nl_hi < rp) {
+            nl_lo = nl_hi;
+            nl_hi = next_nl(nl_hi + 1);
+        }
+        recbeg = (nl_lo >= 0 && nl_lo >= R) ? nl_lo + 1 : R;
+        recend = nl_hi;
+    }
+    __device__ bool left_ok(int64_t p, int64_t recbeg) const {   // recCheckLeftContext 0x402170
+        return !((S->anchors & PM_ANCHOR_START) && p > recbeg && at(p - 1) != (uint8_t)'\n');
+    }
+    __device__ bool right_ok(int64_t q, int64_t recend) const {  // recCheckRightContext 0x4021e0
+        return !((S->anchors & PM_ANCHOR_END) && q < recend && at(q) != (uint8_t)'\n');
+    }
+
+    template <int WB>
+    __device__ static void close(uint64_t* D, int W, const EePart& V) {
+        uint64_t borrow = 0;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            if (w >= W) break;
+            const uint64_t d = D[w], xx = d | V.F[w];
+            const uint64_t sub = xx - borrow - V.I[w];
+            D[w] = ((~sub ^ xx) & V.S[w]) | d;
+            const uint64_t bi = borrow + V.I[w];
+            borrow = (bi < borrow) | (xx < bi);
+        }
+    }
+
+    // checkMatch1's rows of one part: init (0x40e658), row 0 (0x40e8ad) and
+    // row j (0x40e9b0) updates, the alive test (0x40edb9)
+    template <int WB>
+    struct Rows {
+        int W;
+        uint64_t fin, alive;
+        uint64_t R[PM_MAX_K + 1][WB];
+        uint64_t t1[WB], t2[WB];
+    };
+
+    template <int WB>
+    __device__ void rows_init(Rows<WB>& s, const EePart& V, int kmax) const {
+        s.W = V.pw;
+        s.fin = 1ull << ((V.len - 1) & 63);
+        s.alive = s.fin * 2 - 1;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) s.R[0][w] = V.X[w];
+        for (int j = 1; j <= kmax; ++j) {
+            uint64_t carry = 1;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) {
+                const uint64_t old = s.R[j - 1][w];
+                s.R[j][w] = (S->errs & PM_ERR_DEL) ? ((old << 1) | carry) : old;
+                carry = old >> 63;
+            }
+            if (S->errs & PM_ERR_DEL) close<WB>(s.R[j], s.W, V);
+        }
+    }
+    template <int WB>
+    __device__ void row0(Rows<WB>& s, const EePart& V, uint8_t c, uint64_t inj) const {
+        const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
+        const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
+        uint64_t carry = inj;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            if (w >= s.W) break;
+            const uint64_t old = s.R[0][w];
+            s.t1[w] = old;
+            s.t2[w] = (((old << 1) | carry) & B[w]) | (old & A[w]);
+            carry = old >> 63;
+        }
+        close<WB>(s.t2, s.W, V);
+#pragma unroll
+        for (int w = 0; w < WB; ++w) s.R[0][w] = w < s.W ? s.t2[w] : 0ull;
+    }
+    template <int WB>
+    __device__ void rowj(Rows<WB>& s, const EePart& V, int j, uint8_t c, uint64_t inj) const {
+        const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
+        const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
+        uint64_t dc = 0, sc = inj, mc = inj;
+        uint64_t nw[WB];
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            nw[w] = 0;
+            if (w >= s.W) continue;
+            uint64_t r = 0;
+            if (S->errs & PM_ERR_DEL) {
+                r = (s.t2[w] << 1) | dc;
+                dc = s.t2[w] >> 63;
+            }
+            if (S->errs & PM_ERR_INS) r |= s.t1[w];
+            if (S->errs & PM_ERR_SUB) {
+                r |= sc | (s.t1[w] << 1);
+                sc = 1;                                  // 0x40eb7d
+            }
+            const uint64_t old = s.R[j][w];
+            r |= (((old << 1) | mc) & B[w]) | (old & A[w]);
+            mc = old >> 63;
+            nw[w] = r;
+            s.t1[w] = old;
+        }
+        close<WB>(nw, s.W, V);
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            s.t2[w] = nw[w];
+            s.R[j][w] = nw[w];
+        }
+    }
+    template <int WB>
+    __device__ static bool rows_alive(const Rows<WB>& s, int maxk) {
+        uint64_t any = 0;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            if (w >= s.W) break;
+            any |= w == s.W - 1 ? (s.R[maxk][w] & s.alive) : s.R[maxk][w];
+        }
+        return any != 0;
+    }
+    template <int WB>
+    __device__ static bool fin_of(const uint64_t* r, const Rows<WB>& s) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int w = 0; w < WB; ++w)
+            if (w == s.W - 1) v = r[w];
+        return (v & s.fin) != 0;
+    }
+
+    // the left phase (checkMatch1 0x40e3a0 .. 0x40ee6e)
+    template <int WB>
+    __device__ bool left(const EePart& V, int64_t pos, int64_t recbeg, int& nerr, int64_t& start) const {
+        const int k = S->k;
+        if (V.len == 0) {
+            for (int q = 0; q <= k; ++q) {
+                if (left_ok(pos - q, recbeg)) {
+                    start = pos - q;
+                    nerr = q;
+                    return true;
+                }
+                if (pos - q == recbeg || !(S->errs & PM_ERR_INS)) return false;
+            }
+            return false;
+        }
+        Rows<WB> s;
+        rows_init<WB>(s, V, k);
+        int maxk = k, best = k;
+        bool found = false;
+        int64_t fpos = 0;
+        for (int j = 1; j <= maxk; ++j)
+            if (fin_of<WB>(s.R[j], s) && left_ok(pos, recbeg)) {
+                found = true;
+                fpos = pos;
+                best = j;
+                maxk = j - 1;
+            }
+        if (pos != recbeg) {
+            uint64_t inj = 1;
+            uint8_t c = at(pos - 1);
+            for (int64_t X = pos - 2; X != recbeg - 2; --X) {
+                const uint8_t look = X + 1 != recbeg ? at(X) : (uint8_t)0;
+                row0<WB>(s, V, c, inj);
+                if (fin_of<WB>(s.t2, s) && left_ok(X, recbeg)) {
+                    start = X;
+                    nerr = 0;
+                    return true;
+                }
+                for (int j = 1; j <= maxk; ++j) {
+                    rowj<WB>(s, V, j, c, inj);
+                    if (fin_of<WB>(s.t2, s) && left_ok(X, recbeg)) {
+                        int cc = j;                      // 0x40ec54: walk down
+                        while (cc - 1 >= 0 && fin_of<WB>(s.R[cc - 1], s)) --cc;
+                        if (cc == 0) {
+                            start = X;
+                            nerr = 0;
+                            return true;
+                        }
+                        found = true;
+                        fpos = X;
+                        best = cc;
+                        maxk = cc - 1;
+                        break;
+                    }
+                }
+                if (!rows_alive<WB>(s, maxk)) break;
+                inj = 0;
+                c = look;
+            }
+        }
+        if (!found) return false;
+        start = fpos;
+        nerr = best;
+        return true;
+    }
+
+    // the right phase (checkMatch1 0x40ec63 .. 0x40f7be)
+    template <int WB>
+    __device__ bool right(const EePart& V, int64_t pos, int64_t recend, int kmax, int64_t& end) const {
+        if (V.len == 0) {
+            for (int q = 0; q <= kmax; ++q) {
+                if (right_ok(pos + q, recend)) {
+                    end = pos + q;
+                    return true;
+                }
+                if (q == recend - pos || !(S->errs & PM_ERR_INS)) return false;
+            }
+            return false;
+        }
+        if (kmax < 0) return false;
+        Rows<WB> s;
+        rows_init<WB>(s, V, kmax);
+        int maxk = kmax;
+        bool found = false;
+        int64_t fend = 0;
+        for (int j = 1; j <= maxk; ++j)
+            if (fin_of<WB>(s.R[j], s) && right_ok(pos, recend)) {
+                found = true;
+                fend = pos;
+                maxk = j - 1;
+            }
+        if (pos != recend) {
+            uint64_t inj = 1;
+            uint8_t c = at(pos);
+            for (int64_t Y = pos + 1;; ++Y) {
+                const int64_t q = Y - 1;
+                const uint8_t look = q != recend - 1 ? at(Y) : (uint8_t)0;
+                row0<WB>(s, V, c, inj);
+                if (fin_of<WB>(s.t2, s) && right_ok(Y + 1, recend)) {
+                    end = Y + 1;
+                    return true;
+                }
+                for (int j = 1; j <= maxk; ++j) {
+                    rowj<WB>(s, V, j, c, inj);
+                    if (fin_of<WB>(s.t2, s) && right_ok(Y + 1, recend)) {
+                        int cc = j;
+                        while (cc - 1 >= 0 && fin_of<WB>(s.R[cc - 1], s)) --cc;
+                        if (cc == 0) {
+                            end = Y + 1;
+                            return true;
+                        }
+                        found = true;
+                        fend = Y + 1;
+                        maxk = cc - 1;
+                        break;
+                    }
+                }
+                if (!rows_alive<WB>(s, maxk)) break;
+                if (q == recend - 1) break;
+                inj = 0;
+                c = look;
+            }
+        }
+        if (!found) return false;
+        end = fend;
+        return true;
+    }
+
+    // checkMatch 0x40f910
+    template <int WB>
+    __device__ bool check(int q, int64_t pos, int64_t& mb, int64_t& me) {
+        const int64_t rp = S->type == 3 ? pos - 1 : pos;
+        if (rp < R) return false;
+        int64_t recbeg, recend;
+        record(rp, recbeg, recend);
+        if (rp < recbeg || rp >= recend) return false;
+        int64_t start, end;
+        int eL = 0;
+        if (!left<WB>(S->lv[q], pos, recbeg, eL, start)) return false;
+        if (!right<WB>(S->rv[q], pos, recend, S->k - eL, end)) return false;
+        mb = start;
+        me = end;
+        return true;
+    }
+
+    __device__ uint64_t xclose(uint64_t D) const {
+        const uint64_t xx = D | S->fF;
+        return D | ((xx ^ ~(xx - S->fI)) & S->fS);
+    }
+
+    // the scanners over [R, n); false when no candidate <= stop verifies
+    template <int WB>
+    __device__ bool scan(int64_t stop, int64_t& mb, int64_t& me) {
+        const uint64_t* T = tab + S->o_T;
+        const uint64_t* TA = tab + S->o_TA;
+        const uint64_t* T2 = tab + S->o_T2;
+        const int k = S->k;
+        uint64_t Rr[PM_MAX_K + 1], Tr[PM_MAX_K + 1];
+        if (S->simple && S->type == 1) {                 // esimpleScan 0x413780: pieces, exact
+            const int mpc = S->plen;
+            int64_t r9 = R - 1;
+            const int64_t limit = n - mpc;
+            while (r9 < limit) {
+                if (r9 + 1 > stop) return false;
+                uint64_t D = T[at(r9 + mpc)];
+                if (!D) {
+                    r9 += mpc;
+                    continue;
+                }
+                int64_t a = r9 + mpc - 1;
+                int q = mpc - 1;
+                do {
+                    D = (D << 1) & T2[at(a)];
+                    --q;
+                    --a;
+                } while (D && q);
+                if (D)
+                    for (int i = 0; i < S->np; ++i) {    // 0x41384b: 32-bit shift
+                        const int bit = i * mpc + mpc - 1;
+                        const uint64_t msk = (uint64_t)(int64_t)(int32_t)(1u << (bit & 31));
+                        if ((D & msk) && check<WB>(i, r9 + 1, mb, me)) return true;
+                    }
+                r9 += q + 1;
+            }
+            return false;
+        }
+        if (S->simple && S->type == 2) {                 // esimpleScan 0x413b6f: window, ABNDM
+            const int Lw = S->fspan;
+            const uint64_t top = ~0ull << (64 - Lw);
+            const int W = Lw - k;
+            const int64_t limit = n - (Lw - k - 1);
+            for (int64_t s0 = R; s0 < limit;) {
+                if (s0 > stop) return false;
+                const uint64_t b0 = T[at(s0 + W - 1)];
+                Rr[0] = b0;
+                for (int j = 1; j <= k; ++j) {
+                    Rr[j] = top;
+                    Tr[j] = b0;
+                }
+                int64_t rb = W - 2;
+                for (;;) {
+                    const uint64_t bc = T[at(s0 + rb)];
+                    uint64_t oldp = Rr[0];
+                    uint64_t newp = (oldp << 1) & bc;
+                    Rr[0] = newp;
+                    for (int j = 1; j <= k; ++j) {
+                        const uint64_t trans = (bc << 1) & Tr[j];
+                        uint64_t v = ((newp | oldp) << 1) | oldp;
+                        Tr[j] = (oldp << 2) & bc;
+                        v |= trans;
+                        const uint64_t oldj = Rr[j];
+                        v |= (oldj << 1) & bc;
+                        Rr[j] = v;
+                        oldp = oldj;
+                        newp = v;
+                    }
+                    if (rb == 0) {
+                        if ((Rr[k] >> 63) && check<WB>(0, s0, mb, me)) return true;
+                        break;
+                    }
+                    if (!Rr[k] && !Tr[k]) break;
+                    --rb;
+                }
+                s0 += rb + 1;
+            }
+            return false;
+        }
+        if (S->simple) {                                 // esimpleScan 0x413932: prefix, shift-or
+            const uint64_t fin = 1ull << (S->fspan - 1);
+            for (int j = 0; j <= k; ++j) {
+                Rr[j] = ~0ull << j;
+                Tr[j] = ~0ull;
+            }
+            for (int64_t p = R; p < n;) {
+                const uint64_t bc = T[at(p)];
+                ++p;
+                uint64_t oldp = Rr[0];
+                uint64_t newp = (oldp << 1) | bc;
+                Rr[0] = newp;
+                const uint64_t r9 = (bc << 1) | 1;
+                for (int j = 1; j <= k; ++j) {
+                    const uint64_t tr = r9 | Tr[j];
+                    uint64_t v = ((newp & oldp) << 1) & oldp;
+                    Tr[j] = (oldp << 2) | bc;
+                    v &= tr;
+                    const uint64_t oldj = Rr[j];
+                    v &= (oldj << 1) | bc;
+                    Rr[j] = v;
+                    oldp = oldj;
+                    newp = v;
+                }
+                if (!(Rr[k] & fin)) {
+                    if (p > stop) return false;
+                    if (check<WB>(0, p, mb, me)) return true;
+                }
+            }
+            return false;
+        }
+        if (S->type == 1) {                              // eextendedScan 0x40cf05: pieces with '?*+'
+            const int len = S->flen;
+            int64_t pos = R - 1;
+            const int64_t lim = n - len;
+            while (pos < lim) {
+                if (pos + 1 > stop) return false;
+                uint64_t D = T[at(pos + len)];
+                while (!D) {
+                    pos += len;
+                    if (!(pos < lim)) return false;
+                    if (pos + 1 > stop) return false;
+                    D = T[at(pos + len)];
+                }
+                int ebp = len - 1;
+                int64_t c = pos + len - 1;
+                do {
+                    --ebp;
+                    const uint8_t ch = at(c);
+                    --c;
+                    const uint64_t Dc = xclose(D);
+                    D = (Dc & TA[ch]) | ((Dc << 1) & T2[ch]);
+                } while (D && ebp != 0);
+                if (D)
+                    for (int q = 0; q < S->np; ++q)
+                        if ((S->top[q] & D) && check<WB>(q, pos + 1, mb, me)) return true;
+                pos = pos + ebp + 1;
+            }
+            return false;
+        }
+        if (S->type == 2) {                              // eextendedScan 0x40d5a1: window, k errors
+            const int W = S->flen - k - 1;
+            const uint64_t top = S->fspan >= 64 ? ~0ull : ~0ull << (64 - S->fspan);
+            if (W < 1) return false;
+            for (int64_t pos = R; pos < n - W;) {
+                if (pos + 1 > stop) return false;
+                const uint8_t c1 = at(pos + W), c2 = at(pos + W - 1);
+                Rr[0] = xclose(T[c1]);
+                const uint64_t tr0 = (xclose(T[c2]) << 1) & T[c1];
+                for (int j = 1; j <= k; ++j) {
+                    Rr[j] = top;
+                    Tr[j] = tr0;
+                }
+                int64_t ptr = pos + W - 1;
+                int cnt = W - 1;
+                uint8_t c = c2, look = 0;
+                for (;;) {
+                    --cnt;
+                    if (cnt + 1 > 0) look = at(ptr - 1);
+                    uint64_t pold = Rr[0];
+                    uint64_t pnew = xclose((Rr[0] & TA[c]) | ((Rr[0] << 1) & T[c]));
+                    Rr[0] = pnew;
+                    for (int j = 1; j <= k; ++j) {
+                        const uint64_t old = Rr[j];
+                        const uint64_t v = ((old << 1) & T[c]) | (old & TA[c]) | pold | ((pnew | pold) << 1) | Tr[j];
+                        Tr[j] = (xclose((pold & TA[look]) | ((pold << 1) & T[look])) << 1) & T[c];
+                        Rr[j] = xclose(v);
+                        pold = old;
+                        pnew = Rr[j];
+                    }
+                    if (cnt < 0) {
+                        if ((Rr[k] >> 63) && check<WB>(0, pos + 1, mb, me)) return true;
+                        break;
+                    }
+                    if (!Rr[k] && !Tr[k]) break;
+                    --ptr;
+                    c = look;
+                }
+                pos = pos + cnt + 2;
+            }
+            return false;
+        }
+        // eextendedScan 0x40d0f4: the prefix forward with k errors, a
+        // character followed by '\n' never fed; row 0's repeat term only in
+        // the k = 1 / k = 2 specializations
+        const bool ta0 = k <= 2;
+        const uint64_t fin = 1ull << ((S->fspan - 1) & 63);
+        if (R >= n) return false;
+        int64_t p = R;
+        for (;;) {
+            if (p >= n) return false;
+            uint8_t c = at(p);
+            ++p;
+            while (c == (uint8_t)'\n') {
+                if (p == n) return false;
+                ++p;
+                c = at(p - 1);
+            }
+            for (int j = 0; j <= k; ++j) {
+                Rr[j] = j ? ~(~0ull << j) : 0ull;
+                Tr[j] = 0;
+            }
+            int64_t nxt = p;
+            bool restart = false;
+            for (;;) {
+                if (nxt > stop + 1) return false;   // the candidate nxt is past stop
+                uint8_t look = c;
+                if (nxt < n) {
+                    look = at(nxt);
+                    if (look == (uint8_t)'\n') {
+                        p = nxt + 1;
+                        restart = true;
+                        break;
+                    }
+                }
+                uint64_t pold = Rr[0];
+                uint64_t raw0 = ((Rr[0] << 1) | 1) & T[c];
+                if (ta0) raw0 |= Rr[0] & TA[c];
+                uint64_t pnew = xclose(raw0);
+                Rr[0] = pnew;
+                for (int j = 1; j <= k; ++j) {
+                    const uint64_t old = Rr[j];
+                    const uint64_t v = (((old << 1) | 1) & T[c]) | (old & TA[c]) | ((pnew | pold) << 1) | pold | 1ull |
+                                       Tr[j];
+                    const uint64_t u = xclose((pold & TA[look]) | (((pold << 1) | 1) & T[look]));
+                    Tr[j] = (u & TA[c]) | ((u << 1) & T[c]);
+                    Rr[j] = xclose(v);
+                    pold = old;
+                    pnew = Rr[j];
+                }
+                if ((Rr[k] & fin) && nxt <= stop && check<WB>(0, nxt, mb, me)) return true;
+                if (n < nxt + 1) return false;
+                c = look;
+                ++nxt;
+            }
+            if (!restart) return false;
+        }
+    }
+};
+
+// a printed start process_output drops: a header line's byte, the '\n'
+// that ends a header line, or -1 (a match reaching the file's first byte)
+__device__ inline bool ee_dropped(const TextView& tv, int64_t p) {
+    if (p < 0) return true;
+    if (xt_header(tv, (uint64_t)p)) return true;
+    return p > 0 && xt_brk(tv, (uint64_t)p) && xt_byte(tv, (uint64_t)p) == (uint8_t)'\n' &&
+           xt_header(tv, (uint64_t)p - 1);
+}
+
+// at least two '\n' in (a, b), looking back from b at most `cap` positions
+// (false when fewer were found there)
+__device__ inline bool ee_two_nl_between(const TextView& tv, uint64_t a, uint64_t b, uint64_t cap) {
+    const uint64_t lo = b - a > cap ? b - cap : a + 1;
+    int seen = 0;
+    for (uint64_t p = b; p > lo;) {
+        --p;
+        const bool nl = tv.nuc_layout ? (((tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31)) & 1) && xt_byte(tv, p) == '\n')
+                                      : tv.raw[p] == (uint8_t)'\n';
+        if (nl && ++seen == 2) return true;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(EE_T) void k_ee_heads(XtPrep X, const uint64_t* __restrict__ keys,
+                                                   const uint64_t* total_d, uint64_t total_h,
+                                                   uint8_t* __restrict__ acc, TextView tv) {
+    const uint64_t total = total_d ? *total_d : total_h;
+    const EeSlot& S = *X.ee;
+    for (uint64_t i = blockIdx.x * (uint64_t)EE_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * EE_T) {
+        bool head = i == 0 || (keys[i] >> 48) != (keys[i - 1] >> 48);
+        if (!head) {
+            const uint64_t a = keys[i - 1] & EE_POS_MASK, b = keys[i] & EE_POS_MASK;
+            if (xt_region(tv, a) != xt_region(tv, b)) head = true;
+            else if (S.max_len >= 0) head = b - a > 2 * (uint64_t)S.max_len + 2 * (uint64_t)S.k + 8;
+            // unbounded, the window scanner (candidate p + 1 for a window at p
+            // >= R): a line's first candidate depends on whether the line
+            // before printed a match ending past its '\n', so lines with
+            // starts chain; every other scanner: lines are independent
+            else if (S.type == 2 && !S.simple) head = ee_two_nl_between(tv, a, b, EE_SCAN);
+            else head = xt_brk_between(tv, a, b, EE_SCAN);
+        }
+        acc[i] = head ? 2 : 0;
+    }
+}
+
+template <int WB>
+__global__ __launch_bounds__(EE_T) void k_ee_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                  const uint64_t* total_d, uint64_t total_h,
+                                                  uint8_t* __restrict__ acc, TextView tv) {
+    const uint64_t total = total_d ? *total_d : total_h;
+    const EeSlot* S = X.ee;
+    for (uint64_t i = blockIdx.x * (uint64_t)EE_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * EE_T) {
+        if (!(acc[i] & 2)) continue;
+        uint64_t j = i + 1;
+        while (j < total && !(acc[j] & 2)) ++j;
+        const uint64_t pid = keys[i] >> 48;
+        const int64_t first = (int64_t)(keys[i] & EE_POS_MASK), last = (int64_t)(keys[j - 1] & EE_POS_MASK);
+        uint64_t nout = 0;
+        const uint64_t nmax = j - i;
+        if ((int64_t)pid == X.pid) {
+            int64_t R0 = 0, n = (int64_t)tv.n;
+            if (tv.reg.n > 1) {
+                const uint32_t r = region_of(tv.reg, (uint64_t)first);
+                R0 = (int64_t)tv.reg.t[r];
+                n = (int64_t)tv.reg.e[r];
+            }
+            EeWalk w{S, X.tab, tv, n, R0, -1, n};
+            int64_t stop;
+            if (S->max_len >= 0) {
+                const int64_t back = S->max_len + S->k + 4;
+                if (first > R0 + back) w.R = first - back;
+                stop = last + S->max_len;
+            } else {
+                int64_t p = first;
+                while (p > R0 && !w.is_nl(p - 1)) --p;
+                // the line before holds no start: nrgrep's R is before the
+                // '\n' (the window at p - 1 hands p to checkMatch)
+                w.R = S->type == 2 && !S->simple && p > R0 ? p - 1 : p;
+                stop = w.next_nl(last);
+            }
+            w.nl_hi = w.next_nl(w.R);
+            for (;;) {
+                int64_t mb = 0, me = 0;
+                if (!w.template scan<WB>(stop, mb, me)) break;
+                if (!ee_dropped(tv, mb) && nout < nmax) {
+                    keys[i + nout] = (pid << 48) | (uint64_t)mb;
+                    lens[i + nout] = (uint32_t)(me - mb);
+                    acc[i + nout] = (nout == 0 ? 2 : 0) | 1;
+                    ++nout;
+                }
+                if (me >= n) break;                      // 0x4022eb
+                w.R = me;
+            }
+        }
+        for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
+    }
+}
+
+__global__ void k_ee_put_headers(uint64_t* __restrict__ dst, const uint64_t* __restrict__ hdr, uint64_t n,
+                                 uint64_t tag) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = tag | hdr[i];
+}
+
+}  // namespace
+
+uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
+    if (!db->nhdr) return total;
+    hipStream_t s = db->stream;
+    const uint64_t n2 = total + db->nhdr;
+    require(n2 < (1ull << 31), "eextended: too many starts");
+    size_t kc = 0, lc = 0, tc = 0, sc = 0;
+    uint64_t* keys = static_cast<uint64_t*>(pool_get(db->device, n2 * 8, &kc));
+    uint32_t* lens = static_cast<uint32_t*>(pool_get(db->device, n2 * 4, &lc));
+    uint64_t* tmp = static_cast<uint64_t*>(pool_get(db->device, n2 * 8, &tc));
+    if (total) HIPCHK(hipMemcpyAsync(tmp, h->keys, total * 8, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_ee_put_headers, dim3(blocks_for(db->nhdr, 256)), dim3(256), 0, s, tmp + total, db->hdr,
+                       db->nhdr, (uint64_t)pid << 48);
+    HIPCHK(hipGetLastError());
+    size_t sort_bytes = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, tmp, keys, (int)n2, 0, 64, s));
+    void* ws = pool_get(db->device, std::max<size_t>(sort_bytes, 8), &sc);
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(ws, sort_bytes, tmp, keys, (int)n2, 0, 64, s));
+    HIPCHK(hipStreamSynchronize(s));
+    pool_put(db->device, h->keys, h->keys_cap);
+    pool_put(db->device, h->lens, h->lens_cap);
+    h->keys = keys;
+    h->lens = lens;
+    h->keys_cap = kc;
+    h->lens_cap = lc;
+    pool_put(db->device, tmp, tc);
+    pool_put(db->device, ws, sc);
+    return n2;
+}
+
+void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, const TextView& tv, int words, hipStream_t s) {
+    const uint32_t blocks = 1024;
+    hipLaunchKernelGGL(k_ee_heads, dim3(blocks), dim3(EE_T), 0, s, X, keys, total_d, total_h, acc, tv);
+    if (words <= 1) hipLaunchKernelGGL(k_ee_walk<1>, dim3(blocks), dim3(EE_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    else hipLaunchKernelGGL(k_ee_walk<4>, dim3(blocks), dim3(EE_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" int pm_eextended_plan(int m, int words, const uint64_t* byte_mask, const uint64_t* opt_mask,
+                                 const uint64_t* rep_mask, int k, int32_t* out) {
+    return guarded([&] {
+        require(byte_mask != nullptr && opt_mask != nullptr && rep_mask != nullptr && out != nullptr, "null argument");
+        require(words >= 1 && words <= 4 && m >= 1 && m <= 64 * words, "m / words out of range");
+        require(k >= 1 && k <= PM_MAX_K, "k out of range");
+        const EePlan P = ee_plan(byte_mask, words, m, opt_mask, rep_mask, k);
+        out[0] = P.type;
+        out[1] = P.simple;
+        out[2] = P.np;
+        out[3] = P.type == 1 ? P.plen : P.fwd;
+        out[4] = P.wbeg;
+        out[5] = P.wend;
+        for (int i = 0; i < P.np; ++i) {
+            out[6 + 2 * i] = P.off[i];
+            out[7 + 2 * i] = P.pend[i];
+        }
+    });
+}

@@ -49,11 +49,13 @@ namespace {
 inline bool has_bit(const uint64_t* w, int i) { return (w[i >> 6] >> (i & 63)) & 1; }
 inline void set_bit(uint64_t* w, int i) { w[i >> 6] |= 1ull << (i & 63); }
 
-// extendedFindBest 0x411fe0 with K = 0 (extendedPreproc passes r8d = 0):
-// prob / aprob per position, P1 / P2 over [m + 1][m][m + 1]
-void find_best_ext(const std::vector<double>& prob, const std::vector<double>& aprob, const uint64_t* opt, int m,
-                   int* fwd, int* beg, int* end) {
-    const int K = 0;
+}  // namespace
+
+// extendedFindBest 0x411fe0 (K = 0 from extendedPreproc, K = k from
+// eextendedPreproc 0x40ff33): prob / aprob per position, P1 / P2 over
+// [m + 1][m][m + 1]; returns the window's cost (1.0 for the prefix)
+double find_best_ext(const std::vector<double>& prob, const std::vector<double>& aprob, const uint64_t* opt, int m,
+                     int K, int* fwd, int* beg, int* end) {
     // the binary's third index runs to m; t never exceeds a window's 64
     // non-optional positions, so 65 slots hold the same values
     const size_t T1 = (size_t)std::min(m, 64) + 1, MM = (size_t)m * T1;
@@ -125,16 +127,14 @@ void find_best_ext(const std::vector<double>& prob, const std::vector<double>& a
         while (*beg < *end && has_bit(opt, *beg)) ++*beg;
         while (*beg < *end && has_bit(opt, *end - 1)) --*end;
         if (*beg == *end) *fwd = 0;
+        else return best;
     }
-    if (*fwd == 0) {                                     // 0x4128d4: the prefix
-        *end = m <= 64 ? m : 64;
-        while (*end > 0 && has_bit(opt, *end - 1)) --*end;
-    }
+    *end = m <= 64 ? m : 64;                             // 0x4128d4: the prefix
+    while (*end > 0 && has_bit(opt, *end - 1)) --*end;
+    return 1.0;
 }
 
 #pragma clang fp contract(on)
-
-}  // namespace
 
 XtPlan xt_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep) {
     require(W >= 1 && W <= 4 && m >= 1 && m <= 64 * W, "extended plan: m / words out of range");
@@ -150,7 +150,7 @@ XtPlan xt_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint6
                 if (has_bit(rep, i)) aprob[i] += lp[c];
             }
     XtPlan P{};
-    find_best_ext(prob, aprob, opt, m, &P.fwd, &P.beg, &P.end);
+    find_best_ext(prob, aprob, opt, m, 0, &P.fwd, &P.beg, &P.end);
     P.type = P.fwd ? 2 : 3;                              // 0x41336b
     P.L = P.fwd ? P.beg : P.end;
     P.simple = 1;                                        // 0x413485: detClass over the window
@@ -263,56 +263,6 @@ namespace {
 constexpr uint64_t XT_POS_MASK = (1ull << 48) - 1;
 constexpr uint64_t XT_SCAN = 1ull << 16;   // unbounded patterns: how far a head looks back for a line break
 constexpr uint32_t XT_T = 256;
-
-__device__ inline uint8_t xt_fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
-
-// the file's own byte at p (headers and '\n' included), folded
-__device__ inline uint8_t xt_byte(const TextView& tv, uint64_t p) {
-    if (tv.nuc_layout) {
-        const uint4 v = tv.nuc.lin[p >> 5];
-        const uint32_t i = (uint32_t)(p & 31);
-        if (((v.z | v.w) >> i) & 1) return xt_fold(nuc_raw_at(tv.nuc, p));
-        return (uint8_t)((0x54474341u >> (8 * ((((v.x >> i) & 1) << 1) | ((v.y >> i) & 1)))) & 0xff);
-    }
-    return xt_fold(tv.raw[p]);
-}
-
-// a line break or header byte at p (the breaks of the line-bounded scans)
-__device__ inline bool xt_brk(const TextView& tv, uint64_t p) {
-    if (tv.nuc_layout) return (tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31)) & 1;
-    return tv.bytes[p] == (uint8_t)'\n';
-}
-
-// the start of a header line (process_output drops such matches)
-__device__ inline bool xt_header(const TextView& tv, uint64_t p) {
-    if (tv.nuc_layout) return nuc_is_header(tv.nuc, p);
-    return tv.bytes[p] == (uint8_t)'\n' && tv.raw[p] != (uint8_t)'\n';
-}
-
-// a break in (a, b): a and b are starts of matches (sequence positions), so
-// a header byte in between implies the '\n' before its line.  Looks back
-// from b at most `cap` positions; false when none was found there.
-__device__ inline bool xt_brk_between(const TextView& tv, uint64_t a, uint64_t b, uint64_t cap) {
-    const uint64_t lo = b - a > cap ? b - cap : a + 1;
-    if (lo + 1 > b) return false;   // nothing between
-    if (tv.nuc_layout) {
-        for (uint64_t w = (b - 1) >> 5;; --w) {
-            uint32_t z = tv.nuc.lin[w].z;
-            const uint64_t w0 = w << 5;
-            if (w0 + 31 > b - 1) z &= (2u << (uint32_t)((b - 1) - w0)) - 1u;   // positions <= b - 1
-            if (w0 < lo) z &= ~((1u << (uint32_t)(lo - w0)) - 1u);            // positions >= lo
-            if (z) return true;
-            if (w0 <= lo) return false;
-        }
-    }
-    for (uint64_t p = b - 1; p >= lo; --p) {
-        if (tv.bytes[p] == (uint8_t)'\n') return true;
-        if (p == lo) break;
-    }
-    return false;
-}
-
-__device__ inline uint32_t xt_region(const TextView& tv, uint64_t p) { return tv.reg.n > 1 ? region_of(tv.reg, p) : 0u; }
 
 __global__ __launch_bounds__(XT_T) void k_xt_heads(XtPrep X, const uint64_t* __restrict__ keys, const uint64_t* total_d,
                                                    uint64_t total_h, uint8_t* __restrict__ acc, TextView tv) {
@@ -630,8 +580,12 @@ __global__ __launch_bounds__(256) void k_xt_count(const uint64_t* total_d, uint6
 void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
-    hipLaunchKernelGGL(k_xt_heads, dim3(blocks), dim3(XT_T), 0, s, X, keys, total_d, total_h, acc, tv);
-    hipLaunchKernelGGL(k_xt_walk<4>, dim3(blocks), dim3(XT_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    if (X.ee) {
+        ee_launch(X, keys, lens, total_d, total_h, acc, tv, X.words, s);
+    } else {
+        hipLaunchKernelGGL(k_xt_heads, dim3(blocks), dim3(XT_T), 0, s, X, keys, total_d, total_h, acc, tv);
+        hipLaunchKernelGGL(k_xt_walk<4>, dim3(blocks), dim3(XT_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    }
     hipLaunchKernelGGL(k_xt_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);
     HIPCHK(hipGetLastError());
 }

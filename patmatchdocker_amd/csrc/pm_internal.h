@@ -364,6 +364,10 @@ struct pm_db : pm_lane {
     uint32_t *reg_lut = nullptr, *reg_near = nullptr;
     uint32_t nreg = 0;
     bool reg_blind = false;   // some region ends without a '\n' (a buffer holding none)
+    // the first position of every header line (/^>\S/, sorted): the
+    // eextended walk starts a cluster at each (pm_eextended.hip)
+    uint64_t* hdr = nullptr;
+    uint64_t nhdr = 0;
 };
 
 // A pipelined scan (pm_scan_linear_async) between launch and resolution: the
@@ -682,6 +686,59 @@ struct TextView {
     Regions reg;
 };
 TextView text_view(const pm_db* db);
+
+// the file's own text as nrgrep's extended walks read it (pm_extended.hip,
+// pm_eextended.hip)
+__device__ inline uint8_t xt_fold(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// the file's own byte at p (headers and '\n' included), folded
+__device__ inline uint8_t xt_byte(const TextView& tv, uint64_t p) {
+    if (tv.nuc_layout) {
+        const uint4 v = tv.nuc.lin[p >> 5];
+        const uint32_t i = (uint32_t)(p & 31);
+        if (((v.z | v.w) >> i) & 1) return xt_fold(nuc_raw_at(tv.nuc, p));
+        return (uint8_t)((0x54474341u >> (8 * ((((v.x >> i) & 1) << 1) | ((v.y >> i) & 1)))) & 0xff);
+    }
+    return xt_fold(tv.raw[p]);
+}
+
+// a line break or header byte at p (the breaks of the line-bounded scans)
+__device__ inline bool xt_brk(const TextView& tv, uint64_t p) {
+    if (tv.nuc_layout) return (tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31)) & 1;
+    return tv.bytes[p] == (uint8_t)'\n';
+}
+
+// the start of a header line (process_output drops such matches)
+__device__ inline bool xt_header(const TextView& tv, uint64_t p) {
+    if (tv.nuc_layout) return nuc_is_header(tv.nuc, p);
+    return tv.bytes[p] == (uint8_t)'\n' && tv.raw[p] != (uint8_t)'\n';
+}
+
+// a break in (a, b): a and b are starts of matches (sequence positions), so
+// a header byte in between implies the '\n' before its line.  Looks back
+// from b at most `cap` positions; false when none was found there.
+__device__ inline bool xt_brk_between(const TextView& tv, uint64_t a, uint64_t b, uint64_t cap) {
+    const uint64_t lo = b - a > cap ? b - cap : a + 1;
+    if (lo + 1 > b) return false;   // nothing between
+    if (tv.nuc_layout) {
+        for (uint64_t w = (b - 1) >> 5;; --w) {
+            uint32_t z = tv.nuc.lin[w].z;
+            const uint64_t w0 = w << 5;
+            if (w0 + 31 > b - 1) z &= (2u << (uint32_t)((b - 1) - w0)) - 1u;   // positions <= b - 1
+            if (w0 < lo) z &= ~((1u << (uint32_t)(lo - w0)) - 1u);            // positions >= lo
+            if (z) return true;
+            if (w0 <= lo) return false;
+        }
+    }
+    for (uint64_t p = b - 1; p >= lo; --p) {
+        if (tv.bytes[p] == (uint8_t)'\n') return true;
+        if (p == lo) break;
+    }
+    return false;
+}
+
+__device__ inline uint32_t xt_region(const TextView& tv, uint64_t p) { return tv.reg.n > 1 ? region_of(tv.reg, p) : 0u; }
+
 // true when the pass changes anything for `flags` (cross: candidates may
 // start on header lines)
 bool report_needed(const pm_db* db, uint32_t flags, bool cross);
@@ -809,11 +866,51 @@ struct XtSlot {                // one pattern (device, uploaded as is)
     uint64_t vI[2][4], vF[2][4], vS[2][4], vX[2][4];
     uint64_t o_T, o_TA, o_vB[2], o_vA[2];   // word offsets of [256] / [256][pw] tables in the blob
 };
+// nrgrep's extended engine with errors (eextended, k > 0): the plan of
+// eextendedPreproc 0x40fe30 and one verify part of checkMatch1 0x40e340
+struct EePlan {
+    int type = 0;              // 1: k + 1 pieces, 2: a window backward, 3: the prefix forward
+    int simple = 0;            // no '?*+' in the scanned positions: esimpleScan's loops
+    int np = 1;                // pieces (k + 1 for type 1)
+    int plen = 0;              // the pieces' length in characters (type 1)
+    int fwd = 0, wbeg = 0, wend = 0;   // extendedFindBest's window (K = k)
+    int off[PM_MAX_K + 1] = {}, pend[PM_MAX_K + 1] = {};   // pieces [off, pend) / the window
+    int L[PM_MAX_K + 1] = {};  // pattern positions left of each piece's candidate
+};
+double find_best_ext(const std::vector<double>& prob, const std::vector<double>& aprob, const uint64_t* opt, int m,
+                     int K, int* fwd, int* beg, int* end);
+EePlan ee_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k);
+
+struct EePart {                // extendedLoadVerif 0x412c60: len positions, [256][pw] tables
+    int32_t len, pw;
+    uint64_t I[4], F[4], S[4], X[4];
+    uint64_t o_B, o_A;
+};
+struct EeSlot {                // one pattern (device, uploaded as is)
+    int32_t m, k, errs, type, simple, np, plen, flen, fspan, wbeg, wend, anchors, pid;
+    int64_t max_len;           // the longest alignment (insertions included), -1: unbounded
+    uint64_t fI, fF, fS;       // scanner: optional-block masks
+    uint64_t top[PM_MAX_K + 1];   // type 1 (extended): each piece's top bit
+    uint64_t o_T, o_TA, o_T2;  // [256] scanner tables in the blob
+    EePart lv[PM_MAX_K + 1], rv[PM_MAX_K + 1];
+};
+void ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
+              int64_t max_len, uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab);
+
 struct XtPrep {
     const XtSlot* slot = nullptr;
+    const EeSlot* ee = nullptr;   // k > 0: the eextended walk instead
     const uint64_t* tab = nullptr;
     int32_t pid = 0;
+    int32_t words = 1;            // eextended: the verify parts' widest word count
 };
+// eextended heads + walk on s (keys/lens rewritten in place, acc bit 0 =
+// reported); xt_launch calls it when X.ee is set
+// appends pid << 48 | each header line start to the sorted start list of h
+// (total entries) and sorts it again; returns the new length
+uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
+void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, const TextView& tv, int words, hipStream_t s);
 // builds the plan and tables of one pattern into `up`; returns the slot's
 // and the table blob's offsets
 void xt_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int64_t max_len,

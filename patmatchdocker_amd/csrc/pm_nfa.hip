@@ -515,9 +515,10 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // PM_ESIMPLE: a class sequence at k > 0 reported as nrgrep's esimple
     // engine does (pm_esimple.hip); its walk computes the ends itself
     const bool esimple = (flags & PM_ESIMPLE) && k > 0 && (flags & PM_REPORT_NRGREP);
-    // PM_EXTENDED: an extended pattern at k = 0 reported as nrgrep's
-    // extended engine does (pm_extended.hip); its walk computes the ends
-    const bool extended = (flags & PM_EXTENDED) && k == 0 && (flags & PM_REPORT_NRGREP);
+    // PM_EXTENDED: an extended pattern reported as nrgrep's extended engine
+    // (k = 0, pm_extended.hip) or eextended engine (k > 0, pm_eextended.hip)
+    // does; its walk computes the ends
+    const bool extended = (flags & PM_EXTENDED) && (flags & PM_REPORT_NRGREP);
     uint64_t xopt[4] = {}, xrep[4] = {};
     require(!(flags & PM_EXTENDED) || extended_shape(m, W, first, last, follow, xopt, xrep),
             "PM_EXTENDED needs a sequence of classes with '?', '*', '+'");
@@ -595,16 +596,21 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         es_upload(esb, up, esu);
     }
     size_t o_xslot = 0, o_xtab = 0;
-    if (extended)
+    if (extended && k == 0)
         xt_build(byte_mask, W, m, xopt, xrep, max_len == 0 ? -1 : (int64_t)max_len, (uint32_t)flags, pattern_id, up,
                  o_xslot, o_xtab);
+    else if (extended)
+        ee_build(byte_mask, W, m, xopt, xrep, k, errs, unbounded ? -1 : (int64_t)max_len + ((errs & PM_ERR_INS) ? k : 0),
+                 (uint32_t)flags, pattern_id, up, o_xslot, o_xtab);
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     XtPrep xtp;
     if (extended) {
-        xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
+        if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
+        else xtp.ee = reinterpret_cast<const EeSlot*>(d_up + o_xslot);
         xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
         xtp.pid = pattern_id;
+        xtp.words = W;
     }
     esp.lines = all_pos ? 1 : 0;
 
@@ -720,6 +726,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     double kms = all_pos ? 0.0 : ev.ms() + carry_ms;
     if (all_pos) total = db->n;
     pm_hits* h = all_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
+    // eextended: an alignment starting a header line prints one position
+    // before it (pm_eextended.hip): every header line starts a cluster
+    if (extended && k > 0) total = ee_add_headers(db, h, total, pattern_id);
     if (total && !esimple && !extended) {
         a.starts = h->keys;
         a.nstarts = total;

@@ -365,6 +365,25 @@ def extended_plan(prog: Program) -> dict:
     return {"type": out[0], "fwd": out[1], "window": (out[2], out[3]), "L": out[4], "simple": bool(out[5])}
 
 
+def eextended_plan(prog: Program, k: int) -> dict:
+    """The scan plan nrgrep's eextendedPreproc derives for an extended
+    pattern at ``k`` > 0 errors (pm_eextended_plan, host only): ``type`` 1 =
+    k + 1 ``pieces`` of ``plen`` characters searched exactly, 2 = a window
+    backward, 3 = the prefix forward (``pieces`` then holds it); ``simple``
+    = the scanned positions hold no '?*+' (nrgrep's esimple scanners);
+    ``window`` = extendedFindBest's, ``fwd`` its non-optional positions."""
+    w = nfa_words(prog.m)
+    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
+    opt = np.array(_words(prog.opt_mask, w), dtype=np.uint64)
+    rep = np.array(_words(prog.rep_mask, w), dtype=np.uint64)
+    out = (ctypes.c_int32 * (6 + 2 * (_lib.PM_MAX_K + 1)))()
+    check(_lib.load().pm_eextended_plan(prog.m, w, bm.ctypes.data, opt.ctypes.data, rep.ctypes.data, k, out))
+    np_ = out[2]
+    return {"type": out[0], "simple": bool(out[1]), "plen": out[3] if out[0] == 1 else 0,
+            "fwd": out[3] if out[0] != 1 else 0, "window": (out[4], out[5]),
+            "pieces": [(out[6 + 2 * i], out[7 + 2 * i]) for i in range(np_)]}
+
+
 def kernel_ms(handle) -> float:
     ms = ctypes.c_double()
     check(_lib.load().pm_hits_kernel_ms(handle, ctypes.byref(ms)))
@@ -414,8 +433,8 @@ def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0,
         flags |= _lib.PM_CROSS_LINES
     if k > 0 and prog.linear and prog.kind == "simple":
         flags |= _lib.PM_ESIMPLE   # nrgrep's esimple engine decides the report
-    if k == 0 and prog.kind == "extended":
-        flags |= _lib.PM_EXTENDED  # nrgrep's extended engine decides the report
+    if prog.kind == "extended":
+        flags |= _lib.PM_EXTENDED  # nrgrep's extended / eextended engine decides the report
     out = ctypes.c_void_p()
     check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                        last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,

@@ -51,6 +51,11 @@ QUERIES = [
     ("TTN{0,3}NNNAA", "dna", None, None, None, None, None, 500),
     ("N{0,3}GAATTCN{0,3}", "dna", None, None, None, None, None, 500),
     ("CX{1,3}CX{2}C", "pep", None, None, None, None, None, 500),
+    # ranges at k > 0: nrgrep's eextended engine (configs[3] at -k 1ids)
+    ("CX{2,4}CX{3}[LIVMFYWC]", "pep", None, None, None, None, "1", 500),
+    ("GAN{2,3}TC", "dna", None, None, None, None, "1", 300),
+    ("AN{0,3}GAATTC", "dna", "Both strands", None, None, "substitution", "2", 300),
+    ("CX{1,3}CK", "pep", None, "insertion", "deletion", None, "2", 300),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]

@@ -211,7 +211,7 @@ EePlan ee_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint6
     return P;
 }
 
-void ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
+bool ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
               int64_t max_len, uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab) {
     const EePlan P = ee_plan(B, W, m, opt, rep, k);
     auto cls = [&](int c, int p) { return ((B[(size_t)fold((uint8_t)c) * W + (p >> 6)] >> (p & 63)) & 1) != 0; };
@@ -348,8 +348,16 @@ void ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64
                 else sb(V.X, r);
             }
         }
+    // checkMatch1 carries 1 into every word after the first of its
+    // substitution term (0x40eb7d): a part over 64 positions then never
+    // dies at a level above 0 and reads to its record's end, so a print is
+    // no longer bounded by an alignment -- every line is walked
+    for (int q = 0; q < P.np; ++q)
+        if ((S.lv[q].pw > 1 || S.rv[q].pw > 1) && (errs & PM_ERR_SUB)) S.lines = 1;
+    if (S.lines) S.max_len = -1;
     o_slot = up.add(&S, sizeof(S));
     o_tab = up.add(tab.data(), tab.size() * 8);
+    return S.lines != 0;
 }
 
 #pragma clang fp contract(on)
@@ -1014,19 +1022,19 @@ __global__ void k_ee_put_headers(uint64_t* __restrict__ dst, const uint64_t* __r
 
 }  // namespace
 
-uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
-    if (!db->nhdr) return total;
+namespace {
+
+// merges `extra` (already tagged, device) into h's sorted start list
+uint64_t ee_merge(pm_db* db, pm_hits* h, uint64_t total, const uint64_t* extra, uint64_t nextra) {
     hipStream_t s = db->stream;
-    const uint64_t n2 = total + db->nhdr;
+    const uint64_t n2 = total + nextra;
     require(n2 < (1ull << 31), "eextended: too many starts");
     size_t kc = 0, lc = 0, tc = 0, sc = 0;
     uint64_t* keys = static_cast<uint64_t*>(pool_get(db->device, n2 * 8, &kc));
     uint32_t* lens = static_cast<uint32_t*>(pool_get(db->device, n2 * 4, &lc));
     uint64_t* tmp = static_cast<uint64_t*>(pool_get(db->device, n2 * 8, &tc));
     if (total) HIPCHK(hipMemcpyAsync(tmp, h->keys, total * 8, hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL(k_ee_put_headers, dim3(blocks_for(db->nhdr, 256)), dim3(256), 0, s, tmp + total, db->hdr,
-                       db->nhdr, (uint64_t)pid << 48);
-    HIPCHK(hipGetLastError());
+    if (nextra) HIPCHK(hipMemcpyAsync(tmp + total, extra, nextra * 8, hipMemcpyDeviceToDevice, s));
     size_t sort_bytes = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, tmp, keys, (int)n2, 0, 64, s));
     void* ws = pool_get(db->device, std::max<size_t>(sort_bytes, 8), &sc);
@@ -1040,6 +1048,67 @@ uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
     h->lens_cap = lc;
     pool_put(db->device, tmp, tc);
     pool_put(db->device, ws, sc);
+    return n2;
+}
+
+// a line starts at p: the file start or a '\n' (not a header byte) before it
+struct EeLineStart {
+    TextView tv;
+    __device__ bool operator()(uint64_t p) const {
+        if (p == 0) return true;
+        const uint64_t q = p - 1;
+        if (tv.nuc_layout) return ((tv.nuc.lin[q >> 5].z >> (uint32_t)(q & 31)) & 1) && xt_byte(tv, q) == '\n';
+        return tv.raw[q] == (uint8_t)'\n';
+    }
+};
+
+__global__ void k_ee_tag(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, uint64_t n, uint64_t tag) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = tag | src[i];
+}
+
+}  // namespace
+
+uint64_t ee_add_lines(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
+    hipStream_t s = db->stream;
+    const TextView tv = text_view(db);
+    require(db->n < (1ull << 31), "eextended: a part over 64 positions with substitutions walks every line; "
+                                  "the file is too large", PM_E_UNSUPPORTED);
+    const int n = (int)db->n;
+    size_t pc = 0, cc = 0, sc = 0;
+    uint64_t* pos = static_cast<uint64_t*>(pool_get(db->device, (db->n + db->nreg + 1) * 8, &pc));
+    uint64_t* cnt = static_cast<uint64_t*>(pool_get(db->device, 8, &cc));
+    size_t sel_bytes = 0;
+    hipcub::CountingInputIterator<uint64_t> it(0);
+    HIPCHK(hipcub::DeviceSelect::If(nullptr, sel_bytes, it, pos, cnt, n, EeLineStart{tv}, s));
+    void* ws = pool_get(db->device, std::max<size_t>(sel_bytes, 8), &sc);
+    HIPCHK(hipcub::DeviceSelect::If(ws, sel_bytes, it, pos, cnt, n, EeLineStart{tv}, s));
+    uint64_t nl = 0;
+    HIPCHK(hipMemcpyAsync(&nl, cnt, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (db->nreg) HIPCHK(hipMemcpyAsync(pos + nl, db->reg_t, (size_t)db->nreg * 8, hipMemcpyDeviceToDevice, s));
+    const uint64_t ne = nl + db->nreg;
+    if (ne) {
+        hipLaunchKernelGGL(k_ee_tag, dim3(blocks_for(ne, 256)), dim3(256), 0, s, pos, pos, ne, (uint64_t)pid << 48);
+        HIPCHK(hipGetLastError());
+    }
+    const uint64_t n2 = ee_merge(db, h, total, pos, ne);
+    pool_put(db->device, pos, pc);
+    pool_put(db->device, cnt, cc);
+    pool_put(db->device, ws, sc);
+    return n2;
+}
+
+uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
+    if (!db->nhdr) return total;
+    hipStream_t s = db->stream;
+    size_t tc = 0;
+    uint64_t* tagged = static_cast<uint64_t*>(pool_get(db->device, db->nhdr * 8, &tc));
+    hipLaunchKernelGGL(k_ee_put_headers, dim3(blocks_for(db->nhdr, 256)), dim3(256), 0, s, tagged, db->hdr,
+                       db->nhdr, (uint64_t)pid << 48);
+    HIPCHK(hipGetLastError());
+    const uint64_t n2 = ee_merge(db, h, total, tagged, db->nhdr);
+    pool_put(db->device, tagged, tc);
     return n2;
 }
 

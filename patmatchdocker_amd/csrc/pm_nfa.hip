@@ -599,9 +599,11 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (extended && k == 0)
         xt_build(byte_mask, W, m, xopt, xrep, max_len == 0 ? -1 : (int64_t)max_len, (uint32_t)flags, pattern_id, up,
                  o_xslot, o_xtab);
-    else if (extended)
-        ee_build(byte_mask, W, m, xopt, xrep, k, errs, unbounded ? -1 : (int64_t)max_len + ((errs & PM_ERR_INS) ? k : 0),
-                 (uint32_t)flags, pattern_id, up, o_xslot, o_xtab);
+    bool ee_lines = false;
+    if (extended && k > 0)
+        ee_lines = ee_build(byte_mask, W, m, xopt, xrep, k, errs,
+                            unbounded ? -1 : (int64_t)max_len + ((errs & PM_ERR_INS) ? k : 0), (uint32_t)flags,
+                            pattern_id, up, o_xslot, o_xtab);
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     XtPrep xtp;
@@ -728,7 +730,8 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     pm_hits* h = all_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
     // eextended: an alignment starting a header line prints one position
     // before it (pm_eextended.hip): every header line starts a cluster
-    if (extended && k > 0) total = ee_add_headers(db, h, total, pattern_id);
+    if (extended && k > 0)
+        total = ee_lines ? ee_add_lines(db, h, total, pattern_id) : ee_add_headers(db, h, total, pattern_id);
     if (total && !esimple && !extended) {
         a.starts = h->keys;
         a.nstarts = total;

@@ -212,7 +212,8 @@ EePlan ee_plan(const uint64_t* B, int W, int m, const uint64_t* opt, const uint6
 }
 
 bool ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
-              int64_t max_len, uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab) {
+              int64_t max_len, uint32_t flags, int32_t pid, bool all_lines, Upload& up, size_t& o_slot,
+              size_t& o_tab) {
     const EePlan P = ee_plan(B, W, m, opt, rep, k);
     auto cls = [&](int c, int p) { return ((B[(size_t)fold((uint8_t)c) * W + (p >> 6)] >> (p & 63)) & 1) != 0; };
     auto rp = [&](int c, int p) { return hb(rep, p) && cls(c, p); };
@@ -354,6 +355,8 @@ bool ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64
     // no longer bounded by an alignment -- every line is walked
     for (int q = 0; q < P.np; ++q)
         if ((S.lv[q].pw > 1 || S.rv[q].pw > 1) && (errs & PM_ERR_SUB)) S.lines = 1;
+    // deletions reaching the shortest match: empty alignments anywhere
+    if (all_lines) S.lines = 1;
     if (S.lines) S.max_len = -1;
     o_slot = up.add(&S, sizeof(S));
     o_tab = up.add(tab.data(), tab.size() * 8);
@@ -925,6 +928,14 @@ __device__ inline bool ee_dropped(const TextView& tv, int64_t p) {
            xt_header(tv, (uint64_t)p - 1);
 }
 
+// a '\n' (not a header byte) right before p
+__device__ inline bool ee_nl_before(const TextView& tv, uint64_t p) {
+    if (p == 0) return false;
+    const uint64_t q = p - 1;
+    if (tv.nuc_layout) return ((tv.nuc.lin[q >> 5].z >> (uint32_t)(q & 31)) & 1) && xt_byte(tv, q) == '\n';
+    return tv.raw[q] == (uint8_t)'\n';
+}
+
 // at least two '\n' in (a, b), looking back from b at most `cap` positions
 // (false when fewer were found there)
 __device__ inline bool ee_two_nl_between(const TextView& tv, uint64_t a, uint64_t b, uint64_t cap) {
@@ -949,6 +960,9 @@ __global__ __launch_bounds__(EE_T) void k_ee_heads(XtPrep X, const uint64_t* __r
         if (!head) {
             const uint64_t a = keys[i - 1] & EE_POS_MASK, b = keys[i] & EE_POS_MASK;
             if (xt_region(tv, a) != xt_region(tv, b)) head = true;
+            // every position a key (lines): a line per cluster -- all of a
+            // region for the window scanner, whose lines chain
+            else if (S.lines) head = !(S.type == 2 && !S.simple) && ee_nl_before(tv, b);
             else if (S.max_len >= 0) head = b - a > 2 * (uint64_t)S.max_len + 2 * (uint64_t)S.k + 8;
             // unbounded, the window scanner (candidate p + 1 for a window at p
             // >= R): a line's first candidate depends on whether the line
@@ -994,7 +1008,7 @@ __global__ __launch_bounds__(EE_T) void k_ee_walk(XtPrep X, uint64_t* __restrict
                 // the line before holds no start: nrgrep's R is before the
                 // '\n' (the window at p - 1 hands p to checkMatch)
                 w.R = S->type == 2 && !S->simple && p > R0 ? p - 1 : p;
-                stop = w.next_nl(last);
+                stop = S->lines ? last : w.next_nl(last);
             }
             w.nl_hi = w.next_nl(w.R);
             for (;;) {
@@ -1051,53 +1065,7 @@ uint64_t ee_merge(pm_db* db, pm_hits* h, uint64_t total, const uint64_t* extra, 
     return n2;
 }
 
-// a line starts at p: the file start or a '\n' (not a header byte) before it
-struct EeLineStart {
-    TextView tv;
-    __device__ bool operator()(uint64_t p) const {
-        if (p == 0) return true;
-        const uint64_t q = p - 1;
-        if (tv.nuc_layout) return ((tv.nuc.lin[q >> 5].z >> (uint32_t)(q & 31)) & 1) && xt_byte(tv, q) == '\n';
-        return tv.raw[q] == (uint8_t)'\n';
-    }
-};
-
-__global__ void k_ee_tag(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, uint64_t n, uint64_t tag) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = tag | src[i];
-}
-
 }  // namespace
-
-uint64_t ee_add_lines(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
-    hipStream_t s = db->stream;
-    const TextView tv = text_view(db);
-    require(db->n < (1ull << 31), "eextended: a part over 64 positions with substitutions walks every line; "
-                                  "the file is too large", PM_E_UNSUPPORTED);
-    const int n = (int)db->n;
-    size_t pc = 0, cc = 0, sc = 0;
-    uint64_t* pos = static_cast<uint64_t*>(pool_get(db->device, (db->n + db->nreg + 1) * 8, &pc));
-    uint64_t* cnt = static_cast<uint64_t*>(pool_get(db->device, 8, &cc));
-    size_t sel_bytes = 0;
-    hipcub::CountingInputIterator<uint64_t> it(0);
-    HIPCHK(hipcub::DeviceSelect::If(nullptr, sel_bytes, it, pos, cnt, n, EeLineStart{tv}, s));
-    void* ws = pool_get(db->device, std::max<size_t>(sel_bytes, 8), &sc);
-    HIPCHK(hipcub::DeviceSelect::If(ws, sel_bytes, it, pos, cnt, n, EeLineStart{tv}, s));
-    uint64_t nl = 0;
-    HIPCHK(hipMemcpyAsync(&nl, cnt, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (db->nreg) HIPCHK(hipMemcpyAsync(pos + nl, db->reg_t, (size_t)db->nreg * 8, hipMemcpyDeviceToDevice, s));
-    const uint64_t ne = nl + db->nreg;
-    if (ne) {
-        hipLaunchKernelGGL(k_ee_tag, dim3(blocks_for(ne, 256)), dim3(256), 0, s, pos, pos, ne, (uint64_t)pid << 48);
-        HIPCHK(hipGetLastError());
-    }
-    const uint64_t n2 = ee_merge(db, h, total, pos, ne);
-    pool_put(db->device, pos, pc);
-    pool_put(db->device, cnt, cc);
-    pool_put(db->device, ws, sc);
-    return n2;
-}
 
 uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
     if (!db->nhdr) return total;

@@ -888,7 +888,8 @@ struct EePart {                // extendedLoadVerif 0x412c60: len positions, [25
 };
 struct EeSlot {                // one pattern (device, uploaded as is)
     int32_t m, k, errs, type, simple, np, plen, flen, fspan, wbeg, wend, anchors, pid;
-    int32_t lines;             // every line starts a cluster (a part over 64 positions with substitutions)
+    int32_t lines;             // every position is a key, every line a cluster (es_all_positions): deletions
+                               // reaching the shortest match, or a part over 64 positions with substitutions
     int64_t max_len;           // the longest alignment (insertions included), -1: unbounded or `lines`
     uint64_t fI, fF, fS;       // scanner: optional-block masks
     uint64_t top[PM_MAX_K + 1];   // type 1 (extended): each piece's top bit
@@ -897,7 +898,9 @@ struct EeSlot {                // one pattern (device, uploaded as is)
 };
 // returns EeSlot::lines
 bool ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int k, int errs,
-              int64_t max_len, uint32_t flags, int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab);
+              int64_t max_len, uint32_t flags, int32_t pid, bool all_lines, Upload& up, size_t& o_slot,
+              size_t& o_tab);
+
 
 struct XtPrep {
     const XtSlot* slot = nullptr;
@@ -911,8 +914,7 @@ struct XtPrep {
 // appends pid << 48 | each header line start to the sorted start list of h
 // (total entries) and sorts it again; returns the new length
 uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
-// the same with every line start and every region start (EeSlot::lines)
-uint64_t ee_add_lines(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
+
 void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, const TextView& tv, int words, hipStream_t s);
 // builds the plan and tables of one pattern into `up`; returns the slot's

@@ -527,7 +527,10 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // except for nrgrep's esimple report, whose walk takes every position
     // of every line (es_all_positions; nrgrep then prints empty matches too)
     const bool all_pos = esimple && (errs & PM_ERR_DEL) && min_len <= k;
-    require(!(errs & PM_ERR_DEL) || min_len > k || all_pos,
+    // ... and for nrgrep's eextended report, whose walk then takes every
+    // line (every position a key): the automaton scan is skipped
+    const bool ee_all = extended && k > 0 && (errs & PM_ERR_DEL) && min_len <= k;
+    require(!(errs & PM_ERR_DEL) || min_len > k || all_pos || ee_all,
             "deletions with k >= the shortest match length are not supported by the GPU scan", PM_E_UNSUPPORTED);
     const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
     require((uint64_t)max_len + ins_extra < (1ull << 31), "max_len out of range");
@@ -603,7 +606,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (extended && k > 0)
         ee_lines = ee_build(byte_mask, W, m, xopt, xrep, k, errs,
                             unbounded ? -1 : (int64_t)max_len + ((errs & PM_ERR_INS) ? k : 0), (uint32_t)flags,
-                            pattern_id, up, o_xslot, o_xtab);
+                            pattern_id, ee_all, up, o_xslot, o_xtab);
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     XtPrep xtp;
@@ -700,7 +703,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // a class sequence on the nucleotide planes: the bit-sliced start pass
     // (pm_ids.hip), 32 streams per lane instead of one
     const bool ids = nuc && W == 1 && a.shift_only && !cross && !unbounded && use_ids_kernel(db);
-    for (int attempt = 0; attempt < 2 && !all_pos; ++attempt) {
+    for (int attempt = 0; attempt < 2 && !all_pos && !ee_lines; ++attempt) {
         sb = make_sink(db, 1, db->n, expected);
         a.sink = sb.sink();
         bool launched = false;
@@ -725,13 +728,15 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         require(attempt == 0, "internal: hit bins overflowed twice");
         expected = (uint64_t)(*std::max_element(counts.begin(), counts.end())) * sb.nbins + sb.nbins;
     }
-    double kms = all_pos ? 0.0 : ev.ms() + carry_ms;
-    if (all_pos) total = db->n;
-    pm_hits* h = all_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
+    // eextended walking every line (EeSlot::lines): every position is a key,
+    // the lines are its clusters
+    const bool every_pos = all_pos || ee_lines;
+    double kms = every_pos ? 0.0 : ev.ms() + carry_ms;
+    if (every_pos) total = db->n;
+    pm_hits* h = every_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);
     // eextended: an alignment starting a header line prints one position
     // before it (pm_eextended.hip): every header line starts a cluster
-    if (extended && k > 0)
-        total = ee_lines ? ee_add_lines(db, h, total, pattern_id) : ee_add_headers(db, h, total, pattern_id);
+    if (extended && k > 0 && !ee_lines) total = ee_add_headers(db, h, total, pattern_id);
     if (total && !esimple && !extended) {
         a.starts = h->keys;
         a.nstarts = total;

@@ -96,6 +96,24 @@ def test_three_residue_range_at_k3(engine, oracle_mod):
     _check(engine, oracle_mod, text, progs, 3, "s", alphabet="byte")
 
 
+@pytest.mark.parametrize("alphabet", ["dna", "pep"])
+def test_deletions_reaching_the_shortest_match(engine, oracle_mod, alphabet):
+    """-k <k>ids with k >= the shortest match: empty alignments anywhere, so
+    the walk takes every line (ee_add_lines) instead of refusing."""
+    rng = random.Random(77)
+    text = b"".join(dense_text(rng, alphabet, n_lines=30, width=(10, 120)) for _ in range(2))
+    pats = ["GAN{0,1}TC", "AN{0,2}T"] if alphabet == "dna" else ["CX{0,2}C", "KX{1,2}L"]
+    mode = "-n" if alphabet == "dna" else "-p"
+    progs = [compile_pattern(convert(mode, p)) for p in pats]
+    progs = [p for p in progs if p.kind == "extended"]
+    assert progs
+    layout = "nuc" if alphabet == "dna" else "byte"
+    for prog in progs:
+        k = prog.min_len
+        assert _check(engine, oracle_mod, text, [prog], k, "ids", alphabet=layout) == 1
+        assert _check(engine, oracle_mod, text, [prog], k, "d", alphabet=layout) == 1
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_random_extended_patterns(engine, oracle_mod, seed):
     rng = random.Random(600 + seed)

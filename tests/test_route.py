@@ -33,10 +33,12 @@ def test_refusals_left():
     with pytest.raises(_lib.UnsupportedOnGPU):
         engine.route(prog("ACG"), engine.NUC, 16, "s")
     # every position deletable: class sequences run the esimple walk over
-    # every line (pm_esimple.hip), other patterns are refused
+    # every line (pm_esimple.hip), extended patterns the eextended walk over
+    # every line (pm_eextended.hip); regular patterns are refused
     assert engine.route(prog("ACG"), engine.NUC, 3, "ids") == "nfa"
+    assert engine.route(prog("AC?G"), engine.NUC, 2, "ids") == "nfa"
     with pytest.raises(_lib.UnsupportedOnGPU):
-        engine.route(prog("AC?G"), engine.NUC, 2, "ids")
+        engine.route(prog("A(TC)?G"), engine.NUC, 2, "ids")
 
 
 def test_nfa_words():

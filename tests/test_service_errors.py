@@ -29,8 +29,8 @@ def svc(tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [
-    dict(pattern="AN{0,1}G", seqtype="dna", mismatch="2"),            # -k 2ids: every position deletable
-    dict(pattern="AN{0,1}G", seqtype="dna", mismatch="2", deletion="d"),
+    dict(pattern="A(TC){0,1}G", seqtype="dna", mismatch="2"),         # -k 2ids, a group: every position deletable
+    dict(pattern="A(TC){0,1}G", seqtype="dna", mismatch="2", deletion="d"),
     dict(pattern="A" * 300, seqtype="dna", mismatch="1"),             # 300 automaton positions
     dict(pattern="A" * 40, seqtype="dna", mismatch="16", substitution="s"),   # 16 errors
 ])
@@ -45,3 +45,5 @@ def test_supported_shapes_reach_the_database(svc):
         svc.run_patmatch(FakeRequest(pattern="ACGTAC" * 20, seqtype="dna", mismatch="5"), "t2")   # 120 pos, k=5
     with pytest.raises(AssertionError, match="must not be opened"):   # a class sequence: the esimple walk
         svc.run_patmatch(FakeRequest(pattern="ACG", seqtype="dna", mismatch="3"), "t3")
+    with pytest.raises(AssertionError, match="must not be opened"):   # a range: the eextended walk
+        svc.run_patmatch(FakeRequest(pattern="AN{0,1}G", seqtype="dna", mismatch="2"), "t4")

@@ -654,19 +654,30 @@ void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<ui
         const uint64_t lo = t[r] > REG_NEAR_SPAN ? t[r] - REG_NEAR_SPAN : 0, hi = t[r] + REG_NEAR_SPAN;
         for (uint64_t b = lo >> REG_NEAR_SHIFT; b <= (hi >> REG_NEAR_SHIFT) && b < nblk; ++b) near[b >> 5] |= 1u << (b & 31);
     }
+    // the new tables are built completely before the old ones go: a failed
+    // allocation or copy leaves the database with its previous regions
+    void* nt[4] = {nullptr, nullptr, nullptr, nullptr};
+    try {
+        HIPCHK(hipMalloc(&nt[0], t.size() * 8));
+        HIPCHK(hipMalloc(&nt[1], e.size() * 8));
+        HIPCHK(hipMalloc(&nt[2], nlut * 4));
+        HIPCHK(hipMalloc(&nt[3], near.size() * 4));
+        HIPCHK(hipMemcpy(nt[0], t.data(), t.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(nt[1], e.data(), e.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(nt[2], lut.data(), nlut * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(nt[3], near.data(), near.size() * 4, hipMemcpyHostToDevice));
+    } catch (...) {
+        for (void* p : nt)
+            if (p) (void)hipFree(p);
+        throw;
+    }
     HIPCHK(hipStreamSynchronize(db->stream));   // queued scans may still read the old table
     for (void* p : {(void*)db->reg_t, (void*)db->reg_e, (void*)db->reg_lut, (void*)db->reg_near})
         if (p) HIPCHK(hipFree(p));
-    db->reg_t = db->reg_e = nullptr;
-    db->reg_lut = db->reg_near = nullptr;
-    HIPCHK(hipMalloc(&db->reg_t, t.size() * 8));
-    HIPCHK(hipMalloc(&db->reg_e, e.size() * 8));
-    HIPCHK(hipMalloc(&db->reg_lut, nlut * 4));
-    HIPCHK(hipMalloc(&db->reg_near, near.size() * 4));
-    HIPCHK(hipMemcpy(db->reg_t, t.data(), t.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(db->reg_e, e.data(), e.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(db->reg_lut, lut.data(), nlut * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(db->reg_near, near.data(), near.size() * 4, hipMemcpyHostToDevice));
+    db->reg_t = static_cast<uint64_t*>(nt[0]);
+    db->reg_e = static_cast<uint64_t*>(nt[1]);
+    db->reg_lut = static_cast<uint32_t*>(nt[2]);
+    db->reg_near = static_cast<uint32_t*>(nt[3]);
     db->nreg = (uint32_t)t.size();
     db->reg_blind = false;
     for (size_t r = 0; r + 1 < t.size(); ++r) db->reg_blind |= e[r] != t[r + 1] + 1;
@@ -816,6 +827,7 @@ int pm_db_set_regions(pm_db* db, uint64_t count, const uint64_t* starts, const u
 int pm_db_regions(const pm_db* db, uint64_t cap, uint64_t* starts, uint64_t* ends, uint64_t* count) {
     return guarded([&] {
         require(db != nullptr && count != nullptr && (cap == 0 || (starts && ends)), "null argument");
+        std::lock_guard<std::recursive_mutex> lk(const_cast<pm_db*>(db)->mu);
         *count = db->nreg;
         const uint64_t n = std::min<uint64_t>(cap, db->nreg);
         if (n) {

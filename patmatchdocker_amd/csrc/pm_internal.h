@@ -661,7 +661,10 @@ struct Regions {
 };
 constexpr int REG_LUT_SHIFT = 20;
 constexpr int REG_NEAR_SHIFT = 12;
-constexpr uint64_t REG_NEAR_SPAN = 512;   // > the longest window (PM_MAX_POSITIONS + PM_MAX_K + 1)
+// >= the widest gap inside one esimple cluster (es_gap: 2 (m + k) + 2), so a
+// cluster never straddles a region start unseen
+constexpr uint64_t REG_NEAR_SPAN = 1024;
+static_assert(REG_NEAR_SPAN >= 2 * (PM_MAX_POSITIONS + PM_MAX_K) + 2, "REG_NEAR_SPAN below the esimple gap");
 __device__ inline uint32_t region_of(const Regions& g, uint64_t s) {
     uint32_t r = g.lut[s >> REG_LUT_SHIFT];
     while (r + 1 < g.n && g.t[r + 1] <= s) ++r;

@@ -201,6 +201,10 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
         from . import shards
         device = int(os.environ.get("LOCAL_RANK", "0"))
         with _SHARD_LOCK:
+            # opening a piece is collective (rank 0 reads the region table
+            # for all, shards.shared_regions): agree on the file first
+            if not shards.agree(os.path.isfile(datafile)):
+                raise FileNotFoundError("%s: missing on some rank" % datafile)
             lease = DATABASES.lease(datafile, device, shard=(world, rank))
             try:
                 piece = lease.__enter__()

@@ -261,6 +261,28 @@ def _lib_bufsize() -> int:
     return _lib.PM_NRGREP_BUFFER
 
 
+def shared_regions(data, bufsize: Optional[int] = None, group=None):
+    """nrgrep's search regions of the whole file (``engine.nrgrep_regions``),
+    read once: with torch.distributed initialised over more than one rank,
+    rank 0 computes them (a one-line record over the buffer size makes that
+    a pass over the file) and broadcasts the table -- a collective, every
+    rank of ``group`` calls it.  Otherwise computed here."""
+    from . import engine
+    bufsize = _lib_bufsize() if bufsize is None else bufsize
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        obj = [None]
+        if dist.get_rank(group) == 0:
+            try:
+                obj[0] = engine.nrgrep_regions(data, bufsize)
+            except Exception as exc:   # still broadcast: the peers raise too
+                obj[0] = {"failed": repr(exc)}
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if isinstance(obj[0], dict):
+            raise RuntimeError("shared_regions: rank 0 could not read the file: %s" % obj[0]["failed"])
+        return obj[0]
+    return engine.nrgrep_regions(data, bufsize)
+
+
 class ShardedDatabase:
     """Rank ``rank``'s piece of a FASTA file (``split_fasta``) in HBM, with
     ``HALO`` bytes of the next piece so windows that start in the piece are
@@ -270,7 +292,7 @@ class ShardedDatabase:
     piece is sliced from the map on demand.  Hit offsets are file offsets."""
 
     def __init__(self, data, world: int, rank: int, device: int = 0, alphabet: Optional[str] = None,
-                 halo: int = HALO, open_db: bool = True, bufsize: Optional[int] = None):
+                 halo: int = HALO, open_db: bool = True, bufsize: Optional[int] = None, regions=None):
         self.raw = data
         self.world, self.rank = world, rank
         self.ranges = split_fasta(data, world)
@@ -281,9 +303,12 @@ class ShardedDatabase:
         self.headers = (hs, he)
         # nrgrep's search regions are the whole file's (buffers of -b bytes
         # from offset 0): the piece takes those over [beg, stop), shifted to
-        # its offsets (the first clipped to 0)
+        # its offsets (the first clipped to 0); ``regions`` = the whole
+        # file's table when the caller has it (shared_regions)
         from . import engine
-        gt, ge = engine.nrgrep_regions(data, _lib_bufsize() if bufsize is None else bufsize)
+        gt, ge = regions if regions is not None else engine.nrgrep_regions(
+            data, _lib_bufsize() if bufsize is None else bufsize)
+        gt, ge = np.asarray(gt, dtype=np.int64), np.asarray(ge, dtype=np.int64)
         sel = (gt < self.stop) & (ge > self.beg)
         if self.stop > self.beg and sel.any():
             lt = np.maximum(gt[sel], self.beg) - self.beg
@@ -297,12 +322,16 @@ class ShardedDatabase:
             self.db.set_regions(lt, le)
 
     @classmethod
-    def from_file(cls, path: str, world: int, rank: int, device: int = 0, open_db: bool = True) -> "ShardedDatabase":
+    def from_file(cls, path: str, world: int, rank: int, device: int = 0, open_db: bool = True,
+                  group=None) -> "ShardedDatabase":
+        """Memory-maps ``path``.  With torch.distributed initialised this is
+        a collective (``shared_regions``): every rank of ``group`` opens its
+        piece together, and only rank 0 reads the whole file."""
         import mmap
         with open(path, "rb") as fh:
             size = os.fstat(fh.fileno()).st_size
             data = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_READ) if size else b""
-        return cls(data, world, rank, device, open_db=open_db)
+        return cls(data, world, rank, device, open_db=open_db, regions=shared_regions(data, group=group))
 
     def __len__(self):
         return self.end - self.beg
@@ -387,6 +416,9 @@ def _rechain(piece: ShardedDatabase, prog, cand, chain, R: int):
     return np.array(out_b, dtype=np.int64), np.array(out_e, dtype=np.int64)
 
 
+_RECHAIN_FAILED = -2   # a re-chaining rank's broadcast when its re-chain raised
+
+
 def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str = "ids", group=None,
                  scanner=None) -> List[Tuple[np.ndarray, np.ndarray]]:
     """Every rank scans its piece; returns, on every rank, [(beg, end) per
@@ -395,8 +427,11 @@ def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str
 
     Collective: every rank of ``group`` must call it with the same programs,
     in the same order as its other collective calls.  A rank whose local
-    scan raises still takes part in the first collective (``agree``), so the
-    other ranks raise too instead of blocking."""
+    scan raises still takes part in the first collective (``agree``), and a
+    rank whose re-chain raises still broadcasts (a failure marker), so the
+    other ranks raise too instead of blocking.  A failure inside the final
+    hit gather itself (e.g. out of memory) is left to the process group's
+    timeout."""
     scanner = scanner or piece.scanner()
     P = len(progs)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -433,15 +468,22 @@ def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str
                 continue
             out = torch.empty_like(last)
             if r == piece.rank:
-                cand_cache = {}
-                for p in need:
-                    if n_local:
-                        cand_cache[p] = scanner.candidates(progs[p], k, types)
-                        chains[p] = _rechain(piece, progs[p], cand_cache[p], chains[p], int(state[p]) - beg_r)
-                mine = np.array([int(e[-1]) + piece.beg if e.size else -1 for _, e in chains], dtype=np.int64)
-                out.copy_(torch.from_numpy(np.maximum(mine, state)))
+                try:
+                    for p in need:
+                        if n_local:
+                            cand = scanner.candidates(progs[p], k, types)
+                            chains[p] = _rechain(piece, progs[p], cand, chains[p], int(state[p]) - beg_r)
+                    mine = np.array([int(e[-1]) + piece.beg if e.size else -1 for _, e in chains], dtype=np.int64)
+                    out.copy_(torch.from_numpy(np.maximum(mine, state)))
+                except Exception as exc:   # the broadcast below still happens: the peers see the failure
+                    failure = exc
+                    out.fill_(_RECHAIN_FAILED)
             dist.broadcast(out, src=r, group=group)
             state = out.cpu().numpy()
+            if (state == _RECHAIN_FAILED).any():
+                if failure is not None:
+                    raise failure
+                raise RuntimeError("scan_sharded: rank %d's re-chain failed" % r)
     hs, he = piece.headers
     chains = [drop_header_starts(b, e, hs, he) for b, e in chains]
     if world == 1:

@@ -180,3 +180,89 @@ def test_service_search_output_multi_rank(tmp_path, option):
         want = engine_banner(prog, k) + "\n" + "".join(
             "[%d, %d]: %s\n" % (b, e, data[b:e].decode("latin-1")) for b, e in hits)
         assert got[0][i] == want and got[1][i] == want, pat
+
+
+def _regions_worker(rank, world, port, path, bufsize, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from patmatchdocker_amd import engine
+        calls = []
+        real = engine.nrgrep_regions
+        engine.nrgrep_regions = lambda data, b: calls.append(b) or real(data, bufsize)
+        import mmap
+        with open(path, "rb") as fh:
+            data = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+            gt, ge = shards.shared_regions(data, bufsize)
+            piece = shards.ShardedDatabase(data, world, rank, open_db=False, regions=(gt, ge))
+            q.put((rank, len(calls), [int(x) for x in gt], [int(x) for x in ge],
+                   [int(x) for x in piece.regions[0]], [int(x) for x in piece.regions[1]]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_region_table_read_by_rank_zero_only(tmp_path):
+    """One-line records longer than the buffer (the region scan reads the
+    whole file): rank 0 computes the table, rank 1 receives it, and each
+    piece's regions equal those it derives from the table itself."""
+    rnd = random.Random(3)
+    data = b"".join(b">r%d\n%s\n" % (r, "".join(rnd.choice("ACGT") for _ in range(5000)).encode())
+                    for r in range(4))
+    path = str(tmp_path / "long.fa")
+    open(path, "wb").write(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_regions_worker, args=(r, 2, port, path, 3000, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=100) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from patmatchdocker_amd import engine
+    gt, ge = engine.nrgrep_regions(data, 3000)
+    assert got[0][0] == 1 and got[1][0] == 0          # only rank 0 scanned
+    for r in range(2):
+        assert got[r][1] == [int(x) for x in gt] and got[r][2] == [int(x) for x in ge]
+        local = shards.ShardedDatabase(data, 2, r, open_db=False, bufsize=3000)
+        assert got[r][3] == [int(x) for x in local.regions[0]] and got[r][4] == [int(x) for x in local.regions[1]]
+
+
+def _rechain_fail_worker(rank, world, port, data, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from patmatchdocker_amd.regex import compile_pattern
+        if rank == 1:
+            def boom(*a, **k):
+                raise ValueError("re-chain failed on purpose")
+            shards._rechain = boom
+        piece = shards.ShardedDatabase(data, world, rank, open_db=False)
+        try:
+            shards.scan_sharded(piece, [compile_pattern("....")], k=0, scanner=OracleScanner(piece))
+            q.put((rank, "no error"))
+        except Exception as exc:
+            q.put((rank, type(exc).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_rechain_failure_reaches_every_rank():
+    """A rank whose re-chain raises still broadcasts (a failure marker): the
+    other ranks raise instead of blocking in the broadcast."""
+    data = make_fasta()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rechain_fail_worker, args=(r, 2, port, data, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got == {0: "RuntimeError", 1: "ValueError"}

@@ -168,10 +168,17 @@ def _format_hits(db: engine.SequenceDatabase, beg, end) -> str:
     return "".join(lines)
 
 
+# the rank whose search_output returns the output in a sharded job (the one
+# that answers the request); the others return '' for every pattern
+SHARD_OUTPUT_RANK = int(os.environ.get("PM_SHARD_OUTPUT_RANK", "0"))
+
+
 def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[str]:
     """nrgrep_coords output text for each pattern, from one GPU pass.
 
     A pattern nrgrep would reject ("Syntax error in pattern") yields ''.
+    In a sharded job (torch.distributed) only rank ``SHARD_OUTPUT_RANK``
+    gets the output; the other ranks scan their pieces and return ''.
     """
     k, types = parse_error_option(option)
     progs, slots = [], []
@@ -193,7 +200,7 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
     if world > 1:
         # one process per GPU (torchrun): every rank scans its record-aligned
         # piece of the file, the reports are joined across the cuts and
-        # gathered, every rank returns the whole output.  Collectives must
+        # gathered to SHARD_OUTPUT_RANK, which returns the whole output.  Collectives must
         # pair up across ranks: one request at a time per process
         # (_SHARD_LOCK), every rank serving the same request sequence
         # (INTEGRATION.md §2); a rank that cannot open its piece still takes
@@ -212,8 +219,9 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
                 shards.agree(False)
                 raise
             try:
-                results = shards.scan_sharded(piece, progs, k=k, types=types)
-                for slot, prog, (beg, end) in zip(slots, progs, results):
+                # the hits travel to the serving rank only (dist.gather)
+                results = shards.scan_sharded(piece, progs, k=k, types=types, dst=SHARD_OUTPUT_RANK)
+                for slot, prog, (beg, end) in zip(slots, progs, results or []):
                     outputs[slot] = engine_banner(prog, k) + "\n" + _format_hits(piece, beg, end)
             finally:
                 lease.__exit__(None, None, None)

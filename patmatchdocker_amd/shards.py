@@ -420,10 +420,12 @@ _RECHAIN_FAILED = -2   # a re-chaining rank's broadcast when its re-chain raised
 
 
 def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str = "ids", group=None,
-                 scanner=None) -> List[Tuple[np.ndarray, np.ndarray]]:
-    """Every rank scans its piece; returns, on every rank, [(beg, end) per
-    program] in file offsets -- equal to the single-process scan of the
-    whole file (what nrgrep_coords reports, header-line starts dropped).
+                 scanner=None, dst: Optional[int] = None) -> Optional[List[Tuple[np.ndarray, np.ndarray]]]:
+    """Every rank scans its piece; returns [(beg, end) per program] in file
+    offsets -- equal to the single-process scan of the whole file (what
+    nrgrep_coords reports, header-line starts dropped) -- on rank ``dst``
+    (the hits travel there only: ``dist.gather``), None on the other ranks;
+    ``dst=None``: on every rank (``all_gather``).
 
     Collective: every rank of ``group`` must call it with the same programs,
     in the same order as its other collective calls.  A rank whose local
@@ -492,8 +494,10 @@ def scan_sharded(piece: ShardedDatabase, progs: Sequence, k: int = 0, types: str
     keys = np.concatenate([(np.int64(p) << POS_BITS) | (b + piece.beg) for p, (b, _) in enumerate(chains)]
                           or [np.zeros(0, dtype=np.int64)])
     lens = np.concatenate([(e - b).astype(np.int32) for b, e in chains] or [np.zeros(0, dtype=np.int32)])
-    gk, gl = gather_hits(torch.from_numpy(keys).to(dev), torch.from_numpy(lens).to(dev), group, dst=None)
-    gk, gl = gk.cpu().numpy(), gl.cpu().numpy().astype(np.int64)
+    out = gather_hits(torch.from_numpy(keys).to(dev), torch.from_numpy(lens).to(dev), group, dst=dst)
+    if out is None:
+        return None
+    gk, gl = out[0].cpu().numpy(), out[1].cpu().numpy().astype(np.int64)
     pat = gk >> POS_BITS
     beg = gk & POS_MASK
     res = []

@@ -317,7 +317,7 @@ def main():
         # `traffic` but not here
         positions = info["positions"]
         alg_bytes = -(-positions // 32) * 8
-        achieved = alg_bytes / (mean_kms * 1e-3) / 1e9
+        achieved = alg_bytes / (mean_kms * 1e-3) / 1e9 if mean_kms > 0 else 0.0
         if args.config == 4:
             workload = "configs[4]: batch of %d degenerate 12-nt DNA patterns k=%d vs %.1f Gbp synthetic DNA per GPU" % (
                 len(progs), args.k, args.gbp)

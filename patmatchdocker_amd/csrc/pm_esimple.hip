@@ -1022,7 +1022,9 @@ __global__ __launch_bounds__(256) void k_es_count(const uint64_t* total_d, uint6
 void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, uint32_t* wlist, uint32_t* wcount, uint32_t* bcnt, uint32_t G, const TextView& tv,
                hipStream_t s) {
-    HIPCHK(hipMemsetAsync(wcount, 0, sizeof(uint32_t), s));
+    // a device-side total comes from the speculative sort, which zeroed
+    // wcount too (report_ws puts it right after the total)
+    if (!total_d) HIPCHK(hipMemsetAsync(wcount, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_es_heads, dim3(256), dim3(ES_HEADS_T), 0, s, P0, keys, lens, total_d, total_h, acc, wlist, wcount,
                        tv);
     EsPrep P = P0;

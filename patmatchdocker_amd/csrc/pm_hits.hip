@@ -133,6 +133,9 @@ __global__ __launch_bounds__(THREADS) void k_sort_bins(const uint64_t* __restric
             uint64_t t = 0;
             for (int w = 0; w < THREADS / 64; ++w) t += wsum[w];
             *total_out = t;
+            // the report workspace's walk-list counter follows the total
+            // (report_ws): zeroed here, no memset before the report pass
+            *reinterpret_cast<uint32_t*>(total_out + 1) = 0u;
         }
     }
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
@@ -868,8 +871,10 @@ bool report_needed(const pm_db* db, uint32_t flags, bool cross) {
 
 ReportWs report_ws(pm_db* db, uint64_t cap_items) {
     Carve c;
-    const size_t o_t = c.take(8), o_c = c.take(8), o_m = c.take(REP_G_MAX * 8), o_b = c.take(REP_G_MAX * 4),
-                 o_wc = c.take(8), o_w = c.take(std::max<uint64_t>(cap_items, 1) * 4),
+    // the walk-list counter right after the total: the sort that writes the
+    // device-side total zeroes it too (k_sort_bins)
+    const size_t o_t = c.take(16), o_wc = o_t + 8, o_c = c.take(8), o_m = c.take(REP_G_MAX * 8),
+                 o_b = c.take(REP_G_MAX * 4), o_w = c.take(std::max<uint64_t>(cap_items, 1) * 4),
                  o_a = c.take(std::max<uint64_t>(cap_items, 1));
     uint8_t* d = static_cast<uint8_t*>(reserve(db, db->ws_rep, c.off));
     ReportWs ws;

@@ -66,4 +66,5 @@ def test_two_ranks_equal_whole_file(tmp_path):
             hits = oracle.scan_reported(data, prog, k, opt[1:] or "idst", skip_headers=True)
             want = engine_banner(prog, k) + "\n" + "".join(
                 "[%d, %d]: %s\n" % (b, e, data[b:e].decode("latin-1")) for b, e in hits)
-            assert got[0][1][opt][i] == want and got[1][1][opt][i] == want, (pat, opt)
+            # the hits gather to the serving rank (service.SHARD_OUTPUT_RANK = 0)
+            assert got[0][1][opt][i] == want and got[1][1][opt][i] == "", (pat, opt)

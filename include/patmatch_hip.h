@@ -210,8 +210,9 @@ int pm_scan_nfa(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* fol
 /* pm_scan_nfa with an explicit error-type mask `errs` (PM_ERR_*) -- the
  * general `nrgrep_coords -k <k><ids>` scan.  min_len = the shortest match
  * length of the pattern (regex.py); with PM_ERR_DEL it must exceed k
- * (otherwise PM_E_UNSUPPORTED) unless the pattern is a class sequence
- * reported with PM_ESIMPLE.  Insertions let a match run to
+ * (otherwise PM_E_UNSUPPORTED) unless the report is nrgrep's -- a class
+ * sequence with PM_ESIMPLE or an extended pattern with PM_EXTENDED, whose
+ * walks then take every line.  Insertions let a match run to
  * max_len + k characters.  pm_scan_nfa(...) == pm_scan_nfa_errs(..., 0, k,
  * PM_ERR_SUB, ...). */
 int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, const uint64_t* follow,

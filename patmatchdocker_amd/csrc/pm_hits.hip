@@ -193,6 +193,8 @@ void release_hits(pm_hits* h) {   // every event of h has completed
     delete h->pending;
     pool_put(h->device, h->keys, h->keys_cap);
     pool_put(h->device, h->lens, h->lens_cap);
+    pool_put(h->device, h->old_keys, h->old_keys_cap);
+    pool_put(h->device, h->old_lens, h->old_lens_cap);
     delete h;
 }
 
@@ -404,6 +406,8 @@ void discard_hits(pm_hits* h) {
     if (!h) return;
     pool_put(h->device, h->keys, h->keys_cap);
     pool_put(h->device, h->lens, h->lens_cap);
+    pool_put(h->device, h->old_keys, h->old_keys_cap);
+    pool_put(h->device, h->old_lens, h->old_lens_cap);
     delete h;
 }
 
@@ -935,7 +939,16 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     else
         hipLaunchKernelGGL(k_rep_scatter, dim3(G), dim3(REP_T), 0, s, a);
     HIPCHK(hipGetLastError());
-    retire_buffers(h, s);
+    if (done && !h->old_keys && !h->old_lens) {
+        // the pass's own completion event covers the old buffers: no event
+        // record (a marker packet, ~10 us before the next scan starts)
+        h->old_keys = h->keys;
+        h->old_lens = h->lens;
+        h->old_keys_cap = h->keys_cap;
+        h->old_lens_cap = h->lens_cap;
+    } else {
+        retire_buffers(h, s);
+    }
     h->keys = a.okeys;
     h->lens = a.olens;
     h->keys_cap = kc;

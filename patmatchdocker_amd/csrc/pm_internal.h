@@ -406,6 +406,11 @@ struct pm_hits {
     hipEvent_t ready = nullptr;     // recorded after the last kernel writing keys/lens
     hipEvent_t last_use = nullptr;  // recorded by pm_hits_copy_device on the caller's stream
     pm_pending* pending = nullptr;  // pipelined scan not yet resolved (count unknown)
+    // the list's buffers before its report pass compacted it: free once
+    // `ready` (bound to the pass's last dispatch) has completed
+    uint64_t* old_keys = nullptr;
+    uint32_t* old_lens = nullptr;
+    size_t old_keys_cap = 0, old_lens_cap = 0;
 };
 
 namespace pm {

@@ -2009,6 +2009,11 @@ void hits_finalize(pm_hits* h) {
                      false);
     pool_put(h->device, h->keys, h->keys_cap);
     pool_put(h->device, h->lens, h->lens_cap);
+    if (h->ready && (h->old_keys || h->old_lens)) HIPCHK(hipEventSynchronize(h->ready));
+    pool_put(h->device, h->old_keys, h->old_keys_cap);
+    pool_put(h->device, h->old_lens, h->old_lens_cap);
+    h->old_keys = nullptr;
+    h->old_lens = nullptr;
     h->keys = r->keys;
     h->lens = r->lens;
     h->keys_cap = r->keys_cap;

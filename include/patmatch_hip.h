@@ -80,6 +80,17 @@ int pm_db_regions(const pm_db* db, uint64_t cap, uint64_t* starts, uint64_t* end
 int pm_db_destroy(pm_db* db);
 int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet,
                uint64_t* n_exception_words, uint64_t* device_bytes);
+/* BYTE databases (peptides): the folded bytes are also held as 5-bit
+ * residue codes in five bit-planes (north_star's 5-bit packing: 0.625 byte
+ * per residue); code 0 = a line break (header lines and '\n'), 1..31 = the
+ * file's other distinct bytes in increasing order.  pm_scan_linear scans
+ * the planes (one lane per 32 window starts, bit-parallel class tests)
+ * unless PM_SCAN_BYTES is set or windows may span lines.  *n_codes = the
+ * codes in use, 0 when there are no planes (a nucleotide database, or more
+ * than 31 distinct bytes besides '\n': the byte copy is scanned);
+ * code_of_byte (256 entries, may be NULL) gets each byte's code.  Replaces
+ * nothing in the reference (nrgrep reads the file's bytes).            */
+int pm_db_residue_codes(const pm_db* db, int* n_codes, uint8_t* code_of_byte);
 /* Decode positions [beg, beg+len) back to folded text (bench/debug). */
 int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
 
@@ -107,6 +118,9 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
  * windows are checked against the file's own bytes and may span a line
  * break (pm_scan_linear decides this by itself).                          */
 #define PM_CROSS_LINES 16
+/* pm_scan_linear on a BYTE database: scan the byte copy instead of the
+ * 5-bit residue planes (A/B and tests; same hits).                        */
+#define PM_SCAN_BYTES 256
 /* The pattern is a class sequence (nrgrep's detClass() == 1) searched with
  * k > 0 errors: nrgrep_coords runs its "esimple" engine (searchPreproc
  * 0x402710), whose own candidate order and two-phase verification decide

@@ -23,6 +23,7 @@ PM_MAX_LINEAR_POSITIONS = 64  # pattern length, fixed-length kernel
 PM_ERR_INS, PM_ERR_DEL, PM_ERR_SUB = 1, 2, 4
 PM_REPORT_ALL, PM_REPORT_NRGREP, PM_ANCHOR_START, PM_ANCHOR_END, PM_KEEP_HEADERS = 0, 1, 2, 4, 8
 PM_CROSS_LINES = 16
+PM_SCAN_BYTES = 256           # BYTE databases: scan the byte copy, not the 5-bit residue planes
 PM_ESIMPLE = 64               # a class sequence at k > 0: nrgrep's esimple report
 PM_EXTENDED = 128             # classes with '?*+': nrgrep's extended / eextended report
 
@@ -34,7 +35,7 @@ EXPORTED = (
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
-    "pm_extended_plan", "pm_eextended_plan",
+    "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes",
 )
 PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
@@ -70,6 +71,7 @@ def _declare(lib):
     lib.pm_db_destroy.argtypes = [P]
     lib.pm_db_info.argtypes = [P, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
     lib.pm_db_decode.argtypes = [P, u64, ctypes.c_uint32, ctypes.c_char_p]
+    lib.pm_db_residue_codes.argtypes = [P, ctypes.POINTER(ctypes.c_int), P]
     lib.pm_db_set_regions.argtypes = [P, u64, P, P]
     lib.pm_db_regions.argtypes = [P, u64, P, P, pu64]
     lib.pm_scan_linear.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, PP]

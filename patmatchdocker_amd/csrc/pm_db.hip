@@ -343,6 +343,37 @@ __global__ void k_mark_ranges_bytes(const uint64_t* __restrict__ ranges, uint64_
     for (uint64_t p = b + threadIdx.x; p < e; p += blockDim.x) bytes[p] = '\n';
 }
 
+// which byte values occur (BYTE databases): one flag per value
+__global__ void k_byte_seen(const uint8_t* __restrict__ bytes, uint64_t n, uint32_t* __restrict__ seen) {
+    __shared__ uint32_t s[8];
+    if (threadIdx.x < 8) s[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t b = bytes[i];
+        atomicOr(&s[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && s[threadIdx.x]) atomicOr(&seen[threadIdx.x], s[threadIdx.x]);
+}
+
+// The 5-bit residue planes: thread per 32-position word; plane q bit i =
+// bit q of the code of position 32 w + i (padding words stay 0: breaks).
+__global__ void k_pack_p5(const uint8_t* __restrict__ bytes, uint64_t nbytes, uint64_t nw, const uint8_t* __restrict__ code,
+                          uint32_t* __restrict__ p5) {
+    const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    uint32_t pl[5] = {0u, 0u, 0u, 0u, 0u};
+    const uint64_t b0 = w * 32;
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t c = b0 + i < nbytes ? code[bytes[b0 + i]] : 0u;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) pl[q] |= ((c >> q) & 1u) << i;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) p5[(uint64_t)q * nw + w] = pl[q];
+}
+
 __global__ void k_decode(NucView v, uint64_t beg, uint32_t len, uint8_t* out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < len) out[i] = nuc_raw_at(v, beg + i);
@@ -530,7 +561,7 @@ void free_db(pm_db* db) {
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
     void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->bytes, db->bytes_raw, db->ws_post.p,
+                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -628,6 +659,40 @@ uint8_t* Upload::commit(pm_db* db) {
     db->up_cache = blob;
     db->up_cache_p = d;
     return d;
+}
+
+// The 5-bit residue planes of a BYTE database (pm_db::p5), when its folded
+// bytes take at most 31 values besides '\n'.
+void build_p5(pm_db* db, std::vector<void*>& owned) {
+    hipStream_t s = db->stream;
+    uint32_t* d_seen = tmp_alloc<uint32_t>(owned, 8);
+    HIPCHK(hipMemsetAsync(d_seen, 0, 32, s));
+    hipLaunchKernelGGL(k_byte_seen, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, blocks_for(db->n, 256)))),
+                       dim3(256), 0, s, db->bytes, db->n, d_seen);
+    HIPCHK(hipGetLastError());
+    uint32_t seen[8];
+    HIPCHK(hipMemcpyAsync(seen, d_seen, 32, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memset(db->code_of, 0, sizeof db->code_of);
+    int nc = 0;
+    for (int b = 0; b < 256; ++b)
+        if (b != '\n' && ((seen[b >> 5] >> (b & 31)) & 1)) {
+            if (++nc > 31) {
+                memset(db->code_of, 0, sizeof db->code_of);
+                db->n_codes = 0;
+                return;   // the byte copy is scanned
+            }
+            db->code_of[b] = (uint8_t)nc;
+        }
+    db->n_codes = nc;
+    db->nw5 = (db->n + 31) / 32 + P5_PAD;
+    db->p5 = dalloc<uint32_t>(db, 5 * db->nw5);
+    HIPCHK(hipMemsetAsync(db->p5, 0, 5 * db->nw5 * 4, s));
+    uint8_t* d_code = tmp_alloc<uint8_t>(owned, 256);
+    HIPCHK(hipMemcpyAsync(d_code, db->code_of, 256, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_pack_p5, dim3(blocks_for(db->nw5, 256)), dim3(256), 0, s, db->bytes, db->n, db->nw5, d_code, db->p5);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // d_code is freed with the other temporaries
 }
 
 NucView nuc_view(const pm_db* db) {
@@ -751,6 +816,7 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
                 hipLaunchKernelGGL(k_mark_ranges_bytes, dim3((uint32_t)nr), dim3(256), 0, s, d_ranges, nr, db->bytes);
                 HIPCHK(hipGetLastError());
             }
+            build_p5(db, owned);
         }
         free_all(db, owned);
         std::vector<uint64_t> rt, re;
@@ -865,6 +931,14 @@ int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet, uint64_t* 
         if (alphabet) *alphabet = db->alphabet;
         if (n_exception_words) *n_exception_words = db->nflag;
         if (device_bytes) *device_bytes = db->device_bytes;
+    });
+}
+
+int pm_db_residue_codes(const pm_db* db, int* n_codes, uint8_t* code_of_byte) {
+    return guarded([&] {
+        require(db != nullptr, "db is NULL");
+        if (n_codes) *n_codes = db->n_codes;
+        if (code_of_byte) memcpy(code_of_byte, db->code_of, 256);
     });
 }
 

@@ -680,6 +680,130 @@ __global__ __launch_bounds__(256) void k_bytes_linear(ByteLinArgs a) {
     }
 }
 
+// BYTE databases on the 5-bit residue planes (pm_db::p5; north_star's
+// 5-bit packing).  One lane per 32-position word w = the 32 window starts
+// 32 w .. 32 w + 31: it loads W words of the five planes (coalesced: lane
+// after lane), turns them into one membership word per distinct class of
+// the batch (bit i: the residue at 32 w' + i is in the class) -- an OR of
+// per-code equality words, each five XORs against the code's bits, over the
+// class's codes or, when shorter, the codes it lacks -- staged in LDS, then
+// counts every pattern's mismatches bit-parallel over its 32 windows:
+// position j's word is the class word shifted by j (alignbit of two staged
+// words), a code-0 residue (a line break or header byte) kills the window
+// whatever k is, as it does in k_bytes_linear.  HBM: 0.625 byte per residue
+// instead of the byte copy's 1.
+constexpr int P5_MAX_CLS = 16;   // distinct classes of one scan
+constexpr int P5_LIST = 16;      // codes listed per class (the shorter of the class and its complement)
+constexpr int P5_T = 128;        // threads per block
+struct P5Args {
+    const uint32_t* p5;
+    uint64_t nw;          // words per plane
+    uint64_t nwords;      // words holding window starts
+    const uint8_t* cls;   // [C][2 + P5_LIST]: count, complement flag, codes
+    int C;
+    const uint8_t* pidx;  // [P][64]: class index of each position, 255 = '.' (every residue but code 0)
+    const int32_t* lengths;
+    int P, k;
+    Sink sink;
+};
+
+template <int W>
+__global__ __launch_bounds__(P5_T) void k_p5_linear(P5Args a) {
+    __shared__ uint32_t s_m[P5_MAX_CLS * W][P5_T];   // membership words, lane-contiguous (no bank conflicts)
+    __shared__ uint8_t s_cls[P5_MAX_CLS][2 + P5_LIST];
+    for (int i = threadIdx.x; i < a.C * (2 + P5_LIST); i += P5_T)
+        s_cls[i / (2 + P5_LIST)][i % (2 + P5_LIST)] = a.cls[i];
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * P5_T;
+    for (uint64_t w = blockIdx.x * (uint64_t)P5_T + threadIdx.x; w < a.nwords; w += stride) {
+        uint32_t pl[W][5];
+#pragma unroll
+        for (int i = 0; i < W; ++i)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) pl[i][q] = a.p5[(uint64_t)q * a.nw + w + i];   // zero-padded past the end
+        uint32_t brk[W];   // code 0
+#pragma unroll
+        for (int i = 0; i < W; ++i) brk[i] = ~(pl[i][0] | pl[i][1] | pl[i][2] | pl[i][3] | pl[i][4]);
+        for (int c = 0; c < a.C; ++c) {
+            const int cnt = s_cls[c][0];
+            uint32_t m[W];
+#pragma unroll
+            for (int i = 0; i < W; ++i) m[i] = 0u;
+            for (int e = 0; e < cnt; ++e) {
+                const uint32_t x = s_cls[c][2 + e];
+#pragma unroll
+                for (int i = 0; i < W; ++i) {
+                    uint32_t d = 0u;
+#pragma unroll
+                    for (int q = 0; q < 5; ++q) d |= pl[i][q] ^ (((x >> q) & 1u) ? ~0u : 0u);
+                    m[i] |= ~d;
+                }
+            }
+            const bool comp = s_cls[c][1] != 0;
+#pragma unroll
+            for (int i = 0; i < W; ++i) s_m[c * W + i][threadIdx.x] = comp ? ~m[i] : m[i];
+        }
+        for (int p = 0; p < a.P; ++p) {
+            const int len = a.lengths[p];
+            const uint8_t* pi = a.pidx + p * 64;
+            uint32_t c0 = 0u, c1 = 0u, ge4 = 0u, kill = 0u;
+            for (int j = 0; j < len; ++j) {
+                const int i = j >> 5, sh = j & 31;
+                const uint32_t b0 = i == 0 ? brk[0] : brk[W - 2], b1 = i == 0 ? brk[1] : brk[W - 1];
+                kill |= __builtin_amdgcn_alignbit(b1, b0, sh);
+                const int c = pi[j];
+                if (c == 255) continue;
+                const uint32_t m0 = s_m[c * W + i][threadIdx.x], m1 = s_m[c * W + i + 1][threadIdx.x];
+                const uint32_t x = ~__builtin_amdgcn_alignbit(m1, m0, sh);
+                const uint32_t cy0 = c0 & x;
+                c0 ^= x;
+                const uint32_t cy1 = c1 & cy0;
+                c1 ^= cy0;
+                ge4 |= cy1;
+            }
+            uint32_t dead = ge4 | kill;
+            switch (a.k) {
+                case 0: dead |= c0 | c1; break;
+                case 1: dead |= c1; break;
+                case 2: dead |= c1 & c0; break;
+                default: break;
+            }
+            // one counter reservation per wave when its 64 words fall in
+            // one bin (dense hits would serialize on the bin's counter)
+            uint32_t live = ~dead;
+            const uint64_t w0 = __builtin_amdgcn_readfirstlane((uint32_t)(w & 0xFFFFFFFFu)) |
+                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32);
+            const uint32_t bin0 = a.sink.bin_of((uint32_t)p, w0 * 32), bin1 = a.sink.bin_of((uint32_t)p, w0 * 32 + 64 * 32 - 1);
+            if (bin0 == bin1 && __builtin_amdgcn_ballot_w64(true) == ~0ull) {
+                const uint32_t cnt = __builtin_popcount(live);
+                uint32_t incl = cnt;   // inclusive prefix over the wave
+                const int lane = threadIdx.x & 63;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = __shfl_up(incl, d, 64);
+                    if (lane >= d) incl += o;
+                }
+                const uint32_t tot = __shfl(incl, 63, 64);
+                uint32_t base = 0;
+                if (tot) {
+                    if (lane == 0) base = atomicAdd(&a.sink.bin_cnt[bin0], tot);
+                    base = __shfl(base, 0, 64);
+                }
+                uint32_t o = base + incl - cnt;
+                for (; live; live &= live - 1u, ++o) {
+                    const uint64_t st = w * 32 + (uint64_t)__builtin_ctz(live);
+                    if (o < a.sink.cap) a.sink.out[(uint64_t)bin0 * a.sink.cap + o] = ((uint64_t)p << 48) | st;
+                }
+            } else {
+                for (; live; live &= live - 1u) {
+                    const uint64_t st = w * 32 + (uint64_t)__builtin_ctz(live);
+                    a.sink.push(a.sink.bin_of((uint32_t)p, st), ((uint64_t)p << 48) | st);
+                }
+            }
+        }
+    }
+}
+
 // waves per workgroup = parts of a lane's 32 window words; each wave scans
 // 32 / parts consecutive words of every lane column of the tile.  Two waves
 // of 16 words (12 % fewer VALU instructions per tile: the Lmax - 1 halo words
@@ -1398,10 +1522,66 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
     EsUpload esu;
     const bool esimple = linear_esimple(n_patterns, lengths, pos_class, class_bytes, k, flags, esb);
     if (esimple) es_upload(esb, up, esu);
+    // the 5-bit residue planes when the batch's classes fit the kernel
+    P5Args pa{};
+    const int maxlen = *std::max_element(lengths, lengths + n_patterns);
+    bool p5 = db->p5 && !cross && !(flags & PM_SCAN_BYTES) && k <= 3 && maxlen <= 64;
+    std::vector<uint8_t> cls, pidx((size_t)n_patterns * 64, 255);
+    if (p5) {
+        std::map<int, int> idx;   // class id -> distinct index
+        for (int q = 0; q < n_patterns && p5; ++q)
+            for (int j = 0; j < lengths[q] && p5; ++j) {
+                const int c = pos_class[64 * q + j];
+                if (class_is_any[c]) continue;   // every residue but code 0
+                auto it = idx.find(c);
+                if (it == idx.end()) {
+                    if ((int)idx.size() == P5_MAX_CLS) {
+                        p5 = false;
+                        break;
+                    }
+                    it = idx.emplace(c, (int)idx.size()).first;
+                }
+                pidx[(size_t)64 * q + j] = (uint8_t)it->second;
+            }
+        if (p5) {
+            cls.assign(idx.size() * (2 + P5_LIST), 0);
+            for (const auto& kv : idx) {
+                uint32_t in = 0;   // the class's codes (bytes absent from the file have none)
+                for (int b = 0; b < 256; ++b)
+                    if (((class_bytes[8 * kv.first + b / 32] >> (b % 32)) & 1) && db->code_of[b]) in |= 1u << db->code_of[b];
+                const uint32_t uni = db->n_codes >= 31 ? ~0u : (2u << db->n_codes) - 1u;   // codes 0..n_codes occur
+                const bool comp = __builtin_popcount(in) > __builtin_popcount(uni & ~in);
+                const uint32_t list = comp ? uni & ~in : in;
+                uint8_t* e = &cls[(size_t)kv.second * (2 + P5_LIST)];
+                e[0] = (uint8_t)__builtin_popcount(list);
+                e[1] = comp ? 1 : 0;
+                int t = 0;
+                for (int x = 0; x < 32; ++x)
+                    if ((list >> x) & 1) e[2 + t++] = (uint8_t)x;
+            }
+            pa.C = (int)idx.size();
+        }
+    }
+    size_t o_cls = 0, o_pidx = 0;
+    if (p5) {
+        o_cls = up.add(cls.data(), std::max<size_t>(cls.size(), 1));
+        o_pidx = up.add(pidx.data(), pidx.size());
+    }
+
     uint8_t* d_up = up.commit(db);
     const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     ByteLinArgs a{db->bytes, db->bytes_raw, db->n, d_up + o_pc, reinterpret_cast<const int32_t*>(d_up + o_len),
                   d_up + o_any, reinterpret_cast<const uint32_t*>(d_up + o_cb), n_patterns, k, cross ? 1 : 0, Sink{}};
+    if (p5) {
+        pa.p5 = db->p5;
+        pa.nw = db->nw5;
+        pa.nwords = (db->n + 31) / 32;
+        pa.cls = d_up + o_cls;
+        pa.pidx = d_up + o_pidx;
+        pa.lengths = reinterpret_cast<const int32_t*>(d_up + o_len);
+        pa.P = n_patterns;
+        pa.k = k;
+    }
     uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
     SinkBuffers sb;
     std::vector<uint32_t> counts;
@@ -1411,8 +1591,17 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
     for (int attempt = 0; attempt < 2; ++attempt) {
         sb = make_sink(db, n_patterns, db->n, expected);
         a.sink = sb.sink();
+        pa.sink = sb.sink();
         HIPCHK(hipEventRecord(ev.a, s));
-        hipLaunchKernelGGL(k_bytes_linear, dim3(blocks), dim3(256), 0, s, a);
+        if (p5) {
+            const uint32_t b5 = (uint32_t)std::min<uint64_t>(blocks_for(pa.nwords, P5_T), 256 * 16);
+            if (maxlen <= 32)
+                hipLaunchKernelGGL(k_p5_linear<2>, dim3(b5), dim3(P5_T), 0, s, pa);
+            else
+                hipLaunchKernelGGL(k_p5_linear<3>, dim3(b5), dim3(P5_T), 0, s, pa);
+        } else {
+            hipLaunchKernelGGL(k_bytes_linear, dim3(blocks), dim3(256), 0, s, a);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev.b, s));
         bool overflow = false;
@@ -1450,7 +1639,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             require(lengths[p] >= 1 && lengths[p] <= PM_MAX_LINEAR_POSITIONS, "pattern length out of range");
             for (int j = 0; j < lengths[p]; ++j) require(pos_class[64 * p + j] < n_classes, "class id out of range");
         }
-        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_ESIMPLE)) ==
+        require((flags & ~(uint32_t)(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_ESIMPLE | PM_SCAN_BYTES)) ==
                     0,
                 "bad flags");
         DeviceGuard g(db->device);

@@ -160,6 +160,14 @@ class SequenceDatabase:
         return {"positions": n.value, "alphabet": NUC if alpha.value == 0 else BYTE,
                 "exception_words": nx.value, "device_bytes": nbytes.value}
 
+    def residue_codes(self):
+        """BYTE databases: (number of 5-bit residue codes, code of each byte
+        as a 256-entry uint8 array); 0 codes = no residue planes."""
+        n = ctypes.c_int()
+        table = np.zeros(256, dtype=np.uint8)
+        check(_lib.load().pm_db_residue_codes(self.handle, ctypes.byref(n), table.ctypes.data))
+        return n.value, table
+
     def __len__(self):
         return self.info()["positions"]
 

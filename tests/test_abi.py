@@ -124,3 +124,13 @@ def test_route_indels():
     with pytest.raises(UnsupportedOnGPU):
         engine.route(compile_pattern("(R(GK)?D)"), engine.BYTE, 2, "d")
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 2, "d") == "nfa"
+
+
+def test_flag_values_match_the_header():
+    import re
+    text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                             "patmatch_hip.h")).read()
+    for name in ("PM_REPORT_NRGREP", "PM_KEEP_HEADERS", "PM_CROSS_LINES", "PM_ESIMPLE", "PM_EXTENDED",
+                 "PM_SCAN_BYTES"):
+        m = re.search(r"#define %s (\d+)" % name, text)
+        assert m and int(m.group(1)) == getattr(_lib, name), name

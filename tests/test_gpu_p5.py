@@ -1,0 +1,146 @@
+"""The 5-bit residue planes of BYTE (peptide) databases (pm_db::p5,
+k_p5_linear): class sequences at k = 0..3 substitutions scanned on the
+planes report what the byte kernel and the oracle report (nrgrep's simple /
+esimple engines, patmatch.py:733-743 with -p patterns), on proteome-shaped
+FASTA with headers, ragged lines, lower case, X / B / Z / '*', and on files
+with more than 31 distinct bytes (no planes: the byte copy is scanned)."""
+import random
+
+import pytest
+
+from patmatchdocker_amd import _lib
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+
+pytestmark = pytest.mark.gpu
+
+AA = "ACDEFGHIKLMNPQRSTVWY"
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from patmatchdocker_amd import engine as eng
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+    return eng
+
+
+def proteome(rng, n_records=40, extra="XBZ*", lower=0.05):
+    recs = []
+    for r in range(n_records):
+        n = rng.randint(1, 900)
+        seq = []
+        for _ in range(n):
+            x = rng.random()
+            c = rng.choice(extra) if x < 0.02 else rng.choice("CCKLGST" if x < 0.3 else AA)
+            seq.append(c.lower() if rng.random() < lower else c)
+        s = "".join(seq)
+        w = rng.choice([60, 70, 1000])
+        recs.append(">YP%04d protein %d\n%s\n" % (r, r, "\n".join(s[i:i + w] for i in range(0, len(s), w))))
+    return "".join(recs).encode()
+
+
+PATTERNS = ["CXXC", "C-x(2)-C", "[LIVM]XXG", "RGD", "NX[ST]", "CX{3}[LIVMFYWC]", "GXGXXG", "KK",
+            "[ST]X[RK]", "CC", "W", "C-x-[DN]-x(4)-[FY]-x-C-x-C", "LXXLL"]
+
+
+def _progs():
+    progs = []
+    for p in PATTERNS:
+        prog = compile_pattern(convert("-p", p))
+        if prog.kind == "simple" and prog.m <= _lib.PM_MAX_LINEAR_POSITIONS:
+            progs.append(prog)
+    assert len(progs) >= 10
+    return progs
+
+
+def _pairs(r):
+    return list(zip(r[0].tolist(), r[1].tolist()))
+
+
+def _launch(engine, db, progs, k, flags):
+    batch = engine.LinearBatch(progs)
+    h = engine._collect(batch.launch(db, k, flags=flags))
+    out = []
+    for i in range(len(progs)):
+        sel = h.pattern == i
+        out.append(list(zip(h.beg[sel].tolist(), h.end[sel].tolist())))
+    return out
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_planes_match_the_oracle(engine, oracle_mod, k):
+    rng = random.Random(50 + k)
+    text = proteome(rng)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        n_codes, table = db.residue_codes()
+        assert 20 <= n_codes <= 31
+        assert table[ord("\n")] == 0 and table[ord("A")] > 0
+        progs = _progs()
+        res, _ = engine.scan(db, progs, k=k, types="s")
+        for prog, r in zip(progs, res):
+            assert _pairs(r) == oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True), (prog.source, k)
+    finally:
+        db.close()
+
+
+@pytest.mark.parametrize("k", [0, 2])
+def test_planes_equal_the_byte_kernel(engine, k):
+    """Every candidate (PM_REPORT_ALL, headers kept) of the plane kernel
+    equals the byte kernel's on the same database."""
+    rng = random.Random(70 + k)
+    text = proteome(rng, n_records=60)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        progs = _progs()
+        base = _lib.PM_REPORT_ALL | _lib.PM_KEEP_HEADERS
+        planes = _launch(engine, db, progs, k, base)
+        direct = _launch(engine, db, progs, k, base | _lib.PM_SCAN_BYTES)
+        assert planes == direct
+        assert sum(len(x) for x in planes) > 100
+    finally:
+        db.close()
+
+
+def test_long_patterns_and_many_classes(engine, oracle_mod):
+    """Patterns over 32 positions (three plane words per lane) and a batch
+    with 16 distinct classes."""
+    rng = random.Random(91)
+    text = proteome(rng, n_records=30, lower=0.0)
+    classes = ["[%s]" % "".join(rng.sample(AA, rng.randint(1, 12))) for _ in range(16)]
+    pats = ["".join(rng.choice(classes + ["X"]) for _ in range(rng.randint(33, 60))) for _ in range(3)]
+    pats.append("".join(classes))
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        progs = [compile_pattern(convert("-p", p)) for p in pats]
+        progs = [p for p in progs if p.kind == "simple" and p.m <= _lib.PM_MAX_LINEAR_POSITIONS]
+        assert len(progs) >= 3
+        for k in (2, 3):
+            res, _ = engine.scan(db, progs, k=k, types="s")
+            for prog, r in zip(progs, res):
+                assert _pairs(r) == oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True), (prog.source, k)
+    finally:
+        db.close()
+
+
+def test_more_than_31_distinct_bytes_scans_the_byte_copy(engine, oracle_mod):
+    rng = random.Random(7)
+    text = proteome(rng, n_records=20, extra="XBZ*0123456789#%&", lower=0.0)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        assert db.residue_codes()[0] == 0
+        progs = _progs()
+        res, _ = engine.scan(db, progs, k=1, types="s")
+        for prog, r in zip(progs, res):
+            assert _pairs(r) == oracle_mod.scan_reported(text, prog, 1, "s", skip_headers=True), prog.source
+    finally:
+        db.close()
+
+
+def test_nucleotide_databases_have_no_residue_planes(engine):
+    db = engine.SequenceDatabase.from_bytes(b">a\nACGTNACGT\n", alphabet=engine.NUC, device=0)
+    try:
+        assert db.residue_codes()[0] == 0
+    finally:
+        db.close()

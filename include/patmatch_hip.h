@@ -82,12 +82,13 @@ int pm_db_info(const pm_db* db, uint64_t* n_positions, int* alphabet,
                uint64_t* n_exception_words, uint64_t* device_bytes);
 /* BYTE databases (peptides): the folded bytes are also held as 5-bit
  * residue codes in five bit-planes (north_star's 5-bit packing: 0.625 byte
- * per residue); code 0 = a line break (header lines and '\n'), 1..31 = the
- * file's other distinct bytes in increasing order.  pm_scan_linear scans
- * the planes (one lane per 32 window starts, bit-parallel class tests)
- * unless PM_SCAN_BYTES is set or windows may span lines.  *n_codes = the
- * codes in use, 0 when there are no planes (a nucleotide database, or more
- * than 31 distinct bytes besides '\n': the byte copy is scanned);
+ * per residue); code 0 = a header byte or the padding, 1 = '\n', 2..31 =
+ * the file's other distinct bytes in increasing order.  pm_scan_linear
+ * scans the planes (one lane per 32 window starts, bit-parallel class
+ * tests; windows over header text are re-checked on the file's bytes)
+ * unless PM_SCAN_BYTES is set.  *n_codes = the highest code in use, 0 when
+ * there are no planes (a nucleotide database, or more than 30 distinct
+ * bytes besides '\n': the byte copy is scanned);
  * code_of_byte (256 entries, may be NULL) gets each byte's code.  Replaces
  * nothing in the reference (nrgrep reads the file's bytes).            */
 int pm_db_residue_codes(const pm_db* db, int* n_codes, uint8_t* code_of_byte);

@@ -359,14 +359,16 @@ __global__ void k_byte_seen(const uint8_t* __restrict__ bytes, uint64_t n, uint3
 
 // The 5-bit residue planes: thread per 32-position word; plane q bit i =
 // bit q of the code of position 32 w + i (padding words stay 0: breaks).
-__global__ void k_pack_p5(const uint8_t* __restrict__ bytes, uint64_t nbytes, uint64_t nw, const uint8_t* __restrict__ code,
-                          uint32_t* __restrict__ p5) {
+__global__ void k_pack_p5(const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ raw, uint64_t nbytes, uint64_t nw,
+                          const uint8_t* __restrict__ code, uint32_t* __restrict__ p5) {
     const uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (w >= nw) return;
     uint32_t pl[5] = {0u, 0u, 0u, 0u, 0u};
     const uint64_t b0 = w * 32;
     for (int i = 0; i < 32; ++i) {
-        const uint32_t c = b0 + i < nbytes ? code[bytes[b0 + i]] : 0u;
+        const uint64_t p = b0 + i;
+        // header bytes read '\n' in the byte copy, themselves in raw
+        const uint32_t c = p >= nbytes ? 0u : bytes[p] != '\n' ? code[bytes[p]] : raw[p] == '\n' ? P5_NL : 0u;
 #pragma unroll
         for (int q = 0; q < 5; ++q) pl[q] |= ((c >> q) & 1u) << i;
     }
@@ -561,7 +563,7 @@ void free_db(pm_db* db) {
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
         if (e) (void)hipEventDestroy(e);
     void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->bytes, db->bytes_raw, db->ws_post.p,
+                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->hdr_end, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -662,8 +664,8 @@ uint8_t* Upload::commit(pm_db* db) {
 }
 
 // The 5-bit residue planes of a BYTE database (pm_db::p5), when its folded
-// bytes take at most 31 values besides '\n'.
-void build_p5(pm_db* db, std::vector<void*>& owned) {
+// bytes take at most 30 values besides '\n'; `ranges`: the header lines.
+void build_p5(pm_db* db, std::vector<void*>& owned, const std::vector<uint64_t>& ranges) {
     hipStream_t s = db->stream;
     uint32_t* d_seen = tmp_alloc<uint32_t>(owned, 8);
     HIPCHK(hipMemsetAsync(d_seen, 0, 32, s));
@@ -674,7 +676,8 @@ void build_p5(pm_db* db, std::vector<void*>& owned) {
     HIPCHK(hipMemcpyAsync(seen, d_seen, 32, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     memset(db->code_of, 0, sizeof db->code_of);
-    int nc = 0;
+    db->code_of['\n'] = (uint8_t)P5_NL;
+    int nc = (int)P5_NL;
     for (int b = 0; b < 256; ++b)
         if (b != '\n' && ((seen[b >> 5] >> (b & 31)) & 1)) {
             if (++nc > 31) {
@@ -685,12 +688,19 @@ void build_p5(pm_db* db, std::vector<void*>& owned) {
             db->code_of[b] = (uint8_t)nc;
         }
     db->n_codes = nc;
+    if (db->nhdr) {
+        std::vector<uint64_t> ends(db->nhdr);
+        for (uint64_t r = 0; r < db->nhdr; ++r) ends[r] = ranges[2 * r + 1];
+        db->hdr_end = dalloc<uint64_t>(db, db->nhdr);
+        HIPCHK(hipMemcpy(db->hdr_end, ends.data(), db->nhdr * 8, hipMemcpyHostToDevice));
+    }
     db->nw5 = (db->n + 31) / 32 + P5_PAD;
     db->p5 = dalloc<uint32_t>(db, 5 * db->nw5);
     HIPCHK(hipMemsetAsync(db->p5, 0, 5 * db->nw5 * 4, s));
     uint8_t* d_code = tmp_alloc<uint8_t>(owned, 256);
     HIPCHK(hipMemcpyAsync(d_code, db->code_of, 256, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_pack_p5, dim3(blocks_for(db->nw5, 256)), dim3(256), 0, s, db->bytes, db->n, db->nw5, d_code, db->p5);
+    hipLaunchKernelGGL(k_pack_p5, dim3(blocks_for(db->nw5, 256)), dim3(256), 0, s, db->bytes, db->bytes_raw, db->n, db->nw5,
+                       d_code, db->p5);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));   // d_code is freed with the other temporaries
 }
@@ -816,7 +826,7 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
                 hipLaunchKernelGGL(k_mark_ranges_bytes, dim3((uint32_t)nr), dim3(256), 0, s, d_ranges, nr, db->bytes);
                 HIPCHK(hipGetLastError());
             }
-            build_p5(db, owned);
+            build_p5(db, owned, ranges);
         }
         free_all(db, owned);
         std::vector<uint64_t> rt, re;

@@ -161,6 +161,7 @@ struct NucView {
 };
 
 // the "other"-position list (pm_db::xlist)
+constexpr uint32_t P5_NL = 1;      // the residue code of '\n' (0: header bytes and padding)
 constexpr uint64_t P5_PAD = 4;   // zero words past a 5-bit plane (a window reads up to 3 words ahead)
 constexpr uint64_t XL_POS_MASK = (1ull << 48) - 1;
 constexpr int XL_AHEAD_SHIFT = 48;
@@ -336,12 +337,14 @@ struct pm_db : pm_lane {
     // (k_others_lane's work list, built once per database)
     uint64_t* xlist = nullptr;
     uint64_t nxlist = 0;
-    // BYTE databases: the folded bytes as 5-bit residue codes (0 = a line
-    // break, header bytes and the padding included; 1..31 = the database's
-    // other distinct bytes, in increasing byte order), bit-sliced: plane q of
-    // word w holds bit q of the codes of positions 32 w .. 32 w + 31
-    // (p5[q * nw5 + w]).  None when the file holds more than 31 distinct
-    // bytes besides '\n' (the byte copy is scanned then).
+    // BYTE databases: the folded bytes as 5-bit residue codes (0 = a header
+    // byte or the padding, 1 = '\n', 2..31 = the database's other distinct
+    // bytes, in increasing byte order), bit-sliced: plane q of word w holds
+    // bit q of the codes of positions 32 w .. 32 w + 31 (p5[q * nw5 + w]).
+    // None when the file holds more than 30 distinct bytes besides '\n'
+    // (the byte copy is scanned then).  hdr_end[r]: the end of header line r
+    // (its '\n'; hdr[r] its start) for windows that read header bytes.
+    uint64_t* hdr_end = nullptr;
     uint32_t* p5 = nullptr;
     uint64_t nw5 = 0;      // words per plane (+ P5_PAD zero words read past the end)
     int n_codes = 0;       // residue codes in use (0: no planes)

@@ -707,7 +707,10 @@ struct P5Args {
     Sink sink;
 };
 
-template <int W>
+// CROSS (nrgrep's simple engine at k = 0 with a class that takes '\n'):
+// windows span lines, '\n' (code 1) is a residue like any other and only
+// header bytes (code 0) kill; the windows they kill are k_p5_cross_fix's.
+template <int W, bool CROSS>
 __global__ __launch_bounds__(P5_T) void k_p5_linear(P5Args a) {
     __shared__ uint32_t s_m[P5_MAX_CLS * W][P5_T];   // membership words, lane-contiguous (no bank conflicts)
     __shared__ uint8_t s_cls[P5_MAX_CLS][2 + P5_LIST];
@@ -721,9 +724,10 @@ __global__ __launch_bounds__(P5_T) void k_p5_linear(P5Args a) {
         for (int i = 0; i < W; ++i)
 #pragma unroll
             for (int q = 0; q < 5; ++q) pl[i][q] = a.p5[(uint64_t)q * a.nw + w + i];   // zero-padded past the end
-        uint32_t brk[W];   // code 0
+        uint32_t brk[W];   // code 0 (header bytes, padding), and '\n' unless CROSS
 #pragma unroll
-        for (int i = 0; i < W; ++i) brk[i] = ~(pl[i][0] | pl[i][1] | pl[i][2] | pl[i][3] | pl[i][4]);
+        for (int i = 0; i < W; ++i)
+            brk[i] = CROSS ? ~(pl[i][0] | pl[i][1] | pl[i][2] | pl[i][3] | pl[i][4]) : ~(pl[i][1] | pl[i][2] | pl[i][3] | pl[i][4]);
         for (int c = 0; c < a.C; ++c) {
             const int cnt = s_cls[c][0];
             uint32_t m[W];
@@ -799,6 +803,49 @@ __global__ __launch_bounds__(P5_T) void k_p5_linear(P5Args a) {
                     const uint64_t st = w * 32 + (uint64_t)__builtin_ctz(live);
                     a.sink.push(a.sink.bin_of((uint32_t)p, st), ((uint64_t)p << 48) | st);
                 }
+            }
+        }
+    }
+}
+
+// The windows k_p5_linear<W, true> killed on header bytes, checked against
+// the file's own bytes as k_bytes_linear does: a wave per header line r
+// (a header line and a pattern give ~60-100 windows), the windows that
+// overlap it and no earlier header line.
+struct P5FixArgs {
+    const uint8_t* raw;
+    uint64_t n;
+    const uint64_t* hdr;
+    const uint64_t* hdr_end;
+    uint64_t nhdr;
+    const uint8_t* pos_class;
+    const int32_t* lengths;
+    const uint8_t* class_any;
+    const uint32_t* class_bytes;
+    int P, k;
+    Sink sink;
+};
+
+__global__ __launch_bounds__(64) void k_p5_cross_fix(P5FixArgs a) {   // one wave per header line
+    for (uint64_t r = blockIdx.x; r < a.nhdr; r += gridDim.x) {
+        const int64_t hb = (int64_t)a.hdr[r], he = (int64_t)a.hdr_end[r];
+        const int64_t prev = r ? (int64_t)a.hdr_end[r - 1] : 0;
+        for (int p = 0; p < a.P; ++p) {
+            const int len = a.lengths[p];
+            int64_t lo = hb - len + 1;
+            if (lo < prev) lo = prev;
+            if (lo < 0) lo = 0;
+            for (int64_t s = lo + threadIdx.x; s < he; s += blockDim.x) {
+                if ((uint64_t)s + (uint64_t)len > a.n) continue;
+                int mm = 0;
+                bool ok = true;
+                for (int j = 0; j < len && ok; ++j) {
+                    const uint8_t ch = a.raw[s + j];
+                    const int c = a.pos_class[p * 64 + j];
+                    if (a.class_any[c]) continue;
+                    if (!((a.class_bytes[c * 8 + (ch >> 5)] >> (ch & 31)) & 1) && ++mm > a.k) ok = false;
+                }
+                if (ok) a.sink.push(a.sink.bin_of((uint32_t)p, (uint64_t)s), ((uint64_t)p << 48) | (uint64_t)s);
             }
         }
     }
@@ -1525,7 +1572,7 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
     // the 5-bit residue planes when the batch's classes fit the kernel
     P5Args pa{};
     const int maxlen = *std::max_element(lengths, lengths + n_patterns);
-    bool p5 = db->p5 && !cross && !(flags & PM_SCAN_BYTES) && k <= 3 && maxlen <= 64;
+    bool p5 = db->p5 && !(flags & PM_SCAN_BYTES) && k <= 3 && maxlen <= 64;
     std::vector<uint8_t> cls, pidx((size_t)n_patterns * 64, 255);
     if (p5) {
         std::map<int, int> idx;   // class id -> distinct index
@@ -1595,10 +1642,16 @@ void scan_linear_bytes(pm_db* db, int n_patterns, const int32_t* lengths, const 
         HIPCHK(hipEventRecord(ev.a, s));
         if (p5) {
             const uint32_t b5 = (uint32_t)std::min<uint64_t>(blocks_for(pa.nwords, P5_T), 256 * 16);
-            if (maxlen <= 32)
-                hipLaunchKernelGGL(k_p5_linear<2>, dim3(b5), dim3(P5_T), 0, s, pa);
-            else
-                hipLaunchKernelGGL(k_p5_linear<3>, dim3(b5), dim3(P5_T), 0, s, pa);
+            auto kern = maxlen <= 32 ? (cross ? k_p5_linear<2, true> : k_p5_linear<2, false>)
+                                     : (cross ? k_p5_linear<3, true> : k_p5_linear<3, false>);
+            hipLaunchKernelGGL(kern, dim3(b5), dim3(P5_T), 0, s, pa);
+            if (cross && db->nhdr) {
+                HIPCHK(hipGetLastError());
+                P5FixArgs fa{db->bytes_raw, db->n, db->hdr, db->hdr_end, db->nhdr, d_up + o_pc,
+                             reinterpret_cast<const int32_t*>(d_up + o_len), d_up + o_any,
+                             reinterpret_cast<const uint32_t*>(d_up + o_cb), n_patterns, k, pa.sink};
+                hipLaunchKernelGGL(k_p5_cross_fix, dim3((uint32_t)std::min<uint64_t>(db->nhdr, 65536)), dim3(64), 0, s, fa);
+            }
         } else {
             hipLaunchKernelGGL(k_bytes_linear, dim3(blocks), dim3(256), 0, s, a);
         }

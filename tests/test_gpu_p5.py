@@ -3,7 +3,11 @@ k_p5_linear): class sequences at k = 0..3 substitutions scanned on the
 planes report what the byte kernel and the oracle report (nrgrep's simple /
 esimple engines, patmatch.py:733-743 with -p patterns), on proteome-shaped
 FASTA with headers, ragged lines, lower case, X / B / Z / '*', and on files
-with more than 31 distinct bytes (no planes: the byte copy is scanned)."""
+with more than 30 distinct bytes besides '\\n' (no planes: the byte copy
+is scanned).  At k = 0 a class that takes '\\n' ('X', a negated class)
+lets nrgrep's simple engine match across lines: '\\n' is then a residue
+of its own and the windows over header bytes are checked on the file's
+bytes (k_p5_cross_fix)."""
 import random
 
 import pytest
@@ -76,7 +80,7 @@ def test_planes_match_the_oracle(engine, oracle_mod, k):
     try:
         n_codes, table = db.residue_codes()
         assert 20 <= n_codes <= 31
-        assert table[ord("\n")] == 0 and table[ord("A")] > 0
+        assert table[ord("\n")] == 1 and table[ord("A")] > 1   # 0: header bytes
         progs = _progs()
         res, _ = engine.scan(db, progs, k=k, types="s")
         for prog, r in zip(progs, res):
@@ -142,5 +146,34 @@ def test_nucleotide_databases_have_no_residue_planes(engine):
     db = engine.SequenceDatabase.from_bytes(b">a\nACGTNACGT\n", alphabet=engine.NUC, device=0)
     try:
         assert db.residue_codes()[0] == 0
+    finally:
+        db.close()
+
+
+def test_cross_line_windows_over_headers(engine, oracle_mod):
+    """k = 0 with 'X': windows across '\\n' and into header lines whose
+    text holds the pattern's letters (hits starting in a header are kept with
+    PM_KEEP_HEADERS and dropped by the report, as process_output does)."""
+    rng = random.Random(12)
+    recs = []
+    for r in range(80):
+        hdr = ">%s CKLC%d %s" % ("".join(rng.choice("CKLGST") for _ in range(5)), r, "LCK" * rng.randint(0, 3))
+        seq = "".join(rng.choice("CKLGSTAW") for _ in range(rng.randint(1, 40)))
+        w = rng.choice([3, 5, 7, 60])
+        recs.append(hdr + "\n" + "\n".join(seq[i:i + w] for i in range(0, len(seq), w)) + "\n")
+    text = "".join(recs).encode()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        assert db.residue_codes()[0] > 0
+        progs = [compile_pattern(convert("-p", p)) for p in ("CXXC", "KXL", "CX", "XKXXL", "LXC", "GXXXXXXS")]
+        progs = [p for p in progs if p.kind == "simple"]
+        assert len(progs) >= 5
+        res, _ = engine.scan(db, progs, k=0, types="s")
+        for prog, r in zip(progs, res):
+            assert _pairs(r) == oracle_mod.scan_reported(text, prog, 0, "s", skip_headers=True), prog.source
+        base = _lib.PM_REPORT_ALL | _lib.PM_KEEP_HEADERS
+        planes = _launch(engine, db, progs, 0, base)
+        assert planes == _launch(engine, db, progs, 0, base | _lib.PM_SCAN_BYTES)
+        assert sum(len(x) for x in planes) > 200
     finally:
         db.close()

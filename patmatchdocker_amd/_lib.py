@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpatmatch_hip.so")
+LIB_PATH = os.environ.get("PM_LIB_AB") or os.path.join(_HERE, "libpatmatch_hip.so")   # PM_LIB_AB: A/B runs only
 
 PM_ALPHA_NUC = 0
 PM_ALPHA_BYTE = 1

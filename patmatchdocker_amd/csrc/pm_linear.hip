@@ -30,6 +30,7 @@
 #include <memory>
 #include <set>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <sstream>
 
@@ -915,8 +916,8 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
         }
         for (uint32_t i = lane_t; i < cnt; i += SEG_LANES) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 14);
-            const uint32_t lane = (r.x >> 8) & 63, s = (r.x >> 3) & 31, p = r.x & 7;
+            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 15);
+            const uint32_t lane = (r.x >> 9) & 63, s = (r.x >> 3) & 63, p = r.x & 7;   // s up to 31 + a shift
             if (tile >= a.ntiles) continue;
             const uint32_t w0 = 32u * lane + s;
             uint32_t live = r.y;
@@ -961,7 +962,7 @@ typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
 // Hit records: one uint2 per (tile, lane, step, pattern) with a live window:
-// x = (tile - first tile of the workgroup) << 14 | lane << 8 | word << 3 |
+// x = (tile - first tile of the workgroup) << 15 | lane << 9 | word << 3 |
 // pattern, y = the live mask (bit b = the window of stream b).  Staged per
 // wave in LDS and flushed to the wave's global segment, so the scan loop
 // never waits on a global store; k_linear_expand turns records into keys.
@@ -1129,9 +1130,15 @@ std::string net_dead(std::ostringstream& o, const CountNet& n, int K, int& uid, 
 // once, then 3 per window, instead of 19 per window).  Greedy pairing,
 // each pattern in at most one pair; a pair pays when the block is large
 // and the offset small against the wave's `steps` window words.
+// shift[p]: the pair's member whose block rows sit `off` words later is
+// scanned `off` steps later (its windows at words t + off read the rows
+// its partner's windows at t read): each block is built once per step
+// instead of twice at the wave's right edge (see gen_linear_source).
 std::vector<std::vector<int>> shared_blocks(int P, const int32_t* lengths, const uint8_t* pos_class,
-                                            const uint8_t* class_acgt, const uint8_t* class_is_any, int steps) {
+                                            const uint8_t* class_acgt, const uint8_t* class_is_any, int steps,
+                                            std::vector<int>* shift = nullptr) {
     const int JIT_STEPS = steps;
+    if (shift) shift->assign(P, 0);
     std::vector<std::vector<int>> block(P);   // positions of pattern p in its shared block
     {
         std::vector<bool> used(P, false);
@@ -1153,6 +1160,9 @@ std::vector<std::vector<int>> shared_blocks(int P, const int32_t* lengths, const
                 }
             if (bp < 0) break;
             used[bp] = used[bq] = true;
+            // position j of bp meets j - boff of bq: bq's block at step t + boff
+            // reads bp's rows at step t
+            if (shift) (*shift)[boff > 0 ? bq : bp] = boff > 0 ? boff : -boff;
             for (int j = 0; j < lengths[bp]; ++j)
                 if (j - boff >= 0 && j - boff < lengths[bq] && cls(bp, j) >= 0 && cls(bp, j) == cls(bq, j - boff)) {
                     block[bp].push_back(j);
@@ -1216,12 +1226,30 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // once, then 3 per window, instead of 19 per window).  Greedy pairing,
     // each pattern in at most one pair; a pair pays when the block is large
     // and the offset small against the wave's 8 steps.
-    const std::vector<std::vector<int>> block = shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, JIT_STEPS);
+    std::vector<int> shift;
+    const std::vector<std::vector<int>> block =
+        shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, JIT_STEPS, &shift);
+    // Shifted members (shift[p] > 0) are scanned at steps [t0 + shift,
+    // t1 + shift) so their blocks coincide with the partner's.  The last
+    // wave's steps past 31 are the next lane's first words (for lane 63 the
+    // next stream's; bit 31 -- the next tile -- is left to that tile); the
+    // first wave adds the words [0, shift) of lane 0, bit 0 only (the
+    // tile's own stream 0).  dd[STEPS + e] holds those extras.
+    int XS = 0;
+    for (int p = 0; p < P; ++p) XS = std::max(XS, shift[p]);
+    if (LANE_WORDS + XS + Lmax - 1 > 3 * LANE_WORDS) {   // rows past the halo: no shifts
+        shift.assign(P, 0);
+        XS = 0;
+    }
+    o << "#define XS " << std::max(XS, 1) << "\n";
+    o << "__device__ constexpr int SHIFT[P] = {";
+    for (int p = 0; p < P; ++p) o << (p ? ", " : "") << shift[p];
+    o << "};\n";
     for (int part = 0; part < PARTS; ++part) {
         const int t0 = part * JIT_STEPS, t1 = t0 + JIT_STEPS;
-        const int wend = t1 + Lmax - 1;   // words [t0, wend)
+        const int wend = t1 + XS + Lmax - 1;   // words [0, wend)
         o << "__device__ __forceinline__ void tile_body" << part
-          << "(const uint2* __restrict__ sw, int lane, u32 hb1, u32 hs1, u32 hb2, u32 hs2, u32 (&dd)[STEPS][P]) {\n";
+          << "(const uint2* __restrict__ sw, int lane, u32 hb1, u32 hs1, u32 hb2, u32 hs2, u32 (&dd)[STEPS + XS][P]) {\n";
         std::vector<bool> loaded(wend, false);
         std::map<std::pair<int, int>, std::string> cw;   // (word, ACGT subset) -> class word
         auto class_word = [&](int i, int subset) {
@@ -1241,8 +1269,18 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
         };
         int uid = 0;
         std::map<std::vector<std::string>, CountNet> blocks;   // block inputs -> its compressed count
-        for (int t = t0; t < t1; ++t) {
-            for (int p = 0; p < P; ++p) {
+        // (slot, word) of every window word this wave evaluates, per pattern
+        std::vector<std::tuple<int, int, int>> work;   // (dd slot, pattern, word)
+        for (int s = 0; s < JIT_STEPS; ++s)
+            for (int p = 0; p < P; ++p) work.emplace_back(s, p, t0 + s + shift[p]);
+        if (part == 0)
+            for (int p = 0; p < P; ++p)
+                for (int e = 0; e < shift[p]; ++e) work.emplace_back(JIT_STEPS + e, p, e);
+        std::vector<std::vector<bool>> set(JIT_STEPS + std::max(XS, 1), std::vector<bool>(P, false));
+        for (const auto& wk : work) {
+            {
+                const int slot = std::get<0>(wk), p = std::get<1>(wk), t = std::get<2>(wk);
+                set[slot][p] = true;
                 const uint8_t* pc = pos_class + 64 * p;
                 std::vector<std::string> in, bin;
                 for (int j = 0, b = 0; j < lengths[p]; ++j) {
@@ -1266,9 +1304,15 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
                 o << "  {  // step " << t << ", pattern " << p << "\n";
                 net_add(o, n, in, K, uid, "    ");
                 const std::string d = net_dead(o, n, K, uid, "    ");
-                o << "    dd[" << (t - t0) << "][" << p << "] = " << d << ";\n  }\n";
+                std::string mask;
+                if (slot >= JIT_STEPS) mask = " | (lane == 0 ? 0xFFFFFFFEu : 0xFFFFFFFFu)";   // lane 0, bit 0 only
+                else if (t >= LANE_WORDS) mask = " | (lane == 63 ? 0x80000000u : 0u)";     // the next tile's: its own
+                o << "    dd[" << slot << "][" << p << "] = " << d << mask << ";\n  }\n";
             }
         }
+        for (size_t slot = 0; slot < set.size(); ++slot)
+            for (int p = 0; p < P; ++p)
+                if (!set[slot][p]) o << "  dd[" << slot << "][" << p << "] = ~0u;\n";
         o << "}\n";
     }
     // `waves`: __launch_bounds__ minimum workgroups per CU (4 -> at most
@@ -1276,7 +1320,14 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // bytes DMA'd per tile: the 2048 words and only the halo words a window
     // reads (Lmax - 1 of the 64) -- ~2 % fewer HBM lines per tile for a
     // 15-mer (round 2: 1.036 -> 1.012 x algorithmic traffic)
-    const int halo_used = std::min(HALO, std::max(1, Lmax - 1));
+    int XSh = 0;   // (the generator's shift, recomputed: the halo words the shifted windows read)
+    {
+        std::vector<int> sh;
+        shared_blocks(P, lengths, pos_class, class_acgt, class_is_any, JIT_STEPS, &sh);
+        for (int v : sh) XSh = std::max(XSh, v);
+        if (LANE_WORDS + XSh + Lmax - 1 > 3 * LANE_WORDS) XSh = 0;
+    }
+    const int halo_used = std::min(HALO, std::max(1, Lmax - 1 + XSh));
     const int LOAD_BYTES = std::min(TILE_BYTES, (int)(((STREAM + halo_used) * 8 + 15) / 16 * 16));
     const int LOAD_PIECES = (LOAD_BYTES + 1023) / 1024;
     (void)DMA_PIECES;
@@ -1350,24 +1401,25 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    BARRIER();\n"
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
-         "    u32 dd[STEPS][P];   // dead windows per step and pattern (every path writes all of them)\n";
+         "    u32 dd[STEPS + XS][P];   // dead windows per slot and pattern (every path writes all of them)\n";
     // wid < 4: the last part is the plain else (no ~0 initialization of dd)
     for (int part = 0; part < PARTS; ++part)
         o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
           << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
     o << "    const u32 S0 = wid * STEPS;   // the wave's first window word\n"
          "    u32 all = ~0u;\n"
-         "#pragma unroll\n    for (int s = 0; s < STEPS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
+         "#pragma unroll\n    for (int s = 0; s < STEPS + XS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
          "    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {   // wave-uniform, rare\n"
          "#pragma unroll\n"
-         "      for (int s = 0; s < STEPS; ++s) {\n"
+         "      for (int s = 0; s < STEPS + XS; ++s) {\n"
          "#pragma unroll\n"
          "        for (int p = 0; p < P; ++p) {\n"
          "          const u32 lv = ~dd[s][p];\n"
          "          const u64 m = __builtin_amdgcn_ballot_w64(lv != 0u);\n"
          "          if (m) {\n"
          "            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));\n"
-         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 14 | (u32)lane << 8 | (u32)(S0 + s) << 3 | (u32)p, lv);\n"
+         "            const u32 word = s < STEPS ? S0 + s + SHIFT[p] : s - STEPS;   // the window word (may pass 31)\n"
+         "            if (lv) st[scnt + below] = make_uint2((u32)(tile - t0) << 15 | (u32)lane << 9 | word << 3 | (u32)p, lv);\n"
          "            scnt += (u32)__builtin_popcountll(m);\n"
          "            if (scnt > REC_LDS - 64) {\n"
          "              flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
@@ -1981,7 +2033,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             uint64_t nwg = std::min<uint64_t>(db->ntiles, 256ull * JIT_WG_PER_CU * split);
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
-            require(tpw < (1ull << 18), "database too large for the record encoding", PM_E_UNSUPPORTED);
+            require(tpw < (1ull << 17), "database too large for the record encoding", PM_E_UNSUPPORTED);
             const uint64_t parts = (uint64_t)jit_parts();
             const uint64_t nseg = nwg * parts;   // one lane-record segment per wave
             // segment capacities scale with the tiles a workgroup owns (a

@@ -95,9 +95,10 @@ def test_specialized_kernel_shares_strand_blocks(tmp_path, monkeypatch):
         assert engine.jit_compile(progs, k) > 1000
         return dump.read_text().count("// shared block")
 
-    # 4 waves x (8 + 2) blocks for the bench motif at every k
+    # the shifted partner: 8 blocks per wave, plus 2 in the first wave (its
+    # lane 0, bit 0 words 0..1) -- was 4 waves x (8 + 2)
     for k in (0, 1, 2, 3):
-        assert n_blocks(["TGCTGASTCAGCANW"], k, True) == 40
+        assert n_blocks(["TGCTGASTCAGCANW"], k, True) == 34
     assert n_blocks(SHARED_BLOCK_BATCH, 2, False) > 0
     assert n_blocks(["AAAAAACCCCCC"], 2, True) == 0   # strands agree nowhere
 

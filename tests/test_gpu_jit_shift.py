@@ -1,0 +1,84 @@
+"""pm_linear_jit's shifted strand partner (gen_linear_source: the member of a
+shared-block pair whose block sits `off` words later is scanned `off` steps
+later; the last wave's steps past word 31 are the next lane's / stream's
+first words, the first wave adds lane 0 bit 0's words [0, off)).  Matches
+are planted exactly where that bookkeeping changes hands -- at every tile
+start, stream start and lane boundary of a one-line record -- for the bench
+motif and batches of pairs at offsets -2..+3, both strands, k = 0..3, and
+compared with the oracle."""
+import random
+
+import pytest
+
+from patmatchdocker_amd.convert import convert
+from patmatchdocker_amd.regex import compile_pattern
+
+pytestmark = pytest.mark.gpu
+
+TILE, STREAM = 65536, 2048
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from patmatchdocker_amd import _lib
+    from patmatchdocker_amd import engine as eng
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+    return eng
+
+
+def _mutate(rng, s, n):
+    s = list(s)
+    for i in rng.sample(range(len(s)), n):
+        s[i] = rng.choice("ACGT")
+    return "".join(s)
+
+
+def planted_text(rng, motifs, n_tiles=5):
+    head = ">chr1 planted\n"
+    n = n_tiles * TILE - len(head) - 1
+    seq = [rng.choice("ACGT") for _ in range(n)]
+    spots = set()
+    for t in range(n_tiles):
+        for b in (0, 1, 13, 30, 31):
+            for w in (0, 1, 2, 3, 29, 30, 31, 32, 33, 2044, 2045, 2046, 2047):
+                spots.add(t * TILE + b * STREAM + w)
+        for c in range(0, 64, 7):
+            spots.add(t * TILE + 5 * STREAM + 32 * c + 30)
+    for p in sorted(spots):
+        q = p - len(head) - rng.randint(0, 3)
+        m = rng.choice(motifs)
+        m = _mutate(rng, m, rng.choice([0, 0, 1, 2, 3]))
+        if 0 <= q and q + len(m) <= n:
+            seq[q:q + len(m)] = list(m)
+    return (head + "".join(seq) + "\n").encode()
+
+
+BATCHES = [
+    ["TGCTGASTCAGCANW"],                                               # the bench motif: offset 2
+    ["ACGGTCATTGCAGT", "TTACGGTCATTGCA", "GGTCATTGCAGTCCAA"],         # copies at offsets -2, +2
+    ["GGAATTCCAKW", "GATCCGGATC"],                                      # offset 3; a palindrome (offset 0)
+]
+
+
+@pytest.mark.parametrize("bi", range(len(BATCHES)))
+def test_shifted_partner_at_every_boundary(engine, oracle_mod, monkeypatch, bi):
+    monkeypatch.setenv("PM_JIT", "1")
+    rng = random.Random(31 + bi)
+    pats = BATCHES[bi]
+    progs = []
+    for p in pats:
+        f = convert("-n", p)
+        progs += [compile_pattern(f), compile_pattern(convert("-c", f))]
+    plain = [p.replace("S", "C").replace("W", "A").replace("N", "G").replace("K", "T") for p in pats]
+    text = planted_text(rng, plain)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for k in (0, 1, 2, 3):
+            res, _ = engine.scan(db, progs, k=k, types="s", report="all")
+            for prog, r in zip(progs, res):
+                got = list(zip(r[0].tolist(), r[1].tolist()))
+                want = oracle_mod.scan_threads(text, prog, k, "s", skip_headers=True, threads=8, report="all")
+                assert got == want, (prog.source, k)
+    finally:
+        db.close()

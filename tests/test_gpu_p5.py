@@ -177,3 +177,42 @@ def test_cross_line_windows_over_headers(engine, oracle_mod):
         assert sum(len(x) for x in planes) > 200
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("text", [
+    b"",
+    b">only a header\n",
+    b">h1\n>h2\nC\n",
+    b">a\nC\nC\nW\nCC\n>b desc\nCCWCC",          # no final newline
+    b"CWC\nCCC\n",                                # no header at all
+    b">x\n" + b"C" * 100 + b"\n",
+])
+def test_edge_files(engine, oracle_mod, text):
+    """Empty and header-only files, one-residue lines, a missing final
+    newline, headerless text, a run longer than any window."""
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        progs = [compile_pattern(convert("-p", p)) for p in ("C", "CC", "CXC", "WC", "CCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCCC")]
+        for k in (0, 1, 2):
+            res, _ = engine.scan(db, progs, k=k, types="s")
+            for prog, r in zip(progs, res):
+                assert _pairs(r) == oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True), (prog.source, k, text)
+    finally:
+        db.close()
+
+
+def test_many_patterns_one_batch(engine, oracle_mod):
+    """A batch of 24 patterns (the byte path takes them in one scan)."""
+    rng = random.Random(44)
+    text = proteome(rng, n_records=25)
+    pats = ["".join(rng.choice(AA + "X") for _ in range(rng.randint(2, 9))) for _ in range(24)]
+    progs = [compile_pattern(convert("-p", p)) for p in pats]
+    progs = [p for p in progs if p.kind == "simple"]
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        for k in (0, 2):
+            res, _ = engine.scan(db, progs, k=k, types="s")
+            for prog, r in zip(progs, res):
+                assert _pairs(r) == oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True), (prog.source, k)
+    finally:
+        db.close()

@@ -137,6 +137,16 @@ int subset_table(int s) {
     return t;
 }
 
+// Logical words per lane column (WPL; the generator takes 32, 64 or 128:
+// 2048 / WPL lanes per tile, WPL / 32 tiles per wave).  Longer columns pay
+// the WU warm-up words once per WPL words instead of once per 32 (17 / 28 %
+// fewer steps at the bench's WU = 16), but a step's 64 lanes then read words
+// WPL / 32 apart, over 2 or 4 tiles: 2 or 4 times the cache lines per DMA,
+// each fetched again WPL / 32 times.  Measured per strand on `-k 2ids`:
+// 1.62 / 2.04 ms at 32 / 64 (kernel trace), the step 4.44 / 5.36 / 7.15 ms
+// at 32 / 64 / 128 (round 4, tools/gpu_idsab.sh).
+int ids_wpl(int) { return 32; }
+
 // The kernel's source and its cache signature (everything the source
 // depends on); with want_source false only the signature (a query's cache
 // lookup: generating the source cost ~0.1 ms per query).
@@ -161,7 +171,8 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
         ci[i] = it->second;
     }
     std::ostringstream sg;
-    sg << "ids10:" << m << ":" << k << ":" << sp.errs << ":";
+    const int WPL = ids_wpl(WU);
+    sg << "ids11:" << WPL << ":" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) {
         sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
         if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
@@ -245,18 +256,12 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
         // slot the previous step read
         o << in << "    asm volatile(\"s_waitcnt vmcnt(" << 4 * (IDS_DEPTH - 1) << ")\" ::: \"memory\");\n";
         o << in << "    const uint2 v = make_uint2(ring[sl * 256u + col], ring[sl * 256u + 64u + col]);\n";
-        o << in << "    {\n";
-        o << in << "        const int q2 = qs + IDS_DEPTH, t2 = 31 + WU - q2;\n";
-        // the DMA'd row's exception flags (warm-up: row t2 - 32 of the next
-        // column, or the halo word for lane 63)
-        o << in << "        const u32 rr2 = (u32)(q2 < WU ? t2 - 32 : q2 < WU + 32 ? t2 : 0);\n";
-        o << in << "        const bool ex2 = q2 < WU + 32 && (((u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr2) | "
-                   "(u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr2)) != 0u || "
-                   "(q2 < WU && ((halof >> rr2) & 1ull)));\n";
-        o << in << "        dma_word(q2 < WU ? pn + (long)(t2 - 32) * sn : q2 < WU + 32 ? pm + (long)t2 * 64 : tb, dbo, "
-                   "rbase + snx * 1024u, ex2);\n";
-        o << in << "    }\n";
-        o << in << "    const uint2* " << pv << " = " << (emit ? "pm + (long)(" + tv + ") * 64" : "pn + (long)((" + tv + ") - 32) * sn") << ";\n";
+        o << in << "    issue(qs + IDS_DEPTH, snx);\n";
+        if (emit)
+            o << in << "    const uint2* " << pv << " = pm + (long)(((" << tv << ") & 31) * 64 + ((" << tv << ") >> 5));\n";
+        else
+            o << in << "    const u32 u_ = (u32)(" << tv << ") - WPL;\n"
+              << in << "    const uint2* " << pv << " = pn + (long)((u_ & 31u) * s1 + (u_ >> 5) * s2);\n";
         o << in << "    const u32 sl_ = sl;\n";
         o << in << "    ++qs; sl = sl + 1u == IDS_SLOTS ? 0u : sl + 1u; snx = snx + 1u == IDS_SLOTS ? 0u : snx + 1u;\n";
         for (size_t c = 0; c < rep.size(); ++c) {
@@ -264,14 +269,10 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
             if (p.any) o << in << "    u32 M" << c << " = 0xffffffffu;\n";
             else o << in << "    u32 M" << c << " = B3(v.x, v.y, v.y, " << subset_table(p.acgt) << ");\n";
         }
-        // the row's exception flags (sbflag, fetched per tile): only a row
-        // with a break or an "other" byte in some lane reads the exception
-        // plane (emit: own row t; warm-up: row t - 32 of the next column, or
-        // the halo for lane 63)
-        o << in << "    const u32 rr = (u32)(" << tv << ")" << (emit ? "" : " - 32u") << ";\n";
-        o << in << "    const u32 rf = (u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr) | "
-                   "(u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr);\n";
-        o << in << "    if (rf != 0u" << (emit ? "" : " || ((halof >> rr) & 1ull)") << ") {   // wave-uniform, rare\n";
+        // the step's exception flag (wave-uniform, from the group's masks):
+        // only a step with a break or an "other" byte in some lane's word
+        // reads the exception plane
+        o << in << "    if (" << (emit ? "exo((u32)(" + tv + "))" : "exw(u_)") << ") {   // wave-uniform, rare\n";
         o << in << "        const uint2 e = make_uint2(ring[sl_ * 256u + 128u + col], ring[sl_ * 256u + 192u + col]);\n";
         o << in << "        const u32 nb = ~e.x;\n";
         // "other" bytes: an N (NUC_N_MARK: its hi bit) matches '.' only;
@@ -302,8 +303,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
             for (int j = 0; j <= k; ++j) o << " | " << V(dst, j, 0);
             o << ";\n";
             o << in << "    for (; em; em &= em - 1) {\n";
-            o << in << "        const u64 pos = tile * TILE_POS + (u64)__builtin_ctz(em) * STREAM + col * 32u + (u32)("
-              << tv << ");\n";
+            o << in << "        const u64 pos = posb + (u64)__builtin_ctz(em) * STREAM + (u32)(" << tv << ");\n";
             o << in << "        if (pos < a.n) push(a, pos);\n";
             o << in << "    }\n";
         }
@@ -316,14 +316,20 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     // 4 workgroups per CU: <= 128 VGPRs, 4 waves per SIMD (staging each
     // tile in LDS by LDS-DMA first measured no faster, round 2)
     o << "#define IDS_WG 4\n#define IDS_DEPTH " << IDS_DEPTH << "\n#define IDS_SLOTS " << IDS_DEPTH + 1 << "\n";
+    o << "#define WPL " << WPL << "u\n#define TPW " << WPL / 32 << "u\n#define LPT " << 2048 / WPL << "u\n";
+    o << "#define STRIDE_MASK " << (WPL == 32 ? "0xffffffffffffffffull" : WPL == 64 ? "0x5555555555555555ull"
+                                                                                      : "0x1111111111111111ull") << "\n";
     o << R"IDS(
-// One wave per tile; lane c owns stream column c (logical words 32c ..
-// 32c + 31, physical word t * 64 + c at step t): it scans the next column's
-// first WU words (or the tile's halo, lane 63) right to left as warm-up,
-// then its own 32 words, reporting starts.  The exception plane is read only
-// for rows whose sbflag bits show a break or an "other" byte in some lane:
-// lane r < 32 holds row r's 64 flag bits (one load per tile), a step reads
-// its row's with v_readlane.
+// One wave per TPW tiles; lane c scans column cc = c % LPT of tile c / LPT:
+// logical words WPL cc .. WPL cc + WPL - 1 of its 32 streams (word t of the
+// column: physical row t & 31, column TPW cc + (t >> 5)).  It first scans
+// the next column's first WU words (the tile's halo for the last column)
+// right to left as warm-up, then its own WPL words, reporting starts: WU +
+// WPL steps per WPL words (at WPL = 32 the warm-up was a third of the
+// steps).  The exception plane is read only at steps where some lane's word
+// has a break or an "other" byte: the group's sbflag rows are folded into a
+// wave-uniform mask over t once per group (bit t: own word t; warm-up word u
+// adds the halo's bit u).
 extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) {   // IDS_WG workgroups per CU
     __shared__ __attribute__((aligned(16))) u32 ids_ring[4][IDS_SLOTS * 256];   // per wave: {hi, lo, brk, oth} x 64 lanes per slot
     const u32 col = threadIdx.x & 63;
@@ -332,34 +338,58 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
     const u32 rbase = __builtin_amdgcn_readfirstlane((u32)reinterpret_cast<u64>(ring));   // its LDS byte address
     const u64 wave = (u64)blockIdx.x * 4u + wid, nwaves = gridDim.x * 4ull;
     const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
-    for (u64 tile = wave; tile < a.ntiles; tile += nwaves) {
-        const u64 base = tile * TILE_WORDS;   // a multiple of 32: rows are sbflag word pairs
-        const uint2* tb = a.hl + base;
-        u64 rowf = 0;
-        if (col < 32u) {
-            const u32* sf = a.sbflag + (base >> 5) + 2u * col;
-            rowf = (u64)sf[0] | ((u64)sf[1] << 32);
+    const u64 ngroups = (a.ntiles + TPW - 1) / TPW;
+    const u32 cc = col % LPT;
+    const bool last_col = cc == LPT - 1u;
+    const u32 s1 = last_col ? 1u : 64u, s2 = last_col ? 32u : 1u;   // warm-up word u: (u & 31) s1 + (u >> 5) s2
+    for (u64 tg = wave; tg < ngroups; tg += nwaves) {
+        // (WPL > 32) lanes of a tile past the end scan the last tile again
+        // and report nothing (their positions are >= n)
+        const u64 tile = tg * TPW + col / LPT;
+        const uint2* tb = a.hl + (tile < a.ntiles ? tile : a.ntiles - 1) * TILE_WORDS;
+        const uint2* pm = tb + TPW * cc;                                  // own words
+        const uint2* pn = last_col ? tb + STREAM : tb + TPW * (cc + 1);   // warm-up words
+        const u64 posb = tile * TILE_POS + (u64)WPL * cc;
+        // the group's exception masks: lane r < 32 folds row r of every
+        // tile into TPW bits (bit g: a flagged word in column group g)
+        u32 fold = 0;
+        u64 hm = 0;
+        for (u32 tau = 0; tau < TPW; ++tau) {
+            const u64 tt = tg * TPW + tau < a.ntiles ? tg * TPW + tau : a.ntiles - 1;
+            const u64 base = tt * TILE_WORDS;   // a multiple of 32: rows are sbflag word pairs
+            if (col < 32u) {
+                const u32* sf = a.sbflag + (base >> 5) + 2u * col;
+                const u64 rf = (u64)sf[0] | ((u64)sf[1] << 32);
+                for (u32 g = 0; g < TPW; ++g) fold |= (u32)((rf & (STRIDE_MASK << g)) != 0ull) << g;
+            }
+            const u32* hf = a.sbflag + ((base + STREAM) >> 5);
+            hm |= (u64)hf[0] | ((u64)hf[1] << 32);   // halo words 2048 .. 2111
         }
-        const u32* hf = a.sbflag + ((base + STREAM) >> 5);
-        const u64 halof = (u64)hf[0] | ((u64)hf[1] << 32);   // halo words 2048 .. 2111
-        const uint2* pn = col < 63u ? tb + col + 1 : tb + STREAM;   // warm-up words: t - 32 ..
-        const long sn = col < 63u ? 64 : 1;
-        const uint2* pm = tb + col;                                  // own words: t * 64
-        // step q (0 .. WU + 31) reads word t = 31 + WU - q; the first
-        // IDS_DEPTH words go in flight now (the previous tile's DMAs have all
-        // landed: the slots are free)
+        u64 mlo = 0, mhi = 0;
+        for (u32 g = 0; g < TPW; ++g) {
+            const u64 bl = __ballot((fold >> g) & 1u) & 0xffffffffull;
+            if (g < 2u) mlo |= bl << (32u * g);
+            else mhi |= bl << (32u * (g - 2u));
+        }
+        auto exo = [&](u32 t) { return (((t < 64u ? mlo : mhi) >> (t & 63u)) & 1ull) != 0ull; };
+        auto exw = [&](u32 u) { return ((((mlo | hm) >> u) & 1ull)) != 0ull; };
+        // step q (0 .. WU + WPL - 1) reads word t = WPL - 1 + WU - q (warm-up
+        // word u = t - WPL while q < WU); its DMA goes IDS_DEPTH steps ahead
+        auto issue = [&](int q, u32 slot) {
+            const int t2 = (int)WPL - 1 + WU - q;
+            const bool w2 = q < WU, o2 = !w2 && q < WU + (int)WPL;
+            const u32 u2 = (u32)(t2 - (int)WPL);
+            const bool ex2 = w2 ? exw(u2) : (o2 && exo((u32)t2));
+            const uint2* g2 = w2 ? pn + (long)((u2 & 31u) * s1 + (u2 >> 5) * s2)
+                                 : o2 ? pm + (long)((t2 & 31) * 64 + (t2 >> 5)) : tb;
+            dma_word(g2, dbo, rbase + slot * 1024u, ex2);
+        };
+        // the first IDS_DEPTH words go in flight now (the previous group's
+        // DMAs have all landed: the slots are free)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int qs = 0;
         u32 sl = 0, snx = IDS_DEPTH;
-        for (int q = 0; q < IDS_DEPTH; ++q) {
-            const int t2 = 31 + WU - q;
-            const u32 rr2 = (u32)(q < WU ? t2 - 32 : q < WU + 32 ? t2 : 0);
-            const bool ex2 = q < WU + 32 && (((u32)__builtin_amdgcn_readlane((int)(u32)rowf, (int)rr2) |
-                                              (u32)__builtin_amdgcn_readlane((int)(u32)(rowf >> 32), (int)rr2)) != 0u ||
-                                             (q < WU && ((halof >> rr2) & 1ull)));
-            dma_word(q < WU ? pn + (long)(t2 - 32) * sn : q < WU + 32 ? pm + (long)t2 * 64 : tb, dbo,
-                     rbase + (u32)q * 1024u, ex2);
-        }
+        for (int q = 0; q < IDS_DEPTH; ++q) issue(q, (u32)q);
 )IDS";
     for (int j = 0; j <= k; ++j)
         for (int i = 0; i < m; ++i) o << "        u32 " << V('r', j, i) << " = 0, " << V('s', j, i) << " = 0;\n";
@@ -385,8 +415,8 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
         step(o, b1, b0, "t - 1", "", "p1", own);
         o << "        }\n";
     };
-    phase(31 + WU, WU, false);   // warm-up: t = 32 + WU - 1 .. 32
-    phase(31, 32, true);         // own column: t = 31 .. 0
+    phase(WPL - 1 + WU, WU, false);   // warm-up: t = WPL + WU - 1 .. WPL
+    phase(WPL - 1, WPL, true);        // own column: t = WPL - 1 .. 0
     // the last tile's look-ahead DMAs land before the wave ends (its LDS is
     // released with the workgroup)
     o << "    }\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}\n";
@@ -405,7 +435,7 @@ std::map<std::pair<int, std::string>, IdsKernel> g_ids_cache;
 bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b) {
     if (db->alphabet != PM_ALPHA_NUC || sp.m * (sp.k + 1) > IDS_MAX_REGS || sp.m > 64) return false;
     const int WU = sp.m + ((sp.errs & PM_ERR_INS) ? sp.k : 0) - 1;
-    if (WU > HALO - 1) return false;   // the warm-up must fit the next lane column or the halo
+    if (WU > std::min(HALO - 1, ids_wpl(WU))) return false;   // the warm-up must fit the next lane column or the halo
     std::string sig;
     gen_ids_source(sp, &sig, false);
     hipFunction_t fn;
@@ -426,7 +456,8 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     IArgsHost a{nv.hl, nv.bo, nv.sbflag, nv.sbbase, nv.xbytes, db->lflag, sp.d_bmask, db->ntiles, db->n,
                 sink.out, sink.bin_cnt, sink.cap, sink.bins_per_pattern, sink.pos_shift, (uint32_t)sp.pattern_id};
     void* params[] = {&a};
-    // one wave per tile, waves loop over tiles (every wave reaches the end);
+    // one wave per group of TPW tiles, waves loop over groups (every wave
+    // reaches the end);
     // four rounds of the resident waves (the kernel needs 120 VGPRs: 4 per
     // SIMD): later rounds' workgroups start wherever earlier ones finish,
     // which evens out CUs that run slower (per strand: one round 1.80 ms,
@@ -435,7 +466,8 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, db->device));
     HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0));
     const uint64_t resident = (uint64_t)std::max(ncu, 1) * (uint64_t)std::max(per_cu, 1) * 4;
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((db->ntiles + 3) / 4, resident));
+    const uint64_t tpw = (uint64_t)ids_wpl(WU) / 32, ngroups = (db->ntiles + tpw - 1) / tpw;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ngroups + 3) / 4, resident));
     HIPCHK(hipExtModuleLaunchKernel(fn, blocks * 256u, 1, 1, 256, 1, 1, 0, s, params, nullptr, ev_a, ev_b, 0));
     return true;
 }

@@ -861,6 +861,14 @@ __global__ __launch_bounds__(64) void k_p5_cross_fix(P5FixArgs a) {   // one wav
 // fewer VALU instructions, no LDS) measured slower still, 0.546 vs 0.473 ms:
 // each row load's latency is exposed at 3 waves per SIMD (r04w A/B).
 int jit_parts() { return 4; }
+// the graded tail (scan_linear) with PM_JIT_GRADED=1: measured -1.3 % kernel
+// time at 10 Gbp and -3 % at 100 Gbp, but +1.3 % per configs[2] step before
+// the expansion took the short segments 4 lanes each (round 4, gpu_envab.sh);
+// off by default until that is measured (tests/test_gpu_graded.py runs both)
+bool jit_graded() {
+    const char* e = getenv("PM_JIT_GRADED");
+    return e && atoi(e) != 0;
+}
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
 
@@ -890,6 +898,9 @@ struct ExpandArgs {
     const uint32_t* slot_cap;
     uint32_t nwg, nout, group, tiles_per_wg;
     uint32_t parts;   // waves per pm_linear_jit workgroup (32 / parts words each)
+    // graded tail (JArgs): segments ogA.. hold groupB workgroups of tpwB tiles
+    uint32_t nA, tpwB, ogA, groupB, tpo;
+    uint64_t tilesA;
 };
 
 // One block per output segment (`group` workgroups x 4 wave segments); each
@@ -902,11 +913,15 @@ constexpr uint32_t SEG_LANES = 16;
 
 __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) {
     __shared__ uint32_t cnt_p[JIT_MAX_P];
-    const uint32_t og = blockIdx.x, sub = threadIdx.x / SEG_LANES, lane_t = threadIdx.x % SEG_LANES;
+    // a graded-tail segment holds groupB short workgroups (a quarter of the
+    // records per wave segment): 4 lanes per wave segment, 4x as many in flight
+    const uint32_t og = blockIdx.x, seg_lanes = og < a.ogA ? SEG_LANES : SEG_LANES / 4;
+    const uint32_t sub = threadIdx.x / seg_lanes, lane_t = threadIdx.x % seg_lanes;
     if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t wg0 = og * a.group, pairs = (min(a.nwg, wg0 + a.group) - wg0) * a.parts;
-    for (uint32_t q = sub; q < pairs; q += EXPAND_THREADS / SEG_LANES) {
+    const uint32_t wg0 = og < a.ogA ? og * a.group : a.nA + (og - a.ogA) * a.groupB;
+    const uint32_t pairs = (min(a.nwg, wg0 + (og < a.ogA ? a.group : a.groupB)) - wg0) * a.parts;
+    for (uint32_t q = sub; q < pairs; q += EXPAND_THREADS / seg_lanes) {
         const uint32_t wg = wg0 + q / a.parts, part = q % a.parts;
         const uint32_t seg = wg * a.parts + part;
         uint32_t cnt = a.rec_cnt[seg];
@@ -914,9 +929,14 @@ __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) 
             if (lane_t == 0) atomicMax(a.rec_over, cnt);
             cnt = a.rcap;
         }
-        for (uint32_t i = lane_t; i < cnt; i += SEG_LANES) {
+        for (uint32_t i = lane_t; i < cnt; i += seg_lanes) {
             const uint2 r = a.rec[(uint64_t)seg * a.rcap + i];
-            const uint64_t tile = (uint64_t)wg * a.tiles_per_wg + (r.x >> 15);
+            uint64_t t0 = (uint64_t)wg * a.tiles_per_wg;
+            if (wg >= a.nA) {
+                const uint32_t j = wg - a.nA, sg = j / a.groupB;
+                t0 = a.tilesA + (uint64_t)sg * a.tpo + (uint64_t)(j - sg * a.groupB) * a.tpwB;
+            }
+            const uint64_t tile = t0 + (r.x >> 15);
             const uint32_t lane = (r.x >> 9) & 63, s = (r.x >> 3) & 63, p = r.x & 7;   // s up to 31 + a shift
             if (tile >= a.ntiles) continue;
             const uint32_t w0 = 32u * lane + s;
@@ -973,6 +993,10 @@ struct JArgs {
     u32* aux_zero;          // the sink's record-overflow counter, zeroed by the first launch of a scan (or null)
     u64 ntiles;
     u32 rcap, tiles_per_wg;
+    // graded tail: from tile tilesA on, each output segment's tpo tiles go
+    // to groupB workgroups (nA, nA + 1, ...) of tpwB tiles (the last fewer)
+    u32 nA, tpwB, groupB, tpo;
+    u64 tilesA;
 };
 #define STREAM 2048u
 #define TILE_POS 65536ull
@@ -1000,6 +1024,8 @@ struct JArgsHost {           // must match JArgs in kJitCommon
     uint32_t* aux_zero;
     uint64_t ntiles;
     uint32_t rcap, tiles_per_wg;
+    uint32_t nA, tpwB, groupB, tpo;
+    uint64_t tilesA;
 };
 constexpr int JIT_REC_LDS = 96;       // hit records staged per wave in LDS (3 workgroups per CU)
 // workgroups resident per CU (4: two 16.5 KiB tile slots each fit the LDS)
@@ -1384,9 +1410,18 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  const u32 hb1 = lane + 1 < 64 ? lane + 1 : 32u * lane + 32u, hs1 = lane + 1 < 64 ? 64u : 1u;\n"
          "  const u32 hb2 = lane + 2 < 64 ? lane + 2 : 32u * lane + 64u, hs2 = lane + 2 < 64 ? 64u : 1u;\n"
          "  const u32 lds_base = (u32)reinterpret_cast<u64>(lds);   // LDS byte address (low bits of the flat address)\n"
-         "  // this workgroup's contiguous tile range\n"
-         "  const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
-         "  const u64 tend = t0 + a.tiles_per_wg < a.ntiles ? t0 + a.tiles_per_wg : a.ntiles;\n"
+         "  // this workgroup's contiguous tile range (the graded tail's are shorter)\n"
+         "  u64 t0, tlim;\n"
+         "  if (blockIdx.x < a.nA) {\n"
+         "    t0 = (u64)blockIdx.x * a.tiles_per_wg;\n"
+         "    tlim = t0 + a.tiles_per_wg;\n"
+         "  } else {\n"
+         "    const u32 j = blockIdx.x - a.nA, sg = j / a.groupB;\n"
+         "    const u64 s0 = a.tilesA + (u64)sg * a.tpo;\n"
+         "    t0 = s0 + (u64)(j - sg * a.groupB) * a.tpwB;\n"
+         "    tlim = t0 + a.tpwB < s0 + a.tpo ? t0 + a.tpwB : s0 + a.tpo;\n"
+         "  }\n"
+         "  const u64 tend = tlim < a.ntiles ? tlim : a.ntiles;   // empty for a last segment's spare workgroups\n"
          "  glb_uint2* grec = (glb_uint2*)(a.rec + ((u64)blockIdx.x * NW + wid) * a.rcap);\n"
          "  lds_uint2* st = (lds_uint2*)(size_t)(u32)reinterpret_cast<u64>(&rst[wid][0]);\n"
          "  u32 scnt = 0, gcnt = 0;   // staged / flushed records (wave-uniform)\n"
@@ -2034,16 +2069,30 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             const uint64_t tpw = (db->ntiles + nwg - 1) / nwg;
             nwg = (db->ntiles + tpw - 1) / tpw;
             require(tpw < (1ull << 17), "database too large for the record encoding", PM_E_UNSUPPORTED);
+            // output segments: `split` consecutive workgroups share one
+            // (pattern, segment) hit list, so the sort sees ~1024 segments
+            const uint64_t group = split;
+            const uint64_t nout = (nwg + group - 1) / group;
+            // graded tail: the last segments' tiles (about one round of the
+            // resident workgroups) go to workgroups of tpwB < tpw tiles, so
+            // the CUs run out of work closer together
+            const uint64_t tpo = tpw * group;   // tiles per output segment
+            uint64_t tpwB = tpw, ogA = nout, nA = nwg, tilesA = db->ntiles, groupB = group;
+            const uint64_t ogB = (256ull * JIT_WG_PER_CU * tpw + tpo - 1) / tpo;
+            if (jit_graded() && tpw >= 4 && ogB < nout) {
+                tpwB = tpw / 4;
+                ogA = nout - ogB;
+                nA = ogA * group;
+                tilesA = ogA * tpo;
+                groupB = (tpo + tpwB - 1) / tpwB;
+                nwg = nA + ogB * groupB;
+            }
             const uint64_t parts = (uint64_t)jit_parts();
             const uint64_t nseg = nwg * parts;   // one lane-record segment per wave
             // segment capacities scale with the tiles a workgroup owns (a
             // random 15-mer at k = 2 leaves ~1.4 hits per tile and strand);
             // an overflow re-runs with the counts seen
             uint32_t cap = 256;
-            // output segments: `split` consecutive workgroups share one
-            // (pattern, segment) hit list, so the sort sees ~1024 segments
-            const uint64_t group = split;
-            const uint64_t nout = (nwg + group - 1) / group;
             while (cap < 4096 && cap < 16 * tpw * group) cap *= 2;
             while (cap > 256 && (uint64_t)n_patterns * nout * cap * 8 > (1ull << 30)) cap /= 2;
             // per-pattern capacities: a dense pattern (many hits) gets its own
@@ -2096,7 +2145,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 // measured no faster: the chip is at its power limit)
                 const hipStream_t xs = s;
                 for (const Chunk& ch : chunks) {
-                    JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw};
+                    JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw,
+                                 (uint32_t)nA, (uint32_t)tpwB, (uint32_t)groupB, (uint32_t)tpo, tilesA};
                     void* params[] = {&ja};
                     jev.emplace_back(new EventPair());
                     // the events take the dispatch's own start/end timestamps
@@ -2106,7 +2156,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,
-                                  (uint32_t)tpw, (uint32_t)parts};
+                                  (uint32_t)tpw, (uint32_t)parts, (uint32_t)nA, (uint32_t)tpwB, (uint32_t)ogA,
+                                  (uint32_t)groupB, (uint32_t)tpo, tilesA};
                     hipLaunchKernelGGL(k_linear_expand, dim3((uint32_t)nout), dim3(EXPAND_THREADS), 0, xs, xa);
                     HIPCHK(hipGetLastError());
                     if (exc) launch_others(ch, xs, sb, nout, tpw * group);

@@ -861,13 +861,13 @@ __global__ __launch_bounds__(64) void k_p5_cross_fix(P5FixArgs a) {   // one wav
 // fewer VALU instructions, no LDS) measured slower still, 0.546 vs 0.473 ms:
 // each row load's latency is exposed at 3 waves per SIMD (r04w A/B).
 int jit_parts() { return 4; }
-// the graded tail (scan_linear) with PM_JIT_GRADED=1: measured -1.3 % kernel
-// time at 10 Gbp and -3 % at 100 Gbp, but +1.3 % per configs[2] step before
-// the expansion took the short segments 4 lanes each (round 4, gpu_envab.sh);
-// off by default until that is measured (tests/test_gpu_graded.py runs both)
+// the graded tail (scan_linear), on unless PM_JIT_GRADED=0: kernel -1.4 %
+// at 10 Gbp (frac 0.704 vs 0.694) with the same step time, -3 % kernel and
+// step at 100 Gbp (round 4, gpu_envab.sh; tests/test_gpu_graded.py checks
+// both partitions against each other)
 bool jit_graded() {
     const char* e = getenv("PM_JIT_GRADED");
-    return e && atoi(e) != 0;
+    return !e || atoi(e) != 0;
 }
 constexpr int JIT_MAX_P = 8;   // patterns per specialized kernel
 static_assert(JIT_MAX_P * 64 <= OTH_MAX_POS, "k_linear_others stages a chunk's classes in LDS");
@@ -914,8 +914,9 @@ constexpr uint32_t SEG_LANES = 16;
 __global__ __launch_bounds__(EXPAND_THREADS) void k_linear_expand(ExpandArgs a) {
     __shared__ uint32_t cnt_p[JIT_MAX_P];
     // a graded-tail segment holds groupB short workgroups (a quarter of the
-    // records per wave segment): 4 lanes per wave segment, 4x as many in flight
-    const uint32_t og = blockIdx.x, seg_lanes = og < a.ogA ? SEG_LANES : SEG_LANES / 4;
+    // records per wave segment): 2 lanes per wave segment, so its ~150 wave
+    // segments are all in flight at once
+    const uint32_t og = blockIdx.x, seg_lanes = og < a.ogA ? SEG_LANES : SEG_LANES / 8;
     const uint32_t sub = threadIdx.x / seg_lanes, lane_t = threadIdx.x % seg_lanes;
     if (threadIdx.x < JIT_MAX_P) cnt_p[threadIdx.x] = 0;
     __syncthreads();

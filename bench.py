@@ -131,41 +131,70 @@ def cpu_threads_default():
     return max(1, min(16, n))
 
 
+def sample_pieces(db, sample_bp):
+    """The CPU sample: the database's first `sample_bp` positions and its
+    last `sample_bp` (which hold pm_linear_jit's graded-tail tiles, the
+    default partition's last output segments), each decoded from HBM and
+    cut to whole lines (the tail piece starts after its first '\\n', so at a
+    line start, as the e* engines' records do).  Returns [(offset, text)]."""
+    n = db.info()["positions"]
+    head = db.decode(0, int(min(sample_bp, n)))
+    head = head[:head.rfind(b"\n") + 1]
+    pieces = [(0, head)]
+    tb = max(len(head), n - int(sample_bp))
+    if tb < n:
+        tail = db.decode(tb, n - tb)
+        cut = tail.find(b"\n") + 1
+        if cut > 0 and cut < len(tail):
+            pieces.append((tb + cut, tail[cut:]))
+    return pieces
+
+
 def cpu_baseline(db, progs, k, types, sample_bp, gpu_hits, threads):
-    """CPU baseline + parity spot check on the first `sample_bp` positions
-    (decoded from HBM, so the exact bytes the GPU scanned): what
-    nrgrep_coords prints for every strand, by nrgrep's own esimple engine
-    restated from the binary (oracle/pm_nrgrep.c -- its cost-model plan,
-    piece BNDM scan, two-phase verify and report rule) over `threads` host
-    threads (the text cut at line breaks: e* matches never span one), timed;
-    its matches must equal the GPU's.  Returns (dict, parity_ok)."""
+    """CPU baseline + parity spot check on the first and the last
+    `sample_bp` positions (decoded from HBM, so the exact bytes the GPU
+    scanned; the last ones are the graded tail's tiles): what nrgrep_coords
+    prints for every strand, by nrgrep's own esimple engine restated from
+    the binary (oracle/pm_nrgrep.c -- its cost-model plan, piece BNDM scan,
+    two-phase verify and report rule) over `threads` host threads (the text
+    cut at line breaks: e* matches never span one), timed; its matches must
+    equal the GPU's in both pieces.  Returns (dict, parity_ok, detail)."""
     from oracle import oracle
-    text = db.decode(0, int(sample_bp))
-    text = text[:text.rfind(b"\n") + 1]
+    from patmatchdocker_amd import engine
+    pieces = sample_pieces(db, sample_bp)
     t0, c0 = time.perf_counter(), time.process_time()
-    base = [oracle.scan_threads(text, p, k, types, skip_headers=True, threads=threads, report="nrgrep")
-            for p in progs]
+    base = [[oracle.scan_threads(text, p, k, types, skip_headers=True, threads=threads, report="nrgrep")
+             for p in progs] for _, text in pieces]
     dt = time.perf_counter() - t0
     cpu_s = time.process_time() - c0
-    bases = sum(len(line) for line in text.split(b"\n")) - text.count(b">")
-    ok = True
+    bases = sum(sum(len(line) for line in text.split(b"\n")) - text.count(b">") for _, text in pieces)
+    mask = (1 << 48) - 1
     keys, lens = gpu_hits
     keys = keys.cpu().tolist()
     lens = lens.cpu().tolist()
-    for pid, b in enumerate(base):
-        got = [((kk & ((1 << 48) - 1)), (kk & ((1 << 48) - 1)) + ln) for kk, ln in zip(keys, lens)
-               if (kk >> 48) == pid]
-        ok &= [h for h in got if h[1] <= len(text)] == b
+    ok = True
+    checked = 0
+    for (off, text), want in zip(pieces, base):
+        for pid, b in enumerate(want):
+            got = [((kk & mask) - off, (kk & mask) - off + ln) for kk, ln in zip(keys, lens)
+                   if (kk >> 48) == pid and (kk & mask) >= off and (kk & mask) + ln <= off + len(text)]
+            ok &= got == b
+            checked += len(b)
+    tail_start = engine.graded_tail_start(db.info()["positions"])
+    detail = {"pieces": [[off, off + len(text)] for off, text in pieces], "hits_checked": checked,
+              "graded_tail_start": tail_start,
+              "graded_tail_checked": tail_start is not None and len(pieces) > 1 and pieces[-1][0] <= tail_start}
     plan = oracle.nrgrep_plan(progs[0], k)
     return {"value": bases / dt / 1e9, "unit": "Gbases/s", "cores": threads, "kind": "port",
-            "sample": "first %.0f Mbp of the synthetic database (decoded from HBM), both strands, -k %d%s: "
+            "sample": "first and last %.0f Mbp of the synthetic database (decoded from HBM; the last ones hold "
+                      "the graded tail's tiles), both strands, -k %d%s: "
                       "nrgrep's esimple engine restated from the binary (oracle/pm_nrgrep.c; plan type %d, "
                       "%s) on %d host threads, text cut at line breaks; %.1f s wall, %.1f s CPU, "
                       "%d CPUs in the affinity mask"
                       % (sample_bp / 1e6, k, types, plan["type"],
                          "%d pieces of %d found by BNDM" % (len(plan["L"]), plan["piece_len"])
                          if plan["type"] == 1 else "window %s" % (plan["window"],),
-                         threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok
+                         threads, dt, cpu_s, len(os.sched_getaffinity(0)))}, ok, detail
 
 
 def spawn_ranks(args):
@@ -388,9 +417,10 @@ def main():
             thr = args.cpu_threads or cpu_threads_default()
             # ~10-30 s of CPU work (nrgrep's engine runs ~0.1 Gbases/s per thread)
             mbp = args.sample_mbp if args.sample_mbp is not None else 100.0 * thr
-            cb, ok = cpu_baseline(db, progs, args.k, args.types if args.k else "", mbp * 1e6, result, thr)
+            cb, ok, detail = cpu_baseline(db, progs, args.k, args.types if args.k else "", mbp * 1e6, result, thr)
             line["cpu_baseline"] = cb
             line["parity_sample_bit_exact"] = ok
+            line["parity_sample"] = detail
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

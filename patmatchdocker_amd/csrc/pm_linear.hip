@@ -1264,7 +1264,12 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     // tile's own stream 0).  dd[STEPS + e] holds those extras.
     int XS = 0;
     for (int p = 0; p < P; ++p) XS = std::max(XS, shift[p]);
-    if (LANE_WORDS + XS + Lmax - 1 > 3 * LANE_WORDS) {   // rows past the halo: no shifts
+    // a shifted window reads logical words up to LANE_WORDS + XS + Lmax - 2;
+    // k_lane_flags (pm_db.hip) flags a lane for exceptions in words
+    // [32 l, 32 l + LANE_WORDS + HALO - 1) only, and the expansion's break /
+    // other kill runs only for flagged lanes, so a window must stay inside
+    // that span (a 61-64-mer shifted pair would read word 95): no shifts
+    if (LANE_WORDS + XS + Lmax - 1 > LANE_WORDS + HALO - 1) {
         shift.assign(P, 0);
         XS = 0;
     }

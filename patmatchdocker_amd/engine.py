@@ -32,6 +32,7 @@ fallback by design.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -406,6 +407,26 @@ def destroy_hits(handle):
 
 def scan_linear(db: SequenceDatabase, progs: Sequence[Program], k: int, flags: int = None) -> Hits:
     return _collect(LinearBatch(progs).launch(db, k, flags=flags))
+
+
+def graded_tail_start(positions: int) -> Optional[int]:
+    """First file offset that pm_linear_jit's graded tail scans (the last
+    output segments' tiles go to workgroups of tpw / 4 tiles), or None when
+    the tail does not engage (tpw < 4, below ~2 Gbp).  Mirrors scan_linear's
+    partition in csrc/pm_linear.hip (JIT_WG_PER_CU = 4, split = 8, tiles of
+    65,536 positions, tiles_for in pm_db.hip); tests and bench.py use it to
+    point the oracle at the tiles the tail owns."""
+    tile, wg_per_cu, split = 65536, 4, 8
+    ntiles = (positions + 4096 + 2048 + tile - 1) // tile
+    nwg = min(ntiles, 256 * wg_per_cu * split)
+    tpw = -(-ntiles // nwg)
+    nwg = -(-ntiles // tpw)
+    nout = -(-nwg // split)
+    tpo = tpw * split
+    ogb = -(-(256 * wg_per_cu * tpw) // tpo)
+    if os.environ.get("PM_JIT_GRADED", "1") == "0" or tpw < 4 or ogb >= nout:
+        return None
+    return (nout - ogb) * tpo * tile
 
 
 def error_mask(types: str) -> int:

@@ -81,13 +81,19 @@ class _DatabaseCache:
         self._lock = threading.Lock()
         self._dbs: Dict[Tuple[str, int], _Entry] = {}
 
-    def _acquire(self, path: str, device: int, shard: Optional[Tuple[int, int]] = None) -> _Entry:
+    def _acquire(self, path: str, device: int, shard: Optional[Tuple[int, int]] = None,
+                 mode: Optional[str] = None) -> _Entry:
+        """``mode``: None = reuse the entry while the file's stamp is
+        unchanged; "cached" = reuse it whatever the stamp (the ranks agreed
+        on a hit, so none of them may open alone); "reopen" = open anew (some
+        rank missed, so every rank takes part in the collective open)."""
         st = os.stat(path)
         stamp = (st.st_mtime_ns, st.st_size)
         key = (os.path.realpath(path), device, shard)
         with self._lock:
             ent = self._dbs.get(key)
-            if ent is None or ent.stamp != stamp:
+            stale = ent is None or (ent.stamp != stamp and mode != "cached") or mode == "reopen"
+            if stale:
                 if ent is not None:
                     self._retire(ent)
                 if shard is None:
@@ -111,24 +117,36 @@ class _DatabaseCache:
             if ent.retired and ent.users == 0:
                 ent.db.close()
 
+    def resident(self, path: str, device: int = 0, shard: Optional[Tuple[int, int]] = None) -> bool:
+        """True if ``path`` is resident and unchanged (a lease would not open it)."""
+        try:
+            st = os.stat(path)
+            key = (os.path.realpath(path), device, shard)
+        except OSError:
+            return False
+        with self._lock:
+            ent = self._dbs.get(key)
+            return ent is not None and ent.stamp == (st.st_mtime_ns, st.st_size)
+
     class _Lease:
-        def __init__(self, cache, path, device, shard=None):
-            self.cache, self.path, self.device, self.shard, self.ent = cache, path, device, shard, None
+        def __init__(self, cache, path, device, shard=None, mode=None):
+            self.cache, self.path, self.device, self.shard, self.mode, self.ent = cache, path, device, shard, mode, None
 
         def __enter__(self):
-            self.ent = self.cache._acquire(self.path, self.device, self.shard)
+            self.ent = self.cache._acquire(self.path, self.device, self.shard, self.mode)
             return self.ent.db
 
         def __exit__(self, *exc):
             self.cache._release(self.ent)
             return False
 
-    def lease(self, path: str, device: int = 0, shard: Optional[Tuple[int, int]] = None):
+    def lease(self, path: str, device: int = 0, shard: Optional[Tuple[int, int]] = None, mode: Optional[str] = None):
         """``with DATABASES.lease(path) as db:`` -- the database stays open
         until the block ends, even if the file is replaced meanwhile.
         ``shard=(world, rank)``: this rank's piece of the file
-        (:class:`~patmatchdocker_amd.shards.ShardedDatabase`)."""
-        return self._Lease(self, path, device, shard)
+        (:class:`~patmatchdocker_amd.shards.ShardedDatabase`); ``mode`` as
+        in ``_acquire``."""
+        return self._Lease(self, path, device, shard, mode)
 
     def get(self, path: str, device: int = 0):
         """The resident database (no lease: for single-threaded callers)."""
@@ -212,7 +230,12 @@ def search_output(patterns: Sequence[str], option: str, datafile: str) -> List[s
             # for all, shards.shared_regions): agree on the file first
             if not shards.agree(os.path.isfile(datafile)):
                 raise FileNotFoundError("%s: missing on some rank" % datafile)
-            lease = DATABASES.lease(datafile, device, shard=(world, rank))
+            # the cache decision is collective too: either every rank reuses
+            # its resident piece, or every rank opens anew (a rank that
+            # missed -- first use, a changed file, a failed open last time --
+            # must not meet its peers' scan collectives with its open's)
+            hit = shards.agree(DATABASES.resident(datafile, device, shard=(world, rank)))
+            lease = DATABASES.lease(datafile, device, shard=(world, rank), mode="cached" if hit else "reopen")
             try:
                 piece = lease.__enter__()
             except Exception:

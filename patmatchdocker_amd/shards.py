@@ -74,6 +74,8 @@ def gather_hits(keys: torch.Tensor, lens: Optional[torch.Tensor], group=None, ds
         return None if out is None else (out[0].to(keys.device), out[1].to(keys.device))
     world = dist.get_world_size(group)
     me = dist.get_rank(group)
+    # dst is a rank of ``group``; dist.gather takes the global rank
+    gdst = dst if dst is None or group is None else dist.get_global_rank(group, dst)
     send_lens = fixed_len is None
     if send_lens and lens is None:
         raise ValueError("lens are needed unless fixed_len is given")
@@ -95,10 +97,10 @@ def gather_hits(keys: torch.Tensor, lens: Optional[torch.Tensor], group=None, ds
             dist.all_gather(all_l, pl, group=group)
     else:
         all_k = [torch.empty_like(pk) for _ in range(world)] if me == dst else None
-        dist.gather(pk, all_k, dst=dst, group=group)
+        dist.gather(pk, all_k, dst=gdst, group=group)
         if send_lens:
             all_l = [torch.empty_like(pl) for _ in range(world)] if me == dst else None
-            dist.gather(pl, all_l, dst=dst, group=group)
+            dist.gather(pl, all_l, dst=gdst, group=group)
         if me != dst:
             return None
     parts = [t[:n] for t, n in zip(all_k, sizes)]
@@ -261,18 +263,22 @@ def _lib_bufsize() -> int:
     return _lib.PM_NRGREP_BUFFER
 
 
-def shared_regions(data, bufsize: Optional[int] = None, group=None):
+def shared_regions(data, bufsize: Optional[int] = None, group=None, failed: Optional[BaseException] = None):
     """nrgrep's search regions of the whole file (``engine.nrgrep_regions``),
     read once: with torch.distributed initialised over more than one rank,
     rank 0 computes them (a one-line record over the buffer size makes that
     a pass over the file) and broadcasts the table -- a collective, every
-    rank of ``group`` calls it.  Otherwise computed here."""
+    rank of ``group`` calls it, also one that could not read the file
+    (``failed``: rank 0 then broadcasts the failure, so every rank raises).
+    Otherwise computed here."""
     from . import engine
     bufsize = _lib_bufsize() if bufsize is None else bufsize
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         obj = [None]
         if dist.get_rank(group) == 0:
             try:
+                if failed is not None:
+                    raise failed
                 obj[0] = engine.nrgrep_regions(data, bufsize)
             except Exception as exc:   # still broadcast: the peers raise too
                 obj[0] = {"failed": repr(exc)}
@@ -328,10 +334,17 @@ class ShardedDatabase:
         a collective (``shared_regions``): every rank of ``group`` opens its
         piece together, and only rank 0 reads the whole file."""
         import mmap
-        with open(path, "rb") as fh:
-            size = os.fstat(fh.fileno()).st_size
-            data = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_READ) if size else b""
-        return cls(data, world, rank, device, open_db=open_db, regions=shared_regions(data, group=group))
+        failed = None
+        try:
+            with open(path, "rb") as fh:
+                size = os.fstat(fh.fileno()).st_size
+                data = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_READ) if size else b""
+        except (OSError, ValueError) as exc:   # still take part in the broadcast
+            failed, data = exc, b""
+        regions = shared_regions(data, group=group, failed=failed)
+        if failed is not None:
+            raise failed
+        return cls(data, world, rank, device, open_db=open_db, regions=regions)
 
     def __len__(self):
         return self.end - self.beg

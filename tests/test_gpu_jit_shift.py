@@ -82,3 +82,42 @@ def test_shifted_partner_at_every_boundary(engine, oracle_mod, monkeypatch, bi):
                 assert got == want, (prog.source, k)
     finally:
         db.close()
+
+
+@pytest.mark.parametrize("length,off", [(64, 1), (63, 2), (62, 2)])
+def test_long_shifted_pair_sees_a_break_at_the_lane_span_end(engine, oracle_mod, monkeypatch, length, off):
+    """A shifted pair with shift + length >= 64: the shifted member's window
+    from lane l's last shifted step reads logical word 32 l + shift + length
+    - 1 of its stream, and k_lane_flags flags lane l for breaks / other
+    bytes in words [32 l, 32 l + 95) only.  A '\\n' planted exactly at word
+    32 l + 95 after the pattern's first length - 1 bases makes a window that
+    only the break kills (k >= 1: the '\\n''s plane code counts at most one
+    mismatch); the oracle's line-bounded scan must agree."""
+    monkeypatch.setenv("PM_JIT", "1")
+    rng = random.Random(101 + length)
+    a = "".join(rng.choice("ACGT") for _ in range(length))
+    b = "".join(rng.choice("ACGT") for _ in range(off)) + a[:length - off]   # b[j + off] == a[j]
+    progs = [compile_pattern(convert("-n", a)), compile_pattern(convert("-n", b))]
+    head = ">chr1 lane span\n"
+    n = 4 * TILE - len(head) - 1
+    seq = [rng.choice("ACGT") for _ in range(n)]
+    for t in (1, 2):
+        for bit in (3, 17, 30):
+            for lane in range(0, 61, 5):
+                # a break at lane `lane`'s first word past its flag span, a's
+                # first length - 1 bases before it, and b's 300 bases earlier
+                q = t * TILE + bit * STREAM + 32 * lane + 95 - len(head)
+                seq[q] = "\n"
+                seq[q - (length - 1):q] = list(a[:length - 1])
+                seq[q - 300 - (length - 1):q - 300] = list(b[:length - 1])
+    text = (head + "".join(seq) + "\n").encode()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        for k in (1, 2):
+            res, _ = engine.scan(db, progs, k=k, types="s", report="all")
+            for prog, r in zip(progs, res):
+                got = list(zip(r[0].tolist(), r[1].tolist()))
+                want = oracle_mod.scan_threads(text, prog, k, "s", skip_headers=True, threads=8, report="all")
+                assert got == want, (prog.source, k, len(got), len(want))
+    finally:
+        db.close()

@@ -267,3 +267,72 @@ def test_rechain_failure_reaches_every_rank():
     for p in procs:
         p.join(timeout=60)
     assert got == {0: "RuntimeError", 1: "ValueError"}
+
+
+def _open_fail_worker(rank, world, port, path, where, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mmap
+        from patmatchdocker_amd import service
+        real = shards.ShardedDatabase.from_file
+        state = {"fail": rank == 1}
+
+        def from_file(cls, p, w, r, device=0):
+            piece = real(p, w, r, device, open_db=False)
+            if where == "after" and state["fail"]:      # e.g. pm_db_create out of memory
+                state["fail"] = False
+                raise MemoryError("HBM upload failed on purpose")
+            return piece
+        shards.ShardedDatabase.from_file = classmethod(from_file)
+        shards.ShardedDatabase.scanner = lambda self: OracleScanner(self)
+        if where == "before" and rank == 1:          # the file cannot be mapped (before the broadcast)
+            real_mmap = mmap.mmap
+
+            def bad_mmap(*a, **k):
+                mmap.mmap = real_mmap
+                raise OSError("mmap failed on purpose")
+            mmap.mmap = bad_mmap
+        out = []
+        for _ in range(2):   # the failing request, then one that must serve normally
+            try:
+                out.append(service.search_output(["AC..", "TATA"], "0", path))
+            except Exception as exc:
+                out.append(type(exc).__name__)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("where", ["before", "after"])
+def test_a_failed_open_does_not_desynchronise_the_ranks(tmp_path, where):
+    """A rank whose piece fails to open -- before the region broadcast
+    (mmap) or after it (the HBM upload) -- makes every rank fail that
+    request, and the next request re-opens on every rank together (the cache
+    decision is collective), so the ranks' collectives still pair up and the
+    output is the single-process one."""
+    from oracle import oracle
+    from patmatchdocker_amd.regex import compile_pattern, engine_banner
+    data = make_fasta(seed=13, n_records=10)
+    path = str(tmp_path / "db.fasta")
+    open(path, "wb").write(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_open_fail_worker, args=(r, 2, port, path, where, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert isinstance(got[0][0], str) and isinstance(got[1][0], str)   # both ranks raised
+    want = []
+    for pat in ["AC..", "TATA"]:
+        prog = compile_pattern(pat, ignore_case=True)
+        hits = oracle.scan_reported(data, prog, 0, "idst", skip_headers=True)
+        want.append(engine_banner(prog, 0) + "\n" + "".join(
+            "[%d, %d]: %s\n" % (b, e, data[b:e].decode("latin-1")) for b, e in hits))
+    assert got[0][1] == want and got[1][1] == ["", ""]

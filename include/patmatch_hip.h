@@ -244,6 +244,38 @@ int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, con
                      const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
                      int errs, int pattern_id, int flags, pm_hits** out);
 
+/* The pattern is a general regular expression -- '|' or a repeated group
+ * (nrgrep's detClass() == 3): nrgrep_coords runs its "regular" engine at
+ * k = 0 (searchPreproc -> regularPreproc 0x40c880), whose plan is priced
+ * over its parse tree (regularFindBest 0x40a500 / minCost 0x409940) and
+ * whose window scanner and nearest-boundary checkMatch (0x408ec0) decide
+ * which overlapping match is printed.  A pattern whose best
+ * window is a class sequence or an extended sequence prints nothing at all
+ * (the state word checkMatch reads is only set by regularScan).  Replaces
+ * one nrgrep_coords run on such a pattern (www/FlaskApp/FlaskApp/patmatch.py:
+ * 733-743; GA(TC){1,2}A -> (GA(TC)(TC)?A), www/bin/patmatch_to_nrgrep.pl:
+ * 307-348, 462-495).                                                      */
+#define PM_REGULAR 512
+/* pm_scan_nfa_wide plus nrgrep's simplified parse tree (regex.py
+ * Program.tree): node i = tree[4i .. 4i+3] = (type 0 leaf / 1 '*' / 2 '|' /
+ * 3 concatenation / 4 '?' / 5 '+', left child, right child, the leaf's
+ * position), preorder, node 0 the root; tree_nullable[i] = the node's
+ * parse-time nullable flag.  With PM_REGULAR (and PM_REPORT_NRGREP, k = 0)
+ * the report is the regular engine's.                                      */
+int pm_scan_nfa_tree(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
+                     const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
+                     int errs, int pattern_id, int flags, int nodes, const int32_t* tree,
+                     const int32_t* tree_nullable, pm_hits** out);
+/* The plan nrgrep's regularPreproc derives (host only, no GPU needed):
+ * out[0] = 2 (a window of out[1] characters scanned backward) or 3 (the
+ * automaton scanned forward), out[2] = detClass of the window (1 / 2: the
+ * engine prints nothing), out[3] = the window's states (with the initial
+ * one); masks[0..4] / [5..9] / [10..14] = the window's states, its initial
+ * and its final states in nrgrep's numbering (position + 1).  out must
+ * hold 4 ints, masks 15 words.                                            */
+int pm_regular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
+                    const int32_t* tree_nullable, int32_t* out, uint64_t* masks);
+
 /* Generates and compiles (hipRTC, gfx950) the bit-sliced start pass that
  * pm_scan_nfa_errs / _wide use for a class sequence with insertions /
  * deletions on a nucleotide database (m * (k + 1) <= 64), without

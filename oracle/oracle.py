@@ -25,7 +25,7 @@ ERR_INS, ERR_DEL, ERR_SUB = 1, 2, 4
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "pm_nrgrep.c", "pm_nrgrep_ext.c",
+    srcs = [os.path.join(_HERE, f) for f in ("pm_oracle.c", "pm_cpuscan.c", "pm_nrgrep.c", "pm_nrgrep_ext.c", "pm_nrgrep_reg.c",
                                               "Makefile")]
     if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
@@ -70,6 +70,13 @@ def lib():
         _LIB.pmx_eextended.argtypes = [ctypes.c_char_p, ctypes.c_int64, pu64, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, pu64, pu64, ctypes.c_int, ctypes.c_int, p64, p64,
                                        ctypes.c_int64]
+        pi32 = ctypes.POINTER(ctypes.c_int32)
+        _LIB.pmr_plan.restype = ctypes.c_int
+        _LIB.pmr_plan.argtypes = [pi32, pi32, ctypes.c_int, pu64, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_int), pu64]
+        _LIB.pmr_regular.restype = ctypes.c_int64
+        _LIB.pmr_regular.argtypes = [ctypes.c_char_p, ctypes.c_int64, pi32, pi32, ctypes.c_int, pu64, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -205,6 +212,8 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
         return scan_extended(text, prog, skip_headers, bufsize, regs)
     if report == "nrgrep" and simple is None and mode is None and k > 0 and prog.kind == "extended":
         return scan_eextended(text, prog, k, types, skip_headers, bufsize, regs)
+    if report == "nrgrep" and simple is None and mode is None and k == 0 and prog.kind == "regular":
+        return scan_regular(text, prog, skip_headers, bufsize, regs)
     if regs is not None or (bufsize and len(text) >= bufsize):
         return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, simple, mode, 0),
                          skip_headers, bufsize, regs=regs)
@@ -472,6 +481,68 @@ def scan_eextended(text: bytes, prog, k: int, types: str = "ids", skip_headers: 
                                 end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
         if n < 0:
             raise ValueError("pmx_eextended rejected %s at k=%d" % (prog.source, k))
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+# ---------------------------------------------------------------------------
+# nrgrep's regular engine at k = 0 (pm_nrgrep_reg.c): '|' and repeated
+# groups, restated from the binary's disassembly
+# ---------------------------------------------------------------------------
+
+def _tree_arrays(prog):
+    pi32 = ctypes.POINTER(ctypes.c_int32)
+    tree = np.array([v for node in prog.tree for v in node], dtype=np.int32)
+    null = np.array(prog.tree_nullable, dtype=np.int32)
+    return tree, null, tree.ctypes.data_as(pi32), null.ctypes.data_as(pi32)
+
+
+def regular_plan(prog):
+    """nrgrep's regularPreproc plan for ``prog`` (pmr_plan): ``type`` 2 = a
+    window of ``ell`` characters scanned backward, 3 = the automaton scanned
+    forward; ``cls`` = detClass of the window (1 / 2: the binary never prints
+    a match, pm_nrgrep_reg.c); ``window`` / ``init`` / ``final`` = state sets
+    (nrgrep numbering: position + 1); ``states`` = the window's m'."""
+    if prog.kind != "regular":
+        raise ValueError("not a regular pattern: %s" % prog.source)
+    B = wide_masks(prog)
+    tree, null, tp, np_ = _tree_arrays(prog)
+    out = (ctypes.c_int * 4)()
+    masks = np.zeros(15, dtype=np.uint64)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    if lib().pmr_plan(tp, np_, len(prog.tree), B.ctypes.data_as(pu64), prog.m, 1 if prog.ignore_case else 0, out,
+                      masks.ctypes.data_as(pu64)) < 0:
+        raise ValueError("no regular plan for %s" % prog.source)
+
+    def as_int(ws):
+        return sum(int(w) << (64 * q) for q, w in enumerate(ws))
+    return {"type": out[0], "ell": out[1], "cls": out[2], "states": out[3], "window": as_int(masks[0:5]),
+            "init": as_int(masks[5:10]), "final": as_int(masks[10:15])}
+
+
+def scan_regular(text: bytes, prog, skip_headers: bool = False, bufsize: int = NRGREP_BUFFER, regs=None):
+    """What nrgrep_coords prints for a class-3 pattern at k = 0 (pmr_regular:
+    nrgrep's plan, regularScan, checkMatch and report rule), region by
+    region (``regions``)."""
+    if prog.kind != "regular":
+        raise ValueError("scan_regular needs a regular pattern")
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_regular(t, prog, False, 0), skip_headers, bufsize, regs=regs)
+    B = wide_masks(prog)
+    tree, null, tp, np_ = _tree_arrays(prog)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = lib().pmr_regular(text, len(text), tp, np_, len(prog.tree), B.ctypes.data_as(pu64), prog.m,
+                              1 if prog.ignore_case else 0, mode, beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                              end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pmr_regular rejected %s" % prog.source)
         if n <= cap:
             hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
             return drop_header_hits(text, hits) if skip_headers else hits

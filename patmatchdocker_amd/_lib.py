@@ -26,6 +26,7 @@ PM_CROSS_LINES = 16
 PM_SCAN_BYTES = 256           # BYTE databases: scan the byte copy, not the 5-bit residue planes
 PM_ESIMPLE = 64               # a class sequence at k > 0: nrgrep's esimple report
 PM_EXTENDED = 128             # classes with '?*+': nrgrep's extended / eextended report
+PM_REGULAR = 512              # '|' / repeated groups: nrgrep's regular report (pm_scan_nfa_tree)
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (
@@ -35,7 +36,8 @@ EXPORTED = (
     "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
-    "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes",
+    "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes", "pm_scan_nfa_tree",
+    "pm_regular_plan",
 )
 PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
@@ -82,6 +84,8 @@ def _declare(lib):
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_scan_nfa_wide.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
+    lib.pm_scan_nfa_tree.argtypes = lib.pm_scan_nfa_wide.argtypes[:-1] + [ctypes.c_int, P, P, PP]
+    lib.pm_regular_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P, P, P]
     lib.pm_ids_jit_compile.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, pu64]
     lib.pm_extended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     lib.pm_eextended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P]

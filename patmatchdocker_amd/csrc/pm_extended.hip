@@ -580,7 +580,9 @@ __global__ __launch_bounds__(256) void k_xt_count(const uint64_t* total_d, uint6
 void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
-    if (X.ee) {
+    if (X.rg) {
+        rg_launch(X, keys, lens, total_d, total_h, acc, tv, s);
+    } else if (X.ee) {
         ee_launch(X, keys, lens, total_d, total_h, acc, tv, X.words, s);
     } else {
         hipLaunchKernelGGL(k_xt_heads, dim3(blocks), dim3(XT_T), 0, s, X, keys, total_d, total_h, acc, tv);

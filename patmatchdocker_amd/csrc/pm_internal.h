@@ -924,8 +924,31 @@ bool ee_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64
               size_t& o_tab);
 
 
+// nrgrep's regular engine at k = 0 (pm_regular.hip): a pattern with '|' or a
+// repeated group (detClass() == 3, PM_REGULAR) -- regularFindBest's plan
+// over nrgrep's tree, regularScan and checkMatch replayed per cluster
+constexpr int RG_NW = 5;       // words of a state set: positions + 1 <= 320
+struct RgTree {                // Program.tree (regex.py): node i = type, left, right, position
+    int nodes = 0;
+    const int32_t* tree = nullptr;
+    const int32_t* nullable = nullptr;
+};
+struct RgSlot {                // one pattern (device, uploaded as is)
+    int32_t ms, nw, mp, type, ell, anchors, pid;   // states, words (1 / RG_NW), window states
+    int64_t max_len;           // the longest match, -1: walk whole lines
+    uint64_t finit, ffinal;    // the window scanner's initial / final states
+    uint64_t final_[RG_NW], vis[RG_NW];   // the automaton's final states; the states SLICE sees
+    int32_t unmap[64];         // window state -> automaton state (P->0x860)
+    uint64_t o_arr, o_rev, o_B, o_Bw, o_A, o_fw, o_rw;   // word offsets in the table blob
+};
+// builds the plan and tables into `up`; false when nothing can be printed
+// (the window is a class / extended sequence: P->match is never set)
+bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, uint32_t flags, int32_t pid,
+              Upload& up, size_t& o_slot, size_t& o_tab);
+
 struct XtPrep {
     const XtSlot* slot = nullptr;
+    const RgSlot* rg = nullptr;   // the regular walk instead
     const EeSlot* ee = nullptr;   // k > 0: the eextended walk instead
     const uint64_t* tab = nullptr;
     int32_t pid = 0;
@@ -939,6 +962,10 @@ uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
 
 void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, const TextView& tv, int words, hipStream_t s);
+// regular heads + walk on s (keys/lens rewritten in place, acc bit 0 =
+// reported); xt_launch calls it when X.rg is set
+void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, const TextView& tv, hipStream_t s);
 // builds the plan and tables of one pattern into `up`; returns the slot's
 // and the table blob's offsets
 void xt_build(const uint64_t* B, int W, int m, const uint64_t* opt, const uint64_t* rep, int64_t max_len,

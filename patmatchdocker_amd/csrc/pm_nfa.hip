@@ -489,10 +489,11 @@ bool extended_shape(int m, int W, const uint64_t* first, const uint64_t* last, c
 // words (W = ceil(m / 64)).
 void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t* follow, const uint64_t* first,
               const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
-              pm_hits** out) {
+              pm_hits** out, const RgTree* rgt = nullptr) {
     require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES |
-                       PM_ESIMPLE | PM_EXTENDED)) == 0,
+                       PM_ESIMPLE | PM_EXTENDED | PM_REGULAR)) == 0,
             "bad flags");
+    require(!(flags & PM_REGULAR) || rgt != nullptr, "PM_REGULAR needs nrgrep's tree (pm_scan_nfa_tree)");
     require(db != nullptr, "db is NULL");
     std::lock_guard<std::recursive_mutex> lk(db->mu);
     require(out != nullptr && byte_mask && follow && first && last, "null argument");
@@ -519,6 +520,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // (k = 0, pm_extended.hip) or eextended engine (k > 0, pm_eextended.hip)
     // does; its walk computes the ends
     const bool extended = (flags & PM_EXTENDED) && (flags & PM_REPORT_NRGREP);
+    // PM_REGULAR: a regular pattern reported as nrgrep's regular engine does
+    // at k = 0 (pm_regular.hip); its walk computes the ends
+    const bool regular = (flags & PM_REGULAR) && (flags & PM_REPORT_NRGREP) && k == 0 && !extended;
     uint64_t xopt[4] = {}, xrep[4] = {};
     require(!(flags & PM_EXTENDED) || extended_shape(m, W, first, last, follow, xopt, xrep),
             "PM_EXTENDED needs a sequence of classes with '?', '*', '+'");
@@ -607,9 +611,32 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         ee_lines = ee_build(byte_mask, W, m, xopt, xrep, k, errs,
                             unbounded ? -1 : (int64_t)max_len + ((errs & PM_ERR_INS) ? k : 0), (uint32_t)flags,
                             pattern_id, ee_all, up, o_xslot, o_xtab);
+    bool rg_prints = false;
+    if (regular) {
+        rg_prints = rg_build(*rgt, byte_mask, W, m, unbounded ? -1 : (int64_t)max_len, (uint32_t)flags, pattern_id,
+                             up, o_xslot, o_xtab);
+        if (!rg_prints) {
+            // the window is a class / extended sequence: simpleScan /
+            // extendedScan never set the state word checkMatch reads, so
+            // nrgrep_coords prints no match (pm_regular.hip); no scan runs
+            pm_hits* h = new pm_hits();
+            h->device = db->device;
+            h->keys = static_cast<uint64_t*>(pool_get(db->device, 8, &h->keys_cap));
+            h->lens = static_cast<uint32_t*>(pool_get(db->device, 4, &h->lens_cap));
+            hits_ready(db, h);
+            *out = h;
+            return;
+        }
+    }
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     XtPrep xtp;
+    if (regular) {
+        xtp.rg = reinterpret_cast<const RgSlot*>(d_up + o_xslot);
+        xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
+        xtp.pid = pattern_id;
+        xtp.words = m + 1 <= 64 ? 1 : RG_NW;
+    }
     if (extended) {
         if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
         else xtp.ee = reinterpret_cast<const EeSlot*>(d_up + o_xslot);
@@ -737,7 +764,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // eextended: an alignment starting a header line prints one position
     // before it (pm_eextended.hip): every header line starts a cluster
     if (extended && k > 0 && !ee_lines) total = ee_add_headers(db, h, total, pattern_id);
-    if (total && !esimple && !extended) {
+    if (total && !esimple && !extended && !regular) {
         a.starts = h->keys;
         a.nstarts = total;
         a.lens = h->lens;
@@ -759,7 +786,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     if (esimple) {
         // the walk replaces the lengths; until it runs they are unset
         report_sync(db, h, (uint32_t)flags, total, false, &esp);
-    } else if (extended) {
+    } else if (extended || regular) {
         report_sync(db, h, (uint32_t)flags, total, false, nullptr, &xtp);
     } else if (report_needed(db, (uint32_t)flags, cross)) {
         report_sync(db, h, (uint32_t)flags, total, cross);
@@ -787,6 +814,17 @@ extern "C" int pm_scan_nfa_errs(pm_db* db, int m, const uint64_t* byte_mask, con
         require(m >= 1 && m <= 64, "m out of range (pm_scan_nfa_wide takes longer automata)");
         require(!(flags & PM_CROSS_LINES), "bad flags");
         scan_nfa(db, m, 1, byte_mask, follow, &first, &last, max_len, min_len, k, errs, pattern_id, flags, out);
+    });
+}
+
+extern "C" int pm_scan_nfa_tree(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
+                                const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
+                                int errs, int pattern_id, int flags, int nodes, const int32_t* tree,
+                                const int32_t* tree_nullable, pm_hits** out) {
+    return guarded([&] {
+        require(nodes >= 1 && tree != nullptr && tree_nullable != nullptr, "null tree");
+        const RgTree t{nodes, tree, tree_nullable};
+        scan_nfa(db, m, words, byte_mask, follow, first, last, max_len, min_len, k, errs, pattern_id, flags, out, &t);
     });
 }
 

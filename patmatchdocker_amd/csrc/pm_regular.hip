@@ -1,0 +1,786 @@
+// pm_regular.hip -- what nrgrep_coords reports for a regular pattern at k = 0
+// (nrgrep's "regular" engine), on the GPU.
+//
+// The reference runs `nrgrep_coords -i -b 1600000 -k 0 '<pattern>'`
+// (www/FlaskApp/FlaskApp/patmatch.py:733-743); a PatMatch pattern that
+// repeats a parenthesised group -- GA(TC){1,2}A becomes (GA(TC)(TC)?A)
+// (patmatch_to_nrgrep.pl:307-348, :462-495) -- or a user pattern with '|' is
+// a general regular expression (detClass() == 3) and searchPreproc picks
+// regularPreproc (0x40c880).  The binary's code (disassembled, never run;
+// DESIGN.md §1, oracle/pm_nrgrep_reg.c):
+//
+//  * plan (regularFindBest 0x40a500, minCost 0x409940): every state's
+//    distance to a final state; per state and length, the chance a random
+//    text (letterProb, .data 0x621120) runs along the automaton; minCost
+//    over nrgrep's tree: a leaf opens a window of l levels (the states
+//    reachable within l - 1 arrows), '|' joins both sides' windows, a
+//    concatenation takes its cheaper side, '*' / '?' cannot hold one; the
+//    best cost / (l - cost + 1) under 0.65 is scanned backward (type 2),
+//    else the whole automaton forward (type 3);
+//  * detClass (0x41ac90) of the window: a class sequence (1) or an extended
+//    sequence (2) runs simpleScan / extendedScan, which never set the state
+//    word checkMatch reads (P->match, +0x28, zeroed at 0x40cb91): nothing is
+//    ever printed.  A regular window (3) runs regularScan (0x4091d0);
+//  * scan: backward, windows of l characters read right to left over the
+//    window's reversed automaton with every state initial (a factor test:
+//    a dead character moves the window past it); a whole window whose last
+//    set leads back to the window's initial states goes to checkMatch with
+//    that set.  Forward: the window automaton with state 0 looping, fresh
+//    after each '\n', never tested after the region's last byte;
+//  * verify (checkMatch 0x408ec0): for each state of the set in state order,
+//    inside the line (never before R): the shortest end forward (fwdCheck
+//    0x408bc0) and the nearest start backward (bwdCheck 0x408d50) around it
+//    on the whole automaton (transition tables in slices of W states of one
+//    word: SLICE 0x41b8e0 loses the states of a slice that straddles a word);
+//  * report (recSearchFile 0x402250): the first verified candidate is
+//    printed, R = its end.
+//
+// GPU form.  The automaton kernels (pm_nfa.hip) give every start of a match;
+// a printed match is a match, so its start is one of them and the window
+// that printed it starts inside it.  Every window start that can pass the
+// factor test is examined in increasing order whatever the shifts were, so
+// the result from R depends on R only: starts more than 2 max_len + 2 apart
+// form independent clusters, one thread replays the scanner and checkMatch
+// over a cluster from R = first - max_len - 1 (forward: the automaton's
+// final states are the window's, so an earlier start only matters through
+// a match that ends before it).  Unbounded patterns ('*', '+') and forward
+// plans over more than 64 states walk whole lines.  The printed matches are
+// written in place and compacted by the report pass's scatter.
+#include "pm_internal.h"
+
+#include <algorithm>
+#include <array>
+
+namespace pm {
+
+namespace {
+
+#pragma clang fp contract(off)
+
+enum { T_LEAF = 0, T_STAR = 1, T_OR = 2, T_CAT = 3, T_OPT = 4, T_PLUS = 5 };
+
+using Set = std::array<uint64_t, RG_NW>;
+
+inline bool has(const Set& s, int i) { return (s[i >> 6] >> (i & 63)) & 1; }
+inline void put(Set& s, int i) { s[i >> 6] |= 1ull << (i & 63); }
+inline void join(Set& d, const Set& s) {
+    for (int q = 0; q < RG_NW; ++q) d[q] |= s[q];
+}
+inline bool meets(const Set& a, const Set& b) {
+    uint64_t x = 0;
+    for (int q = 0; q < RG_NW; ++q) x |= a[q] & b[q];
+    return x != 0;
+}
+inline int bits(const Set& s) {
+    int n = 0;
+    for (int q = 0; q < RG_NW; ++q) n += __builtin_popcountll(s[q]);
+    return n;
+}
+
+struct Node {
+    int type, a, b, state;
+    bool nullable;
+    Set pm{}, first{}, last{};
+};
+
+// the automaton over nrgrep's states (regularLength 0x40b2a0: state 0 is
+// the initial one, leaves are numbered 1.. left to right)
+struct Automaton {
+    int ms = 0;
+    std::vector<Node> nd;
+    std::vector<Set> arrows, rev;
+    Set final_{}, vis{};
+    std::vector<Set> B;   // [256] by folded byte
+
+    void masks(int i) {   // firstLast 0x4086b0 / setMaskPos 0x41ad90
+        Node& e = nd[i];
+        if (e.type == T_LEAF) {
+            put(e.pm, e.state);
+            put(e.first, e.state);
+            put(e.last, e.state);
+            return;
+        }
+        masks(e.a);
+        const Node& a = nd[e.a];
+        e.pm = a.pm;
+        if (e.type == T_OR || e.type == T_CAT) {
+            masks(e.b);
+            const Node& b = nd[e.b];
+            join(e.pm, b.pm);
+            if (e.type == T_OR) {
+                e.first = a.first;
+                join(e.first, b.first);
+                e.last = a.last;
+                join(e.last, b.last);
+            } else {
+                e.first = a.first;
+                if (a.nullable) join(e.first, b.first);
+                e.last = b.last;
+                if (b.nullable) join(e.last, a.last);
+            }
+        } else {
+            e.first = a.first;
+            e.last = a.last;
+        }
+    }
+    void follow(int i, int s, Set& out) const {   // follow 0x4089b0
+        const Node& e = nd[i];
+        if (e.type == T_LEAF) return;
+        if (e.type == T_OPT) return follow(e.a, s, out);
+        if (e.type == T_STAR || e.type == T_PLUS) {
+            follow(e.a, s, out);
+            if (has(nd[e.a].last, s)) join(out, nd[e.a].first);
+            return;
+        }
+        if (e.type == T_CAT && has(nd[e.a].last, s)) join(out, nd[e.b].first);
+        if (has(nd[e.a].pm, s)) follow(e.a, s, out);
+        if (has(nd[e.b].pm, s)) follow(e.b, s, out);
+    }
+};
+
+Automaton make_automaton(const RgTree& t, const uint64_t* B, int W, int npos) {
+    Automaton A;
+    require(t.nodes >= 1 && t.tree && t.nullable, "regular: no tree");
+    require(npos >= 1 && npos + 1 <= 64 * RG_NW, "regular: positions out of range");
+    A.ms = npos + 1;
+    A.nd.resize(t.nodes);
+    int leaves = 0;
+    for (int i = 0; i < t.nodes; ++i) {
+        Node& e = A.nd[i];
+        e.type = t.tree[4 * i];
+        e.a = t.tree[4 * i + 1];
+        e.b = t.tree[4 * i + 2];
+        e.nullable = t.nullable[i] != 0;
+        require(e.type >= 0 && e.type <= 5, "regular: bad node type");
+        if (e.type == T_LEAF) {
+            // an empty leaf inside the tree has no state (its minCost would
+            // read an unset field): refused
+            require(t.tree[4 * i + 3] == leaves, "regular: leaves must be numbered left to right", PM_E_UNSUPPORTED);
+            e.state = ++leaves;
+        } else {
+            require(e.a > i && e.a < t.nodes, "regular: bad child");
+            require(!(e.type == T_OR || e.type == T_CAT) || (e.b > i && e.b < t.nodes), "regular: bad child");
+        }
+    }
+    require(leaves == npos, "regular: the tree's leaves are not the automaton's positions");
+    A.masks(0);
+    A.arrows.assign(A.ms, Set{});
+    A.rev.assign(A.ms, Set{});
+    A.arrows[0] = A.nd[0].first;
+    for (int s = 1; s < A.ms; ++s) A.follow(0, s, A.arrows[s]);
+    A.final_ = A.nd[0].last;
+    for (int s = 0; s < A.ms; ++s)
+        for (int q = 0; q < A.ms; ++q)
+            if (has(A.arrows[s], q)) put(A.rev[q], s);
+    A.B.assign(256, Set{});
+    for (int c = 0; c < 256; ++c) {
+        const uint64_t* bp = B + (size_t)fold((uint8_t)c) * W;
+        for (int p = 0; p < npos; ++p)
+            if ((bp[p >> 6] >> (p & 63)) & 1) put(A.B[c], p + 1);
+    }
+    const int ntab = (A.ms + 15) / 16, Wd = (A.ms - 1 + ntab) / ntab;   // regularPreproc 0x40cb26
+    for (int tb = 0; tb < ntab; ++tb)
+        for (int b = tb * Wd; b < tb * Wd + Wd && b < A.ms; ++b)
+            if ((b >> 6) == ((tb * Wd) >> 6)) put(A.vis, b);
+    return A;
+}
+
+struct Costs {
+    int L = 0;
+    std::vector<int> dist;
+    std::vector<double> C;       // [ms][L]
+    std::vector<Set> M50, M70;   // [ms][L]
+};
+
+double min_cost(const Automaton& A, const Costs& c, int i, int ell, Set& win, Set& ini, Set& fin) {
+    const Node& e = A.nd[i];
+    switch (e.type) {
+    case T_LEAF: {
+        if (c.dist[e.state] < ell) return ell + 1.0;
+        win = c.M70[(size_t)e.state * c.L + ell];
+        ini = Set{};
+        put(ini, e.state);
+        fin = c.M50[(size_t)e.state * c.L + ell];
+        return c.C[(size_t)e.state * c.L + ell];
+    }
+    case T_STAR:
+    case T_OPT:
+        return ell + 1.0;
+    case T_PLUS:
+        return min_cost(A, c, e.a, ell, win, ini, fin);
+    case T_OR: {
+        Set w2{}, i2{}, f2{};
+        const double c1 = min_cost(A, c, e.a, ell, win, ini, fin);
+        const double c2 = min_cost(A, c, e.b, ell, w2, i2, f2);
+        join(win, w2);
+        join(ini, i2);
+        fin = f2;
+        if (bits(win) > 64) {
+            win = ini = fin = Set{};
+            return ell + 1.0;
+        }
+        return std::max(c1, c2);
+    }
+    default: {
+        Set w2{}, i2{}, f2{};
+        const double c1 = min_cost(A, c, e.a, ell, win, ini, fin);
+        const double c2 = min_cost(A, c, e.b, ell, w2, i2, f2);
+        if (c2 >= c1) return c1;
+        win = w2;
+        ini = i2;
+        fin = f2;
+        return c2;
+    }
+    }
+}
+
+int det_class(const Automaton& A, int i, const Set& pos) {   // detClass 0x41ac90 / detClass1 0x418420
+    const Node& e = A.nd[i];
+    if (!meets(e.pm, pos)) return 1;
+    if (e.type == T_LEAF) return 1;
+    if (e.type == T_OR) return 3;
+    if (e.type == T_CAT) return std::max(det_class(A, e.a, pos), det_class(A, e.b, pos));
+    int r = det_class(A, e.a, pos);
+    if (r == 1) r = 2;
+    return A.nd[e.a].type == T_LEAF ? r : 3;
+}
+
+struct Plan {
+    int type = 3, ell = 0, cls = 3;
+    Set win{}, winit{}, wfinal{};
+};
+
+Plan plan_of(const Automaton& A) {   // regularFindBest 0x40a500 (K = 0)
+    const int ms = A.ms;
+    Costs c;
+    c.dist.assign(ms, 1);
+    for (int i = 0; i < ms; ++i) {
+        Set S{};
+        put(S, i);
+        while (!meets(S, A.final_) && c.dist[i] <= ms + 1) {
+            ++c.dist[i];
+            Set T{};
+            for (int j = 0; j < ms; ++j)
+                if (has(S, j)) join(T, A.arrows[j]);
+            join(S, T);
+        }
+    }
+    const int L = std::min(c.dist[0], 64);
+    c.L = L;
+    double lp[256];
+    letter_probs(lp);
+    std::vector<double> prob(ms, 0.0);
+    for (int i = 0; i < ms; ++i)
+        for (int ch = 0; ch < 256; ++ch)
+            if (has(A.B[ch], i)) prob[i] += lp[ch];
+    const size_t ML = (size_t)ms * L;
+    std::vector<double> cost(ML, 0.0);
+    c.M50.assign(ML, Set{});
+    c.M70.assign(ML, Set{});
+    for (int i = 0; i < ms; ++i) {
+        cost[(size_t)i * L] = 1.0;
+        if (L > 1) {
+            cost[(size_t)i * L + 1] = prob[i];
+            put(c.M50[(size_t)i * L + 1], i);
+            put(c.M70[(size_t)i * L + 1], i);
+        }
+    }
+    for (int l = 1; l + 1 < L; ++l)
+        for (int i = 0; i < ms; ++i) {
+            double s = 0.0;
+            Set M{};
+            for (int j = 0; j < ms; ++j)
+                if (has(A.arrows[i], j)) {
+                    s += cost[(size_t)j * L + l];
+                    join(M, c.M50[(size_t)j * L + l]);
+                }
+            s *= prob[i];
+            cost[(size_t)i * L + l + 1] = 1.0 < s ? 1.0 : s;
+            c.M50[(size_t)i * L + l + 1] = M;
+            c.M70[(size_t)i * L + l + 1] = c.M70[(size_t)i * L + l];
+            join(c.M70[(size_t)i * L + l + 1], M);
+        }
+    std::vector<double> P((size_t)ms * L * L, 0.0);
+    auto pi = [&](int i, int l, int a) -> double& { return P[((size_t)i * L + l) * L + a]; };
+    for (int i = 0; i < ms; ++i)
+        for (int l = 0; l < L; ++l) pi(i, l, 0) = 1.0;
+    for (int l = 1; l < L; ++l)
+        for (int a = 1; a <= l; ++a)
+            for (int i = 0; i < ms; ++i) {
+                double v = cost[(size_t)i * L + a];
+                if (a < l)
+                    for (int j = 0; j < ms; ++j)
+                        if (has(A.arrows[i], j)) v = 1.0 - (1.0 - v) * (1.0 - pi(j, l - 1, a));
+                pi(i, l, a) = v;
+            }
+    c.C.assign(ML, 0.0);
+    for (int i = 0; i < ms; ++i)
+        for (int l = 0; l < L; ++l) {
+            double s = 0.0;   // K = 0
+            for (int a = 0; a <= l; ++a) s += pi(i, l, a);
+            c.C[(size_t)i * L + l] = s;
+        }
+    Plan p;
+    double best = 0.65;
+    int ell = L - 1;
+    if (ell > 0 && !(1.0 >= 0.65 * ell)) {
+        for (;;) {
+            Set w{}, in{}, fi{};
+            const double cc = min_cost(A, c, 0, ell, w, in, fi);
+            if (ell + 1.0 > cc) {
+                const double r = cc / ((double)ell - cc + 1.0);
+                if (best > r) {
+                    best = r;
+                    p.win = w;
+                    p.winit = in;
+                    p.wfinal = fi;
+                    p.ell = ell;
+                }
+            }
+            if (--ell == 0 || 1.0 >= best * ell) break;
+        }
+    }
+    if (0.65 > best) {
+        p.type = 2;
+    } else {
+        p.type = 3;
+        p.ell = 0;
+        p.win = p.winit = Set{};
+        put(p.winit, 0);
+        if (ms <= 64) {
+            for (int s = 0; s < ms; ++s) put(p.win, s);
+            p.wfinal = A.final_;
+        } else {   // 0x40b175: breadth-first layers while at most 64 states are reached
+            Set reach = p.winit, layer{};
+            while (bits(reach) <= 64) {
+                for (int q = 0; q < RG_NW; ++q) layer[q] = reach[q] & ~p.win[q];
+                join(p.win, reach);
+                reach = Set{};
+                for (int s = 0; s < ms; ++s)
+                    if (has(p.win, s)) join(reach, A.arrows[s]);
+            }
+            p.wfinal = layer;
+            join(p.wfinal, A.final_);
+            for (int q = 0; q < RG_NW; ++q) p.wfinal[q] &= p.win[q];
+        }
+    }
+    p.cls = det_class(A, 0, p.win);
+    return p;
+}
+
+int window_states(const Plan& p, int ms) {
+    int mp = 1;
+    for (int s = 1; s < ms; ++s) mp += has(p.win, s);
+    return mp;
+}
+
+}  // namespace
+
+bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, uint32_t flags, int32_t pid,
+              Upload& up, size_t& o_slot, size_t& o_tab) {
+    const Automaton A = make_automaton(t, B, W, npos);
+    const Plan P = plan_of(A);
+    if (P.cls != 3) return false;   // simpleScan / extendedScan never leave P->match set: nothing prints
+    const int ms = A.ms, mp = window_states(P, ms);
+    require(mp <= 64, "regular: a window of more than 64 states", PM_E_UNSUPPORTED);
+    RgSlot S{};
+    S.ms = ms;
+    S.nw = ms <= 64 ? 1 : RG_NW;
+    S.mp = mp;
+    S.type = P.type;
+    S.ell = P.ell;
+    S.anchors = (int32_t)(flags & (PM_ANCHOR_START | PM_ANCHOR_END));
+    S.pid = pid;
+    // bounded clusters unless the pattern is unbounded or the forward
+    // window's final states are not the automaton's (more than 64 states)
+    S.max_len = (max_len < 0 || (P.type == 3 && ms > 64)) ? -1 : max_len;
+    for (int q = 0; q < RG_NW; ++q) {
+        S.final_[q] = A.final_[q];
+        S.vis[q] = A.vis[q];
+    }
+    // regularRemapStates 0x40bab0: window states 1.. in state order, 0 the
+    // virtual initial state
+    std::vector<int> map(ms, 0);
+    int k = 0;
+    for (int s = 1; s < ms; ++s)
+        if (has(P.win, s)) map[s] = ++k;
+    for (int s = 0; s < ms; ++s)
+        if (has(P.win, s)) S.unmap[map[s]] = s;
+    std::vector<uint64_t> tab;
+    auto take = [&](size_t words) {
+        const uint64_t o = tab.size();
+        tab.resize(tab.size() + words, 0);
+        return o;
+    };
+    const int nw = S.nw;
+    S.o_arr = take((size_t)ms * nw);
+    S.o_rev = take((size_t)ms * nw);
+    S.o_B = take((size_t)256 * nw);
+    S.o_Bw = take(256);
+    S.o_A = take(256);
+    S.o_fw = take(64);
+    S.o_rw = take(64);
+    for (int s = 0; s < ms; ++s)
+        for (int q = 0; q < nw; ++q) {
+            tab[S.o_arr + (size_t)s * nw + q] = A.arrows[s][q];
+            tab[S.o_rev + (size_t)s * nw + q] = A.rev[s][q];
+        }
+    for (int c = 0; c < 256; ++c)
+        for (int q = 0; q < nw; ++q) tab[S.o_B + (size_t)c * nw + q] = A.B[c][q];
+    uint64_t* fw = tab.data() + S.o_fw;
+    for (int s = 0; s < ms; ++s)
+        if (has(P.winit, s)) fw[0] |= 1ull << map[s];
+    for (int s = 0; s < ms; ++s)
+        if (has(P.win, s))
+            for (int q = 0; q < ms; ++q)
+                if (has(P.win, q) && has(A.arrows[s], q)) fw[map[s]] |= 1ull << map[q];
+    uint64_t fin = 0;
+    for (int s = 0; s < ms; ++s)
+        if (has(P.wfinal, s)) fin |= 1ull << map[s];
+    uint64_t* Bw = tab.data() + S.o_Bw;
+    for (int c = 0; c < 256; ++c)
+        for (int s = 0; s < ms; ++s)
+            if (has(P.win, s) && has(A.B[c], s)) Bw[c] |= 1ull << map[s];
+    const uint64_t all = mp >= 64 ? ~0ull : (1ull << mp) - 1;
+    if (P.type == 2) {   // regularLoadFast 0x40c5dd: reversed, every state initial
+        uint64_t* rw = tab.data() + S.o_rw;
+        for (int a = 0; a < mp; ++a)
+            for (int b = 0; b < mp; ++b)
+                if ((fw[a] >> b) & 1) rw[b] |= 1ull << a;
+        S.finit = all;
+        S.ffinal = 1;
+        uint64_t* Av = tab.data() + S.o_A;
+        for (int c = 0; c < 256; ++c) {
+            const uint64_t d = all & Bw[c];
+            for (int q = 0; q < mp; ++q)
+                if ((d >> q) & 1) Av[c] |= rw[q];
+        }
+    } else {             // 0x40c771: state 0 loops on every byte
+        fw[0] |= 1;
+        for (int c = 0; c < 256; ++c) Bw[c] |= 1;
+        S.finit = 1;
+        S.ffinal = fin;
+    }
+    o_slot = up.add(&S, sizeof(S));
+    o_tab = up.add(tab.data(), tab.size() * 8);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// device: the per-cluster replay
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t RG_POS_MASK = (1ull << 48) - 1;
+constexpr uint64_t RG_SCAN = 1ull << 16;   // lines mode: how far a head looks back for a line break
+constexpr uint32_t RG_T = 256;
+constexpr uint64_t RG_NONE = ~0ull;
+
+__global__ __launch_bounds__(RG_T) void k_rg_heads(XtPrep X, const uint64_t* __restrict__ keys, const uint64_t* total_d,
+                                                   uint64_t total_h, uint8_t* __restrict__ acc, TextView tv) {
+    const uint64_t total = total_d ? *total_d : total_h;
+    const RgSlot& S = *X.rg;
+    for (uint64_t i = blockIdx.x * (uint64_t)RG_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * RG_T) {
+        bool head = i == 0 || (keys[i] >> 48) != (keys[i - 1] >> 48);
+        if (!head) {
+            const uint64_t a = keys[i - 1] & RG_POS_MASK, b = keys[i] & RG_POS_MASK;
+            if (xt_region(tv, a) != xt_region(tv, b)) head = true;
+            else if (S.max_len >= 0) head = b - a > 2 * (uint64_t)S.max_len + 2;
+            else head = xt_brk_between(tv, a, b, RG_SCAN);
+        }
+        acc[i] = head ? 2 : 0;
+    }
+}
+
+template <int NW>
+struct RgWalk {
+    const RgSlot* S;
+    const uint64_t* tab;
+    TextView tv;
+    uint64_t n;        // the region end
+    uint64_t R;
+    uint64_t nl_lo;    // the last '\n' seen below the record cursor (~0: none since the walk began)
+    uint64_t nl_hi;    // the first '\n' at or after it (n: none)
+
+    __device__ uint8_t at(uint64_t p) const { return xt_byte(tv, p); }
+    __device__ bool is_nl(uint64_t p) const { return xt_brk(tv, p) && at(p) == (uint8_t)'\n'; }
+    __device__ uint64_t next_nl(uint64_t p) const {
+        if (tv.nuc_layout) {
+            while (p < n) {
+                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
+                if (!z) {
+                    p = ((p >> 5) + 1) << 5;
+                    continue;
+                }
+                p += (uint64_t)__builtin_ctz(z);
+                if (p >= n) break;
+                if (at(p) == (uint8_t)'\n') return p;
+                ++p;
+            }
+            return n;
+        }
+        for (; p < n; ++p)
+            if (tv.raw[p] == (uint8_t)'\n') return p;
+        return n;
+    }
+    // recGetRecord 0x402030 (rp non-decreasing over a walk)
+    __device__ void record(uint64_t rp, uint64_t& rb, uint64_t& re) {
+        while (nl_hi < rp) {
+            nl_lo = nl_hi;
+            nl_hi = next_nl(nl_hi + 1);
+        }
+        rb = (nl_lo != ~0ull && nl_lo >= R) ? nl_lo + 1 : R;
+        re = nl_hi;
+    }
+    __device__ bool left_ok(uint64_t p, uint64_t lim) const {
+        return !((S->anchors & PM_ANCHOR_START) && p > lim && at(p - 1) != (uint8_t)'\n');
+    }
+    __device__ bool right_ok(uint64_t q, uint64_t lim) const {
+        return !((S->anchors & PM_ANCHOR_END) && q < lim && at(q) != (uint8_t)'\n');
+    }
+    // one step of the whole automaton over the states SLICE sees
+    __device__ void step(const uint64_t (&D)[NW], const uint64_t* tr, uint64_t (&T)[NW]) const {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) T[q] = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            uint64_t b = D[q] & S->vis[q];
+            while (b) {
+                const int s = 64 * q + __builtin_ctzll(b);
+                b &= b - 1;
+                const uint64_t* row = tr + (size_t)s * NW;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) T[w] |= row[w];
+            }
+        }
+    }
+    // fwdCheck 0x408bc0: the shortest end from state s reading t[p]
+    __device__ uint64_t fwd(uint64_t p, uint64_t lim, int s) const {
+        uint64_t D[NW], T[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) D[q] = q == (s >> 6) ? 1ull << (s & 63) : 0ull;
+        const uint64_t* B = tab + S->o_B;
+        for (;;) {
+            uint64_t hit = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) hit |= D[q] & S->final_[q];
+            if (hit && right_ok(p + 1, lim + 1)) return p;
+            if (p == lim) return RG_NONE;
+            step(D, tab + S->o_arr, T);
+            ++p;
+            const uint64_t* b = B + (size_t)at(p) * NW;
+            uint64_t any = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                D[q] = T[q] & b[q];
+                any |= D[q];
+            }
+            if (!any) return RG_NONE;
+        }
+    }
+    // bwdCheck 0x408d50: the nearest start, state s reading t[p - 1]
+    __device__ uint64_t bwd(uint64_t p, uint64_t lim, int s) const {
+        uint64_t D[NW], T[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) D[q] = q == (s >> 6) ? 1ull << (s & 63) : 0ull;
+        const uint64_t* B = tab + S->o_B;
+        for (;;) {
+            if ((D[0] & 1) && left_ok(p, lim)) return p;
+            if (p == lim) return RG_NONE;
+            --p;
+            const uint64_t* b = B + (size_t)at(p) * NW;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) D[q] &= b[q];
+            step(D, tab + S->o_rev, T);
+            uint64_t any = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                D[q] = T[q];
+                any |= T[q];
+            }
+            if (!any) return RG_NONE;
+        }
+    }
+    // checkMatch 0x408ec0: the states of `match` in state order
+    __device__ bool check(uint64_t pos, uint64_t match, uint64_t& mb, uint64_t& me) {
+        if (S->type == 3 && pos == 0) return false;
+        const uint64_t rp = S->type == 3 ? pos - 1 : pos;
+        uint64_t rb, re;
+        record(rp, rb, re);
+        if (rp < rb || rp >= re) return false;
+        const uint64_t lim = S->mp >= 64 ? ~0ull : (1ull << S->mp) - 1;
+        match &= lim;
+        while (match) {
+            const int i = __builtin_ctzll(match);
+            match &= match - 1;
+            const int s = S->unmap[i];
+            uint64_t st, en;
+            if (S->type == 3) {
+                st = bwd(pos, rb, s);
+                if (st == RG_NONE) continue;
+                en = fwd(pos - 1, re - 1, s);
+                if (en == RG_NONE) continue;
+            } else {
+                en = fwd(pos, re - 1, s);
+                if (en == RG_NONE) continue;
+                st = bwd(pos + 1, rb, s);
+                if (st == RG_NONE) continue;
+            }
+            mb = st;
+            me = en + 1;
+            return true;
+        }
+        return false;
+    }
+    __device__ static uint64_t wtrans(const uint64_t* tb, uint64_t d) {
+        uint64_t r = 0;
+        while (d) {
+            r |= tb[__builtin_ctzll(d)];
+            d &= d - 1;
+        }
+        return r;
+    }
+    // regularScan 0x4091d0 from R; false when no candidate <= stop verifies
+    __device__ bool scan(uint64_t stop, uint64_t& mb, uint64_t& me) {
+        const uint64_t* Bw = tab + S->o_Bw;
+        if (S->type == 2) {   // backward windows (0x40921c)
+            const uint64_t ell = (uint64_t)S->ell;
+            const uint64_t* A = tab + S->o_A;
+            const uint64_t* rw = tab + S->o_rw;
+            uint64_t ws = R;
+            while (ws + ell <= n) {
+                if (ws > stop) return false;
+                uint64_t rsi = A[at(ws + ell - 1)];
+                if (!rsi) {
+                    ws += ell;
+                    continue;
+                }
+                uint64_t D = 0;
+                bool dead = false;
+                for (uint64_t e = ell - 1; e > 0; --e) {   // positions ws + ell - 2 .. ws
+                    const uint64_t c = ws + e - 1;
+                    D = rsi & Bw[at(c)];
+                    rsi = wtrans(rw, D);
+                    if (!rsi) {
+                        ws = c + 1;
+                        dead = true;
+                        break;
+                    }
+                }
+                if (dead) continue;
+                if ((rsi & S->ffinal) && check(ws, D, mb, me)) return true;
+                ++ws;
+            }
+            return false;
+        }
+        const uint64_t* fw = tab + S->o_fw;   // forward (0x409500)
+        uint64_t p = R, D = S->finit;
+        if (p < n && (D & S->ffinal) && check(p, D & S->ffinal, mb, me)) return true;
+        while (p < n) {
+            if (p >= stop) return false;   // the next candidate p + 1 is past it
+            const uint8_t c = at(p++);
+            if (c == (uint8_t)'\n') {
+                if (p >= n) return false;
+                D = S->finit;
+            } else {
+                D = wtrans(fw, D) & Bw[c];
+                if (p == n) return false;
+            }
+            const uint64_t f = D & S->ffinal;
+            if (f && check(p, f, mb, me)) return true;
+        }
+        return false;
+    }
+};
+
+// One thread per cluster head: the printed matches are written in place
+// from the head on (acc bit 0), every other entry of the cluster is cleared.
+template <int NW>
+__global__ __launch_bounds__(RG_T) void k_rg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                  const uint64_t* total_d, uint64_t total_h,
+                                                  uint8_t* __restrict__ acc, TextView tv) {
+    const uint64_t total = total_d ? *total_d : total_h;
+    const RgSlot* S = X.rg;
+    for (uint64_t i = blockIdx.x * (uint64_t)RG_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * RG_T) {
+        if (!(acc[i] & 2)) continue;
+        uint64_t j = i + 1;
+        while (j < total && !(acc[j] & 2)) ++j;
+        const uint64_t pid = keys[i] >> 48;
+        const uint64_t first = keys[i] & RG_POS_MASK, last = keys[j - 1] & RG_POS_MASK;
+        uint64_t nout = 0;
+        const uint64_t nmax = j - i;
+        if ((int64_t)pid == X.pid) {
+            uint64_t R0 = 0, n = tv.n;
+            if (tv.reg.n > 1) {
+                const uint32_t r = region_of(tv.reg, first);
+                R0 = tv.reg.t[r];
+                n = tv.reg.e[r];
+            }
+            RgWalk<NW> w{S, X.tab, tv, n, R0, ~0ull, n};
+            uint64_t stop;
+            if (S->max_len >= 0) {
+                const uint64_t back = (uint64_t)S->max_len + 1;
+                if (first > R0 + back) w.R = first - back;
+                stop = last + (uint64_t)S->max_len;
+            } else {
+                uint64_t p = first;
+                while (p > R0 && !w.is_nl(p - 1)) --p;
+                w.R = p;
+                stop = w.next_nl(last);
+            }
+            w.nl_hi = w.next_nl(w.R);
+            for (;;) {
+                uint64_t mb = 0, me = 0;
+                if (!w.scan(stop, mb, me)) break;
+                if (!xt_header(tv, mb) && nout < nmax) {
+                    keys[i + nout] = (pid << 48) | mb;
+                    lens[i + nout] = (uint32_t)(me - mb);
+                    acc[i + nout] = (nout == 0 ? 2 : 0) | 1;
+                    ++nout;
+                }
+                if (me >= n) break;                      // 0x4022eb
+                w.R = me;
+            }
+        }
+        for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
+    }
+}
+
+}  // namespace
+
+void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
+               uint8_t* acc, const TextView& tv, hipStream_t s) {
+    const uint32_t blocks = 1024;
+    hipLaunchKernelGGL(k_rg_heads, dim3(blocks), dim3(RG_T), 0, s, X, keys, total_d, total_h, acc, tv);
+    if (X.words == 1)
+        hipLaunchKernelGGL(k_rg_walk<1>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    else
+        hipLaunchKernelGGL(k_rg_walk<RG_NW>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc,
+                           tv);
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace pm
+
+using namespace pm;
+
+extern "C" int pm_regular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
+                               const int32_t* tree_nullable, int32_t* out, uint64_t* masks) {
+    return guarded([&] {
+        require(byte_mask != nullptr && tree != nullptr && tree_nullable != nullptr && out != nullptr &&
+                    masks != nullptr,
+                "null argument");
+        require(words >= 1 && words <= 4 && m >= 1 && m <= 64 * words, "m / words out of range");
+        const Automaton A = make_automaton(RgTree{nodes, tree, tree_nullable}, byte_mask, words, m);
+        const Plan P = plan_of(A);
+        out[0] = P.type;
+        out[1] = P.ell;
+        out[2] = P.cls;
+        out[3] = P.cls == 3 ? window_states(P, A.ms) : 0;
+        for (int q = 0; q < RG_NW; ++q) {
+            masks[q] = P.win[q];
+            masks[RG_NW + q] = P.winit[q];
+            masks[2 * RG_NW + q] = P.wfinal[q];
+        }
+    });
+}

@@ -453,6 +453,36 @@ def _nfa_tables(prog: Program):
     return t
 
 
+def _tree_tables(prog: Program):
+    """Program.tree as pm_scan_nfa_tree takes it (int32 [nodes][4], [nodes])."""
+    t = prog.__dict__.get("_tree_tables")
+    if t is None:
+        t = (np.array([v for node in prog.tree for v in node], dtype=np.int32),
+             np.array(prog.tree_nullable, dtype=np.int32))
+        prog.__dict__["_tree_tables"] = t
+    return t
+
+
+def regular_plan(prog: Program) -> dict:
+    """The plan nrgrep's regularPreproc derives for a regular pattern
+    (pm_regular_plan, host only): ``type`` 2 = a window of ``ell``
+    characters scanned backward, 3 = the automaton forward; ``cls`` = the
+    window's detClass (1 / 2: nrgrep prints nothing); ``window`` / ``init``
+    / ``final`` = state sets (position + 1)."""
+    w = nfa_words(prog.m)
+    bm = np.array([_words(x, w) for x in prog.byte_masks()], dtype=np.uint64)
+    tree, tnull = _tree_tables(prog)
+    out = (ctypes.c_int32 * 4)()
+    masks = np.zeros(15, dtype=np.uint64)
+    check(_lib.load().pm_regular_plan(prog.m, w, bm.ctypes.data, len(prog.tree), tree.ctypes.data,
+                                      tnull.ctypes.data, out, masks.ctypes.data))
+
+    def as_int(ws):
+        return sum(int(x) << (64 * q) for q, x in enumerate(ws))
+    return {"type": out[0], "ell": out[1], "cls": out[2], "states": out[3], "window": as_int(masks[0:5]),
+            "init": as_int(masks[5:10]), "final": as_int(masks[10:15])}
+
+
 def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
                flags: int = None):
     """pm_scan_nfa_wide; returns the raw pm_hits handle (caller destroys),
@@ -467,6 +497,15 @@ def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0,
     if prog.kind == "extended":
         flags |= _lib.PM_EXTENDED  # nrgrep's extended / eextended engine decides the report
     out = ctypes.c_void_p()
+    if prog.kind == "regular" and k == 0:
+        # nrgrep's regular engine decides the report; its plan is priced over
+        # nrgrep's parse tree
+        tree, tnull = _tree_tables(prog)
+        check(_lib.load().pm_scan_nfa_tree(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
+                                           last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,
+                                           flags | _lib.PM_REGULAR, len(prog.tree), tree.ctypes.data,
+                                           tnull.ctypes.data, ctypes.byref(out)))
+        return out
     check(_lib.load().pm_scan_nfa_wide(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                        last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,
                                        flags, ctypes.byref(out)))
@@ -482,8 +521,9 @@ def scan_nfa(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, t
 
 
 def _same_automaton(a: Program, b: Program) -> bool:
+    # (the regular engine's plan also depends on nrgrep's tree)
     return (a.classes == b.classes and a.follow == b.follow and a.first == b.first and a.last == b.last
-            and a.anchor_start == b.anchor_start and a.anchor_end == b.anchor_end)
+            and a.anchor_start == b.anchor_start and a.anchor_end == b.anchor_end and a.tree == b.tree)
 
 
 def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str = "ids",

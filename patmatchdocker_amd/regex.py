@@ -325,6 +325,33 @@ def _det_class(n: _Node) -> int:
     return best
 
 
+def _serialize(n: _Node):
+    """Preorder node list of a simplified tree (``Program.tree``): leaves are
+    numbered in the order _glushkov numbers ``classes`` (left to right,
+    regularLength 0x40b2a0 numbers nrgrep's states the same way, from 1)."""
+    nodes, nulls = [], []
+    pos = [0]
+
+    def walk(x) -> int:
+        i = len(nodes)
+        nodes.append(None)
+        nulls.append(1 if x.nullable else 0)
+        if x.type == _LEAF:
+            p = -1
+            if x.cls is not None:
+                p = pos[0]
+                pos[0] += 1
+            nodes[i] = (x.type, -1, -1, p)
+            return i
+        a = walk(x.a)
+        b = walk(x.b) if x.type in (_OR, _CAT) else -1
+        nodes[i] = (x.type, a, b, -1)
+        return i
+
+    walk(n)
+    return tuple(nodes), tuple(nulls)
+
+
 def _to_ast(n: _Node):
     if n.type == _LEAF:
         return ("eps",) if n.cls is None else ("sym", n.cls)
@@ -404,6 +431,12 @@ class Program:
     kind: str = "simple"         # nrgrep engine class: simple / extended / regular
     opt_mask: int = 0            # extended: optional positions ('?', '*')
     rep_mask: int = 0            # extended: repeatable positions ('+', '*')
+    # nrgrep's simplified tree (regular patterns' minCost / detClass run over
+    # it): node i = (type, left, right, position) in preorder, node 0 the
+    # root, position = the leaf's index into ``classes`` (-1: an empty
+    # leaf, -1 children); ``tree_nullable[i]`` = the parse-time flag
+    tree: Tuple[Tuple[int, int, int, int], ...] = ()
+    tree_nullable: Tuple[int, ...] = ()
 
     @property
     def m(self) -> int:
@@ -542,8 +575,9 @@ def compile_pattern(pattern, ignore_case: bool = True) -> Program:
     lo, hi = _length_bounds(ast)
     kind = _KINDS[_det_class(tree)]
     opt, rep = _extended_flags(tree) if kind == "extended" else (0, 0)
+    tnodes, tnull = _serialize(tree)
     return Program(source=source.decode("latin-1"), classes=classes, first=first,
                    last=last, follow=follow, nullable=nullable, min_len=lo,
                    max_len=hi, linear=_is_linear(ast), ignore_case=ignore_case,
                    precede=precede, anchor_start=a_start, anchor_end=a_end, kind=kind,
-                   opt_mask=opt, rep_mask=rep)
+                   opt_mask=opt, rep_mask=rep, tree=tnodes, tree_nullable=tnull)

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 DNA_GROUPS = ["GA(TC){1,2}A", "G(TATA){2,}C", "(CA){2,4}GT", "A(TG){0,2}C", "(GA){1,3}(TC){2}",
               "NN(TC){1,2}GAATTC", "GAATTC(CA){2,3}N", "T(AT){1,3}[AG]", "(TA){2,3}(GC){1,2}"]
-PEP_GROUPS = ["C(AG){1,3}L", "C-(x-P){2,3}-C", "(C)x(2,4)(GH){1,2}W", "K(RK){1,2}x(2)C"]
+PEP_GROUPS = ["C(AG){1,3}L", "K(RK){1,2}XXC", "(GH){2,4}W", "W(CP){1,2}[LIV]", "(RK){2,}G", "KX(RK){1,2}C"]
 
 
 @pytest.fixture(scope="module")
@@ -88,9 +88,9 @@ def test_dna_group_repeats_on_tandem_repeats(engine, oracle_mod, width):
 def test_peptide_group_repeats(engine, oracle_mod):
     progs = [compile_pattern(convert("-p", p)) for p in PEP_GROUPS]
     progs = [p for p in progs if p.kind == "regular"]
-    assert len(progs) >= 3
-    text = tandem_fasta(4, ["CAG", "AG", "CP", "GH", "RK", "C", "W", "L"], letters="ACDEFGHIKLMNPQRSTVWY",
-                        n_runs=False)
+    assert len(progs) == len(PEP_GROUPS)
+    text = tandem_fasta(4, ["CAG", "AG", "CP", "GH", "RK", "C", "W", "L", "CAGL", "KRKRK", "WCPL", "GHW", "RKG"],
+                        letters="ACDEFGHIKLMNPQRSTVWY", n_runs=False)
     assert _check(engine, oracle_mod, text, progs, alphabet="byte") > 50
 
 

@@ -66,6 +66,9 @@ def parse_args():
                     help="BASELINE.json configs[i]: 2 = one motif both strands k=2 (default, the metric's "
                          "workload); 4 = batch of 256 degenerate patterns, 12.5 Gbp per GPU (100 Gbp on 8)")
     ap.add_argument("--batch", type=int, default=256, help="patterns in the config-5 batch")
+    ap.add_argument("--dump-keys", default=None,
+                    help="tests: rank 0 saves the last step's gathered hit keys and lengths (<path>.keys.npy, "
+                         "<path>.lens.npy)")
     args = ap.parse_args()
     if args.config == 4 and "--gbp" not in sys.argv:
         args.gbp = 12.5
@@ -335,6 +338,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if rank == 0 and args.dump_keys and result is not None:
+        import numpy as np
+        np.save(args.dump_keys + ".keys.npy", result[0].cpu().numpy())
+        np.save(args.dump_keys + ".lens.npy", result[1].cpu().numpy())
     if rank == 0:
         bases_total = bases_local * world
         ms_step = elapsed / args.steps * 1e3

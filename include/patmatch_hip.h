@@ -260,8 +260,13 @@ int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, con
  * Program.tree): node i = tree[4i .. 4i+3] = (type 0 leaf / 1 '*' / 2 '|' /
  * 3 concatenation / 4 '?' / 5 '+', left child, right child, the leaf's
  * position), preorder, node 0 the root; tree_nullable[i] = the node's
- * parse-time nullable flag.  With PM_REGULAR (and PM_REPORT_NRGREP, k = 0)
- * the report is the regular engine's.                                      */
+ * parse-time nullable flag.  With PM_REGULAR (and PM_REPORT_NRGREP) the
+ * report is the regular engine's at k = 0 and the eregular engine's at
+ * k > 0 (eregularPreproc 0x406a20: k + 1 exact pieces, a window with k
+ * errors or the automaton forward; checkMatch 0x406010; at most 63
+ * positions, else PM_E_UNSUPPORTED; deletions with k >= min_len are
+ * answered, every line walked).  A k > 0 plan whose first window is an
+ * extended sequence prints nothing (eregularPreproc dies, 0x4081ed).      */
 int pm_scan_nfa_tree(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
                      const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
                      int errs, int pattern_id, int flags, int nodes, const int32_t* tree,
@@ -275,6 +280,17 @@ int pm_scan_nfa_tree(pm_db* db, int m, int words, const uint64_t* byte_mask, con
  * hold 4 ints, masks 15 words.                                            */
 int pm_regular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
                     const int32_t* tree_nullable, int32_t* out, uint64_t* masks);
+/* The plan nrgrep's eregularPreproc derives at k errors (host only):
+ * out[0] = 1 (k + 1 pieces of out[1] characters found exactly), 2 (a window
+ * of out[1] characters scanned backward with k errors) or 3 (the automaton
+ * forward), out[2] = detClass of the first window (1: esimple's scanners,
+ * 2: the binary dies, 3: eregularScan), out[3] = 0 when the binary would
+ * read memory it never wrote for this plan, out[4] = the windows;
+ * masks[3i .. 3i+2] = window i, its initial and its final states,
+ * masks[48] = checkMatch's state word for class 1.  out: 5 ints, masks: 49
+ * words.  At most 63 positions (PM_E_UNSUPPORTED above).                   */
+int pm_eregular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
+                     const int32_t* tree_nullable, int k, int32_t* out, uint64_t* masks);
 
 /* Generates and compiles (hipRTC, gfx950) the bit-sliced start pass that
  * pm_scan_nfa_errs / _wide use for a class sequence with insertions /

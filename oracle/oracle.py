@@ -77,6 +77,13 @@ def lib():
         _LIB.pmr_regular.restype = ctypes.c_int64
         _LIB.pmr_regular.argtypes = [ctypes.c_char_p, ctypes.c_int64, pi32, pi32, ctypes.c_int, pu64, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, p64, p64, ctypes.c_int64]
+        _LIB.pmr_eplan.restype = ctypes.c_int
+        _LIB.pmr_eplan.argtypes = [pi32, pi32, ctypes.c_int, pu64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int), pu64]
+        _LIB.pmr_eregular.restype = ctypes.c_int64
+        _LIB.pmr_eregular.argtypes = [ctypes.c_char_p, ctypes.c_int64, pi32, pi32, ctypes.c_int, pu64, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, p64, p64,
+                                      ctypes.c_int64]
         _LIB.pmo_index.restype = ctypes.c_int64
         _LIB.pmo_index.argtypes = [ctypes.c_char_p, ctypes.c_int64, p64, p64, p64, p64,
                                    ctypes.c_int64]
@@ -214,6 +221,8 @@ def scan_reported(text: bytes, prog, k: int = 0, types: str = "ids", skip_header
         return scan_eextended(text, prog, k, types, skip_headers, bufsize, regs)
     if report == "nrgrep" and simple is None and mode is None and k == 0 and prog.kind == "regular":
         return scan_regular(text, prog, skip_headers, bufsize, regs)
+    if report == "nrgrep" and simple is None and mode is None and k > 0 and prog.kind == "regular":
+        return scan_eregular(text, prog, k, types, skip_headers, bufsize, regs)
     if regs is not None or (bufsize and len(text) >= bufsize):
         return by_region(text, lambda t: scan_reported(t, prog, k, types, False, report, simple, mode, 0),
                          skip_headers, bufsize, regs=regs)
@@ -543,6 +552,60 @@ def scan_regular(text: bytes, prog, skip_headers: bool = False, bufsize: int = N
                               end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
         if n < 0:
             raise ValueError("pmr_regular rejected %s" % prog.source)
+        if n <= cap:
+            hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
+            return drop_header_hits(text, hits) if skip_headers else hits
+        cap = int(n)
+
+
+def eregular_plan(prog, k: int, types: str = "ids"):
+    """nrgrep's eregularPreproc plan for ``prog`` at ``k`` errors (pmr_eplan):
+    ``type`` 1 = K + 1 pieces of ``ell`` characters found exactly, 2 = a
+    window of ``ell`` characters scanned backward with k errors, 3 = the
+    automaton forward; ``cls`` = detClass of the first window (1: esimple's
+    scanners, 2: the binary dies, nothing prints); ``windows`` = [(window,
+    init, final)] state sets (nrgrep numbering); ``match`` = checkMatch's
+    state word for class 1; ``defined`` = False when nrgrep reads memory it
+    never wrote for this plan (pm_nrgrep_reg.c, parity unpinned)."""
+    if prog.kind != "regular":
+        raise ValueError("not a regular pattern: %s" % prog.source)
+    B = wide_masks(prog)
+    tree, null, tp, np_ = _tree_arrays(prog)
+    out = (ctypes.c_int * 6)()
+    masks = np.zeros(3 * 17 + 1, dtype=np.uint64)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    if lib().pmr_eplan(tp, np_, len(prog.tree), B.ctypes.data_as(pu64), prog.m, 1 if prog.ignore_case else 0, k,
+                       err_flags(types), out, masks.ctypes.data_as(pu64)) < 0:
+        raise ValueError("no eregular plan for %s at k=%d" % (prog.source, k))
+    wins = [(int(masks[3 * i]), int(masks[3 * i + 1]), int(masks[3 * i + 2])) for i in range(out[5])]
+    return {"type": out[0], "ell": out[1], "cls": out[2], "states": out[3], "defined": bool(out[4]),
+            "windows": wins, "match": int(masks[51])}
+
+
+def scan_eregular(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False,
+                  bufsize: int = NRGREP_BUFFER, regs=None):
+    """What nrgrep_coords prints for a class-3 pattern at k > 0 (pmr_eregular:
+    nrgrep's eregular plan, its scanners, checkMatch and report rule), region
+    by region (``regions``).  Automata of at most 64 states."""
+    if prog.kind != "regular":
+        raise ValueError("scan_eregular needs a regular pattern")
+    if regs is not None or (bufsize and len(text) >= bufsize):
+        return by_region(text, lambda t: scan_eregular(t, prog, k, types, False, 0), skip_headers, bufsize,
+                         regs=regs)
+    B = wide_masks(prog)
+    tree, null, tp, np_ = _tree_arrays(prog)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    mode = (PMO_START if prog.anchor_start else 0) | (PMO_END if prog.anchor_end else 0)
+    cap = 1 << 16
+    while True:
+        beg = np.empty(cap, dtype=np.int64)
+        end = np.empty(cap, dtype=np.int64)
+        n = lib().pmr_eregular(text, len(text), tp, np_, len(prog.tree), B.ctypes.data_as(pu64), prog.m,
+                               1 if prog.ignore_case else 0, mode, k, err_flags(types),
+                               beg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                               end.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap)
+        if n < 0:
+            raise ValueError("pmr_eregular rejected %s at k=%d" % (prog.source, k))
         if n <= cap:
             hits = list(zip(beg[:n].tolist(), end[:n].tolist()))
             return drop_header_hits(text, hits) if skip_headers else hits

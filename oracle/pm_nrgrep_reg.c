@@ -750,3 +750,812 @@ int64_t pmr_regular(const uint8_t* text, int64_t n, const int32_t* tree, const i
     ctx_free(x);
     return count;
 }
+
+/* ========================================================================
+ * eregular: the same patterns at k > 0 (searchPreproc: OptErrors != 0 and
+ * detClass == 3 -> eregularPreproc 0x406a20).  Restated for automata of at
+ * most 64 states (one word: every SLICE sees every state).
+ *
+ *   eregularPreproc 0x406a20:
+ *     regularFindBest 0x40a500 with K (its cost C carries + K) -> a window
+ *       plan and its ratio fb;
+ *     the breadth-first levels of the automaton from state 0 to the first
+ *       level holding a final state (0x406db8 / 0x406f69), the piece length
+ *       pl = min(minlen - K * OptTransp, 64) / (K + 1) (0x406e54);
+ *     per state and length the chance a random text runs along it (A,
+ *       0x40707a), its factor chance per window position (Bt, 0x4072a0) and
+ *       per level the cost C = 1 + sum over the level's states (0x40742d);
+ *     a DP over K + 1 pieces of pl characters starting on levels >= 1, each
+ *       piece (pl + OptTransp) levels after the previous (0x4076a0 ..
+ *       0x407b5e): cost x = C / (pl - C + 1) (1 when C >= pl + 1), pieces
+ *       combined as 1 - (1 - x)(1 - rest), best under 0.78, pl shrinking
+ *       while 1 / pl <= best;
+ *     pieces win (type 1) when their cost < 0.78 and < (K + 1) 1.3 fb
+ *       (0x40842a); piece i's window = the states within pl arrows of its
+ *       level, its final states those 1 .. pl arrows away (0x408337);
+ *       otherwise regularFindBest's window (type 2 backward when ell > 0,
+ *       3 forward);
+ *     detClass of windows[0]: 1 -> esimpleLoadFast 0x415370 + esimpleScan
+ *       0x4136d0 with checkMatch's state word P->0x28 = the first state of
+ *       each piece window (0x407e4b); 2 -> a store through a null pointer
+ *       (0x4081ed: the process dies, nothing is printed); 3 ->
+ *       eregularLoadFast 0x406860 (regularLoadFast over the union of the
+ *       windows) + eregularScan 0x4048b0.
+ *   eregularScan: type 1 the pieces exactly, backward windows of pl
+ *     characters (0x4052b9, like regularScan); type 2 bwdScanrk 0x402d50:
+ *     windows of ell - K characters, K + 1 rows of at most j errors with
+ *     every edit and transpositions (a filter), P->0x28 = row K before the
+ *     window's first character; type 3 fwdScanrk 0x402830: the same rows
+ *     forward, fresh after every run of '\n', the final states of row K
+ *     after each character except the region's last.
+ *   checkMatch 0x406010: for each state s of P->0x28 in order (at most
+ *     P->0x24, mapped back by P->0x858): type 1/2 fwdCheck 0x403310 from s
+ *     reading t[pos + 1] on (budget K), then bwdCheck 0x403df0 from s reading
+ *     t[pos] back (the rest of the budget); type 3 the other way round from
+ *     pos - 1.  The first state whose first phase succeeds decides: a failed
+ *     second phase fails the candidate.  fwdCheck / bwdCheck keep K + 1 rows
+ *     (OptIns, OptDel, OptSubs as given): the nearest boundary with the
+ *     fewest errors, row 0 ends the phase at once, a find at j errors caps
+ *     the rows at j - 1 (0x403a01).
+ *
+ * Two places where the binary reads memory it never wrote (parity unpinned,
+ * restated as noted):
+ *   - without OptDel, fwdCheck / bwdCheck never initialise rows 1 .. K
+ *     (0x4034d3 / 0x403f93): they hold whatever the previous check left (the
+ *     first time: fresh heap).  Restated as rows 1 .. K = row 0 (the state
+ *     the phase starts from, reached with at most j errors).
+ *   - class 1 reads windows[1 .. K] (0x407e95) even for a window plan, where
+ *     only windows[0] was set unless the piece DP filled them.  Restated as
+ *     windows[0] alone.
+ * ====================================================================== */
+
+#define PME_MAXK 16
+#define PME_INS 1
+#define PME_DEL 2
+#define PME_SUB 4
+
+typedef struct {
+    rctx_t* x;
+    int K, errs;
+    int etype, ell, cls, npieces, pieces_computed, defined;
+    double pbest, fbest;
+    uint64_t pwin[PME_MAXK + 1], pini[PME_MAXK + 1], pfin[PME_MAXK + 1];
+    int first[PME_MAXK + 1];
+    /* the automaton in one word */
+    int m;
+    uint64_t arr[64], rev[64], B[256], final;
+    /* checkMatch */
+    uint64_t match0;            /* class 1: P->0x28 */
+    int nstates;                /* P->0x24 */
+    int unmap[64];              /* P->0x858 */
+} ectx_t;
+
+static inline uint64_t etrans(const uint64_t* tab, uint64_t d) {
+    uint64_t r = 0;
+    while (d) {
+        r |= tab[__builtin_ctzll(d)];
+        d &= d - 1;
+    }
+    return r;
+}
+
+/* eregularPreproc's plan (transpositions off: PatMatch's -k letters are
+ * i/d/s only, patmatch.py:299-314) */
+static int eplan(ectx_t* e, int K) {
+    rctx_t* x = e->x;
+    const int m = x->m;
+    if (m > 64 || K < 1 || K > PME_MAXK) return -1;
+    e->m = m;
+    e->K = K;
+    for (int s = 0; s < m; ++s) {
+        e->arr[s] = x->arrows[s].w[0];
+        e->rev[s] = x->rev[s].w[0];
+    }
+    for (int c = 0; c < 256; ++c) e->B[c] = x->B[c].w[0];
+    e->final = x->final.w[0];
+    if (find_best(x, K) < 0) return -1;                     /* 0x406d39 */
+    e->fbest = x->best;
+    const int transp = 0;
+    /* levels (0x406db8) */
+    uint64_t seen = 1;
+    int nlev = 1;
+    while (!(seen & e->final)) {
+        ++nlev;
+        seen |= etrans(e->arr, seen);
+        if (nlev > m + 2) return -1;
+    }
+    const int minlen = nlev - 1;
+    uint64_t lev[66];
+    lev[0] = 1;
+    seen = 1;
+    for (int i = 1; i <= minlen; ++i) {                    /* 0x406f69 */
+        const uint64_t succ = etrans(e->arr, seen);
+        lev[i] = succ & ~seen;
+        seen |= succ;
+    }
+    int pl0 = minlen - K * transp;                         /* 0x406e54 */
+    if ((unsigned)pl0 > 64u) pl0 = 64;
+    pl0 = pl0 / (K + 1);
+    const int PL1 = pl0 + 1;
+    double best = 0.78;                                    /* .rodata 0x41d1e8 */
+    int chosen = 0;
+    uint64_t pieces[PME_MAXK + 1];
+    memset(pieces, 0, sizeof pieces);
+    if (PL1 > 1 && pl0 != 1 && !(1.0 / (double)pl0 > 0.78)) {
+        double prob[64];
+        for (int i = 0; i < m; ++i) {                      /* 0x407031 */
+            prob[i] = 0.0;
+            for (int c = 0; c < 256; ++c)
+                if ((e->B[c] >> i) & 1) prob[i] += pmn_letter_prob[c];
+        }
+        double* A = calloc((size_t)m * PL1, sizeof(double));
+        for (int i = 0; i < m; ++i) {
+            A[(size_t)i * PL1] = 1.0;
+            A[(size_t)i * PL1 + 1] = prob[i];
+        }
+        for (int l = 2; l < PL1; ++l)                      /* 0x407118 */
+            for (int i = 0; i < m; ++i) {
+                double s = 0.0;
+                for (int j = 0; j < m; ++j)
+                    if ((e->arr[i] >> j) & 1) s += A[(size_t)j * PL1 + l - 1];
+                s *= prob[i];
+                A[(size_t)i * PL1 + l] = 1.0 < s ? 1.0 : s;
+            }
+        double* Bt = calloc((size_t)m * PL1 * PL1, sizeof(double));
+#define BT(i, l, a) Bt[((size_t)(i) * PL1 + (l)) * PL1 + (a)]
+        for (int i = 0; i < m; ++i)
+            for (int l = 0; l < PL1; ++l) BT(i, l, 0) = 1.0;
+        for (int l = 1; l < PL1; ++l)                      /* 0x4072a0 */
+            for (int a = 1; a <= l; ++a)
+                for (int i = 0; i < m; ++i) {
+                    double v = A[(size_t)i * PL1 + a];
+                    if (a < l)
+                        for (int j = 0; j < m; ++j)
+                            if ((e->arr[i] >> j) & 1) v = 1.0 - (1.0 - v) * (1.0 - BT(j, l - 1, a));
+                    BT(i, l, a) = v;
+                }
+        double* C = calloc((size_t)nlev * PL1, sizeof(double));
+        for (int lv = 0; lv < nlev; ++lv)                  /* 0x40742d */
+            for (int l = 0; l < PL1; ++l) {
+                double s = 1.0;
+                for (int i = 0; i < m; ++i)
+                    if (((lev[lv] >> i) & 1) && l != 0)
+                        for (int a = 1; a <= l; ++a) s += BT(i, l, a);
+                C[(size_t)lv * PL1 + l] = s;
+            }
+#undef BT
+        const int W2 = K + 2;
+        double* D = calloc((size_t)(nlev + 1) * W2, sizeof(double));
+        int* E = calloc((size_t)(nlev + 1) * W2, sizeof(int));
+        for (int pl = pl0;;) {                             /* 0x40772e */
+            for (int r = 1; r <= nlev; ++r) D[(size_t)r * W2] = 0.0;
+            for (int c = 1, esi = nlev - pl; c <= K + 1; ++c, esi -= pl + transp)
+                for (int r = (esi < 0 ? 0 : esi) + 1; r <= nlev; ++r) D[(size_t)r * W2 + c] = 1.0;
+            for (int c = 1; c <= K + 1; ++c) {             /* 0x407850 */
+                const int r11 = nlev - pl - (c - 1) * (pl + transp);
+                for (int r = r11; r >= 1; --r) {
+                    double v = C[(size_t)r * PL1 + pl];
+                    if ((double)(pl + 1) > v) {
+                        v = v / ((double)pl - v + 1.0);
+                        v = 1.0 < v ? 1.0 : v;             /* minsd */
+                    } else {
+                        v = 1.0;
+                    }
+                    if (c > 1) v = 1.0 - (1.0 - v) * (1.0 - D[(size_t)(r + pl + transp) * W2 + c - 1]);
+                    E[(size_t)r * W2 + c] = r;
+                    const double y = D[(size_t)(r + 1) * W2 + c];
+                    if (v > y) {
+                        v = y;
+                        E[(size_t)r * W2 + c] = E[(size_t)(r + 1) * W2 + c];
+                    }
+                    D[(size_t)r * W2 + c] = v;
+                }
+            }
+            if (best > D[W2 + K + 1]) {                    /* 0x407a0b */
+                int r = 1;
+                for (int i = 0, c = K + 1; c >= 1; ++i, --c) {
+                    const int s = E[(size_t)r * W2 + c];
+                    pieces[i] = lev[s];
+                    r = s + pl + transp;
+                }
+                best = D[W2 + K + 1];
+                chosen = pl;
+            }
+            if (--pl == 1) break;                          /* 0x407ae0 */
+            if (!(1.0 / (double)pl <= best)) break;
+        }
+        free(A);
+        free(Bt);
+        free(C);
+        free(D);
+        free(E);
+    }
+    e->pbest = best;
+    int use_pieces = 0;
+    if (best < 0.78) {                                     /* 0x4082c9 */
+        e->pieces_computed = 1;
+        for (int i = 0; i <= K; ++i) {
+            uint64_t w = pieces[i], last = 0;
+            for (int st = 0; st < chosen; ++st) {
+                last = etrans(e->arr, w);
+                w |= last;
+            }
+            e->pwin[i] = w;
+            e->pini[i] = pieces[i];
+            e->pfin[i] = last;
+        }
+        if (!(best >= (double)(K + 1) * 1.3 * e->fbest) && chosen != 0) use_pieces = 1;   /* 0x40842a */
+    }
+    if (use_pieces) {
+        e->etype = 1;
+        e->ell = chosen;
+        e->npieces = K + 1;
+    } else {                                               /* 0x407bb9 */
+        e->etype = x->ell == 0 ? 3 : 2;
+        e->ell = x->ell;
+        e->npieces = 1;
+        e->pwin[0] = x->win.w[0];
+        e->pini[0] = x->winit.w[0];
+        e->pfin[0] = x->wfinal.w[0];
+    }
+    rset w0;
+    memset(&w0, 0, sizeof w0);
+    w0.w[0] = e->pwin[0];
+    e->cls = det_class1(x, 0, &w0);                        /* 0x407c97 */
+    e->defined = 1;
+    for (int i = 0; i < 64; ++i) e->unmap[i] = -1;
+    if (e->cls == 1) {                                     /* 0x407e4b */
+        const int nw = (e->etype == 1 || e->pieces_computed) ? K + 1 : 1;
+        if (nw < K + 1) e->defined = 0;
+        e->match0 = 0;
+        for (int i = 0; i < nw; ++i) {
+            int f = 0;
+            while (f < m && !((e->pwin[i] >> f) & 1)) ++f;
+            e->first[i] = f;
+            if (e->ell != 0) e->match0 |= 1ull << (f & 63);
+            else {
+                int r = f + 1;
+                while (r < m && ((e->pwin[i] >> r) & 1)) ++r;
+                e->match0 |= 1ull << (r & 63);
+            }
+        }
+        e->nstates = m;
+        for (int i = 0; i < m; ++i) e->unmap[i] = i;
+    } else if (e->cls == 3) {                              /* 0x407fe9 */
+        rset uw, ui, uf;
+        memset(&uw, 0, sizeof uw);
+        memset(&ui, 0, sizeof ui);
+        memset(&uf, 0, sizeof uf);
+        for (int i = 0; i < e->npieces; ++i) {
+            uw.w[0] |= e->pwin[i];
+            ui.w[0] |= e->pini[i];
+            uf.w[0] |= e->pfin[i];
+        }
+        x->win = uw;
+        x->winit = ui;
+        x->wfinal = uf;
+        x->ell = e->ell;
+        if (load_fast(x) < 0) return -1;
+        e->nstates = x->mp;
+        for (int s = 0; s < m; ++s)
+            if ((uw.w[0] >> s) & 1) e->unmap[x->map[s]] = s;   /* 0x40807f */
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * fwdCheck 0x403310 / bwdCheck 0x403df0 with K + 1 rows; *kio: the budget
+ * in, the errors used out.  -1: none.
+ * ---------------------------------------------------------------------- */
+
+static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
+    const rctx_t* x = e->x;
+    const int K = *kio, ins = e->errs & PME_INS, del = e->errs & PME_DEL, sub = e->errs & PME_SUB;
+    uint64_t rows[PME_MAXK + 1];
+    rows[0] = 1ull << s;
+    if (rows[0] & e->final) {                              /* 0x40339d: insertions to the right context */
+        *kio = 0;
+        for (int64_t q = p + 1;; ++q) {
+            if (right_ok(x, q, lim + 1)) return q - 1;
+            if (q == lim + 1 || !ins) return -1;
+            if (++*kio > K) return -1;
+        }
+    }
+    int kmax = K;
+    int64_t best = -1;
+    for (int j = 1; j <= kmax; ++j) {                      /* 0x4034c0 */
+        if (!del) {
+            rows[j] = rows[j - 1];                         /* (unset in the binary: see the header) */
+            continue;
+        }
+        rows[j] = rows[j - 1] | etrans(e->arr, rows[j - 1]);
+        if ((rows[j] & e->final) && right_ok(x, p + 1, lim + 1)) {   /* 0x403d82 */
+            *kio = j;
+            kmax = j - 1;
+            best = p;
+        }
+    }
+    if (p == lim) return best;
+    for (int64_t cur = p;;) {
+        ++cur;
+        const uint64_t bc = e->B[x->t[cur]];
+        const uint64_t n0 = etrans(e->arr, rows[0]) & bc;
+        if ((n0 & e->final) && right_ok(x, cur + 1, lim + 1)) {
+            *kio = 0;
+            return cur;
+        }
+        uint64_t oldp = rows[0], last = n0;
+        rows[0] = n0;
+        for (int j = 1; j <= kmax; ++j) {                  /* 0x4037a0 */
+            uint64_t v = del ? etrans(e->arr, last) : 0;
+            if (ins) v |= oldp;
+            if (sub) v |= etrans(e->arr, oldp);
+            v |= etrans(e->arr, rows[j]) & bc;
+            const uint64_t oj = rows[j];
+            rows[j] = v;
+            last = v;
+            if ((v & e->final) && right_ok(x, cur + 1, lim + 1)) {   /* 0x403a01: the fewest errors */
+                int c = j;
+                while (c - 1 >= 0 && (rows[c - 1] & e->final)) --c;
+                if (c == 0) {
+                    *kio = 0;
+                    return cur;
+                }
+                *kio = c;
+                kmax = c - 1;
+                best = cur;
+                break;
+            }
+            oldp = oj;
+        }
+        if (!last) return best;                            /* 0x403afc */
+        if (cur == lim) return best;
+    }
+}
+
+static int64_t ebwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
+    const rctx_t* x = e->x;
+    const int K = *kio, ins = e->errs & PME_INS, del = e->errs & PME_DEL, sub = e->errs & PME_SUB;
+    uint64_t rows[PME_MAXK + 1];
+    rows[0] = 1ull << s;
+    if (rows[0] & 1) {                                     /* 0x403e71: insertions to the left context */
+        *kio = 0;
+        for (int64_t q = p;;) {
+            if (left_ok(x, q, lim)) return q;
+            if (q == lim) return -1;
+            --q;
+            if (!ins) return -1;
+            if (++*kio > K) return -1;
+        }
+    }
+    int kmax = K;
+    int64_t best = -1;
+    for (int j = 1; j <= kmax; ++j) {                      /* 0x403f80 */
+        if (!del) {
+            rows[j] = rows[j - 1];
+            continue;
+        }
+        rows[j] = rows[j - 1] | etrans(e->rev, rows[j - 1]);
+        if ((rows[j] & 1) && left_ok(x, p, lim)) {         /* 0x40484e */
+            *kio = j;
+            kmax = j - 1;
+            best = p;
+        }
+    }
+    if (p == lim) return best;
+    for (int64_t cur = p;;) {
+        --cur;
+        const uint64_t bc = e->B[x->t[cur]];
+        const uint64_t n0 = etrans(e->rev, rows[0] & bc);
+        if ((n0 & 1) && left_ok(x, cur, lim)) {
+            *kio = 0;
+            return cur;
+        }
+        uint64_t oldp = rows[0], last = n0;
+        rows[0] = n0;
+        for (int j = 1; j <= kmax; ++j) {                  /* 0x404230 */
+            uint64_t v = del ? etrans(e->rev, last) : 0;
+            if (ins) v |= oldp;
+            if (sub) v |= etrans(e->rev, oldp);
+            v |= etrans(e->rev, rows[j] & bc);
+            const uint64_t oj = rows[j];
+            rows[j] = v;
+            last = v;
+            if ((v & 1) && left_ok(x, cur, lim)) {         /* 0x404479 */
+                int c = j;
+                while (c - 1 >= 0 && (rows[c - 1] & 1)) --c;
+                if (c == 0) {
+                    *kio = 0;
+                    return cur;
+                }
+                *kio = c;
+                kmax = c - 1;
+                best = cur;
+                break;
+            }
+            oldp = oj;
+        }
+        if (!last) return best;                            /* 0x404579 */
+        if (cur == lim) return best;
+    }
+}
+
+/* checkMatch 0x406010 */
+static int echeck(const ectx_t* e, int64_t pos, int64_t R, uint64_t match, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int64_t rp = e->etype == 3 ? pos - 1 : pos;
+    int64_t lo = 0, hi = x->nnl;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (x->nl[mid] < rp) lo = mid + 1; else hi = mid;
+    }
+    int64_t rb = R;
+    if (lo > 0 && x->nl[lo - 1] >= R) rb = x->nl[lo - 1] + 1;
+    const int64_t re = lo < x->nnl ? x->nl[lo] : x->n;
+    if (rp < rb || rp >= re) return 0;
+    for (int i = 0; i < e->nstates && i < 64; ++i) {       /* 0x4060b9 */
+        if (!((match >> i) & 1) || e->unmap[i] < 0) continue;
+        const int s = e->unmap[i];
+        int k1 = e->K, k2;
+        int64_t st, en;
+        if (e->etype != 3) {
+            en = efwd(e, pos, re - 1, s, &k1);
+            if (en < 0) continue;
+            k2 = e->K - k1;
+            st = ebwd(e, pos + 1, rb, s, &k2);
+            if (st < 0) return 0;                          /* 0x406248 */
+        } else {                                           /* 0x406320 */
+            st = ebwd(e, pos, rb, s, &k1);
+            if (st < 0) continue;
+            k2 = e->K - k1;
+            en = efwd(e, pos - 1, re - 1, s, &k2);
+            if (en < 0) return 0;
+        }
+        *mb = st;
+        *me = en + 1;
+        return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * eregularScan 0x4048b0 (class 3) and esimpleScan 0x4136d0 (class 1) over
+ * the region [R, n)
+ * ---------------------------------------------------------------------- */
+
+/* type 1: the pieces exactly (0x4052b9) */
+static int escan_pieces3(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int ell = e->ell;
+    const uint8_t* t = x->t;
+    int64_t pos = R - 1;
+    const int64_t lim = x->n - ell;
+    while (pos < lim) {
+        uint64_t rcx = x->A[t[pos + ell]];
+        if (!rcx) {
+            pos += ell;
+            continue;
+        }
+        uint64_t D = 0;
+        int64_t c = pos + ell - 1;
+        int dead = 0;
+        for (;;) {
+            D = rcx & x->Bw[t[c]];
+            rcx = wtrans(x->rw, x->mp, D);
+            if (!rcx) {
+                dead = 1;
+                break;
+            }
+            if (--c == pos) break;
+        }
+        if (dead) {
+            pos = c;
+            continue;
+        }
+        if ((rcx & x->ffinal) && echeck(e, pos + 1, R, D, mb, me)) return 1;
+        ++pos;
+    }
+    return 0;
+}
+
+/* type 2: bwdScanrk 0x402d50 */
+static int escan_backward(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int K = e->K, W = e->ell - K;
+    const uint8_t* t = x->t;
+    uint64_t rows[PME_MAXK + 1], old[PME_MAXK + 1];
+    int64_t pos = R - 1;
+    const int64_t lim = x->n - W;
+    while (pos < lim) {                                    /* 0x402f21 */
+        const uint8_t c0 = t[pos + W];
+        uint64_t bprev = x->Bw[c0];
+        rows[0] = x->A[c0];
+        for (int j = 1; j <= K; ++j) rows[j] = x->finit;
+        for (int j = 0; j <= K; ++j) old[j] = x->finit;
+        int64_t cur = pos + W - 1;
+        for (;;) {                                         /* 0x403044 */
+            const uint64_t bc = x->Bw[t[cur]];
+            uint64_t po = rows[0];
+            uint64_t pn = wtrans(x->rw, x->mp, bc & po);
+            rows[0] = pn;
+            for (int j = 1; j <= K; ++j) {                 /* 0x4030d0 */
+                const uint64_t r10 = pn | po;
+                const uint64_t oj = rows[j];
+                uint64_t v = po | wtrans(x->rw, x->mp, r10) | wtrans(x->rw, x->mp, bc & oj);
+                const uint64_t tr = wtrans(x->rw, x->mp, bc & old[j - 1]) & bprev;
+                v |= wtrans(x->rw, x->mp, tr);
+                old[j - 1] = po;
+                rows[j] = v;
+                po = oj;
+                pn = v;
+            }
+            if (!pn) {                                     /* 0x403230: dead */
+                pos = cur;
+                break;
+            }
+            if (--cur == pos) {                            /* 0x4031ed */
+                if ((pn & x->ffinal) && echeck(e, pos + 1, R, po, mb, me)) return 1;
+                ++pos;
+                break;
+            }
+            bprev = bc;
+        }
+    }
+    return 0;
+}
+
+/* type 3: fwdScanrk 0x402830 */
+static int escan_forward(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int K = e->K;
+    const uint8_t* t = x->t;
+    const int64_t n = x->n;
+    uint64_t rows[PME_MAXK + 1], old[PME_MAXK + 1];
+    int64_t cur = R;
+    for (;;) {
+        /* a record start (0x4028db): the next character that is not '\n' */
+        if (cur >= n) return 0;
+        uint8_t c = t[cur++];
+        while (c == '\n') {
+            if (cur == n) return 0;
+            c = t[cur++];
+        }
+        uint64_t s = x->finit;                             /* 0x402911 */
+        rows[0] = old[0] = s;
+        for (int j = 1; j <= K; ++j) {
+            s |= wtrans(x->fw, x->mp, s);
+            rows[j] = old[j] = s;
+        }
+        uint64_t bc = x->Bw[c];
+        uint64_t po = rows[0], pn = wtrans(x->fw, x->mp, po) & bc;
+        rows[0] = pn;
+        for (int j = 1; j <= K; ++j) {                     /* 0x402a31 */
+            const uint64_t r = pn | po;
+            const uint64_t oj = rows[j];
+            const uint64_t v = r | (wtrans(x->fw, x->mp, oj) & bc) | wtrans(x->fw, x->mp, r);
+            rows[j] = v;
+            po = oj;
+            pn = v;
+        }
+        if (cur >= n) return 0;
+        uint64_t bprev = bc;
+        if ((pn & x->ffinal) && echeck(e, cur, R, pn & x->ffinal, mb, me)) return 1;
+        for (;;) {                                         /* 0x402ac0 */
+            c = t[cur++];
+            if (c == '\n') break;
+            bc = x->Bw[c];
+            po = rows[0];
+            pn = wtrans(x->fw, x->mp, po) & bc;
+            rows[0] = pn;
+            for (int j = 1; j <= K; ++j) {                 /* 0x402b68 */
+                const uint64_t r10 = pn | po;
+                const uint64_t oj = rows[j];
+                uint64_t v = po | (wtrans(x->fw, x->mp, oj) & bc) | wtrans(x->fw, x->mp, r10);
+                const uint64_t tr = wtrans(x->fw, x->mp, old[j - 1]) & bc;
+                v |= wtrans(x->fw, x->mp, tr) & bprev;
+                old[j - 1] = po;
+                rows[j] = v;
+                po = oj;
+                pn = v;
+            }
+            if (cur == n) return 0;                        /* 0x402c3c */
+            if ((pn & x->ffinal) && echeck(e, cur, R, pn & x->ffinal, mb, me)) return 1;
+            bprev = bc;
+        }
+    }
+}
+
+/* class 1, type 1: esimpleScan's multi-piece BNDM (0x413780) over the
+ * pieces' states first[r] .. first[r] + pl - 1 (esimpleLoadFast 0x4153fa) */
+static int escan_pieces1(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int mpc = e->ell, np = e->K + 1;
+    uint64_t T0[256], T2[256];
+    for (int c = 0; c < 256; ++c) {
+        T0[c] = T2[c] = 0;
+        for (int r = 0; r < np; ++r)
+            for (int pp = 0; pp < mpc; ++pp) {
+                const int st = e->first[r] + mpc - 1 - pp;
+                if (st < 64 && ((e->B[c] >> st) & 1)) {
+                    const uint64_t bit = 1ull << (r * mpc + pp);
+                    T0[c] |= bit;
+                    if (pp > 0) T2[c] |= bit;
+                }
+            }
+    }
+    const uint8_t* t = x->t;
+    int64_t r9 = R - 1;
+    const int64_t limit = x->n - mpc;
+    while (r9 < limit) {
+        uint64_t D = T0[t[r9 + mpc]];
+        if (!D) {
+            r9 += mpc;
+            continue;
+        }
+        int64_t a = r9 + mpc - 1;
+        int k = mpc - 1;
+        do {
+            D = (D << 1) & T2[t[a]];
+            --k;
+            --a;
+        } while (D && k);
+        if (D) {
+            for (int i = 0; i < np; ++i) {                 /* 0x41384b: 32-bit shift */
+                const int bit = i * mpc + mpc - 1;
+                const uint64_t msk = (uint64_t)(int64_t)(int32_t)(1u << (bit & 31));
+                if ((D & msk) && echeck(e, r9 + 1, R, e->match0, mb, me)) return 1;
+            }
+        }
+        r9 += k + 1;
+    }
+    return 0;
+}
+
+/* class 1, type 2: esimpleScan's ABNDM (0x413b6f) over the window's states
+ * first .. first + ell - 1 (simpleLoadFast 0x417561) */
+static int escan_window1(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
+    const rctx_t* x = e->x;
+    const int beg = e->first[0], Lw = e->ell, k = e->K;
+    uint64_t T[256];
+    for (int c = 0; c < 256; ++c) {
+        T[c] = 0;
+        for (int r = 0; r < Lw; ++r) {
+            const int st = beg + Lw - 1 - r;
+            if (st < 64 && ((e->B[c] >> st) & 1)) T[c] |= 1ull << (64 - Lw + r);
+        }
+    }
+    const uint64_t top = ~0ull << (64 - Lw);
+    const int W = Lw - k;
+    const int64_t limit = x->n - (Lw - k - 1);
+    uint64_t Rr[PME_MAXK + 1], Tr[PME_MAXK + 1];
+    const uint8_t* t = x->t;
+    for (int64_t s = R; s < limit;) {
+        const uint64_t b0 = T[t[s + W - 1]];
+        Rr[0] = b0;
+        for (int j = 1; j <= k; ++j) {
+            Rr[j] = top;
+            Tr[j] = b0;
+        }
+        int64_t rb = W - 2;
+        for (;;) {
+            const uint64_t bc = T[t[s + rb]];
+            uint64_t oldp = Rr[0];
+            uint64_t newp = (oldp << 1) & bc;
+            Rr[0] = newp;
+            for (int j = 1; j <= k; ++j) {
+                const uint64_t trans = (bc << 1) & Tr[j];
+                uint64_t v = ((newp | oldp) << 1) | oldp;
+                Tr[j] = (oldp << 2) & bc;
+                v |= trans;
+                const uint64_t oldj = Rr[j];
+                v |= (oldj << 1) & bc;
+                Rr[j] = v;
+                oldp = oldj;
+                newp = v;
+            }
+            if (rb == 0) {
+                if ((Rr[k] >> 63) && echeck(e, s, R, e->match0, mb, me)) return 1;
+                break;
+            }
+            if (!Rr[k] && !Tr[k]) break;
+            --rb;
+        }
+        s += rb + 1;
+    }
+    return 0;
+}
+
+static ectx_t* ectx_new(const int32_t* tree, const int32_t* nullable, int nodes, const uint64_t* Bpos, int npos,
+                        int icase, int mode, int K, int errs) {
+    ectx_t* e = calloc(1, sizeof(ectx_t));
+    if (!e) return NULL;
+    e->x = calloc(1, sizeof(rctx_t));
+    if (!e->x) {
+        free(e);
+        return NULL;
+    }
+    e->x->mode = mode;
+    e->errs = errs;
+    if (build(e->x, tree, nodes, nullable, Bpos, npos, icase) < 0 || eplan(e, K) < 0) {
+        ctx_free(e->x);
+        free(e);
+        return NULL;
+    }
+    return e;
+}
+
+static void ectx_free(ectx_t* e) {
+    ctx_free(e->x);
+    free(e);
+}
+
+/* out[0] = type (1 pieces, 2 backward window, 3 forward), out[1] = the
+ * pieces' length or the window's ell, out[2] = detClass of windows[0],
+ * out[3] = P->0x24, out[4] = 1 unless nrgrep reads memory it never wrote,
+ * out[5] = the number of windows; masks[3 i .. 3 i + 2] = window i, its
+ * initial and its final states; masks[51] = P->0x28 (class 1) */
+int pmr_eplan(const int32_t* tree, const int32_t* nullable, int nodes, const uint64_t* Bpos, int npos, int icase,
+              int K, int errs, int* out, uint64_t* masks) {
+    ectx_t* e = ectx_new(tree, nullable, nodes, Bpos, npos, icase, 0, K, errs);
+    if (!e) return -1;
+    out[0] = e->etype;
+    out[1] = e->ell;
+    out[2] = e->cls;
+    out[3] = e->nstates;
+    out[4] = e->defined;
+    out[5] = e->npieces;
+    for (int i = 0; i < e->npieces; ++i) {
+        masks[3 * i] = e->pwin[i];
+        masks[3 * i + 1] = e->pini[i];
+        masks[3 * i + 2] = e->pfin[i];
+    }
+    masks[3 * (PME_MAXK + 1)] = e->match0;
+    ectx_free(e);
+    return 0;
+}
+
+/* What nrgrep_coords prints for a class-3 pattern at k = K > 0 over one
+ * region (recSearchFile 0x402250).  errs: 1 insertions, 2 deletions, 4
+ * substitutions.  Returns the number of matches (may exceed cap), -1 if
+ * refused (more than 64 states). */
+int64_t pmr_eregular(const uint8_t* text, int64_t n, const int32_t* tree, const int32_t* nullable, int nodes,
+                     const uint64_t* Bpos, int npos, int icase, int mode, int K, int errs, int64_t* out_beg,
+                     int64_t* out_end, int64_t cap) {
+    ectx_t* e = ectx_new(tree, nullable, nodes, Bpos, npos, icase, mode, K, errs);
+    if (!e) return -1;
+    if (e->cls == 2) {                                     /* 0x4081ed: the process dies before the scan */
+        ectx_free(e);
+        return 0;
+    }
+    rctx_t* x = e->x;
+    x->t = text;
+    x->n = n;
+    int64_t nnl = 0;
+    for (int64_t p = 0; p < n; ++p) nnl += text[p] == '\n';
+    int64_t* nl = malloc(sizeof(int64_t) * (size_t)(nnl + 1));
+    nnl = 0;
+    for (int64_t p = 0; p < n; ++p)
+        if (text[p] == '\n') nl[nnl++] = p;
+    x->nl = nl;
+    x->nnl = nnl;
+    int64_t count = 0, R = 0;
+    while (R < n) {
+        int64_t mb = 0, me = 0;
+        int ok;
+        if (e->cls == 1) ok = e->etype == 1 ? escan_pieces1(e, R, &mb, &me) : escan_window1(e, R, &mb, &me);
+        else if (e->etype == 1) ok = escan_pieces3(e, R, &mb, &me);
+        else if (e->etype == 2) ok = escan_backward(e, R, &mb, &me);
+        else ok = escan_forward(e, R, &mb, &me);
+        if (!ok) break;
+        if (count < cap) {
+            out_beg[count] = mb;
+            out_end[count] = me;
+        }
+        ++count;
+        if (me == n) break;
+        R = me;
+    }
+    free(nl);
+    ectx_free(e);
+    return count;
+}

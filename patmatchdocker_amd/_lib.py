@@ -38,6 +38,7 @@ EXPORTED = (
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
     "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes", "pm_scan_nfa_tree",
     "pm_regular_plan",
+    "pm_eregular_plan",
 )
 PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
@@ -86,6 +87,7 @@ def _declare(lib):
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]
     lib.pm_scan_nfa_tree.argtypes = lib.pm_scan_nfa_wide.argtypes[:-1] + [ctypes.c_int, P, P, PP]
     lib.pm_regular_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P, P, P]
+    lib.pm_eregular_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_int, P, P]
     lib.pm_ids_jit_compile.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_int, pu64]
     lib.pm_extended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     lib.pm_eextended_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int, P]

@@ -935,16 +935,24 @@ struct RgTree {                // Program.tree (regex.py): node i = type, left, 
 };
 struct RgSlot {                // one pattern (device, uploaded as is)
     int32_t ms, nw, mp, type, ell, anchors, pid;   // states, words (1 / RG_NW), window states
-    int64_t max_len;           // the longest match, -1: walk whole lines
+    int64_t max_len;           // the longest text a match covers, -1: walk whole lines
+    int64_t gap;               // consecutive starts further apart start a new cluster (-1: lines)
     uint64_t finit, ffinal;    // the window scanner's initial / final states
     uint64_t final_[RG_NW], vis[RG_NW];   // the automaton's final states; the states SLICE sees
-    int32_t unmap[64];         // window state -> automaton state (P->0x860)
+    int32_t unmap[64];         // window state -> automaton state (P->0x860 / P->0x858), -1 none
     uint64_t o_arr, o_rev, o_B, o_Bw, o_A, o_fw, o_rw;   // word offsets in the table blob
+    // eregular (k > 0, one word; pm_regular.hip): type 1 pieces, 2 backward
+    // window, 3 forward; cls 1 (esimple's scanners) or 3 (eregularScan)
+    int32_t k, errs, cls, nstates, lines;   // nstates: P->0x24; lines: clusters break at '\n' too
+    uint64_t match0;           // class 1: checkMatch's state word P->0x28
+    int32_t first[PM_MAX_K + 1];   // class 1: each window's first state
+    uint64_t o_T0, o_T2;       // class 1: esimpleLoadFast's tables
 };
 // builds the plan and tables into `up`; false when nothing can be printed
-// (the window is a class / extended sequence: P->match is never set)
-bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, uint32_t flags, int32_t pid,
-              Upload& up, size_t& o_slot, size_t& o_tab);
+// (k = 0: the window is a class / extended sequence, P->match is never set;
+// k > 0: detClass 2, the binary dies)
+bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, int k, int errs, uint32_t flags,
+              int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab);
 
 struct XtPrep {
     const XtSlot* slot = nullptr;
@@ -953,6 +961,7 @@ struct XtPrep {
     const uint64_t* tab = nullptr;
     int32_t pid = 0;
     int32_t words = 1;            // eextended: the verify parts' widest word count
+    int32_t eregular = 0;         // rg: k > 0 (pm_regular.hip k_erg_walk)
 };
 // eextended heads + walk on s (keys/lens rewritten in place, acc bit 0 =
 // reported); xt_launch calls it when X.ee is set

@@ -520,9 +520,10 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // (k = 0, pm_extended.hip) or eextended engine (k > 0, pm_eextended.hip)
     // does; its walk computes the ends
     const bool extended = (flags & PM_EXTENDED) && (flags & PM_REPORT_NRGREP);
-    // PM_REGULAR: a regular pattern reported as nrgrep's regular engine does
-    // at k = 0 (pm_regular.hip); its walk computes the ends
-    const bool regular = (flags & PM_REGULAR) && (flags & PM_REPORT_NRGREP) && k == 0 && !extended;
+    // PM_REGULAR: a regular pattern reported as nrgrep's regular engine
+    // (k = 0) or eregular engine (k > 0) does (pm_regular.hip); its walk
+    // computes the ends
+    const bool regular = (flags & PM_REGULAR) && (flags & PM_REPORT_NRGREP) && !extended;
     uint64_t xopt[4] = {}, xrep[4] = {};
     require(!(flags & PM_EXTENDED) || extended_shape(m, W, first, last, follow, xopt, xrep),
             "PM_EXTENDED needs a sequence of classes with '?', '*', '+'");
@@ -534,7 +535,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // ... and for nrgrep's eextended report, whose walk then takes every
     // line (every position a key): the automaton scan is skipped
     const bool ee_all = extended && k > 0 && (errs & PM_ERR_DEL) && min_len <= k;
-    require(!(errs & PM_ERR_DEL) || min_len > k || all_pos || ee_all,
+    // ... and for nrgrep's eregular report (every line a cluster)
+    const bool rg_all = regular && k > 0 && (errs & PM_ERR_DEL) && min_len <= k;
+    require(!(errs & PM_ERR_DEL) || min_len > k || all_pos || ee_all || rg_all,
             "deletions with k >= the shortest match length are not supported by the GPU scan", PM_E_UNSUPPORTED);
     const int ins_extra = (errs & PM_ERR_INS) ? k : 0;   // insertions lengthen a match
     require((uint64_t)max_len + ins_extra < (1ull << 31), "max_len out of range");
@@ -613,12 +616,13 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
                             pattern_id, ee_all, up, o_xslot, o_xtab);
     bool rg_prints = false;
     if (regular) {
-        rg_prints = rg_build(*rgt, byte_mask, W, m, unbounded ? -1 : (int64_t)max_len, (uint32_t)flags, pattern_id,
-                             up, o_xslot, o_xtab);
+        rg_prints = rg_build(*rgt, byte_mask, W, m, unbounded ? -1 : (int64_t)max_len, k, errs, (uint32_t)flags,
+                             pattern_id, up, o_xslot, o_xtab);
         if (!rg_prints) {
-            // the window is a class / extended sequence: simpleScan /
-            // extendedScan never set the state word checkMatch reads, so
-            // nrgrep_coords prints no match (pm_regular.hip); no scan runs
+            // k = 0: the window is a class / extended sequence, simpleScan /
+            // extendedScan never set the state word checkMatch reads; k > 0:
+            // detClass 2, eregularPreproc dies -- nrgrep_coords prints no
+            // match (pm_regular.hip); no scan runs
             pm_hits* h = new pm_hits();
             h->device = db->device;
             h->keys = static_cast<uint64_t*>(pool_get(db->device, 8, &h->keys_cap));
@@ -636,6 +640,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
         xtp.pid = pattern_id;
         xtp.words = m + 1 <= 64 ? 1 : RG_NW;
+        xtp.eregular = k > 0 ? 1 : 0;
     }
     if (extended) {
         if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
@@ -730,7 +735,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // a class sequence on the nucleotide planes: the bit-sliced start pass
     // (pm_ids.hip), 32 streams per lane instead of one
     const bool ids = nuc && W == 1 && a.shift_only && !cross && !unbounded && use_ids_kernel(db);
-    for (int attempt = 0; attempt < 2 && !all_pos && !ee_lines; ++attempt) {
+    for (int attempt = 0; attempt < 2 && !all_pos && !ee_lines && !rg_all; ++attempt) {
         sb = make_sink(db, 1, db->n, expected);
         a.sink = sb.sink();
         bool launched = false;
@@ -757,7 +762,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     }
     // eextended walking every line (EeSlot::lines): every position is a key,
     // the lines are its clusters
-    const bool every_pos = all_pos || ee_lines;
+    const bool every_pos = all_pos || ee_lines || rg_all;
     double kms = every_pos ? 0.0 : ev.ms() + carry_ms;
     if (every_pos) total = db->n;
     pm_hits* h = every_pos ? es_all_positions(db, pattern_id) : sink_to_hits(db, sb, counts, total);

@@ -247,10 +247,11 @@ int det_class(const Automaton& A, int i, const Set& pos) {   // detClass 0x41ac9
 
 struct Plan {
     int type = 3, ell = 0, cls = 3;
+    double best = 0.65;   // regularFindBest's return value (xmm0)
     Set win{}, winit{}, wfinal{};
 };
 
-Plan plan_of(const Automaton& A) {   // regularFindBest 0x40a500 (K = 0)
+Plan plan_of(const Automaton& A, int K = 0) {   // regularFindBest 0x40a500 (its cost C carries + K)
     const int ms = A.ms;
     Costs c;
     c.dist.assign(ms, 1);
@@ -316,7 +317,7 @@ Plan plan_of(const Automaton& A) {   // regularFindBest 0x40a500 (K = 0)
     c.C.assign(ML, 0.0);
     for (int i = 0; i < ms; ++i)
         for (int l = 0; l < L; ++l) {
-            double s = 0.0;   // K = 0
+            double s = (double)K;
             for (int a = 0; a <= l; ++a) s += pi(i, l, a);
             c.C[(size_t)i * L + l] = s;
         }
@@ -340,6 +341,7 @@ Plan plan_of(const Automaton& A) {   // regularFindBest 0x40a500 (K = 0)
             if (--ell == 0 || 1.0 >= best * ell) break;
         }
     }
+    p.best = best;
     if (0.65 > best) {
         p.type = 2;
     } else {
@@ -374,44 +376,349 @@ int window_states(const Plan& p, int ms) {
     return mp;
 }
 
-}  // namespace
+// ---------------------------------------------------------------------------
+// eregular (k > 0, at most 64 states: one word): eregularPreproc 0x406a20
+// ---------------------------------------------------------------------------
 
-bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, uint32_t flags, int32_t pid,
-              Upload& up, size_t& o_slot, size_t& o_tab) {
-    const Automaton A = make_automaton(t, B, W, npos);
-    const Plan P = plan_of(A);
-    if (P.cls != 3) return false;   // simpleScan / extendedScan never leave P->match set: nothing prints
-    const int ms = A.ms, mp = window_states(P, ms);
-    require(mp <= 64, "regular: a window of more than 64 states", PM_E_UNSUPPORTED);
-    RgSlot S{};
-    S.ms = ms;
-    S.nw = ms <= 64 ? 1 : RG_NW;
-    S.mp = mp;
-    S.type = P.type;
-    S.ell = P.ell;
-    S.anchors = (int32_t)(flags & (PM_ANCHOR_START | PM_ANCHOR_END));
-    S.pid = pid;
-    // bounded clusters unless the pattern is unbounded or the forward
-    // window's final states are not the automaton's (more than 64 states)
-    S.max_len = (max_len < 0 || (P.type == 3 && ms > 64)) ? -1 : max_len;
-    for (int q = 0; q < RG_NW; ++q) {
-        S.final_[q] = A.final_[q];
-        S.vis[q] = A.vis[q];
+inline uint64_t trans1(const std::vector<Set>& tab, uint64_t d) {
+    uint64_t r = 0;
+    while (d) {
+        r |= tab[__builtin_ctzll(d)][0];
+        d &= d - 1;
     }
-    // regularRemapStates 0x40bab0: window states 1.. in state order, 0 the
-    // virtual initial state
+    return r;
+}
+
+struct EPlan {
+    int etype = 3, ell = 0, cls = 3, npieces = 1;
+    bool pieces_computed = false, defined = true;
+    uint64_t pwin[PM_MAX_K + 1] = {}, pini[PM_MAX_K + 1] = {}, pfin[PM_MAX_K + 1] = {};
+    int first[PM_MAX_K + 1] = {};
+    uint64_t match0 = 0;   // class 1: P->0x28
+};
+
+// regularFindBest with K, the breadth-first levels, the piece DP against
+// 0.78 and (K + 1) 1.3 fb, detClass of windows[0] (oracle/pm_nrgrep_reg.c
+// eplan; transpositions off, PatMatch's letters are i/d/s)
+EPlan eplan_of(const Automaton& A, int K) {
+    require(A.ms <= 64, "eregular: more than 64 states", PM_E_UNSUPPORTED);
+    require(K >= 1 && K <= PM_MAX_K, "eregular: k out of range");
+    const Plan fb = plan_of(A, K);
+    const int m = A.ms, transp = 0;
+    const uint64_t fin = A.final_[0];
+    uint64_t seen = 1;
+    int nlev = 1;
+    while (!(seen & fin)) {   // 0x406db8
+        ++nlev;
+        seen |= trans1(A.arrows, seen);
+        require(nlev <= m + 2, "eregular: no final state reachable");
+    }
+    const int minlen = nlev - 1;
+    std::vector<uint64_t> lev(nlev, 0);
+    lev[0] = 1;
+    seen = 1;
+    for (int i = 1; i <= minlen; ++i) {   // 0x406f69
+        const uint64_t succ = trans1(A.arrows, seen);
+        lev[i] = succ & ~seen;
+        seen |= succ;
+    }
+    int pl0 = minlen - K * transp;   // 0x406e54
+    if ((unsigned)pl0 > 64u) pl0 = 64;
+    pl0 = pl0 / (K + 1);
+    const int PL1 = pl0 + 1;
+    double best = 0.78;
+    int chosen = 0;
+    uint64_t pieces[PM_MAX_K + 1] = {};
+    if (PL1 > 1 && pl0 != 1 && !(1.0 / (double)pl0 > 0.78)) {
+        double lp[256];
+        letter_probs(lp);
+        std::vector<double> prob(m, 0.0);
+        for (int i = 0; i < m; ++i)
+            for (int c = 0; c < 256; ++c)
+                if ((A.B[c][0] >> i) & 1) prob[i] += lp[c];
+        std::vector<double> Av((size_t)m * PL1, 0.0);
+        for (int i = 0; i < m; ++i) {
+            Av[(size_t)i * PL1] = 1.0;
+            Av[(size_t)i * PL1 + 1] = prob[i];
+        }
+        for (int l = 2; l < PL1; ++l)   // 0x407118
+            for (int i = 0; i < m; ++i) {
+                double sum = 0.0;
+                for (int j = 0; j < m; ++j)
+                    if ((A.arrows[i][0] >> j) & 1) sum += Av[(size_t)j * PL1 + l - 1];
+                sum *= prob[i];
+                Av[(size_t)i * PL1 + l] = 1.0 < sum ? 1.0 : sum;
+            }
+        std::vector<double> Bt((size_t)m * PL1 * PL1, 0.0);
+        auto bt = [&](int i, int l, int a) -> double& { return Bt[((size_t)i * PL1 + l) * PL1 + a]; };
+        for (int i = 0; i < m; ++i)
+            for (int l = 0; l < PL1; ++l) bt(i, l, 0) = 1.0;
+        for (int l = 1; l < PL1; ++l)   // 0x4072a0
+            for (int a = 1; a <= l; ++a)
+                for (int i = 0; i < m; ++i) {
+                    double v = Av[(size_t)i * PL1 + a];
+                    if (a < l)
+                        for (int j = 0; j < m; ++j)
+                            if ((A.arrows[i][0] >> j) & 1) v = 1.0 - (1.0 - v) * (1.0 - bt(j, l - 1, a));
+                    bt(i, l, a) = v;
+                }
+        std::vector<double> C((size_t)nlev * PL1, 0.0);
+        for (int lv = 0; lv < nlev; ++lv)   // 0x40742d
+            for (int l = 0; l < PL1; ++l) {
+                double sum = 1.0;
+                for (int i = 0; i < m; ++i)
+                    if (((lev[lv] >> i) & 1) && l != 0)
+                        for (int a = 1; a <= l; ++a) sum += bt(i, l, a);
+                C[(size_t)lv * PL1 + l] = sum;
+            }
+        const int W2 = K + 2;
+        std::vector<double> D((size_t)(nlev + 1) * W2, 0.0);
+        std::vector<int> E((size_t)(nlev + 1) * W2, 0);
+        for (int pl = pl0;;) {   // 0x40772e
+            for (int r = 1; r <= nlev; ++r) D[(size_t)r * W2] = 0.0;
+            for (int c = 1, esi = nlev - pl; c <= K + 1; ++c, esi -= pl + transp)
+                for (int r = (esi < 0 ? 0 : esi) + 1; r <= nlev; ++r) D[(size_t)r * W2 + c] = 1.0;
+            for (int c = 1; c <= K + 1; ++c) {   // 0x407850
+                const int r11 = nlev - pl - (c - 1) * (pl + transp);
+                for (int r = r11; r >= 1; --r) {
+                    double v = C[(size_t)r * PL1 + pl];
+                    if ((double)(pl + 1) > v) {
+                        v = v / ((double)pl - v + 1.0);
+                        v = 1.0 < v ? 1.0 : v;
+                    } else {
+                        v = 1.0;
+                    }
+                    if (c > 1) v = 1.0 - (1.0 - v) * (1.0 - D[(size_t)(r + pl + transp) * W2 + c - 1]);
+                    E[(size_t)r * W2 + c] = r;
+                    const double y = D[(size_t)(r + 1) * W2 + c];
+                    if (v > y) {
+                        v = y;
+                        E[(size_t)r * W2 + c] = E[(size_t)(r + 1) * W2 + c];
+                    }
+                    D[(size_t)r * W2 + c] = v;
+                }
+            }
+            if (best > D[W2 + K + 1]) {   // 0x407a0b
+                int r = 1;
+                for (int i = 0, c = K + 1; c >= 1; ++i, --c) {
+                    const int st = E[(size_t)r * W2 + c];
+                    pieces[i] = lev[st];
+                    r = st + pl + transp;
+                }
+                best = D[W2 + K + 1];
+                chosen = pl;
+            }
+            if (--pl == 1) break;
+            if (!(1.0 / (double)pl <= best)) break;
+        }
+    }
+    EPlan e;
+    bool use_pieces = false;
+    if (best < 0.78) {   // 0x4082c9
+        e.pieces_computed = true;
+        for (int i = 0; i <= K; ++i) {
+            uint64_t w = pieces[i], last = 0;
+            for (int st = 0; st < chosen; ++st) {
+                last = trans1(A.arrows, w);
+                w |= last;
+            }
+            e.pwin[i] = w;
+            e.pini[i] = pieces[i];
+            e.pfin[i] = last;
+        }
+        use_pieces = !(best >= (double)(K + 1) * 1.3 * fb.best) && chosen != 0;   // 0x40842a
+    }
+    if (use_pieces) {
+        e.etype = 1;
+        e.ell = chosen;
+        e.npieces = K + 1;
+    } else {   // 0x407bb9
+        e.etype = fb.ell == 0 ? 3 : 2;
+        e.ell = fb.ell;
+        e.npieces = 1;
+        e.pwin[0] = fb.win[0];
+        e.pini[0] = fb.winit[0];
+        e.pfin[0] = fb.wfinal[0];
+    }
+    Set w0{};
+    w0[0] = e.pwin[0];
+    e.cls = det_class(A, 0, w0);
+    if (e.cls == 1) {   // 0x407e4b: the first state of each window (windows[1 .. K] unset for a window plan)
+        const int nw = (e.etype == 1 || e.pieces_computed) ? K + 1 : 1;
+        e.defined = nw == K + 1;
+        for (int i = 0; i < nw; ++i) {
+            int f = 0;
+            while (f < m && !((e.pwin[i] >> f) & 1)) ++f;
+            e.first[i] = f;
+            if (e.ell != 0) {
+                e.match0 |= 1ull << (f & 63);
+            } else {
+                int r = f + 1;
+                while (r < m && ((e.pwin[i] >> r) & 1)) ++r;
+                e.match0 |= 1ull << (r & 63);
+            }
+        }
+    }
+    return e;
+}
+
+// The window automaton's tables (regularRemapStates 0x40bab0 +
+// regularLoadFast 0x40c4f0): window states 1.. in state order, 0 the virtual
+// initial one; backward (ell > 0): reversed, every state initial; forward:
+// state 0 loops on every byte.
+void window_tables(const Automaton& A, const Set& win, const Set& winit, const Set& wfinal, int ell, RgSlot& S,
+                   std::vector<uint64_t>& tab, bool eregular) {
+    const int ms = A.ms;
+    int mp = 1;
+    for (int q = 1; q < ms; ++q) mp += has(win, q);
+    require(mp <= 64, "regular: a window of more than 64 states", PM_E_UNSUPPORTED);
+    S.mp = mp;
     std::vector<int> map(ms, 0);
     int k = 0;
-    for (int s = 1; s < ms; ++s)
-        if (has(P.win, s)) map[s] = ++k;
-    for (int s = 0; s < ms; ++s)
-        if (has(P.win, s)) S.unmap[map[s]] = s;
+    for (int q = 1; q < ms; ++q)
+        if (has(win, q)) map[q] = ++k;
+    for (int i = 0; i < 64; ++i) S.unmap[i] = eregular ? -1 : 0;
+    for (int q = 0; q < ms; ++q)
+        if (has(win, q)) S.unmap[map[q]] = q;
+    uint64_t* fw = tab.data() + S.o_fw;
+    for (int q = 0; q < ms; ++q)
+        if (has(winit, q)) fw[0] |= 1ull << map[q];
+    for (int q = 0; q < ms; ++q)
+        if (has(win, q))
+            for (int t = 0; t < ms; ++t)
+                if (has(win, t) && has(A.arrows[q], t)) fw[map[q]] |= 1ull << map[t];
+    uint64_t fin = 0;
+    for (int q = 0; q < ms; ++q)
+        if (has(wfinal, q)) fin |= 1ull << map[q];
+    uint64_t* Bw = tab.data() + S.o_Bw;
+    for (int c = 0; c < 256; ++c)
+        for (int q = 0; q < ms; ++q)
+            if (has(win, q) && has(A.B[c], q)) Bw[c] |= 1ull << map[q];
+    const uint64_t all = mp >= 64 ? ~0ull : (1ull << mp) - 1;
+    if (ell > 0) {   // regularLoadFast 0x40c5dd: reversed, every state initial
+        uint64_t* rw = tab.data() + S.o_rw;
+        for (int a = 0; a < mp; ++a)
+            for (int b = 0; b < mp; ++b)
+                if ((fw[a] >> b) & 1) rw[b] |= 1ull << a;
+        S.finit = all;
+        S.ffinal = 1;
+        uint64_t* Av = tab.data() + S.o_A;
+        for (int c = 0; c < 256; ++c) {
+            const uint64_t d = all & Bw[c];
+            for (int q = 0; q < mp; ++q)
+                if ((d >> q) & 1) Av[c] |= rw[q];
+        }
+    } else {         // 0x40c771: state 0 loops on every byte
+        fw[0] |= 1;
+        for (int c = 0; c < 256; ++c) Bw[c] |= 1;
+        S.finit = 1;
+        S.ffinal = fin;
+    }
+}
+
+}  // namespace
+
+bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_len, int k, int errs, uint32_t flags,
+              int32_t pid, Upload& up, size_t& o_slot, size_t& o_tab) {
+    const Automaton A = make_automaton(t, B, W, npos);
+    const int ms = A.ms;
+    RgSlot S{};
+    S.ms = ms;
+    S.anchors = (int32_t)(flags & (PM_ANCHOR_START | PM_ANCHOR_END));
+    S.pid = pid;
+    S.k = k;
+    S.errs = errs;
     std::vector<uint64_t> tab;
     auto take = [&](size_t words) {
         const uint64_t o = tab.size();
         tab.resize(tab.size() + words, 0);
         return o;
     };
+    if (k > 0) {
+        const EPlan E = eplan_of(A, k);
+        // class 2: eregularPreproc stores through a null pointer (0x4081ed),
+        // nrgrep_coords dies before the scan: nothing prints
+        if (E.cls == 2) return false;
+        S.nw = 1;
+        S.type = E.etype;
+        S.ell = E.ell;
+        S.cls = E.cls;
+        S.match0 = E.match0;
+        for (int i = 0; i <= PM_MAX_K; ++i) S.first[i] = E.first[i];
+        // a match covers at most max_len + k characters (insertions); the
+        // walk replays from span + 4 before a cluster, clusters break at
+        // 2 span + 4 or at a line break
+        S.max_len = max_len < 0 ? -1 : max_len + k;
+        S.gap = max_len < 0 ? -1 : 2 * S.max_len + 4;
+        S.lines = 1;
+        S.final_[0] = A.final_[0];
+        S.o_arr = take(64);
+        S.o_rev = take(64);
+        S.o_B = take(256);
+        S.o_Bw = take(256);
+        S.o_A = take(256);
+        S.o_fw = take(64);
+        S.o_rw = take(64);
+        S.o_T0 = take(256);
+        S.o_T2 = take(256);
+        for (int q = 0; q < ms; ++q) {
+            tab[S.o_arr + q] = A.arrows[q][0];
+            tab[S.o_rev + q] = A.rev[q][0];
+        }
+        for (int c = 0; c < 256; ++c) tab[S.o_B + c] = A.B[c][0];
+        if (E.cls == 3) {   // eregularLoadFast 0x406860: the union of the windows
+            Set uw{}, ui{}, uf{};
+            for (int i = 0; i < E.npieces; ++i) {
+                uw[0] |= E.pwin[i];
+                ui[0] |= E.pini[i];
+                uf[0] |= E.pfin[i];
+            }
+            window_tables(A, uw, ui, uf, E.ell, S, tab, true);
+            S.nstates = S.mp;
+        } else {            // esimpleLoadFast 0x415370 over the states first[r] ..
+            S.nstates = ms;
+            S.mp = ms;
+            for (int i = 0; i < 64; ++i) S.unmap[i] = i < ms ? i : -1;
+            uint64_t* T0 = tab.data() + S.o_T0;
+            uint64_t* T2 = tab.data() + S.o_T2;
+            for (int c = 0; c < 256; ++c) {
+                const uint64_t bc = A.B[c][0];
+                if (E.etype == 1) {   // 0x4153fa: the pieces, bit r * pl + pp
+                    for (int r = 0; r <= k; ++r)
+                        for (int pp = 0; pp < E.ell; ++pp) {
+                            const int st = E.first[r] + E.ell - 1 - pp;
+                            if (st < 64 && ((bc >> st) & 1)) {
+                                const uint64_t bit = 1ull << (r * E.ell + pp);
+                                T0[c] |= bit;
+                                if (pp > 0) T2[c] |= bit;
+                            }
+                        }
+                } else {              // simpleLoadFast 0x417561: the window backward
+                    for (int r = 0; r < E.ell; ++r) {
+                        const int st = E.first[0] + E.ell - 1 - r;
+                        if (st < 64 && ((bc >> st) & 1)) T0[c] |= 1ull << (64 - E.ell + r);
+                    }
+                }
+            }
+        }
+        o_slot = up.add(&S, sizeof(S));
+        o_tab = up.add(tab.data(), tab.size() * 8);
+        return true;
+    }
+    const Plan P = plan_of(A);
+    if (P.cls != 3) return false;   // simpleScan / extendedScan never leave P->match set: nothing prints
+    S.nw = ms <= 64 ? 1 : RG_NW;
+    S.type = P.type;
+    S.ell = P.ell;
+    S.cls = 3;
+    // bounded clusters unless the pattern is unbounded or the forward
+    // window's final states are not the automaton's (more than 64 states)
+    S.max_len = (max_len < 0 || (P.type == 3 && ms > 64)) ? -1 : max_len;
+    S.gap = S.max_len < 0 ? -1 : 2 * S.max_len + 2;
+    for (int q = 0; q < RG_NW; ++q) {
+        S.final_[q] = A.final_[q];
+        S.vis[q] = A.vis[q];
+    }
     const int nw = S.nw;
     S.o_arr = take((size_t)ms * nw);
     S.o_rev = take((size_t)ms * nw);
@@ -427,40 +734,7 @@ bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_l
         }
     for (int c = 0; c < 256; ++c)
         for (int q = 0; q < nw; ++q) tab[S.o_B + (size_t)c * nw + q] = A.B[c][q];
-    uint64_t* fw = tab.data() + S.o_fw;
-    for (int s = 0; s < ms; ++s)
-        if (has(P.winit, s)) fw[0] |= 1ull << map[s];
-    for (int s = 0; s < ms; ++s)
-        if (has(P.win, s))
-            for (int q = 0; q < ms; ++q)
-                if (has(P.win, q) && has(A.arrows[s], q)) fw[map[s]] |= 1ull << map[q];
-    uint64_t fin = 0;
-    for (int s = 0; s < ms; ++s)
-        if (has(P.wfinal, s)) fin |= 1ull << map[s];
-    uint64_t* Bw = tab.data() + S.o_Bw;
-    for (int c = 0; c < 256; ++c)
-        for (int s = 0; s < ms; ++s)
-            if (has(P.win, s) && has(A.B[c], s)) Bw[c] |= 1ull << map[s];
-    const uint64_t all = mp >= 64 ? ~0ull : (1ull << mp) - 1;
-    if (P.type == 2) {   // regularLoadFast 0x40c5dd: reversed, every state initial
-        uint64_t* rw = tab.data() + S.o_rw;
-        for (int a = 0; a < mp; ++a)
-            for (int b = 0; b < mp; ++b)
-                if ((fw[a] >> b) & 1) rw[b] |= 1ull << a;
-        S.finit = all;
-        S.ffinal = 1;
-        uint64_t* Av = tab.data() + S.o_A;
-        for (int c = 0; c < 256; ++c) {
-            const uint64_t d = all & Bw[c];
-            for (int q = 0; q < mp; ++q)
-                if ((d >> q) & 1) Av[c] |= rw[q];
-        }
-    } else {             // 0x40c771: state 0 loops on every byte
-        fw[0] |= 1;
-        for (int c = 0; c < 256; ++c) Bw[c] |= 1;
-        S.finit = 1;
-        S.ffinal = fin;
-    }
+    window_tables(A, P.win, P.winit, P.wfinal, P.type == 2 ? P.ell : 0, S, tab, false);
     o_slot = up.add(&S, sizeof(S));
     o_tab = up.add(tab.data(), tab.size() * 8);
     return true;
@@ -485,8 +759,10 @@ __global__ __launch_bounds__(RG_T) void k_rg_heads(XtPrep X, const uint64_t* __r
         if (!head) {
             const uint64_t a = keys[i - 1] & RG_POS_MASK, b = keys[i] & RG_POS_MASK;
             if (xt_region(tv, a) != xt_region(tv, b)) head = true;
-            else if (S.max_len >= 0) head = b - a > 2 * (uint64_t)S.max_len + 2;
-            else head = xt_brk_between(tv, a, b, RG_SCAN);
+            else if (S.gap >= 0 && b - a > (uint64_t)S.gap) head = true;
+            // (a break at a itself: every position is a key when deletions
+            // can empty the pattern)
+            else if (S.gap < 0 || S.lines) head = xt_brk(tv, a) || xt_brk_between(tv, a, b, RG_SCAN);
         }
         acc[i] = head ? 2 : 0;
     }
@@ -693,6 +969,476 @@ struct RgWalk {
     }
 };
 
+// eregular (k > 0, one word): the scanners and checkMatch of
+// oracle/pm_nrgrep_reg.c over the cluster's text
+struct ErgWalk {
+    const RgSlot* S;
+    const uint64_t* tab;
+    TextView tv;
+    uint64_t n;        // the region end
+    uint64_t R;
+    uint64_t nl_lo, nl_hi;
+
+    __device__ uint8_t at(uint64_t p) const { return xt_byte(tv, p); }
+    __device__ uint64_t next_nl(uint64_t p) const {
+        if (tv.nuc_layout) {
+            while (p < n) {
+                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
+                if (!z) {
+                    p = ((p >> 5) + 1) << 5;
+                    continue;
+                }
+                p += (uint64_t)__builtin_ctz(z);
+                if (p >= n) break;
+                if (at(p) == (uint8_t)'\n') return p;
+                ++p;
+            }
+            return n;
+        }
+        for (; p < n; ++p)
+            if (tv.raw[p] == (uint8_t)'\n') return p;
+        return n;
+    }
+    __device__ void record(uint64_t rp, uint64_t& rb, uint64_t& re) {   // recGetRecord 0x402030
+        while (nl_hi < rp) {
+            nl_lo = nl_hi;
+            nl_hi = next_nl(nl_hi + 1);
+        }
+        rb = (nl_lo != ~0ull && nl_lo >= R) ? nl_lo + 1 : R;
+        re = nl_hi;
+    }
+    __device__ bool left_ok(uint64_t p, uint64_t lim) const {
+        return !((S->anchors & PM_ANCHOR_START) && p > lim && at(p - 1) != (uint8_t)'\n');
+    }
+    __device__ bool right_ok(uint64_t q, uint64_t lim) const {
+        return !((S->anchors & PM_ANCHOR_END) && q < lim && at(q) != (uint8_t)'\n');
+    }
+    __device__ static uint64_t tr(const uint64_t* tb, uint64_t d) {
+        uint64_t r = 0;
+        while (d) {
+            r |= tb[__builtin_ctzll(d)];
+            d &= d - 1;
+        }
+        return r;
+    }
+    // fwdCheck 0x403310: from state s (it read t[p]) forward; kio: budget in,
+    // errors used out
+    __device__ uint64_t efwd(uint64_t p, uint64_t lim, int s, int& kio) const {
+        const int K = kio, ins = S->errs & PM_ERR_INS, del = S->errs & PM_ERR_DEL, sub = S->errs & PM_ERR_SUB;
+        const uint64_t* arr = tab + S->o_arr;
+        const uint64_t* B = tab + S->o_B;
+        const uint64_t F = S->final_[0];
+        uint64_t rows[PM_MAX_K + 1];
+        rows[0] = 1ull << s;
+        if (rows[0] & F) {   // 0x40339d: insertions up to the right context
+            kio = 0;
+            for (uint64_t q = p + 1;; ++q) {
+                if (right_ok(q, lim + 1)) return q - 1;
+                if (q == lim + 1 || !ins) return RG_NONE;
+                if (++kio > K) return RG_NONE;
+            }
+        }
+        int kmax = K;
+        uint64_t best = RG_NONE;
+        for (int j = 1; j <= kmax; ++j) {   // 0x4034c0 (rows left unset without OptDel: row 0)
+            rows[j] = del ? rows[j - 1] | tr(arr, rows[j - 1]) : rows[j - 1];
+            if (del && (rows[j] & F) && right_ok(p + 1, lim + 1)) {
+                kio = j;
+                kmax = j - 1;
+                best = p;
+            }
+        }
+        if (p == lim) return best;
+        for (uint64_t cur = p;;) {
+            ++cur;
+            const uint64_t bc = B[at(cur)];
+            const uint64_t n0 = tr(arr, rows[0]) & bc;
+            if ((n0 & F) && right_ok(cur + 1, lim + 1)) {
+                kio = 0;
+                return cur;
+            }
+            uint64_t oldp = rows[0], last = n0;
+            rows[0] = n0;
+            for (int j = 1; j <= kmax; ++j) {   // 0x4037a0
+                uint64_t v = del ? tr(arr, last) : 0;
+                if (ins) v |= oldp;
+                if (sub) v |= tr(arr, oldp);
+                v |= tr(arr, rows[j]) & bc;
+                const uint64_t oj = rows[j];
+                rows[j] = v;
+                last = v;
+                if ((v & F) && right_ok(cur + 1, lim + 1)) {   // 0x403a01: the fewest errors
+                    int c = j;
+                    while (c - 1 >= 0 && (rows[c - 1] & F)) --c;
+                    if (c == 0) {
+                        kio = 0;
+                        return cur;
+                    }
+                    kio = c;
+                    kmax = c - 1;
+                    best = cur;
+                    break;
+                }
+                oldp = oj;
+            }
+            if (!last || cur == lim) return best;
+        }
+    }
+    // bwdCheck 0x403df0: from state s (it reads t[p - 1]) backward
+    __device__ uint64_t ebwd(uint64_t p, uint64_t lim, int s, int& kio) const {
+        const int K = kio, ins = S->errs & PM_ERR_INS, del = S->errs & PM_ERR_DEL, sub = S->errs & PM_ERR_SUB;
+        const uint64_t* rev = tab + S->o_rev;
+        const uint64_t* B = tab + S->o_B;
+        uint64_t rows[PM_MAX_K + 1];
+        rows[0] = 1ull << s;
+        if (rows[0] & 1) {   // 0x403e71: insertions down to the left context
+            kio = 0;
+            for (uint64_t q = p;;) {
+                if (left_ok(q, lim)) return q;
+                if (q == lim) return RG_NONE;
+                --q;
+                if (!ins) return RG_NONE;
+                if (++kio > K) return RG_NONE;
+            }
+        }
+        int kmax = K;
+        uint64_t best = RG_NONE;
+        for (int j = 1; j <= kmax; ++j) {   // 0x403f80
+            rows[j] = del ? rows[j - 1] | tr(rev, rows[j - 1]) : rows[j - 1];
+            if (del && (rows[j] & 1) && left_ok(p, lim)) {
+                kio = j;
+                kmax = j - 1;
+                best = p;
+            }
+        }
+        if (p == lim) return best;
+        for (uint64_t cur = p;;) {
+            --cur;
+            const uint64_t bc = B[at(cur)];
+            const uint64_t n0 = tr(rev, rows[0] & bc);
+            if ((n0 & 1) && left_ok(cur, lim)) {
+                kio = 0;
+                return cur;
+            }
+            uint64_t oldp = rows[0], last = n0;
+            rows[0] = n0;
+            for (int j = 1; j <= kmax; ++j) {   // 0x404230
+                uint64_t v = del ? tr(rev, last) : 0;
+                if (ins) v |= oldp;
+                if (sub) v |= tr(rev, oldp);
+                v |= tr(rev, rows[j] & bc);
+                const uint64_t oj = rows[j];
+                rows[j] = v;
+                last = v;
+                if ((v & 1) && left_ok(cur, lim)) {
+                    int c = j;
+                    while (c - 1 >= 0 && (rows[c - 1] & 1)) --c;
+                    if (c == 0) {
+                        kio = 0;
+                        return cur;
+                    }
+                    kio = c;
+                    kmax = c - 1;
+                    best = cur;
+                    break;
+                }
+                oldp = oj;
+            }
+            if (!last || cur == lim) return best;
+        }
+    }
+    // checkMatch 0x406010: the states of `match` in order; the first whose
+    // first phase succeeds decides
+    __device__ bool check(uint64_t pos, uint64_t match, uint64_t& mb, uint64_t& me) {
+        if (S->type == 3 && pos == 0) return false;
+        const uint64_t rp = S->type == 3 ? pos - 1 : pos;
+        uint64_t rb, re;
+        record(rp, rb, re);
+        if (rp < rb || rp >= re) return false;
+        if (S->nstates < 64) match &= (1ull << S->nstates) - 1;
+        while (match) {
+            const int i = __builtin_ctzll(match);
+            match &= match - 1;
+            const int s = S->unmap[i];
+            if (s < 0) continue;
+            int k1 = S->k, k2;
+            uint64_t st, en;
+            if (S->type != 3) {
+                en = efwd(pos, re - 1, s, k1);
+                if (en == RG_NONE) continue;
+                k2 = S->k - k1;
+                st = ebwd(pos + 1, rb, s, k2);
+            } else {
+                st = ebwd(pos, rb, s, k1);
+                if (st == RG_NONE) continue;
+                k2 = S->k - k1;
+                en = efwd(pos - 1, re - 1, s, k2);
+            }
+            if (st == RG_NONE || en == RG_NONE) return false;   // 0x406248: the second phase fails the candidate
+            mb = st;
+            me = en + 1;
+            return true;
+        }
+        return false;
+    }
+    // eregularScan / esimpleScan from R; false when no candidate at or
+    // before stop verifies
+    __device__ bool scan(uint64_t stop, uint64_t& mb, uint64_t& me) {
+        const int K = S->k, ell = S->ell;
+        if (S->cls == 1 && S->type == 1) {   // esimpleScan's pieces (0x413780)
+            const uint64_t* T0 = tab + S->o_T0;
+            const uint64_t* T2 = tab + S->o_T2;
+            const int np = K + 1;
+            if (n < (uint64_t)ell) return false;
+            int64_t r9 = (int64_t)R - 1;
+            const int64_t limit = (int64_t)n - ell;
+            while (r9 < limit) {
+                if ((uint64_t)(r9 + 1) > stop) return false;
+                uint64_t D = T0[at((uint64_t)(r9 + ell))];
+                if (!D) {
+                    r9 += ell;
+                    continue;
+                }
+                int64_t a = r9 + ell - 1;
+                int kk = ell - 1;
+                do {
+                    D = (D << 1) & T2[at((uint64_t)a)];
+                    --kk;
+                    --a;
+                } while (D && kk);
+                if (D) {
+                    bool any = false;
+                    for (int i = 0; i < np; ++i) {   // 0x41384b: a 32-bit shift
+                        const int bit = i * ell + ell - 1;
+                        any |= (D & (uint64_t)(int64_t)(int32_t)(1u << (bit & 31))) != 0;
+                    }
+                    if (any && check((uint64_t)(r9 + 1), S->match0, mb, me)) return true;
+                }
+                r9 += kk + 1;
+            }
+            return false;
+        }
+        if (S->cls == 1) {                   // esimpleScan's ABNDM window (0x413b6f)
+            const uint64_t* T = tab + S->o_T0;
+            const uint64_t top = ~0ull << (64 - ell);
+            const int W = ell - K;
+            if (n < (uint64_t)(ell - K - 1)) return false;
+            const uint64_t limit = n - (uint64_t)(ell - K - 1);
+            uint64_t Rr[PM_MAX_K + 1], Tr[PM_MAX_K + 1];
+            for (uint64_t s = R; s < limit;) {
+                if (s > stop) return false;
+                const uint64_t b0 = T[at(s + W - 1)];
+                Rr[0] = b0;
+                for (int j = 1; j <= K; ++j) {
+                    Rr[j] = top;
+                    Tr[j] = b0;
+                }
+                int64_t rb = W - 2;
+                for (;;) {
+                    const uint64_t bc = T[at(s + (uint64_t)rb)];
+                    uint64_t oldp = Rr[0], newp = (oldp << 1) & bc;
+                    Rr[0] = newp;
+                    for (int j = 1; j <= K; ++j) {
+                        const uint64_t trans = (bc << 1) & Tr[j];
+                        uint64_t v = ((newp | oldp) << 1) | oldp;
+                        Tr[j] = (oldp << 2) & bc;
+                        v |= trans;
+                        const uint64_t oldj = Rr[j];
+                        v |= (oldj << 1) & bc;
+                        Rr[j] = v;
+                        oldp = oldj;
+                        newp = v;
+                    }
+                    if (rb == 0) {
+                        if ((Rr[K] >> 63) && check(s, S->match0, mb, me)) return true;
+                        break;
+                    }
+                    if (!Rr[K] && !Tr[K]) break;
+                    --rb;
+                }
+                s += (uint64_t)(rb + 1);
+            }
+            return false;
+        }
+        const uint64_t* Bw = tab + S->o_Bw;
+        const uint64_t* Av = tab + S->o_A;
+        const uint64_t* rw = tab + S->o_rw;
+        const uint64_t* fw = tab + S->o_fw;
+        if (S->type == 1) {                  // the pieces exactly (0x4052b9)
+            if (n < (uint64_t)ell) return false;
+            int64_t pos = (int64_t)R - 1;
+            const int64_t lim = (int64_t)n - ell;
+            while (pos < lim) {
+                if ((uint64_t)(pos + 1) > stop) return false;
+                uint64_t rcx = Av[at((uint64_t)(pos + ell))];
+                if (!rcx) {
+                    pos += ell;
+                    continue;
+                }
+                uint64_t D = 0;
+                int64_t c = pos + ell - 1;
+                bool dead = false;
+                for (;;) {
+                    D = rcx & Bw[at((uint64_t)c)];
+                    rcx = tr(rw, D);
+                    if (!rcx) {
+                        dead = true;
+                        break;
+                    }
+                    if (--c == pos) break;
+                }
+                if (dead) {
+                    pos = c;
+                    continue;
+                }
+                if ((rcx & S->ffinal) && check((uint64_t)(pos + 1), D, mb, me)) return true;
+                ++pos;
+            }
+            return false;
+        }
+        uint64_t rows[PM_MAX_K + 1], old[PM_MAX_K + 1];
+        if (S->type == 2) {                  // bwdScanrk 0x402d50
+            const int W = ell - K;
+            if (n < (uint64_t)W) return false;
+            int64_t pos = (int64_t)R - 1;
+            const int64_t lim = (int64_t)n - W;
+            while (pos < lim) {
+                if ((uint64_t)(pos + 1) > stop) return false;
+                const uint8_t c0 = at((uint64_t)(pos + W));
+                uint64_t bprev = Bw[c0];
+                rows[0] = Av[c0];
+                for (int j = 1; j <= K; ++j) rows[j] = S->finit;
+                for (int j = 0; j <= K; ++j) old[j] = S->finit;
+                int64_t cur = pos + W - 1;
+                for (;;) {
+                    const uint64_t bc = Bw[at((uint64_t)cur)];
+                    uint64_t po = rows[0], pn = tr(rw, bc & po);
+                    rows[0] = pn;
+                    for (int j = 1; j <= K; ++j) {   // 0x4030d0
+                        const uint64_t oj = rows[j];
+                        uint64_t v = po | tr(rw, pn | po) | tr(rw, bc & oj);
+                        v |= tr(rw, tr(rw, bc & old[j - 1]) & bprev);
+                        old[j - 1] = po;
+                        rows[j] = v;
+                        po = oj;
+                        pn = v;
+                    }
+                    if (!pn) {               // 0x403230
+                        pos = cur;
+                        break;
+                    }
+                    if (--cur == pos) {      // 0x4031ed
+                        if ((pn & S->ffinal) && check((uint64_t)(pos + 1), po, mb, me)) return true;
+                        ++pos;
+                        break;
+                    }
+                    bprev = bc;
+                }
+            }
+            return false;
+        }
+        uint64_t cur = R;                    // fwdScanrk 0x402830
+        for (;;) {
+            if (cur >= n || cur + 1 > stop) return false;
+            uint8_t c = at(cur++);
+            while (c == (uint8_t)'\n') {
+                if (cur == n) return false;
+                c = at(cur++);
+            }
+            uint64_t st = S->finit;
+            rows[0] = old[0] = st;
+            for (int j = 1; j <= K; ++j) {
+                st |= tr(fw, st);
+                rows[j] = old[j] = st;
+            }
+            uint64_t bc = Bw[c];
+            uint64_t po = rows[0], pn = tr(fw, po) & bc;
+            rows[0] = pn;
+            for (int j = 1; j <= K; ++j) {   // 0x402a31
+                const uint64_t r = pn | po, oj = rows[j];
+                const uint64_t v = r | (tr(fw, oj) & bc) | tr(fw, r);
+                rows[j] = v;
+                po = oj;
+                pn = v;
+            }
+            if (cur >= n) return false;
+            uint64_t bprev = bc;
+            if ((pn & S->ffinal) && check(cur, pn & S->ffinal, mb, me)) return true;
+            for (;;) {                       // 0x402ac0
+                if (cur + 1 > stop) return false;
+                c = at(cur++);
+                if (c == (uint8_t)'\n') break;
+                bc = Bw[c];
+                po = rows[0];
+                pn = tr(fw, po) & bc;
+                rows[0] = pn;
+                for (int j = 1; j <= K; ++j) {   // 0x402b68
+                    const uint64_t oj = rows[j];
+                    uint64_t v = po | (tr(fw, oj) & bc) | tr(fw, pn | po);
+                    v |= tr(fw, tr(fw, old[j - 1]) & bc) & bprev;
+                    old[j - 1] = po;
+                    rows[j] = v;
+                    po = oj;
+                    pn = v;
+                }
+                if (cur == n) return false;
+                if ((pn & S->ffinal) && check(cur, pn & S->ffinal, mb, me)) return true;
+                bprev = bc;
+            }
+        }
+    }
+};
+
+__global__ __launch_bounds__(RG_T) void k_erg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                   const uint64_t* total_d, uint64_t total_h,
+                                                   uint8_t* __restrict__ acc, TextView tv) {
+    const uint64_t total = total_d ? *total_d : total_h;
+    const RgSlot* S = X.rg;
+    for (uint64_t i = blockIdx.x * (uint64_t)RG_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * RG_T) {
+        if (!(acc[i] & 2)) continue;
+        uint64_t j = i + 1;
+        while (j < total && !(acc[j] & 2)) ++j;
+        const uint64_t pid = keys[i] >> 48;
+        const uint64_t first = keys[i] & RG_POS_MASK, last = keys[j - 1] & RG_POS_MASK;
+        uint64_t nout = 0;
+        const uint64_t nmax = j - i;
+        if ((int64_t)pid == X.pid) {
+            uint64_t R0 = 0, n = tv.n;
+            if (tv.reg.n > 1) {
+                const uint32_t r = region_of(tv.reg, first);
+                R0 = tv.reg.t[r];
+                n = tv.reg.e[r];
+            }
+            ErgWalk w{S, X.tab, tv, n, R0, ~0ull, n};
+            // from the start of first's line, at most span + 4 before it
+            // (the scanners' rows then agree with the whole scan's, and no
+            // match found before first can start at another cluster's key)
+            uint64_t lo = R0;
+            if (S->max_len >= 0 && first > R0 + (uint64_t)S->max_len + 4) lo = first - (uint64_t)S->max_len - 4;
+            uint64_t p = first;
+            while (p > lo && !(xt_brk(tv, p - 1) && w.at(p - 1) == (uint8_t)'\n')) --p;
+            w.R = p;
+            // up to last's line end, at most span + 2 after it
+            uint64_t stop = w.next_nl(last);
+            if (S->max_len >= 0) stop = umin64(stop, last + (uint64_t)S->max_len + 2);
+            w.nl_hi = w.next_nl(w.R);
+            for (;;) {
+                uint64_t mb = 0, me = 0;
+                if (!w.scan(stop, mb, me)) break;
+                if (!xt_header(tv, mb) && nout < nmax) {
+                    keys[i + nout] = (pid << 48) | mb;
+                    lens[i + nout] = (uint32_t)(me - mb);
+                    acc[i + nout] = (nout == 0 ? 2 : 0) | 1;
+                    ++nout;
+                }
+                if (me >= n) break;                      // 0x4022eb
+                w.R = me;
+            }
+        }
+        for (uint64_t q = i + nout; q < j; ++q) acc[q] = q == i ? 2 : 0;
+    }
+}
+
 // One thread per cluster head: the printed matches are written in place
 // from the head on (acc bit 0), every other entry of the cluster is cleared.
 template <int NW>
@@ -752,7 +1498,9 @@ void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
                uint8_t* acc, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
     hipLaunchKernelGGL(k_rg_heads, dim3(blocks), dim3(RG_T), 0, s, X, keys, total_d, total_h, acc, tv);
-    if (X.words == 1)
+    if (X.eregular)
+        hipLaunchKernelGGL(k_erg_walk, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    else if (X.words == 1)
         hipLaunchKernelGGL(k_rg_walk<1>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
     else
         hipLaunchKernelGGL(k_rg_walk<RG_NW>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc,
@@ -782,5 +1530,28 @@ extern "C" int pm_regular_plan(int m, int words, const uint64_t* byte_mask, int 
             masks[RG_NW + q] = P.winit[q];
             masks[2 * RG_NW + q] = P.wfinal[q];
         }
+    });
+}
+
+extern "C" int pm_eregular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
+                                const int32_t* tree_nullable, int k, int32_t* out, uint64_t* masks) {
+    return guarded([&] {
+        require(byte_mask != nullptr && tree != nullptr && tree_nullable != nullptr && out != nullptr &&
+                    masks != nullptr,
+                "null argument");
+        require(words >= 1 && words <= 4 && m >= 1 && m <= 64 * words, "m / words out of range");
+        const Automaton A = make_automaton(RgTree{nodes, tree, tree_nullable}, byte_mask, words, m);
+        const EPlan E = eplan_of(A, k);
+        out[0] = E.etype;
+        out[1] = E.ell;
+        out[2] = E.cls;
+        out[3] = E.defined ? 1 : 0;
+        out[4] = E.npieces;
+        for (int i = 0; i < E.npieces; ++i) {
+            masks[3 * i] = E.pwin[i];
+            masks[3 * i + 1] = E.pini[i];
+            masks[3 * i + 2] = E.pfin[i];
+        }
+        masks[3 * (PM_MAX_K + 1)] = E.match0;
     });
 }

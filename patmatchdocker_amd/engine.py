@@ -266,13 +266,17 @@ def route(prog: Program, alphabet: str, k: int, types: str) -> str:
         raise UnsupportedOnGPU("patterns longer than %d positions are not supported" % _lib.PM_MAX_POSITIONS)
     if k > _lib.PM_MAX_K or (nfa_words(prog.m) == 4 and k > 7):
         raise UnsupportedOnGPU("k=%d errors is not supported by the GPU kernels for %d positions" % (k, prog.m))
-    if indel and "d" in types and prog.min_len <= k and prog.kind not in ("simple", "extended"):
+    if indel and "d" in types and prog.min_len <= k and prog.kind not in ("simple", "extended", "regular"):
         # a class sequence runs nrgrep's esimple report, whose walk takes
         # every position of every line then (pm_esimple.hip,
         # es_all_positions); an extended pattern nrgrep's eextended report,
-        # whose walk takes every line (pm_eextended.hip, ee_add_lines)
+        # whose walk takes every line (pm_eextended.hip, ee_add_lines); a
+        # regular one nrgrep's eregular report, every line a cluster
+        # (pm_regular.hip)
         raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
                                % (k, prog.min_len))
+    if k > 0 and prog.kind == "regular" and prog.m + 1 > 64:
+        raise UnsupportedOnGPU("nrgrep's eregular report is restated for at most 63 positions (%d)" % prog.m)
     return "nfa"   # automaton kernels: anything else, long oligos and k > 3 included
 
 
@@ -483,6 +487,26 @@ def regular_plan(prog: Program) -> dict:
             "init": as_int(masks[5:10]), "final": as_int(masks[10:15])}
 
 
+def eregular_plan(prog: Program, k: int) -> dict:
+    """The plan nrgrep's eregularPreproc derives at ``k`` errors
+    (pm_eregular_plan, host only): ``type`` 1 = k + 1 pieces of ``ell``
+    characters found exactly, 2 = a window of ``ell`` characters scanned
+    backward with k errors, 3 = the automaton forward; ``cls`` = detClass of
+    the first window (2: nothing prints); ``windows`` = [(window, init,
+    final)]; ``match`` = checkMatch's state word for class 1."""
+    if prog.kind != "regular":
+        raise ValueError("not a regular pattern: %s" % prog.source)
+    w, bm, _, _, _ = _nfa_tables(prog)
+    tree, tnull = _tree_tables(prog)
+    out = np.zeros(5, dtype=np.int32)
+    masks = np.zeros(3 * (_lib.PM_MAX_K + 1) + 1, dtype=np.uint64)
+    check(_lib.load().pm_eregular_plan(prog.m, w, bm.ctypes.data, len(prog.tree), tree.ctypes.data, tnull.ctypes.data,
+                                       k, out.ctypes.data, masks.ctypes.data))
+    wins = [(int(masks[3 * i]), int(masks[3 * i + 1]), int(masks[3 * i + 2])) for i in range(int(out[4]))]
+    return {"type": int(out[0]), "ell": int(out[1]), "cls": int(out[2]), "defined": bool(out[3]),
+            "windows": wins, "match": int(masks[3 * (_lib.PM_MAX_K + 1)])}
+
+
 def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
                flags: int = None):
     """pm_scan_nfa_wide; returns the raw pm_hits handle (caller destroys),
@@ -497,9 +521,9 @@ def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0,
     if prog.kind == "extended":
         flags |= _lib.PM_EXTENDED  # nrgrep's extended / eextended engine decides the report
     out = ctypes.c_void_p()
-    if prog.kind == "regular" and k == 0:
-        # nrgrep's regular engine decides the report; its plan is priced over
-        # nrgrep's parse tree
+    if prog.kind == "regular" and (flags & _lib.PM_REPORT_NRGREP):
+        # nrgrep's regular (k = 0) / eregular (k > 0) engine decides the
+        # report; its plan is priced over nrgrep's parse tree
         tree, tnull = _tree_tables(prog)
         check(_lib.load().pm_scan_nfa_tree(db.handle, prog.m, w, bm.ctypes.data, fol.ctypes.data, first.ctypes.data,
                                            last.ctypes.data, prog.max_len or 0, prog.min_len, k, errs, pattern_id,

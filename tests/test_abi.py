@@ -117,13 +117,15 @@ def test_route_indels():
     assert engine.route(lin, engine.NUC, 0, "") == "linear"
     assert engine.parse_error_types(2, "") == "ids"
     assert engine.error_mask("ids") == 7 and engine.error_mask("d") == 2
-    # deletions with k >= the shortest match: class sequences and extended
-    # patterns (the esimple / eextended walks over every line); regular
-    # patterns are refused loudly
+    # deletions with k >= the shortest match: class sequences, extended and
+    # regular patterns (the esimple / eextended / eregular walks over every
+    # line); more than 63 positions at k > 0 are refused loudly for regular
+    # patterns
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 3, "d") == "nfa"
     assert engine.route(compile_pattern("(RG?D)"), engine.BYTE, 2, "d") == "nfa"
+    assert engine.route(compile_pattern("(R(GK)?D)"), engine.BYTE, 2, "d") == "nfa"
     with pytest.raises(UnsupportedOnGPU):
-        engine.route(compile_pattern("(R(GK)?D)"), engine.BYTE, 2, "d")
+        engine.route(compile_pattern("(R(GK)?D" + "A" * 60 + ")"), engine.BYTE, 2, "d")
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 2, "d") == "nfa"
 
 

@@ -57,15 +57,17 @@ def tandem_fasta(seed, units, n_records=6, rec_len=5000, width=60, letters="ACGT
     return "".join(out).encode()
 
 
-def _check(engine, oracle_mod, text, progs, alphabet=None):
+def _check(engine, oracle_mod, text, progs, alphabet=None, k=0, types=""):
     db = engine.SequenceDatabase.from_bytes(text, alphabet=alphabet, device=0)
     total = 0
     try:
-        res, _ = engine.scan(db, progs, k=0)
+        res, _ = engine.scan(db, progs, k=k, types=types)
         for prog, r in zip(progs, res):
-            want = oracle_mod.scan_reported(text, prog, 0, "", skip_headers=True)
+            want = oracle_mod.scan_reported(text, prog, k, types, skip_headers=True)
             got = _pairs(r)
-            assert got == want, (prog.source, oracle_mod.regular_plan(prog), len(got), len(want))
+            plan = oracle_mod.regular_plan(prog) if k == 0 else oracle_mod.eregular_plan(prog, k, types)
+            assert got == want, (prog.source, k, types, plan, len(got), len(want),
+                                 sorted(set(got) ^ set(want))[:6])
             total += len(want)
     finally:
         db.close()
@@ -135,3 +137,71 @@ def test_long_records_many_clusters(engine, oracle_mod):
     text = "".join(recs).encode()
     progs = [compile_pattern(convert("-n", "GA(TC){1,2}A")), compile_pattern(convert("-c", "GA(TC){1,2}A"))]
     assert _check(engine, oracle_mod, text, progs) > 1000
+
+
+# ---------------------------------------------------------------------------
+# k > 0: nrgrep's eregular engine (pieces, backward windows with k errors,
+# the automaton forward; esimple's scanners when the first window is a class
+# sequence) against the oracle's replay (pm_nrgrep_reg.c)
+# ---------------------------------------------------------------------------
+
+EREG_ERRS = [(1, "ids"), (1, "s"), (2, "ids"), (1, "d"), (2, "is")]
+
+
+@pytest.mark.parametrize("k,types", EREG_ERRS)
+def test_dna_group_repeats_with_errors(engine, oracle_mod, k, types):
+    progs = []
+    for p in DNA_GROUPS:
+        progs += [compile_pattern(convert("-n", p)), compile_pattern(convert("-c", convert("-n", p)))]
+    progs = [p for p in progs if p.kind == "regular" and p.m + 1 <= 64]
+    plans = [oracle_mod.eregular_plan(p, k, types) for p in progs]
+    assert {pl["type"] for pl in plans} >= {1, 3}
+    text = tandem_fasta(5 + k, ["GATC", "GATCTCA", "TATA", "CA", "TC", "GA", "TG", "GAATTC", "GC", "AT"],
+                        n_records=4, rec_len=3000)
+    assert _check(engine, oracle_mod, text, progs, k=k, types=types) > 100
+
+
+@pytest.mark.parametrize("k,types", [(1, "ids"), (1, "s"), (2, "ids")])
+def test_peptide_group_repeats_with_errors(engine, oracle_mod, k, types):
+    progs = [compile_pattern(convert("-p", p)) for p in PEP_GROUPS]
+    progs = [p for p in progs if p.kind == "regular"]
+    text = tandem_fasta(6, ["CAG", "AG", "CP", "GH", "RK", "C", "W", "L", "CAGL", "KRKRK", "WCPL", "GHW", "RKG"],
+                        letters="ACDEFGHIKLMNPQRSTVWY", n_runs=False, n_records=4, rec_len=3000)
+    assert _check(engine, oracle_mod, text, progs, alphabet="byte", k=k, types=types) > 20
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_regular_patterns_with_errors(engine, oracle_mod, seed):
+    pats = [p for _, p in _patterns(20, 300 + seed) if p.m + 1 <= 64]
+    tokens = ["A", "C", "G", "T", "AC", "GT", "TA", "CCG", "AAT", "GAGA"]
+    text = tandem_fasta(20 + seed, tokens, n_records=3, rec_len=2000)
+    for k, types in [(1, "ids"), (2, "s"), (1, "d")]:
+        ok = [p for p in pats if not ("d" in types and p.min_len <= k)]
+        _check(engine, oracle_mod, text, ok, k=k, types=types)
+
+
+def test_deletions_to_nothing_every_line(engine, oracle_mod):
+    """k >= the shortest match with deletions: every position is a key, every
+    line a cluster; nrgrep prints empty matches too."""
+    progs = [compile_pattern("(G(CA)?(CA)?T)"), compile_pattern(convert("-n", "GA(TC){1,2}A"))]
+    text = tandem_fasta(31, ["GCAT", "GT", "CA", "GATC", "TCA"], n_records=3, rec_len=600)
+    assert _check(engine, oracle_mod, text, progs[:1], k=2, types="ids") > 100
+    assert _check(engine, oracle_mod, text, progs[1:], k=5, types="d") > 10
+
+
+def test_long_records_with_errors(engine, oracle_mod):
+    """2 Mbp of one-line records, planted GA(TC){1,2}A variants, -k 1ids: two
+    search regions, clusters inside a line."""
+    rng = random.Random(19)
+    recs = []
+    for r in range(2):
+        seq, n = [], 0
+        while n < 1_000_000:
+            piece = rng.choice(["GATCA", "GATCTCA", "GTTCA", "GATTCA", "GACTCA"]) if rng.random() < 0.05 else \
+                "".join(rng.choice("ACGT") for _ in range(rng.randint(20, 400)))
+            seq.append(piece)
+            n += len(piece)
+        recs.append(">chr%d\n%s\n" % (r, "".join(seq)))
+    text = "".join(recs).encode()
+    progs = [compile_pattern(convert("-n", "GA(TC){1,2}A"))]
+    assert _check(engine, oracle_mod, text, progs, k=1, types="ids") > 1000

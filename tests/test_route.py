@@ -33,12 +33,16 @@ def test_refusals_left():
     with pytest.raises(_lib.UnsupportedOnGPU):
         engine.route(prog("ACG"), engine.NUC, 16, "s")
     # every position deletable: class sequences run the esimple walk over
-    # every line (pm_esimple.hip), extended patterns the eextended walk over
-    # every line (pm_eextended.hip); regular patterns are refused
+    # every line (pm_esimple.hip), extended patterns the eextended walk,
+    # regular patterns the eregular walk (pm_regular.hip)
     assert engine.route(prog("ACG"), engine.NUC, 3, "ids") == "nfa"
     assert engine.route(prog("AC?G"), engine.NUC, 2, "ids") == "nfa"
+    assert engine.route(prog("A(TC)?G"), engine.NUC, 2, "ids") == "nfa"
+    # the eregular restatement covers automata of at most 64 states
+    assert engine.route(prog("A(TC)?G" + "A" * 59), engine.NUC, 1, "ids") == "nfa"
+    assert engine.route(prog("A(TC)?G" + "A" * 60), engine.NUC, 0, "") == "nfa"
     with pytest.raises(_lib.UnsupportedOnGPU):
-        engine.route(prog("A(TC)?G"), engine.NUC, 2, "ids")
+        engine.route(prog("A(TC)?G" + "A" * 60), engine.NUC, 1, "ids")
 
 
 def test_nfa_words():

@@ -29,8 +29,8 @@ def svc(tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [
-    dict(pattern="A(TC){0,1}G", seqtype="dna", mismatch="2"),         # -k 2ids, a group: every position deletable
-    dict(pattern="A(TC){0,1}G", seqtype="dna", mismatch="2", deletion="d"),
+    dict(pattern="A(TC){0,1}G" + "A" * 62, seqtype="dna", mismatch="1"),    # a group, 66 positions, k > 0
+    dict(pattern="A(TC){0,1}G" + "A" * 62, seqtype="dna", mismatch="2", deletion="d"),
     dict(pattern="A" * 300, seqtype="dna", mismatch="1"),             # 300 automaton positions
     dict(pattern="A" * 40, seqtype="dna", mismatch="16", substitution="s"),   # 16 errors
 ])

@@ -1425,7 +1425,11 @@ __global__ __launch_bounds__(RG_T) void k_erg_walk(XtPrep X, uint64_t* __restric
             for (;;) {
                 uint64_t mb = 0, me = 0;
                 if (!w.scan(stop, mb, me)) break;
-                if (!xt_header(tv, mb) && nout < nmax) {
+                // process_output drops a start on a header line, its '\n'
+                // included (an empty or erroneous first character can start
+                // there at k > 0)
+                const bool hdr = xt_header(tv, mb) || (mb > 0 && w.at(mb) == (uint8_t)'\n' && xt_header(tv, mb - 1));
+                if (!hdr && nout < nmax) {
                     keys[i + nout] = (pid << 48) | mb;
                     lens[i + nout] = (uint32_t)(me - mb);
                     acc[i + nout] = (nout == 0 ? 2 : 0) | 1;

@@ -56,6 +56,14 @@ QUERIES = [
     ("GAN{2,3}TC", "dna", None, None, None, None, "1", 300),
     ("AN{0,3}GAATTC", "dna", "Both strands", None, None, "substitution", "2", 300),
     ("CX{1,3}CK", "pep", None, "insertion", "deletion", None, "2", 300),
+    # repeated groups: nrgrep's regular engine (k = 0) and eregular engine
+    # (k > 0); the -c strand of a group repeat is an extended pattern
+    ("GA(TC){1,2}A", "dna", None, None, None, None, None, 500),
+    ("GA(TC){1,2}A", "dna", None, None, None, None, "1", 500),
+    ("G(TATA){2,}C", "dna", "Watson strand", None, None, "substitution", "1", 300),
+    ("(CA){2,4}GT", "dna", None, "insertion", "deletion", None, "2", 300),
+    ("C(AG){1,3}L", "pep", None, None, None, None, "1", 300),
+    ("K(RK){1,2}XXC", "pep", None, None, None, "substitution", "2", 300),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]

@@ -1216,6 +1216,13 @@ std::vector<std::vector<int>> shared_blocks(int P, const int32_t* lengths, const
 // is wave-uniform), every (step, pattern) with live windows leaves an 8-byte
 // record with its live mask (wave ballot + mbcnt into an LDS stage, flushed
 // rarely); k_linear_expand turns records into hit keys.
+// PM_JIT_ROTATE=0: every wave keeps its part (the round-4 form, for A/B
+// measurements); default: the parts rotate from tile to tile
+bool jit_rotate() {
+    const char* e = getenv("PM_JIT_ROTATE");
+    return !(e && e[0] == '0');
+}
+
 std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                               const uint8_t* class_acgt, const uint8_t* class_is_any, int waves, int parts) {
     const int PARTS = parts;                     // waves per workgroup
@@ -1443,11 +1450,17 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
          "    u32 dd[STEPS + XS][P];   // dead windows per slot and pattern (every path writes all of them)\n";
-    // wid < 4: the last part is the plain else (no ~0 initialization of dd)
+    // The parts rotate over the waves from tile to tile: part 0 (the words
+    // the shifted partner adds) is the longest, and a workgroup's waves sit
+    // on different SIMDs -- a fixed part 0 would load one SIMD more than the
+    // others, which then idle at the tile barrier.  b < PARTS: the last part
+    // is the plain else (no ~0 initialization of dd).
+    o << (jit_rotate() ? "    const u32 b = (wid + (u32)tile) % NW;   // this tile's part for the wave (wave-uniform)\n"
+                       : "    const u32 b = wid;\n");
     for (int part = 0; part < PARTS; ++part)
-        o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (wid == " + std::to_string(part) + ") " : "")
+        o << "    " << (part ? "else " : "") << (part + 1 < PARTS ? "if (b == " + std::to_string(part) + ") " : "")
           << "tile_body" << part << "(sw, lane, hb1, hs1, hb2, hs2, dd);\n";
-    o << "    const u32 S0 = wid * STEPS;   // the wave's first window word\n"
+    o << "    const u32 S0 = b * STEPS;   // the part's first window word\n"
          "    u32 all = ~0u;\n"
          "#pragma unroll\n    for (int s = 0; s < STEPS + XS; ++s)\n#pragma unroll\n      for (int p = 0; p < P; ++p) all &= dd[s][p];\n"
          "    if (__builtin_expect(__builtin_amdgcn_ballot_w64(all != ~0u) != 0, 0)) {   // wave-uniform, rare\n"
@@ -1539,7 +1552,7 @@ std::string jit_signature(int P, int K, const int32_t* lengths, const uint8_t* p
 hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
-    const auto key = std::make_pair(device, std::to_string(parts) + "/" +
+    const auto key = std::make_pair(device, std::to_string(parts) + (jit_rotate() ? "r/" : "f/") +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);

@@ -384,27 +384,11 @@ struct EeWalk {
     int64_t nl_lo;     // the last '\n' below the record cursor (-1: none since the walk began)
     int64_t nl_hi;     // the first '\n' at or after it (n: none)
 
-    __device__ uint8_t at(int64_t p) const { return xt_byte(tv, (uint64_t)p); }
+    mutable TxtCache tc;   // the thread's text window (LDS)
+
+    __device__ uint8_t at(int64_t p) const { return tc.get(tv, (uint64_t)p); }
     __device__ bool is_nl(int64_t p) const { return xt_brk(tv, (uint64_t)p) && at(p) == (uint8_t)'\n'; }
-    __device__ int64_t next_nl(int64_t p) const {
-        if (tv.nuc_layout) {
-            while (p < n) {
-                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
-                if (!z) {
-                    p = ((p >> 5) + 1) << 5;
-                    continue;
-                }
-                p += (int64_t)__builtin_ctz(z);
-                if (p >= n) break;
-                if (at(p) == (uint8_t)'\n') return p;
-                ++p;
-            }
-            return n;
-        }
-        for (; p < n; ++p)
-            if (tv.raw[p] == (uint8_t)'\n') return p;
-        return n;
-    }
+    __device__ int64_t next_nl(int64_t p) const { return (int64_t)xt_next_nl(tv, (uint64_t)p, (uint64_t)n); }
     // recGetRecord 0x402030 for rp (non-decreasing over a walk)
     __device__ void record(int64_t rp, int64_t& recbeg, int64_t& recend) {
         while (nl_hi < rp) {
@@ -976,12 +960,22 @@ __global__ __launch_bounds__(EE_T) void k_ee_heads(XtPrep X, const uint64_t* __r
 }
 
 template <int WB>
-__global__ __launch_bounds__(EE_T) void k_ee_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
-                                                  const uint64_t* total_d, uint64_t total_h,
-                                                  uint8_t* __restrict__ acc, TextView tv) {
+__global__ __launch_bounds__(WALK_T) void k_ee_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                    const uint64_t* total_d, uint64_t total_h,
+                                                    uint8_t* __restrict__ acc, TextView tv) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t walk_lds[];
     const uint64_t total = total_d ? *total_d : total_h;
     const EeSlot* S = X.ee;
-    for (uint64_t i = blockIdx.x * (uint64_t)EE_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * EE_T) {
+    const size_t tb = walk_tab_bytes(X.tab_words);
+    const uint64_t* tab = X.tab;
+    if (tb) {
+        uint64_t* lt = reinterpret_cast<uint64_t*>(walk_lds);
+        for (uint32_t q = threadIdx.x; q < X.tab_words; q += blockDim.x) lt[q] = X.tab[q];
+        tab = lt;
+    }
+    __syncthreads();
+    uint8_t* const tcbuf = walk_lds + tb + threadIdx.x * TC_WIN;
+    for (uint64_t i = blockIdx.x * (uint64_t)WALK_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * WALK_T) {
         if (!(acc[i] & 2)) continue;
         uint64_t j = i + 1;
         while (j < total && !(acc[j] & 2)) ++j;
@@ -996,7 +990,7 @@ __global__ __launch_bounds__(EE_T) void k_ee_walk(XtPrep X, uint64_t* __restrict
                 R0 = (int64_t)tv.reg.t[r];
                 n = (int64_t)tv.reg.e[r];
             }
-            EeWalk w{S, X.tab, tv, n, R0, -1, n};
+            EeWalk w{S, tab, tv, n, R0, -1, n, TxtCache{tcbuf, 0, 0}};
             int64_t stop;
             if (S->max_len >= 0) {
                 const int64_t back = S->max_len + S->k + 4;
@@ -1084,8 +1078,11 @@ void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
                uint8_t* acc, const TextView& tv, int words, hipStream_t s) {
     const uint32_t blocks = 1024;
     hipLaunchKernelGGL(k_ee_heads, dim3(blocks), dim3(EE_T), 0, s, X, keys, total_d, total_h, acc, tv);
-    if (words <= 1) hipLaunchKernelGGL(k_ee_walk<1>, dim3(blocks), dim3(EE_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
-    else hipLaunchKernelGGL(k_ee_walk<4>, dim3(blocks), dim3(EE_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+    const size_t lds = walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN;
+    if (words <= 1)
+        hipLaunchKernelGGL(k_ee_walk<1>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
+    else
+        hipLaunchKernelGGL(k_ee_walk<4>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
     HIPCHK(hipGetLastError());
 }
 

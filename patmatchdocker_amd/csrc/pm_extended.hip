@@ -290,28 +290,11 @@ struct XtWalk {
     uint64_t R;
     uint64_t nl_lo;    // the last '\n' seen below the record cursor (~0: none since the walk began)
     uint64_t nl_hi;    // the first '\n' at or after it (n: none)
+    mutable TxtCache tc;   // the thread's text window (LDS)
 
-    __device__ uint8_t at(uint64_t p) const { return xt_byte(tv, p); }
+    __device__ uint8_t at(uint64_t p) const { return tc.get(tv, p); }
     __device__ bool is_nl(uint64_t p) const { return xt_brk(tv, p) && at(p) == (uint8_t)'\n'; }
-    __device__ uint64_t next_nl(uint64_t p) const {
-        if (tv.nuc_layout) {
-            while (p < n) {   // a word's breaks at once, then the '\n' among them
-                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
-                if (!z) {
-                    p = ((p >> 5) + 1) << 5;
-                    continue;
-                }
-                p += (uint64_t)__builtin_ctz(z);
-                if (p >= n) break;
-                if (at(p) == (uint8_t)'\n') return p;
-                ++p;
-            }
-            return n;
-        }
-        for (; p < n; ++p)
-            if (tv.raw[p] == (uint8_t)'\n') return p;
-        return n;
-    }
+    __device__ uint64_t next_nl(uint64_t p) const { return xt_next_nl(tv, p, n); }
     // recGetRecord 0x402030 for rp (non-decreasing over a walk): the last
     // '\n' before rp searched back to R only, the first at or after it
     __device__ void record(uint64_t rp, uint64_t& recbeg, uint64_t& recend) {
@@ -506,12 +489,23 @@ struct XtWalk {
 // One thread per cluster head: the printed matches are written in place
 // from the head on (acc bit 0), every other entry of the cluster is cleared.
 template <int WB>
-__global__ __launch_bounds__(XT_T) void k_xt_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
-                                                  const uint64_t* total_d, uint64_t total_h,
-                                                  uint8_t* __restrict__ acc, TextView tv) {
+__global__ __launch_bounds__(WALK_T) void k_xt_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                    const uint64_t* total_d, uint64_t total_h,
+                                                    uint8_t* __restrict__ acc, TextView tv) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t walk_lds[];
     const uint64_t total = total_d ? *total_d : total_h;
     const XtSlot* S = X.slot;
-    for (uint64_t i = blockIdx.x * (uint64_t)XT_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * XT_T) {
+    // the tables in LDS when they fit, then the thread's text window
+    const size_t tb = walk_tab_bytes(X.tab_words);
+    const uint64_t* tab = X.tab;
+    if (tb) {
+        uint64_t* lt = reinterpret_cast<uint64_t*>(walk_lds);
+        for (uint32_t q = threadIdx.x; q < X.tab_words; q += blockDim.x) lt[q] = X.tab[q];
+        tab = lt;
+    }
+    __syncthreads();
+    uint8_t* const tcbuf = walk_lds + tb + threadIdx.x * TC_WIN;
+    for (uint64_t i = blockIdx.x * (uint64_t)WALK_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * WALK_T) {
         if (!(acc[i] & 2)) continue;
         uint64_t j = i + 1;   // the next cluster's head keeps bit 1 whatever its owner writes
         while (j < total && !(acc[j] & 2)) ++j;
@@ -526,7 +520,7 @@ __global__ __launch_bounds__(XT_T) void k_xt_walk(XtPrep X, uint64_t* __restrict
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            XtWalk w{S, X.tab, tv, n, R0, ~0ull, n};
+            XtWalk w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             uint64_t stop;
             if (S->max_len >= 0) {
                 // candidates in [first, last + max_len] can print the
@@ -586,7 +580,8 @@ void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
         ee_launch(X, keys, lens, total_d, total_h, acc, tv, X.words, s);
     } else {
         hipLaunchKernelGGL(k_xt_heads, dim3(blocks), dim3(XT_T), 0, s, X, keys, total_d, total_h, acc, tv);
-        hipLaunchKernelGGL(k_xt_walk<4>, dim3(blocks), dim3(XT_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+        hipLaunchKernelGGL(k_xt_walk<4>, dim3(blocks), dim3(WALK_T), walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN, s, X,
+                           keys, lens, total_d, total_h, acc, tv);
     }
     hipLaunchKernelGGL(k_xt_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);
     HIPCHK(hipGetLastError());

@@ -761,6 +761,105 @@ __device__ inline bool xt_brk_between(const TextView& tv, uint64_t a, uint64_t b
 
 __device__ inline uint32_t xt_region(const TextView& tv, uint64_t p) { return tv.reg.n > 1 ? region_of(tv.reg, p) : 0u; }
 
+// A walk thread's window of the file's own folded bytes (xt_byte) in LDS:
+// the per-cluster walks of nrgrep's report (pm_extended / pm_eextended /
+// pm_regular.hip) read the text one character per dependent step, so each
+// read from memory was a full round trip.  A miss refills TC_WIN bytes from
+// TC_BACK before the position with independent 16-byte loads (one round trip
+// per refill); the scanners move forward and every verify phase reads at most
+// a pattern's span back.
+constexpr uint32_t TC_WIN = 256, TC_BACK = 96;
+constexpr uint32_t WALK_T = 128;   // walk threads per block: WALK_T * TC_WIN bytes of LDS
+__device__ inline uint32_t fold4(uint32_t v) {   // xt_fold on four bytes
+    const uint32_t ge_a = (v | 0x80808080u) - 0x61616161u, gt_z = (v | 0x80808080u) - 0x7b7b7b7bu;
+    const uint32_t lower = ge_a & ~gt_z & ~v & 0x80808080u;   // 0x61 <= b <= 0x7a
+    return v - (lower >> 2);                                   // 0x80 >> 2 = 0x20
+}
+struct TxtCache {
+    uint8_t* buf;       // TC_WIN bytes of LDS (16-byte aligned)
+    uint64_t lo, hi;    // positions cached: [lo, hi)
+    __device__ void fill(const TextView& tv, uint64_t p) {
+        if (tv.nuc_layout) {
+            const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~31ull : 0ull, h = umin64(l + TC_WIN, tv.n);
+            uint4 w[TC_WIN / 32];
+#pragma unroll
+            for (uint32_t q = 0; q < TC_WIN / 32; ++q) w[q] = l + 32ull * q < h ? tv.nuc.lin[(l >> 5) + q] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t q = 0; q < TC_WIN / 32; ++q)
+                for (uint32_t i = 0; i < 32; ++i) {
+                    const uint64_t pos = l + 32ull * q + i;
+                    if (pos >= h) break;
+                    uint8_t c;
+                    if (((w[q].z | w[q].w) >> i) & 1) c = xt_fold(nuc_raw_at(tv.nuc, pos));
+                    else c = (uint8_t)((0x54474341u >> (8 * ((((w[q].x >> i) & 1) << 1) | ((w[q].y >> i) & 1)))) & 0xff);
+                    buf[32 * q + i] = c;
+                }
+            lo = l;
+            hi = h;
+            return;
+        }
+        const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~15ull : 0ull, h = umin64(l + TC_WIN, tv.n);
+        uint4 v[TC_WIN / 16];
+#pragma unroll
+        for (uint32_t q = 0; q < TC_WIN / 16; ++q)
+            v[q] = l + 16ull * q + 16 <= tv.n ? *reinterpret_cast<const uint4*>(tv.raw + l + 16ull * q) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t q = 0; q < TC_WIN / 16; ++q) {
+            if (l + 16ull * q + 16 > tv.n) {   // the text's last partial chunk
+                for (uint32_t i = 0; i < 16 && l + 16ull * q + i < tv.n; ++i) buf[16 * q + i] = xt_fold(tv.raw[l + 16ull * q + i]);
+            } else {
+                *reinterpret_cast<uint4*>(buf + 16 * q) = make_uint4(fold4(v[q].x), fold4(v[q].y), fold4(v[q].z), fold4(v[q].w));
+            }
+        }
+        lo = l;
+        hi = h;
+    }
+    __device__ uint8_t get(const TextView& tv, uint64_t p) {
+        if (p >= tv.n) return (uint8_t)'\n';
+        if (p - lo >= hi - lo) fill(tv, p);
+        return buf[p - lo];
+    }
+};
+// the first '\n' at or after p (n: none), p < n <= tv.n: a word of break
+// flags (NUC) or 16 bytes (BYTE) per dependent load
+__device__ inline uint64_t xt_next_nl(const TextView& tv, uint64_t p, uint64_t n) {
+    if (tv.nuc_layout) {
+        while (p < n) {
+            uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
+            if (!z) {
+                p = ((p >> 5) + 1) << 5;
+                continue;
+            }
+            p += (uint64_t)__builtin_ctz(z);
+            if (p >= n) break;
+            if (xt_byte(tv, p) == (uint8_t)'\n') return p;
+            ++p;
+        }
+        return n;
+    }
+    for (; p < n && (p & 15); ++p)
+        if (tv.raw[p] == (uint8_t)'\n') return p;
+    for (; p + 16 <= n; p += 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(tv.raw + p);
+        const uint32_t w[4] = {v.x ^ 0x0a0a0a0au, v.y ^ 0x0a0a0a0au, v.z ^ 0x0a0a0a0au, v.w ^ 0x0a0a0a0au};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t z = (w[q] - 0x01010101u) & ~w[q] & 0x80808080u;   // a zero byte = a '\n'
+            if (z) return p + 4ull * q + (uint64_t)(__builtin_ctz(z) >> 3);
+        }
+    }
+    for (; p < n; ++p)
+        if (tv.raw[p] == (uint8_t)'\n') return p;
+    return n;
+}
+
+// the walks' dynamic LDS: the plan's tables (when they fit, TAB_LDS_MAX) then
+// TC_WIN bytes per thread
+constexpr size_t TAB_LDS_MAX = 24 << 10;
+__host__ __device__ inline size_t walk_tab_bytes(uint32_t tab_words) {
+    return tab_words * 8ull <= TAB_LDS_MAX ? ((tab_words * 8ull + 15) & ~15ull) : 0;
+}
+
 // true when the pass changes anything for `flags` (cross: candidates may
 // start on header lines)
 bool report_needed(const pm_db* db, uint32_t flags, bool cross);
@@ -962,6 +1061,7 @@ struct XtPrep {
     int32_t pid = 0;
     int32_t words = 1;            // eextended: the verify parts' widest word count
     int32_t eregular = 0;         // rg: k > 0 (pm_regular.hip k_erg_walk)
+    uint32_t tab_words = 0;       // words of the table blob at tab (copied to LDS when small)
 };
 // eextended heads + walk on s (keys/lens rewritten in place, acc bit 0 =
 // reported); xt_launch calls it when X.ee is set

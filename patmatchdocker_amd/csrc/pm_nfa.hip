@@ -632,6 +632,8 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
             return;
         }
     }
+    // the walk tables are the last upload of their build (xt / ee / rg)
+    const uint32_t walk_tab_words = (extended || regular) ? (uint32_t)((up.blob.size() - o_xtab) / 8) : 0u;
     uint8_t* d_up = up.commit(db);
     EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
     XtPrep xtp;
@@ -641,6 +643,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         xtp.pid = pattern_id;
         xtp.words = m + 1 <= 64 ? 1 : RG_NW;
         xtp.eregular = k > 0 ? 1 : 0;
+        xtp.tab_words = walk_tab_words;
     }
     if (extended) {
         if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
@@ -648,6 +651,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
         xtp.pid = pattern_id;
         xtp.words = W;
+        xtp.tab_words = walk_tab_words;
     }
     esp.lines = all_pos ? 1 : 0;
 

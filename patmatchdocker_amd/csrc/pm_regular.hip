@@ -778,27 +778,11 @@ struct RgWalk {
     uint64_t nl_lo;    // the last '\n' seen below the record cursor (~0: none since the walk began)
     uint64_t nl_hi;    // the first '\n' at or after it (n: none)
 
-    __device__ uint8_t at(uint64_t p) const { return xt_byte(tv, p); }
+    mutable TxtCache tc;   // the thread's text window (LDS)
+
+    __device__ uint8_t at(uint64_t p) const { return tc.get(tv, p); }
     __device__ bool is_nl(uint64_t p) const { return xt_brk(tv, p) && at(p) == (uint8_t)'\n'; }
-    __device__ uint64_t next_nl(uint64_t p) const {
-        if (tv.nuc_layout) {
-            while (p < n) {
-                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
-                if (!z) {
-                    p = ((p >> 5) + 1) << 5;
-                    continue;
-                }
-                p += (uint64_t)__builtin_ctz(z);
-                if (p >= n) break;
-                if (at(p) == (uint8_t)'\n') return p;
-                ++p;
-            }
-            return n;
-        }
-        for (; p < n; ++p)
-            if (tv.raw[p] == (uint8_t)'\n') return p;
-        return n;
-    }
+    __device__ uint64_t next_nl(uint64_t p) const { return xt_next_nl(tv, p, n); }
     // recGetRecord 0x402030 (rp non-decreasing over a walk)
     __device__ void record(uint64_t rp, uint64_t& rb, uint64_t& re) {
         while (nl_hi < rp) {
@@ -979,26 +963,10 @@ struct ErgWalk {
     uint64_t R;
     uint64_t nl_lo, nl_hi;
 
-    __device__ uint8_t at(uint64_t p) const { return xt_byte(tv, p); }
-    __device__ uint64_t next_nl(uint64_t p) const {
-        if (tv.nuc_layout) {
-            while (p < n) {
-                uint32_t z = tv.nuc.lin[p >> 5].z >> (uint32_t)(p & 31);
-                if (!z) {
-                    p = ((p >> 5) + 1) << 5;
-                    continue;
-                }
-                p += (uint64_t)__builtin_ctz(z);
-                if (p >= n) break;
-                if (at(p) == (uint8_t)'\n') return p;
-                ++p;
-            }
-            return n;
-        }
-        for (; p < n; ++p)
-            if (tv.raw[p] == (uint8_t)'\n') return p;
-        return n;
-    }
+    mutable TxtCache tc;   // the thread's text window (LDS)
+
+    __device__ uint8_t at(uint64_t p) const { return tc.get(tv, p); }
+    __device__ uint64_t next_nl(uint64_t p) const { return xt_next_nl(tv, p, n); }
     __device__ void record(uint64_t rp, uint64_t& rb, uint64_t& re) {   // recGetRecord 0x402030
         while (nl_hi < rp) {
             nl_lo = nl_hi;
@@ -1389,12 +1357,22 @@ struct ErgWalk {
     }
 };
 
-__global__ __launch_bounds__(RG_T) void k_erg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
-                                                   const uint64_t* total_d, uint64_t total_h,
-                                                   uint8_t* __restrict__ acc, TextView tv) {
+__global__ __launch_bounds__(WALK_T) void k_erg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                     const uint64_t* total_d, uint64_t total_h,
+                                                     uint8_t* __restrict__ acc, TextView tv) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t walk_lds[];
+    const size_t tb = walk_tab_bytes(X.tab_words);
+    const uint64_t* tab = X.tab;
+    if (tb) {
+        uint64_t* lt = reinterpret_cast<uint64_t*>(walk_lds);
+        for (uint32_t q = threadIdx.x; q < X.tab_words; q += blockDim.x) lt[q] = X.tab[q];
+        tab = lt;
+    }
+    __syncthreads();
+    uint8_t* const tcbuf = walk_lds + tb + threadIdx.x * TC_WIN;
     const uint64_t total = total_d ? *total_d : total_h;
     const RgSlot* S = X.rg;
-    for (uint64_t i = blockIdx.x * (uint64_t)RG_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * RG_T) {
+    for (uint64_t i = blockIdx.x * (uint64_t)WALK_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * WALK_T) {
         if (!(acc[i] & 2)) continue;
         uint64_t j = i + 1;
         while (j < total && !(acc[j] & 2)) ++j;
@@ -1409,7 +1387,7 @@ __global__ __launch_bounds__(RG_T) void k_erg_walk(XtPrep X, uint64_t* __restric
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            ErgWalk w{S, X.tab, tv, n, R0, ~0ull, n};
+            ErgWalk w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             // from the start of first's line, at most span + 4 before it
             // (the scanners' rows then agree with the whole scan's, and no
             // match found before first can start at another cluster's key)
@@ -1446,12 +1424,22 @@ __global__ __launch_bounds__(RG_T) void k_erg_walk(XtPrep X, uint64_t* __restric
 // One thread per cluster head: the printed matches are written in place
 // from the head on (acc bit 0), every other entry of the cluster is cleared.
 template <int NW>
-__global__ __launch_bounds__(RG_T) void k_rg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
-                                                  const uint64_t* total_d, uint64_t total_h,
-                                                  uint8_t* __restrict__ acc, TextView tv) {
+__global__ __launch_bounds__(WALK_T) void k_rg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
+                                                    const uint64_t* total_d, uint64_t total_h,
+                                                    uint8_t* __restrict__ acc, TextView tv) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t walk_lds[];
+    const size_t tb = walk_tab_bytes(X.tab_words);
+    const uint64_t* tab = X.tab;
+    if (tb) {
+        uint64_t* lt = reinterpret_cast<uint64_t*>(walk_lds);
+        for (uint32_t q = threadIdx.x; q < X.tab_words; q += blockDim.x) lt[q] = X.tab[q];
+        tab = lt;
+    }
+    __syncthreads();
+    uint8_t* const tcbuf = walk_lds + tb + threadIdx.x * TC_WIN;
     const uint64_t total = total_d ? *total_d : total_h;
     const RgSlot* S = X.rg;
-    for (uint64_t i = blockIdx.x * (uint64_t)RG_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * RG_T) {
+    for (uint64_t i = blockIdx.x * (uint64_t)WALK_T + threadIdx.x; i < total; i += (uint64_t)gridDim.x * WALK_T) {
         if (!(acc[i] & 2)) continue;
         uint64_t j = i + 1;
         while (j < total && !(acc[j] & 2)) ++j;
@@ -1466,7 +1454,7 @@ __global__ __launch_bounds__(RG_T) void k_rg_walk(XtPrep X, uint64_t* __restrict
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            RgWalk<NW> w{S, X.tab, tv, n, R0, ~0ull, n};
+            RgWalk<NW> w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             uint64_t stop;
             if (S->max_len >= 0) {
                 const uint64_t back = (uint64_t)S->max_len + 1;
@@ -1502,12 +1490,13 @@ void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
                uint8_t* acc, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
     hipLaunchKernelGGL(k_rg_heads, dim3(blocks), dim3(RG_T), 0, s, X, keys, total_d, total_h, acc, tv);
+    const size_t lds = walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN;
     if (X.eregular)
-        hipLaunchKernelGGL(k_erg_walk, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+        hipLaunchKernelGGL(k_erg_walk, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
     else if (X.words == 1)
-        hipLaunchKernelGGL(k_rg_walk<1>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc, tv);
+        hipLaunchKernelGGL(k_rg_walk<1>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
     else
-        hipLaunchKernelGGL(k_rg_walk<RG_NW>, dim3(blocks), dim3(RG_T), 0, s, X, keys, lens, total_d, total_h, acc,
+        hipLaunchKernelGGL(k_rg_walk<RG_NW>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc,
                            tv);
     HIPCHK(hipGetLastError());
 }

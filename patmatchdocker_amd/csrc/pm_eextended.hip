@@ -375,6 +375,7 @@ constexpr uint64_t EE_POS_MASK = (1ull << 48) - 1;
 constexpr uint64_t EE_SCAN = 1ull << 16;   // unbounded: how far a head looks back for a line break
 constexpr uint32_t EE_T = 256;
 
+template <int WB, int KR, int SC>
 struct EeWalk {
     const EeSlot* S;
     const uint64_t* tab;
@@ -386,7 +387,21 @@ struct EeWalk {
 
     mutable TxtCache tc;   // the thread's text window (LDS)
 
-    __device__ uint8_t at(int64_t p) const { return tc.get(tv, (uint64_t)p); }
+    // SC is the scanner (ee_scanner: a kernel holds one scanner and one
+    // inlined checkMatch); KR is the row count the kernel was built for: k itself for k <= 3
+    // (every row loop unrolls and the rows stay in registers), PM_MAX_K
+    // otherwise (loops bounded by the run-time k)
+    __device__ __forceinline__ int kk() const { return KR < PM_MAX_K ? KR : S->k; }
+    template <int N>
+    __device__ __forceinline__ static uint64_t pick(const uint64_t (&a)[N], int i) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j == i) v = a[j];
+        return v;
+    }
+
+    __device__ __forceinline__ uint8_t at(int64_t p) const { return tc.get(tv, (uint64_t)p); }
     __device__ bool is_nl(int64_t p) const { return xt_brk(tv, (uint64_t)p) && at(p) == (uint8_t)'\n'; }
     __device__ int64_t next_nl(int64_t p) const { return (int64_t)xt_next_nl(tv, (uint64_t)p, (uint64_t)n); }
     // recGetRecord 0x402030 for rp (non-decreasing over a walk)
@@ -405,8 +420,7 @@ struct EeWalk {
         return !((S->anchors & PM_ANCHOR_END) && q < recend && at(q) != (uint8_t)'\n');
     }
 
-    template <int WB>
-    __device__ static void close(uint64_t* D, int W, const EePart& V) {
+    __device__ __forceinline__ static void close(uint64_t* D, int W, const EePart& V) {
         uint64_t borrow = 0;
 #pragma unroll
         for (int w = 0; w < WB; ++w) {
@@ -421,22 +435,22 @@ struct EeWalk {
 
     // checkMatch1's rows of one part: init (0x40e658), row 0 (0x40e8ad) and
     // row j (0x40e9b0) updates, the alive test (0x40edb9)
-    template <int WB>
     struct Rows {
         int W;
         uint64_t fin, alive;
-        uint64_t R[PM_MAX_K + 1][WB];
+        uint64_t R[KR + 1][WB];
         uint64_t t1[WB], t2[WB];
     };
 
-    template <int WB>
-    __device__ void rows_init(Rows<WB>& s, const EePart& V, int kmax) const {
+    __device__ __forceinline__ void rows_init(Rows& s, const EePart& V, int kmax) const {
         s.W = V.pw;
         s.fin = 1ull << ((V.len - 1) & 63);
         s.alive = s.fin * 2 - 1;
 #pragma unroll
         for (int w = 0; w < WB; ++w) s.R[0][w] = V.X[w];
-        for (int j = 1; j <= kmax; ++j) {
+#pragma unroll
+        for (int j = 1; j <= KR; ++j) {
+            if (j > kmax) break;
             uint64_t carry = 1;
 #pragma unroll
             for (int w = 0; w < WB; ++w) {
@@ -444,11 +458,10 @@ struct EeWalk {
                 s.R[j][w] = (S->errs & PM_ERR_DEL) ? ((old << 1) | carry) : old;
                 carry = old >> 63;
             }
-            if (S->errs & PM_ERR_DEL) close<WB>(s.R[j], s.W, V);
+            if (S->errs & PM_ERR_DEL) close(s.R[j], s.W, V);
         }
     }
-    template <int WB>
-    __device__ void row0(Rows<WB>& s, const EePart& V, uint8_t c, uint64_t inj) const {
+    __device__ __forceinline__ void row0(Rows& s, const EePart& V, uint8_t c, uint64_t inj) const {
         const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
         const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
         uint64_t carry = inj;
@@ -460,12 +473,11 @@ struct EeWalk {
             s.t2[w] = (((old << 1) | carry) & B[w]) | (old & A[w]);
             carry = old >> 63;
         }
-        close<WB>(s.t2, s.W, V);
+        close(s.t2, s.W, V);
 #pragma unroll
         for (int w = 0; w < WB; ++w) s.R[0][w] = w < s.W ? s.t2[w] : 0ull;
     }
-    template <int WB>
-    __device__ void rowj(Rows<WB>& s, const EePart& V, int j, uint8_t c, uint64_t inj) const {
+    __device__ __forceinline__ void rowj(Rows& s, const EePart& V, int j, uint8_t c, uint64_t inj) const {
         const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
         const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
         uint64_t dc = 0, sc = inj, mc = inj;
@@ -490,25 +502,27 @@ struct EeWalk {
             nw[w] = r;
             s.t1[w] = old;
         }
-        close<WB>(nw, s.W, V);
+        close(nw, s.W, V);
 #pragma unroll
         for (int w = 0; w < WB; ++w) {
             s.t2[w] = nw[w];
             s.R[j][w] = nw[w];
         }
     }
-    template <int WB>
-    __device__ static bool rows_alive(const Rows<WB>& s, int maxk) {
+    __device__ __forceinline__ static bool rows_alive(const Rows& s, int maxk) {
         uint64_t any = 0;
 #pragma unroll
-        for (int w = 0; w < WB; ++w) {
-            if (w >= s.W) break;
-            any |= w == s.W - 1 ? (s.R[maxk][w] & s.alive) : s.R[maxk][w];
+        for (int j = 0; j <= KR; ++j) {
+            if (j != maxk) continue;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) {
+                if (w >= s.W) break;
+                any |= w == s.W - 1 ? (s.R[j][w] & s.alive) : s.R[j][w];
+            }
         }
         return any != 0;
     }
-    template <int WB>
-    __device__ static bool fin_of(const uint64_t* r, const Rows<WB>& s) {
+    __device__ __forceinline__ static bool fin_of(const uint64_t* r, const Rows& s) {
         uint64_t v = 0;
 #pragma unroll
         for (int w = 0; w < WB; ++w)
@@ -517,9 +531,8 @@ struct EeWalk {
     }
 
     // the left phase (checkMatch1 0x40e3a0 .. 0x40ee6e)
-    template <int WB>
-    __device__ bool left(const EePart& V, int64_t pos, int64_t recbeg, int& nerr, int64_t& start) const {
-        const int k = S->k;
+    __device__ __forceinline__ bool left(const EePart& V, int64_t pos, int64_t recbeg, int& nerr, int64_t& start) const {
+        const int k = kk();
         if (V.len == 0) {
             for (int q = 0; q <= k; ++q) {
                 if (left_ok(pos - q, recbeg)) {
@@ -531,34 +544,41 @@ struct EeWalk {
             }
             return false;
         }
-        Rows<WB> s;
-        rows_init<WB>(s, V, k);
+        Rows s;
+        rows_init(s, V, k);
         int maxk = k, best = k;
         bool found = false;
         int64_t fpos = 0;
-        for (int j = 1; j <= maxk; ++j)
-            if (fin_of<WB>(s.R[j], s) && left_ok(pos, recbeg)) {
+#pragma unroll
+        for (int j = 1; j <= KR; ++j) {
+            if (j > maxk) break;
+            if (fin_of(s.R[j], s) && left_ok(pos, recbeg)) {
                 found = true;
                 fpos = pos;
                 best = j;
                 maxk = j - 1;
             }
+        }
         if (pos != recbeg) {
             uint64_t inj = 1;
             uint8_t c = at(pos - 1);
             for (int64_t X = pos - 2; X != recbeg - 2; --X) {
                 const uint8_t look = X + 1 != recbeg ? at(X) : (uint8_t)0;
-                row0<WB>(s, V, c, inj);
-                if (fin_of<WB>(s.t2, s) && left_ok(X, recbeg)) {
+                row0(s, V, c, inj);
+                if (fin_of(s.t2, s) && left_ok(X, recbeg)) {
                     start = X;
                     nerr = 0;
                     return true;
                 }
-                for (int j = 1; j <= maxk; ++j) {
-                    rowj<WB>(s, V, j, c, inj);
-                    if (fin_of<WB>(s.t2, s) && left_ok(X, recbeg)) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > maxk) break;
+                    rowj(s, V, j, c, inj);
+                    if (fin_of(s.t2, s) && left_ok(X, recbeg)) {
                         int cc = j;                      // 0x40ec54: walk down
-                        while (cc - 1 >= 0 && fin_of<WB>(s.R[cc - 1], s)) --cc;
+#pragma unroll
+                        for (int d = KR - 1; d >= 0; --d)   // while fin(R[cc - 1]): --cc
+                            if (d == cc - 1 && fin_of(s.R[d], s)) cc = d;
                         if (cc == 0) {
                             start = X;
                             nerr = 0;
@@ -571,7 +591,7 @@ struct EeWalk {
                         break;
                     }
                 }
-                if (!rows_alive<WB>(s, maxk)) break;
+                if (!rows_alive(s, maxk)) break;
                 inj = 0;
                 c = look;
             }
@@ -583,8 +603,7 @@ struct EeWalk {
     }
 
     // the right phase (checkMatch1 0x40ec63 .. 0x40f7be)
-    template <int WB>
-    __device__ bool right(const EePart& V, int64_t pos, int64_t recend, int kmax, int64_t& end) const {
+    __device__ __forceinline__ bool right(const EePart& V, int64_t pos, int64_t recend, int kmax, int64_t& end) const {
         if (V.len == 0) {
             for (int q = 0; q <= kmax; ++q) {
                 if (right_ok(pos + q, recend)) {
@@ -596,33 +615,40 @@ struct EeWalk {
             return false;
         }
         if (kmax < 0) return false;
-        Rows<WB> s;
-        rows_init<WB>(s, V, kmax);
+        Rows s;
+        rows_init(s, V, kmax);
         int maxk = kmax;
         bool found = false;
         int64_t fend = 0;
-        for (int j = 1; j <= maxk; ++j)
-            if (fin_of<WB>(s.R[j], s) && right_ok(pos, recend)) {
+#pragma unroll
+        for (int j = 1; j <= KR; ++j) {
+            if (j > maxk) break;
+            if (fin_of(s.R[j], s) && right_ok(pos, recend)) {
                 found = true;
                 fend = pos;
                 maxk = j - 1;
             }
+        }
         if (pos != recend) {
             uint64_t inj = 1;
             uint8_t c = at(pos);
             for (int64_t Y = pos + 1;; ++Y) {
                 const int64_t q = Y - 1;
                 const uint8_t look = q != recend - 1 ? at(Y) : (uint8_t)0;
-                row0<WB>(s, V, c, inj);
-                if (fin_of<WB>(s.t2, s) && right_ok(Y + 1, recend)) {
+                row0(s, V, c, inj);
+                if (fin_of(s.t2, s) && right_ok(Y + 1, recend)) {
                     end = Y + 1;
                     return true;
                 }
-                for (int j = 1; j <= maxk; ++j) {
-                    rowj<WB>(s, V, j, c, inj);
-                    if (fin_of<WB>(s.t2, s) && right_ok(Y + 1, recend)) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > maxk) break;
+                    rowj(s, V, j, c, inj);
+                    if (fin_of(s.t2, s) && right_ok(Y + 1, recend)) {
                         int cc = j;
-                        while (cc - 1 >= 0 && fin_of<WB>(s.R[cc - 1], s)) --cc;
+#pragma unroll
+                        for (int d = KR - 1; d >= 0; --d)   // while fin(R[cc - 1]): --cc
+                            if (d == cc - 1 && fin_of(s.R[d], s)) cc = d;
                         if (cc == 0) {
                             end = Y + 1;
                             return true;
@@ -633,7 +659,7 @@ struct EeWalk {
                         break;
                     }
                 }
-                if (!rows_alive<WB>(s, maxk)) break;
+                if (!rows_alive(s, maxk)) break;
                 if (q == recend - 1) break;
                 inj = 0;
                 c = look;
@@ -645,8 +671,7 @@ struct EeWalk {
     }
 
     // checkMatch 0x40f910
-    template <int WB>
-    __device__ bool check(int q, int64_t pos, int64_t& mb, int64_t& me) {
+    __device__ __forceinline__ bool check(int q, int64_t pos, int64_t& mb, int64_t& me) {
         const int64_t rp = S->type == 3 ? pos - 1 : pos;
         if (rp < R) return false;
         int64_t recbeg, recend;
@@ -654,8 +679,8 @@ struct EeWalk {
         if (rp < recbeg || rp >= recend) return false;
         int64_t start, end;
         int eL = 0;
-        if (!left<WB>(S->lv[q], pos, recbeg, eL, start)) return false;
-        if (!right<WB>(S->rv[q], pos, recend, S->k - eL, end)) return false;
+        if (!left(S->lv[q], pos, recbeg, eL, start)) return false;
+        if (!right(S->rv[q], pos, recend, S->k - eL, end)) return false;
         mb = start;
         me = end;
         return true;
@@ -667,14 +692,13 @@ struct EeWalk {
     }
 
     // the scanners over [R, n); false when no candidate <= stop verifies
-    template <int WB>
-    __device__ bool scan(int64_t stop, int64_t& mb, int64_t& me) {
+    __device__ __forceinline__ bool scan(int64_t stop, int64_t& mb, int64_t& me) {
         const uint64_t* T = tab + S->o_T;
         const uint64_t* TA = tab + S->o_TA;
         const uint64_t* T2 = tab + S->o_T2;
-        const int k = S->k;
-        uint64_t Rr[PM_MAX_K + 1], Tr[PM_MAX_K + 1];
-        if (S->simple && S->type == 1) {                 // esimpleScan 0x413780: pieces, exact
+        const int k = kk();
+        uint64_t Rr[KR + 1], Tr[KR + 1];
+        if constexpr (SC == 0) {                         // esimpleScan 0x413780: pieces, exact
             const int mpc = S->plen;
             int64_t r9 = R - 1;
             const int64_t limit = n - mpc;
@@ -696,13 +720,13 @@ struct EeWalk {
                     for (int i = 0; i < S->np; ++i) {    // 0x41384b: 32-bit shift
                         const int bit = i * mpc + mpc - 1;
                         const uint64_t msk = (uint64_t)(int64_t)(int32_t)(1u << (bit & 31));
-                        if ((D & msk) && check<WB>(i, r9 + 1, mb, me)) return true;
+                        if ((D & msk) && check(i, r9 + 1, mb, me)) return true;
                     }
                 r9 += q + 1;
             }
             return false;
         }
-        if (S->simple && S->type == 2) {                 // esimpleScan 0x413b6f: window, ABNDM
+        if constexpr (SC == 1) {                         // esimpleScan 0x413b6f: window, ABNDM
             const int Lw = S->fspan;
             const uint64_t top = ~0ull << (64 - Lw);
             const int W = Lw - k;
@@ -711,7 +735,9 @@ struct EeWalk {
                 if (s0 > stop) return false;
                 const uint64_t b0 = T[at(s0 + W - 1)];
                 Rr[0] = b0;
-                for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > k) break;
                     Rr[j] = top;
                     Tr[j] = b0;
                 }
@@ -721,7 +747,9 @@ struct EeWalk {
                     uint64_t oldp = Rr[0];
                     uint64_t newp = (oldp << 1) & bc;
                     Rr[0] = newp;
-                    for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                    for (int j = 1; j <= KR; ++j) {
+                        if (j > k) break;
                         const uint64_t trans = (bc << 1) & Tr[j];
                         uint64_t v = ((newp | oldp) << 1) | oldp;
                         Tr[j] = (oldp << 2) & bc;
@@ -733,19 +761,21 @@ struct EeWalk {
                         newp = v;
                     }
                     if (rb == 0) {
-                        if ((Rr[k] >> 63) && check<WB>(0, s0, mb, me)) return true;
+                        if ((pick(Rr, k) >> 63) && check(0, s0, mb, me)) return true;
                         break;
                     }
-                    if (!Rr[k] && !Tr[k]) break;
+                    if (!pick(Rr, k) && !pick(Tr, k)) break;
                     --rb;
                 }
                 s0 += rb + 1;
             }
             return false;
         }
-        if (S->simple) {                                 // esimpleScan 0x413932: prefix, shift-or
+        if constexpr (SC == 2) {                         // esimpleScan 0x413932: prefix, shift-or
             const uint64_t fin = 1ull << (S->fspan - 1);
-            for (int j = 0; j <= k; ++j) {
+#pragma unroll
+            for (int j = 0; j <= KR; ++j) {
+                if (j > k) break;
                 Rr[j] = ~0ull << j;
                 Tr[j] = ~0ull;
             }
@@ -756,7 +786,9 @@ struct EeWalk {
                 uint64_t newp = (oldp << 1) | bc;
                 Rr[0] = newp;
                 const uint64_t r9 = (bc << 1) | 1;
-                for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > k) break;
                     const uint64_t tr = r9 | Tr[j];
                     uint64_t v = ((newp & oldp) << 1) & oldp;
                     Tr[j] = (oldp << 2) | bc;
@@ -767,14 +799,14 @@ struct EeWalk {
                     oldp = oldj;
                     newp = v;
                 }
-                if (!(Rr[k] & fin)) {
+                if (!(pick(Rr, k) & fin)) {
                     if (p > stop) return false;
-                    if (check<WB>(0, p, mb, me)) return true;
+                    if (check(0, p, mb, me)) return true;
                 }
             }
             return false;
         }
-        if (S->type == 1) {                              // eextendedScan 0x40cf05: pieces with '?*+'
+        if constexpr (SC == 3) {                         // eextendedScan 0x40cf05: pieces with '?*+'
             const int len = S->flen;
             int64_t pos = R - 1;
             const int64_t lim = n - len;
@@ -798,12 +830,12 @@ struct EeWalk {
                 } while (D && ebp != 0);
                 if (D)
                     for (int q = 0; q < S->np; ++q)
-                        if ((S->top[q] & D) && check<WB>(q, pos + 1, mb, me)) return true;
+                        if ((S->top[q] & D) && check(q, pos + 1, mb, me)) return true;
                 pos = pos + ebp + 1;
             }
             return false;
         }
-        if (S->type == 2) {                              // eextendedScan 0x40d5a1: window, k errors
+        if constexpr (SC == 4) {                         // eextendedScan 0x40d5a1: window, k errors
             const int W = S->flen - k - 1;
             const uint64_t top = S->fspan >= 64 ? ~0ull : ~0ull << (64 - S->fspan);
             if (W < 1) return false;
@@ -812,7 +844,9 @@ struct EeWalk {
                 const uint8_t c1 = at(pos + W), c2 = at(pos + W - 1);
                 Rr[0] = xclose(T[c1]);
                 const uint64_t tr0 = (xclose(T[c2]) << 1) & T[c1];
-                for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > k) break;
                     Rr[j] = top;
                     Tr[j] = tr0;
                 }
@@ -825,7 +859,9 @@ struct EeWalk {
                     uint64_t pold = Rr[0];
                     uint64_t pnew = xclose((Rr[0] & TA[c]) | ((Rr[0] << 1) & T[c]));
                     Rr[0] = pnew;
-                    for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                    for (int j = 1; j <= KR; ++j) {
+                        if (j > k) break;
                         const uint64_t old = Rr[j];
                         const uint64_t v = ((old << 1) & T[c]) | (old & TA[c]) | pold | ((pnew | pold) << 1) | Tr[j];
                         Tr[j] = (xclose((pold & TA[look]) | ((pold << 1) & T[look])) << 1) & T[c];
@@ -834,10 +870,10 @@ struct EeWalk {
                         pnew = Rr[j];
                     }
                     if (cnt < 0) {
-                        if ((Rr[k] >> 63) && check<WB>(0, pos + 1, mb, me)) return true;
+                        if ((pick(Rr, k) >> 63) && check(0, pos + 1, mb, me)) return true;
                         break;
                     }
-                    if (!Rr[k] && !Tr[k]) break;
+                    if (!pick(Rr, k) && !pick(Tr, k)) break;
                     --ptr;
                     c = look;
                 }
@@ -861,7 +897,9 @@ struct EeWalk {
                 ++p;
                 c = at(p - 1);
             }
-            for (int j = 0; j <= k; ++j) {
+#pragma unroll
+            for (int j = 0; j <= KR; ++j) {
+                if (j > k) break;
                 Rr[j] = j ? ~(~0ull << j) : 0ull;
                 Tr[j] = 0;
             }
@@ -883,7 +921,9 @@ struct EeWalk {
                 if (ta0) raw0 |= Rr[0] & TA[c];
                 uint64_t pnew = xclose(raw0);
                 Rr[0] = pnew;
-                for (int j = 1; j <= k; ++j) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > k) break;
                     const uint64_t old = Rr[j];
                     const uint64_t v = (((old << 1) | 1) & T[c]) | (old & TA[c]) | ((pnew | pold) << 1) | pold | 1ull |
                                        Tr[j];
@@ -893,7 +933,7 @@ struct EeWalk {
                     pold = old;
                     pnew = Rr[j];
                 }
-                if ((Rr[k] & fin) && nxt <= stop && check<WB>(0, nxt, mb, me)) return true;
+                if ((pick(Rr, k) & fin) && nxt <= stop && check(0, nxt, mb, me)) return true;
                 if (n < nxt + 1) return false;
                 c = look;
                 ++nxt;
@@ -959,7 +999,7 @@ __global__ __launch_bounds__(EE_T) void k_ee_heads(XtPrep X, const uint64_t* __r
     }
 }
 
-template <int WB>
+template <int WB, int KR, int SC>
 __global__ __launch_bounds__(WALK_T) void k_ee_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
                                                     const uint64_t* total_d, uint64_t total_h,
                                                     uint8_t* __restrict__ acc, TextView tv) {
@@ -990,7 +1030,7 @@ __global__ __launch_bounds__(WALK_T) void k_ee_walk(XtPrep X, uint64_t* __restri
                 R0 = (int64_t)tv.reg.t[r];
                 n = (int64_t)tv.reg.e[r];
             }
-            EeWalk w{S, tab, tv, n, R0, -1, n, TxtCache{tcbuf, 0, 0}};
+            EeWalk<WB, KR, SC> w{S, tab, tv, n, R0, -1, n, TxtCache{tcbuf, 0, 0}};
             int64_t stop;
             if (S->max_len >= 0) {
                 const int64_t back = S->max_len + S->k + 4;
@@ -1007,7 +1047,7 @@ __global__ __launch_bounds__(WALK_T) void k_ee_walk(XtPrep X, uint64_t* __restri
             w.nl_hi = w.next_nl(w.R);
             for (;;) {
                 int64_t mb = 0, me = 0;
-                if (!w.template scan<WB>(stop, mb, me)) break;
+                if (!w.scan(stop, mb, me)) break;
                 if (!ee_dropped(tv, mb) && nout < nmax) {
                     keys[i + nout] = (pid << 48) | (uint64_t)mb;
                     lens[i + nout] = (uint32_t)(me - mb);
@@ -1074,15 +1114,53 @@ uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid) {
     return n2;
 }
 
+namespace {
+
+template <class F>
+void ee_walk_by_sc(int sc, F&& f) {
+    switch (sc) {
+        case 0: f(std::integral_constant<int, 0>{}); break;
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        case 4: f(std::integral_constant<int, 4>{}); break;
+        default: f(std::integral_constant<int, 5>{}); break;
+    }
+}
+
+}  // namespace
+
+int ee_scanner(const Upload& up, size_t o_slot) {
+    EeSlot S;
+    memcpy(&S, up.blob.data() + o_slot, sizeof(S));
+    if (S.simple) return S.type == 1 ? 0 : S.type == 2 ? 1 : 2;
+    return S.type == 1 ? 3 : S.type == 2 ? 4 : 5;
+}
+
 void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, const TextView& tv, int words, hipStream_t s) {
     const uint32_t blocks = 1024;
     hipLaunchKernelGGL(k_ee_heads, dim3(blocks), dim3(EE_T), 0, s, X, keys, total_d, total_h, acc, tv);
     const size_t lds = walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN;
-    if (words <= 1)
-        hipLaunchKernelGGL(k_ee_walk<1>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
-    else
-        hipLaunchKernelGGL(k_ee_walk<4>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
+    // the scanner and the row count (below 4 errors: rows in registers) are
+    // template arguments
+    ee_walk_by_sc(X.scanner, [&](auto sc) {
+        constexpr int SC = decltype(sc)::value;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
+        };
+        const int k = X.k;
+        if (words <= 1)
+            k == 1   ? go(k_ee_walk<1, 1, SC>)
+            : k == 2 ? go(k_ee_walk<1, 2, SC>)
+            : k == 3 ? go(k_ee_walk<1, 3, SC>)
+                     : go(k_ee_walk<1, PM_MAX_K, SC>);
+        else
+            k == 1   ? go(k_ee_walk<4, 1, SC>)
+            : k == 2 ? go(k_ee_walk<4, 2, SC>)
+            : k == 3 ? go(k_ee_walk<4, 3, SC>)
+                     : go(k_ee_walk<4, PM_MAX_K, SC>);
+    });
     HIPCHK(hipGetLastError());
 }
 

@@ -775,44 +775,73 @@ __device__ inline uint32_t fold4(uint32_t v) {   // xt_fold on four bytes
     const uint32_t lower = ge_a & ~gt_z & ~v & 0x80808080u;   // 0x61 <= b <= 0x7a
     return v - (lower >> 2);                                   // 0x80 >> 2 = 0x20
 }
+// A refill is out of line (one copy for every read site of a walk; a walk
+// inlines dozens) and takes plain pointers, not the TextView aggregate.
+// NUC: [l, h) from the position planes four bytes at a time, then the
+// flagged positions (exceptions, breaks) from the side tables.
+static __device__ __attribute__((noinline)) void tc_fill_nuc(uint8_t* buf, const uint4* lin, const uint2* hl,
+                                                             const uint2* bo, const uint32_t* sbflag,
+                                                             const uint32_t* sbbase, const uint8_t* xbytes,
+                                                             uint64_t l, uint64_t h) {
+    const NucView nv{hl, bo, sbflag, sbbase, xbytes, lin};
+    uint4 w[TC_WIN / 32];
+#pragma unroll
+    for (uint32_t q = 0; q < TC_WIN / 32; ++q) w[q] = l + 32ull * q < h ? lin[(l >> 5) + q] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t q = 0; q < TC_WIN / 32; ++q) {
+        uint32_t o[8];
+#pragma unroll
+        for (uint32_t g = 0; g < 8; ++g) {
+            uint32_t v = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t b = 4 * g + i;
+                const uint32_t code = (((w[q].x >> b) & 1) << 1) | ((w[q].y >> b) & 1);
+                v |= ((0x54474341u >> (8 * code)) & 0xffu) << (8 * i);   // "ACGT"
+            }
+            o[g] = v;
+        }
+        uint4* d = reinterpret_cast<uint4*>(buf + 32 * q);
+        d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+    for (uint32_t q = 0; q < TC_WIN / 32; ++q) {
+        uint32_t ex = w[q].z | w[q].w;
+        while (ex) {
+            const uint32_t i = (uint32_t)__builtin_ctz(ex);
+            ex &= ex - 1;
+            const uint64_t pos = l + 32ull * q + i;
+            if (pos < h) buf[32 * q + i] = xt_fold(nuc_raw_at(nv, pos));
+        }
+    }
+}
+// BYTE: [l, h) with 16-byte loads, folded four bytes at a time
+static __device__ __attribute__((noinline)) void tc_fill_raw(uint8_t* buf, const uint8_t* raw, uint64_t n, uint64_t l) {
+    uint4 v[TC_WIN / 16];
+#pragma unroll
+    for (uint32_t q = 0; q < TC_WIN / 16; ++q)
+        v[q] = l + 16ull * q + 16 <= n ? *reinterpret_cast<const uint4*>(raw + l + 16ull * q) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t q = 0; q < TC_WIN / 16; ++q)
+        *reinterpret_cast<uint4*>(buf + 16 * q) = make_uint4(fold4(v[q].x), fold4(v[q].y), fold4(v[q].z), fold4(v[q].w));
+    for (uint64_t p = l + 16ull * ((n > l ? n - l : 0) / 16); p < n && p < l + TC_WIN; ++p)   // the last partial chunk
+        buf[p - l] = xt_fold(raw[p]);
+}
 struct TxtCache {
     uint8_t* buf;       // TC_WIN bytes of LDS (16-byte aligned)
     uint64_t lo, hi;    // positions cached: [lo, hi)
     __device__ void fill(const TextView& tv, uint64_t p) {
         if (tv.nuc_layout) {
-            const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~31ull : 0ull, h = umin64(l + TC_WIN, tv.n);
-            uint4 w[TC_WIN / 32];
-#pragma unroll
-            for (uint32_t q = 0; q < TC_WIN / 32; ++q) w[q] = l + 32ull * q < h ? tv.nuc.lin[(l >> 5) + q] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t q = 0; q < TC_WIN / 32; ++q)
-                for (uint32_t i = 0; i < 32; ++i) {
-                    const uint64_t pos = l + 32ull * q + i;
-                    if (pos >= h) break;
-                    uint8_t c;
-                    if (((w[q].z | w[q].w) >> i) & 1) c = xt_fold(nuc_raw_at(tv.nuc, pos));
-                    else c = (uint8_t)((0x54474341u >> (8 * ((((w[q].x >> i) & 1) << 1) | ((w[q].y >> i) & 1)))) & 0xff);
-                    buf[32 * q + i] = c;
-                }
+            const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~31ull : 0ull;
+            hi = umin64(l + TC_WIN, tv.n);
+            tc_fill_nuc(buf, tv.nuc.lin, tv.nuc.hl, tv.nuc.bo, tv.nuc.sbflag, tv.nuc.sbbase, tv.nuc.xbytes, l, hi);
             lo = l;
-            hi = h;
             return;
         }
-        const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~15ull : 0ull, h = umin64(l + TC_WIN, tv.n);
-        uint4 v[TC_WIN / 16];
-#pragma unroll
-        for (uint32_t q = 0; q < TC_WIN / 16; ++q)
-            v[q] = l + 16ull * q + 16 <= tv.n ? *reinterpret_cast<const uint4*>(tv.raw + l + 16ull * q) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (uint32_t q = 0; q < TC_WIN / 16; ++q) {
-            if (l + 16ull * q + 16 > tv.n) {   // the text's last partial chunk
-                for (uint32_t i = 0; i < 16 && l + 16ull * q + i < tv.n; ++i) buf[16 * q + i] = xt_fold(tv.raw[l + 16ull * q + i]);
-            } else {
-                *reinterpret_cast<uint4*>(buf + 16 * q) = make_uint4(fold4(v[q].x), fold4(v[q].y), fold4(v[q].z), fold4(v[q].w));
-            }
-        }
+        const uint64_t l = p > TC_BACK ? (p - TC_BACK) & ~15ull : 0ull;
+        tc_fill_raw(buf, tv.raw, tv.n, l);
         lo = l;
-        hi = h;
+        hi = umin64(l + TC_WIN, tv.n);
     }
     __device__ uint8_t get(const TextView& tv, uint64_t p) {
         if (p >= tv.n) return (uint8_t)'\n';
@@ -1061,6 +1090,8 @@ struct XtPrep {
     int32_t pid = 0;
     int32_t words = 1;            // eextended: the verify parts' widest word count
     int32_t eregular = 0;         // rg: k > 0 (pm_regular.hip k_erg_walk)
+    int32_t k = 0;                // errors (the walks' row count template argument)
+    int32_t scanner = 0;          // ee / eregular: ee_scanner / erg_scanner of the slot (a template argument of the walk)
     uint32_t tab_words = 0;       // words of the table blob at tab (copied to LDS when small)
 };
 // eextended heads + walk on s (keys/lens rewritten in place, acc bit 0 =
@@ -1069,6 +1100,12 @@ struct XtPrep {
 // (total entries) and sorts it again; returns the new length
 uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
 
+// the eextended walk's scanner kind: 0..2 esimpleScan pieces / window /
+// prefix, 3..5 eextendedScan pieces / window / prefix
+int ee_scanner(const Upload& up, size_t o_slot);
+// the eregular walk's scanner kind: 0..1 esimpleScan pieces / window,
+// 2 the pieces exactly, 3 bwdScanrk, 4 fwdScanrk
+int erg_scanner(const Upload& up, size_t o_slot);
 void ee_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, const TextView& tv, int words, hipStream_t s);
 // regular heads + walk on s (keys/lens rewritten in place, acc bit 0 =

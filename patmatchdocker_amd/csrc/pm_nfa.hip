@@ -240,15 +240,48 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
         if (a.in_state && chunk_id + 1 < a.nchunks && j <= a.k)
             R[j] = bits_of<W>(a.in_state + (chunk_id + 1) * a.st_stride + j * W);
     }
-    for (uint64_t p = top; p-- > c0;) {
-        bool kill;
-        const uint8_t ch = char_at<NUC>(a, p, kill);
+    auto step = [&](uint64_t p, uint8_t ch, bool kill) {
         nfa_rev_step<K, W>(R, bits_of<W>(s_b + ch * W), !kill, s_prec, a);
         Bits<W> any = bits_zero<W>();
 #pragma unroll
         for (int j = 0; j <= K; ++j) any = any | R[j];
         if (live && p < c1 && p < a.n && meets<W>(any, a.first))
             a.sink.push(a.sink.bin_of(0, p), ((uint64_t)a.pattern_id << 48) | p);
+    };
+    if constexpr (NUC) {
+        for (uint64_t p = top; p-- > c0;) {
+            bool kill;
+            const uint8_t ch = char_at<NUC>(a, p, kill);
+            step(p, ch, kill);
+        }
+    } else {
+        // the lane's bytes arrive 16 at a time (aligned uint4 loads), the
+        // next group in flight while this one is stepped: the text reads no
+        // longer sit on the state chain
+        const uint8_t* src = a.cross ? a.bytes_raw : a.bytes;
+        auto group = [&](uint64_t g) {
+            return g + 16 <= a.n ? *reinterpret_cast<const uint4*>(src + g) : make_uint4(0, 0, 0, 0);
+        };
+        uint64_t g = (top - 1) & ~15ull;
+        uint4 cur = group(g), nxt = g >= 16 ? group(g - 16) : make_uint4(0, 0, 0, 0);
+        for (uint64_t p = top; p-- > c0;) {
+            if ((p & ~15ull) != g) {   // p moved into the group below
+                g -= 16;
+                cur = nxt;
+                nxt = g >= 16 ? group(g - 16) : make_uint4(0, 0, 0, 0);
+            }
+            bool kill;
+            uint8_t ch;
+            if (g + 16 <= a.n) {
+                const uint32_t i = (uint32_t)(p & 15);
+                const uint32_t wv = i < 8 ? (i < 4 ? cur.x : cur.y) : (i < 12 ? cur.z : cur.w);
+                ch = (uint8_t)(wv >> (8 * (i & 3)));
+                kill = !a.cross && ch == (uint8_t)'\n';
+            } else {
+                ch = char_at<NUC>(a, p, kill);   // the file's last partial group and past it
+            }
+            step(p, ch, kill);
+        }
     }
 }
 
@@ -643,14 +676,18 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         xtp.pid = pattern_id;
         xtp.words = m + 1 <= 64 ? 1 : RG_NW;
         xtp.eregular = k > 0 ? 1 : 0;
+        xtp.k = k;
+        if (k > 0) xtp.scanner = erg_scanner(up, o_xslot);
         xtp.tab_words = walk_tab_words;
     }
     if (extended) {
         if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
         else xtp.ee = reinterpret_cast<const EeSlot*>(d_up + o_xslot);
+        if (k > 0) xtp.scanner = ee_scanner(up, o_xslot);
         xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);
         xtp.pid = pattern_id;
         xtp.words = W;
+        xtp.k = k;
         xtp.tab_words = walk_tab_words;
     }
     esp.lines = all_pos ? 1 : 0;
@@ -687,8 +724,13 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // chunk per lane: a power of two (so that on the nucleotide layout
     // the lanes of a wave walk the streams of one tile in lock step and
     // their loads coincide), enough lanes to fill the chip; reads stop at
-    // the end of the file (char_at), so the halo needs no padding
-    uint64_t chunk = 64;
+    // the end of the file (char_at), so the halo needs no padding.  A small
+    // file gets chunks down to 16 positions: a lane's scan is a chain of
+    // dependent steps, so lanes (not the halo's re-read) set the time
+    // (configs[3], 3.5 MB at k = 1: 64-position chunks left < 1 wave per
+    // SIMD).  Unbounded patterns keep 64 (their carry rounds grow with the
+    // chunks per record).
+    uint64_t chunk = unbounded ? 64 : 16;
     while (chunk < (uint64_t)MAX_NFA_CHUNK && db->n / (chunk * 2) >= 256ull * 4 * 64 * 2) chunk *= 2;
     if (db->alphabet == PM_ALPHA_NUC) chunk = std::min<uint64_t>(chunk, STREAM);
     a.chunk = (int)chunk;

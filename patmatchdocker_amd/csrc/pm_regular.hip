@@ -955,6 +955,7 @@ struct RgWalk {
 
 // eregular (k > 0, one word): the scanners and checkMatch of
 // oracle/pm_nrgrep_reg.c over the cluster's text
+template <int KR, int SC>
 struct ErgWalk {
     const RgSlot* S;
     const uint64_t* tab;
@@ -964,6 +965,20 @@ struct ErgWalk {
     uint64_t nl_lo, nl_hi;
 
     mutable TxtCache tc;   // the thread's text window (LDS)
+
+    // SC is the scanner (erg_scanner: a kernel holds one scanner and one
+    // inlined checkMatch); KR the row count the kernel was built for: k
+    // itself for k <= 3 (row loops unroll, the rows stay in registers),
+    // PM_MAX_K otherwise (loops bounded by the run-time k)
+    __device__ __forceinline__ int kk() const { return KR < PM_MAX_K ? KR : S->k; }
+    template <int N>
+    __device__ __forceinline__ static uint64_t pick(const uint64_t (&a)[N], int i) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j == i) v = a[j];
+        return v;
+    }
 
     __device__ uint8_t at(uint64_t p) const { return tc.get(tv, p); }
     __device__ uint64_t next_nl(uint64_t p) const { return xt_next_nl(tv, p, n); }
@@ -996,7 +1011,7 @@ struct ErgWalk {
         const uint64_t* arr = tab + S->o_arr;
         const uint64_t* B = tab + S->o_B;
         const uint64_t F = S->final_[0];
-        uint64_t rows[PM_MAX_K + 1];
+        uint64_t rows[KR + 1];
         rows[0] = 1ull << s;
         if (rows[0] & F) {   // 0x40339d: insertions up to the right context
             kio = 0;
@@ -1008,7 +1023,9 @@ struct ErgWalk {
         }
         int kmax = K;
         uint64_t best = RG_NONE;
-        for (int j = 1; j <= kmax; ++j) {   // 0x4034c0 (rows left unset without OptDel: row 0)
+#pragma unroll
+        for (int j = 1; j <= KR; ++j) {   // 0x4034c0 (rows left unset without OptDel: row 0)
+            if (j > kmax) break;
             rows[j] = del ? rows[j - 1] | tr(arr, rows[j - 1]) : rows[j - 1];
             if (del && (rows[j] & F) && right_ok(p + 1, lim + 1)) {
                 kio = j;
@@ -1027,7 +1044,9 @@ struct ErgWalk {
             }
             uint64_t oldp = rows[0], last = n0;
             rows[0] = n0;
-            for (int j = 1; j <= kmax; ++j) {   // 0x4037a0
+#pragma unroll
+            for (int j = 1; j <= KR; ++j) {   // 0x4037a0
+                if (j > kmax) break;
                 uint64_t v = del ? tr(arr, last) : 0;
                 if (ins) v |= oldp;
                 if (sub) v |= tr(arr, oldp);
@@ -1037,7 +1056,9 @@ struct ErgWalk {
                 last = v;
                 if ((v & F) && right_ok(cur + 1, lim + 1)) {   // 0x403a01: the fewest errors
                     int c = j;
-                    while (c - 1 >= 0 && (rows[c - 1] & F)) --c;
+#pragma unroll
+                    for (int d = KR - 1; d >= 0; --d)   // while rows[c - 1] is final: --c
+                        if (d == c - 1 && (rows[d] & F)) c = d;
                     if (c == 0) {
                         kio = 0;
                         return cur;
@@ -1057,7 +1078,7 @@ struct ErgWalk {
         const int K = kio, ins = S->errs & PM_ERR_INS, del = S->errs & PM_ERR_DEL, sub = S->errs & PM_ERR_SUB;
         const uint64_t* rev = tab + S->o_rev;
         const uint64_t* B = tab + S->o_B;
-        uint64_t rows[PM_MAX_K + 1];
+        uint64_t rows[KR + 1];
         rows[0] = 1ull << s;
         if (rows[0] & 1) {   // 0x403e71: insertions down to the left context
             kio = 0;
@@ -1071,7 +1092,9 @@ struct ErgWalk {
         }
         int kmax = K;
         uint64_t best = RG_NONE;
-        for (int j = 1; j <= kmax; ++j) {   // 0x403f80
+#pragma unroll
+        for (int j = 1; j <= KR; ++j) {   // 0x403f80
+            if (j > kmax) break;
             rows[j] = del ? rows[j - 1] | tr(rev, rows[j - 1]) : rows[j - 1];
             if (del && (rows[j] & 1) && left_ok(p, lim)) {
                 kio = j;
@@ -1090,7 +1113,9 @@ struct ErgWalk {
             }
             uint64_t oldp = rows[0], last = n0;
             rows[0] = n0;
-            for (int j = 1; j <= kmax; ++j) {   // 0x404230
+#pragma unroll
+            for (int j = 1; j <= KR; ++j) {   // 0x404230
+                if (j > kmax) break;
                 uint64_t v = del ? tr(rev, last) : 0;
                 if (ins) v |= oldp;
                 if (sub) v |= tr(rev, oldp);
@@ -1100,7 +1125,9 @@ struct ErgWalk {
                 last = v;
                 if ((v & 1) && left_ok(cur, lim)) {
                     int c = j;
-                    while (c - 1 >= 0 && (rows[c - 1] & 1)) --c;
+#pragma unroll
+                    for (int d = KR - 1; d >= 0; --d)   // while rows[c - 1] is final: --c
+                        if (d == c - 1 && (rows[d] & 1)) c = d;
                     if (c == 0) {
                         kio = 0;
                         return cur;
@@ -1152,8 +1179,8 @@ struct ErgWalk {
     // eregularScan / esimpleScan from R; false when no candidate at or
     // before stop verifies
     __device__ bool scan(uint64_t stop, uint64_t& mb, uint64_t& me) {
-        const int K = S->k, ell = S->ell;
-        if (S->cls == 1 && S->type == 1) {   // esimpleScan's pieces (0x413780)
+        const int K = kk(), ell = S->ell;
+        if constexpr (SC == 0) {             // esimpleScan's pieces (0x413780)
             const uint64_t* T0 = tab + S->o_T0;
             const uint64_t* T2 = tab + S->o_T2;
             const int np = K + 1;
@@ -1186,18 +1213,20 @@ struct ErgWalk {
             }
             return false;
         }
-        if (S->cls == 1) {                   // esimpleScan's ABNDM window (0x413b6f)
+        if constexpr (SC == 1) {             // esimpleScan's ABNDM window (0x413b6f)
             const uint64_t* T = tab + S->o_T0;
             const uint64_t top = ~0ull << (64 - ell);
             const int W = ell - K;
             if (n < (uint64_t)(ell - K - 1)) return false;
             const uint64_t limit = n - (uint64_t)(ell - K - 1);
-            uint64_t Rr[PM_MAX_K + 1], Tr[PM_MAX_K + 1];
+            uint64_t Rr[KR + 1], Tr[KR + 1];
             for (uint64_t s = R; s < limit;) {
                 if (s > stop) return false;
                 const uint64_t b0 = T[at(s + W - 1)];
                 Rr[0] = b0;
-                for (int j = 1; j <= K; ++j) {
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {
+                    if (j > K) break;
                     Rr[j] = top;
                     Tr[j] = b0;
                 }
@@ -1206,7 +1235,9 @@ struct ErgWalk {
                     const uint64_t bc = T[at(s + (uint64_t)rb)];
                     uint64_t oldp = Rr[0], newp = (oldp << 1) & bc;
                     Rr[0] = newp;
-                    for (int j = 1; j <= K; ++j) {
+#pragma unroll
+                    for (int j = 1; j <= KR; ++j) {
+                        if (j > K) break;
                         const uint64_t trans = (bc << 1) & Tr[j];
                         uint64_t v = ((newp | oldp) << 1) | oldp;
                         Tr[j] = (oldp << 2) & bc;
@@ -1218,10 +1249,10 @@ struct ErgWalk {
                         newp = v;
                     }
                     if (rb == 0) {
-                        if ((Rr[K] >> 63) && check(s, S->match0, mb, me)) return true;
+                        if ((pick(Rr, K) >> 63) && check(s, S->match0, mb, me)) return true;
                         break;
                     }
-                    if (!Rr[K] && !Tr[K]) break;
+                    if (!pick(Rr, K) && !pick(Tr, K)) break;
                     --rb;
                 }
                 s += (uint64_t)(rb + 1);
@@ -1232,7 +1263,7 @@ struct ErgWalk {
         const uint64_t* Av = tab + S->o_A;
         const uint64_t* rw = tab + S->o_rw;
         const uint64_t* fw = tab + S->o_fw;
-        if (S->type == 1) {                  // the pieces exactly (0x4052b9)
+        if constexpr (SC == 2) {             // the pieces exactly (0x4052b9)
             if (n < (uint64_t)ell) return false;
             int64_t pos = (int64_t)R - 1;
             const int64_t lim = (int64_t)n - ell;
@@ -1264,8 +1295,8 @@ struct ErgWalk {
             }
             return false;
         }
-        uint64_t rows[PM_MAX_K + 1], old[PM_MAX_K + 1];
-        if (S->type == 2) {                  // bwdScanrk 0x402d50
+        uint64_t rows[KR + 1], old[KR + 1];
+        if constexpr (SC == 3) {             // bwdScanrk 0x402d50
             const int W = ell - K;
             if (n < (uint64_t)W) return false;
             int64_t pos = (int64_t)R - 1;
@@ -1275,14 +1306,20 @@ struct ErgWalk {
                 const uint8_t c0 = at((uint64_t)(pos + W));
                 uint64_t bprev = Bw[c0];
                 rows[0] = Av[c0];
-                for (int j = 1; j <= K; ++j) rows[j] = S->finit;
-                for (int j = 0; j <= K; ++j) old[j] = S->finit;
+#pragma unroll
+                for (int j = 1; j <= KR; ++j)
+                    if (j <= K) rows[j] = S->finit;
+#pragma unroll
+                for (int j = 0; j <= KR; ++j)
+                    if (j <= K) old[j] = S->finit;
                 int64_t cur = pos + W - 1;
                 for (;;) {
                     const uint64_t bc = Bw[at((uint64_t)cur)];
                     uint64_t po = rows[0], pn = tr(rw, bc & po);
                     rows[0] = pn;
-                    for (int j = 1; j <= K; ++j) {   // 0x4030d0
+#pragma unroll
+                    for (int j = 1; j <= KR; ++j) {   // 0x4030d0
+                        if (j > K) break;
                         const uint64_t oj = rows[j];
                         uint64_t v = po | tr(rw, pn | po) | tr(rw, bc & oj);
                         v |= tr(rw, tr(rw, bc & old[j - 1]) & bprev);
@@ -1315,14 +1352,18 @@ struct ErgWalk {
             }
             uint64_t st = S->finit;
             rows[0] = old[0] = st;
-            for (int j = 1; j <= K; ++j) {
+#pragma unroll
+            for (int j = 1; j <= KR; ++j) {
+                if (j > K) break;
                 st |= tr(fw, st);
                 rows[j] = old[j] = st;
             }
             uint64_t bc = Bw[c];
             uint64_t po = rows[0], pn = tr(fw, po) & bc;
             rows[0] = pn;
-            for (int j = 1; j <= K; ++j) {   // 0x402a31
+#pragma unroll
+            for (int j = 1; j <= KR; ++j) {   // 0x402a31
+                if (j > K) break;
                 const uint64_t r = pn | po, oj = rows[j];
                 const uint64_t v = r | (tr(fw, oj) & bc) | tr(fw, r);
                 rows[j] = v;
@@ -1340,7 +1381,9 @@ struct ErgWalk {
                 po = rows[0];
                 pn = tr(fw, po) & bc;
                 rows[0] = pn;
-                for (int j = 1; j <= K; ++j) {   // 0x402b68
+#pragma unroll
+                for (int j = 1; j <= KR; ++j) {   // 0x402b68
+                    if (j > K) break;
                     const uint64_t oj = rows[j];
                     uint64_t v = po | (tr(fw, oj) & bc) | tr(fw, pn | po);
                     v |= tr(fw, tr(fw, old[j - 1]) & bc) & bprev;
@@ -1357,6 +1400,7 @@ struct ErgWalk {
     }
 };
 
+template <int KR, int SC>
 __global__ __launch_bounds__(WALK_T) void k_erg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
                                                      const uint64_t* total_d, uint64_t total_h,
                                                      uint8_t* __restrict__ acc, TextView tv) {
@@ -1387,7 +1431,7 @@ __global__ __launch_bounds__(WALK_T) void k_erg_walk(XtPrep X, uint64_t* __restr
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            ErgWalk w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
+            ErgWalk<KR, SC> w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             // from the start of first's line, at most span + 4 before it
             // (the scanners' rows then agree with the whole scan's, and no
             // match found before first can start at another cluster's key)
@@ -1486,14 +1530,39 @@ __global__ __launch_bounds__(WALK_T) void k_rg_walk(XtPrep X, uint64_t* __restri
 
 }  // namespace
 
+int erg_scanner(const Upload& up, size_t o_slot) {
+    RgSlot S;
+    memcpy(&S, up.blob.data() + o_slot, sizeof(S));
+    if (S.cls == 1) return S.type == 1 ? 0 : 1;
+    return S.type == 1 ? 2 : S.type == 2 ? 3 : 4;
+}
+
 void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
     hipLaunchKernelGGL(k_rg_heads, dim3(blocks), dim3(RG_T), 0, s, X, keys, total_d, total_h, acc, tv);
     const size_t lds = walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN;
-    if (X.eregular)
-        hipLaunchKernelGGL(k_erg_walk, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
-    else if (X.words == 1)
+    if (X.eregular) {
+        // the scanner and the row count (below 4 errors: rows in registers)
+        // are template arguments
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
+        };
+        auto by_k = [&](auto sc) {
+            constexpr int SC = decltype(sc)::value;
+            X.k == 1   ? go(k_erg_walk<1, SC>)
+            : X.k == 2 ? go(k_erg_walk<2, SC>)
+            : X.k == 3 ? go(k_erg_walk<3, SC>)
+                       : go(k_erg_walk<PM_MAX_K, SC>);
+        };
+        switch (X.scanner) {
+            case 0: by_k(std::integral_constant<int, 0>{}); break;
+            case 1: by_k(std::integral_constant<int, 1>{}); break;
+            case 2: by_k(std::integral_constant<int, 2>{}); break;
+            case 3: by_k(std::integral_constant<int, 3>{}); break;
+            default: by_k(std::integral_constant<int, 4>{}); break;
+        }
+    } else if (X.words == 1)
         hipLaunchKernelGGL(k_rg_walk<1>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
     else
         hipLaunchKernelGGL(k_rg_walk<RG_NW>, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc,

@@ -404,7 +404,7 @@ namespace {
 constexpr uint64_t ES_POS_MASK = (1ull << 48) - 1;
 
 constexpr int ES_CHUNK = 16;     // positions staged per refill of a thread's window
-constexpr int ES_THREADS = 64;   // walk threads per block (one wave)
+constexpr int ES_THREADS = 256;  // walk threads per block (4 waves: the block's tables in LDS serve them all)
 constexpr int ES_SPAN = 16;      // window starts whose pieces one shift-and pass finds
 constexpr size_t ES_TAB_LDS = 16 << 10;   // compact tables kept in LDS up to this size
 
@@ -780,6 +780,8 @@ __global__ void k_es_iota(uint64_t* __restrict__ keys, uint64_t n, uint64_t pid)
 // One thread per cluster of the walk list (grid-stride): nrgrep's candidate
 // order over the cluster's text; the printed matches are written in place
 // from the head on (acc bit 0), every other entry of the cluster is cleared.
+// (capping the registers for 3 blocks per CU -- 168 VGPRs, 68-190 B of
+// spills -- measured slower: -k 2ids 5.02 vs 4.86 ms per step, r05k)
 template <int WB, int KR>
 __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
                                                         const uint64_t* total_d, uint64_t total_h,
@@ -788,9 +790,9 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
     const uint64_t total = total_d ? *total_d : total_h;
     const uint32_t nw = *wcount;
     const uint32_t stride = gridDim.x * blockDim.x;
-    // list entry t goes to lane t / gridDim.x of block t % gridDim.x: a short
-    // list is spread one cluster per wave (a wave runs its lanes' divergent
-    // walks one after the other)
+    // list entry t goes to block t % gridDim.x, thread rank t / gridDim.x
+    // (below): a short list is spread one cluster per wave (a wave runs its
+    // lanes' divergent walks one after the other)
     if (blockIdx.x >= nw) return;   // (block-uniform) nothing to walk
     // the compact tables (when they fit) and the byte -> code map in LDS
     uint8_t* cmap = es_lds + P.map_off;
@@ -802,7 +804,10 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         tab = lt;
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x * gridDim.x + blockIdx.x; t < nw; t += stride) {
+    // the thread's rank lane * waves + wave: consecutive entries of a block
+    // go to different waves
+    const uint32_t rank = (threadIdx.x & 63u) * (ES_THREADS / 64) + (threadIdx.x >> 6);
+    for (uint32_t t = rank * gridDim.x + blockIdx.x; t < nw; t += stride) {
         const uint64_t i = wlist[t];
         uint64_t j = i + 1;   // the next cluster's head keeps bit 1 set whatever its owner writes
         while (j < total && !(acc[j] & 2)) ++j;
@@ -1033,26 +1038,33 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
     // ring keeps the last win positions (a read before them goes to memory)
     uint32_t win = 64;
     while (win < (uint32_t)P.gap_max + ES_SPAN + 32) win <<= 1;
-    P.win = win <= 512 ? win : 0;   // wider patterns read memory directly
+    // wider patterns read memory directly (a block's rings, piece words and
+    // tables stay within the CU's LDS)
+    P.win = (size_t)ES_THREADS * win + (size_t)ES_THREADS * ES_SPAN * 8 + ES_TAB_LDS + 256 <= (160u << 10) ? win : 0;
     P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
     // then the compact tables (up to ES_TAB_LDS bytes) and the code map
     P.tab_off = P.dl_off + ES_THREADS * ES_SPAN * 8;
     P.tab_lds = (size_t)P.tab_words * 8 <= ES_TAB_LDS ? 1 : 0;
     P.map_off = P.tab_off + (P.tab_lds ? P.tab_words * 8 : 0);
     const size_t lds = P.map_off + 256;
-    // one wave per block (a cluster's walk is a chain of dependent steps,
-    // and the ring takes LDS): 8 per CU, all resident, striding over the
-    // walk list (its length is on the device)
+    // a cluster's walk is a chain of dependent steps, so as many waves as
+    // the registers allow: blocks of ES_THREADS share the tables in LDS, all
+    // resident, striding over the walk list (its length is on the device)
     int dev = 0, ncu = 0;
     HIPCHK(hipGetDevice(&dev));
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160u << 10) / lds));
     const uint32_t blocks = (uint32_t)std::max(1, ncu) * per_cu;
     // WB: position words; KR: the rows unrolled (k <= 3, the common case,
-    // keeps the row vectors in few registers)
-    auto kern = P.kmax <= 3 ? (P.wmax <= 1 ? k_es_walk<1, 3> : P.wmax == 2 ? k_es_walk<2, 3> : k_es_walk<4, 3>)
-                            : (P.wmax <= 1 ? k_es_walk<1, PM_MAX_K> : P.wmax == 2 ? k_es_walk<2, PM_MAX_K>
-                                                                                  : k_es_walk<4, PM_MAX_K>);
+    // keeps the row vectors in few registers: k itself)
+    auto by_w = [&](auto kr) {
+        constexpr int KR = decltype(kr)::value;
+        return P.wmax <= 1 ? k_es_walk<1, KR> : P.wmax == 2 ? k_es_walk<2, KR> : k_es_walk<4, KR>;
+    };
+    auto kern = P.kmax <= 1   ? by_w(std::integral_constant<int, 1>{})
+                : P.kmax == 2 ? by_w(std::integral_constant<int, 2>{})
+                : P.kmax == 3 ? by_w(std::integral_constant<int, 3>{})
+                              : by_w(std::integral_constant<int, PM_MAX_K>{});
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(ES_THREADS), lds, s, P, keys,
                        lens, total_d, total_h, acc, wlist, wcount, tv);
     hipLaunchKernelGGL(k_es_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);

@@ -8,7 +8,8 @@
 // position) space in increasing order; each bin is sorted in LDS by one
 // workgroup and written at its exclusive offset, which yields the same
 // order as the reference's concatenated runs without a global sort.  Bins
-// too large for LDS fall back to a device radix sort of everything.
+// too large for LDS (a dense pattern of a big batch) are gathered and radix
+// sorted by themselves, then copied to their offsets.
 #include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
@@ -144,6 +145,93 @@ __global__ __launch_bounds__(THREADS) void k_sort_bins(const uint64_t* __restric
     }
 }
 
+// Bins of up to T * IPT keys from a list (one bin per block at a time): a
+// bin holds one pattern slot and a position range, so its keys sort as the
+// 32-bit offsets from its smallest position -- a block radix sort over the
+// range's significant bits (4096 keys: ~4 passes of an LDS rank, where the
+// bitonic network took 78 barrier rounds).  A range of 2^32 positions or
+// more (no sink makes one) takes a rank sort over the bin in memory.
+template <int T, int IPT>
+__global__ __launch_bounds__(T) void k_radix_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
+                                                  const uint64_t* __restrict__ off, BinShape sh,
+                                                  uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
+                                                  uint32_t* __restrict__ lens, const uint32_t* __restrict__ bin_list,
+                                                  uint32_t nitems) {
+    using Sort = hipcub::BlockRadixSort<uint32_t, T, IPT>;
+    __shared__ typename Sort::TempStorage ts;
+    __shared__ uint64_t red_lo[T / 64], red_hi[T / 64];
+    constexpr uint64_t PM = (1ull << 48) - 1;
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const uint32_t bin = bin_list[it];
+        const uint32_t c = min(cnt[bin], sh.cap(bin));
+        const uint64_t* src = sh.src(out, bin);
+        const uint64_t base = off[bin];
+        uint64_t k[IPT];
+        uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {   // striped: a wave's loads are contiguous
+            const uint32_t q = (uint32_t)j * T + threadIdx.x;
+            k[j] = q < c ? src[q] : 0ull;
+            if (q < c) {
+                lo = umin64(lo, k[j] & PM);
+                hi = umax64(hi, k[j] & PM);
+            }
+        }
+        for (int d = 32; d > 0; d >>= 1) {
+            const uint64_t ol = ((uint64_t)__shfl_xor((uint32_t)(lo >> 32), d, 64) << 32) | __shfl_xor((uint32_t)lo, d, 64);
+            const uint64_t oh = ((uint64_t)__shfl_xor((uint32_t)(hi >> 32), d, 64) << 32) | __shfl_xor((uint32_t)hi, d, 64);
+            lo = umin64(lo, ol);
+            hi = umax64(hi, oh);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red_lo[threadIdx.x >> 6] = lo;
+            red_hi[threadIdx.x >> 6] = hi;
+        }
+        __syncthreads();
+        lo = ~0ull;
+        hi = 0;
+        for (int w = 0; w < T / 64; ++w) {
+            lo = umin64(lo, red_lo[w]);
+            hi = umax64(hi, red_hi[w]);
+        }
+        const uint64_t tag = src[0] & ~PM;   // the bin's pattern slot
+        const uint32_t len = slot_len ? (uint32_t)slot_len[bin / sh.bins_per_slot] : 0u;
+        if (hi - lo < 0xFFFFFFFFull) {
+            // offsets from lo; the padding (hi - lo + 1) sorts after every key
+            const uint32_t pad = (uint32_t)(hi - lo + 1);
+            const int bits = 32 - __builtin_clz(pad);
+            uint32_t v[IPT];
+            // blocked input (thread t: items t * IPT + j); any order will do
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) v[j] = (uint32_t)j * T + threadIdx.x < c ? (uint32_t)((k[j] & PM) - lo) : pad;
+            Sort(ts).SortBlockedToStriped(v, 0, bits);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {   // striped: rank j * T + t
+                const uint32_t r = (uint32_t)j * T + threadIdx.x;
+                if (r < c) {
+                    dst[base + r] = tag | (lo + v[j]);
+                    if (slot_len) lens[base + r] = len;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t q = (uint32_t)j * T + threadIdx.x;
+                if (q >= c) continue;
+                const uint64_t kq = src[q];   // (reloaded: k[] is dead past the offsets)
+                uint32_t r = 0;
+                for (uint32_t x = 0; x < c; ++x) {
+                    const uint64_t y = src[x];
+                    r += (y < kq) | ((y == kq) & (x < q));
+                }
+                dst[base + r] = kq;
+                if (slot_len) lens[base + r] = len;
+            }
+        }
+        __syncthreads();   // ts and red_* are reused by the next bin
+    }
+}
+
 // clamped bin count (the keys a bin contributes to the list)
 struct BinCount {
     const uint32_t* cnt;
@@ -151,8 +239,8 @@ struct BinCount {
     __device__ uint64_t operator()(uint32_t b) const { return min(cnt[b], sh.cap(b)); }
 };
 
-// pos_bits > 0: keys packed as pattern << pos_bits | position, so the radix
-// sort runs over the significant bits only (k_unpack_keys restores them)
+// The whole list radix sorted (many large bins): gathered at the bins'
+// offsets, packed as pattern << pos_bits | position when pos_bits > 0
 __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* __restrict__ cnt,
                               const uint64_t* __restrict__ off, BinShape sh, uint64_t* __restrict__ dst,
                               uint32_t pos_bits) {
@@ -165,13 +253,42 @@ __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* 
         dst[o + i] = pos_bits ? ((k >> 48) << pos_bits) | (k & ((1ull << 48) - 1)) : k;
     }
 }
-
 __global__ void k_unpack_keys(uint64_t* __restrict__ keys, uint64_t n, uint32_t pos_bits) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t k = keys[i];
     keys[i] = ((k >> pos_bits) << 48) | (k & ((1ull << pos_bits) - 1));
 }
+
+// the bins too large for an LDS sort: gathered into one list (bin order),
+// radix sorted, copied back to each bin's offset.  pos_bits > 0: keys
+// packed as pattern << pos_bits | position while sorted, so the radix sort
+// runs over the significant bits only
+struct HugeBin {
+    uint32_t bin, c;
+    uint64_t src_off, dst_off;
+};
+__global__ void k_gather_huge(const uint64_t* __restrict__ out, BinShape sh, const HugeBin* __restrict__ hb,
+                              uint64_t* __restrict__ dst, uint32_t pos_bits) {
+    const HugeBin b = hb[blockIdx.x];
+    const uint64_t* src = sh.src(out, b.bin);
+    for (uint32_t i = threadIdx.x; i < b.c; i += blockDim.x) {
+        const uint64_t k = src[i];
+        dst[b.src_off + i] = pos_bits ? ((k >> 48) << pos_bits) | (k & ((1ull << 48) - 1)) : k;
+    }
+}
+__global__ void k_scatter_huge(const uint64_t* __restrict__ sorted, BinShape sh, const HugeBin* __restrict__ hb,
+                               uint64_t* __restrict__ dst, const int32_t* __restrict__ slot_len,
+                               uint32_t* __restrict__ lens, uint32_t pos_bits) {
+    const HugeBin b = hb[blockIdx.x];
+    const uint32_t len = slot_len ? (uint32_t)slot_len[b.bin / sh.bins_per_slot] : 0u;
+    for (uint32_t i = threadIdx.x; i < b.c; i += blockDim.x) {
+        const uint64_t k = sorted[b.src_off + i];
+        dst[b.dst_off + i] = pos_bits ? ((k >> pos_bits) << 48) | (k & ((1ull << pos_bits) - 1)) : k;
+        if (slot_len) lens[b.dst_off + i] = len;
+    }
+}
+
 
 std::mutex g_pool_mu;
 std::map<std::pair<int, size_t>, std::vector<void*>> g_pool;   // (device, capacity) -> free buffers
@@ -428,30 +545,68 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         // bins of up to LDS_SORT_CAP_MAX keys: one LDS sort block each; a few
         // larger ones (dense patterns of a big batch) up to LDS_SORT_CAP_HUGE:
         // a second pass over their list, 128 KB of LDS per block; beyond
-        // that one radix sort of the whole list
-        const bool lds = maxc <= LDS_SORT_CAP_HUGE;
+        // that (configs[4]: one pattern's ~24 Ki keys per segment) the bins
+        // are radix sorted by themselves -- 6 M keys instead of the whole
+        // 31 M-key list
         std::vector<uint32_t> big;
-        if (lds && maxc > LDS_SORT_CAP_MAX)
-            for (uint32_t b = 0; b < sb.nbins; ++b)
-                if (std::min(counts[b], sb.slot_cap_h[b / sb.bins_per_pattern]) > LDS_SORT_CAP_MAX) big.push_back(b);
+        std::vector<HugeBin> huge;
+        uint64_t nhuge = 0, nlarge = 0;   // keys in bins over LDS_SORT_CAP_HUGE / over LDS_SORT_SMALL
+        if (maxc > LDS_SORT_SMALL) {
+            uint64_t at = 0;
+            for (uint32_t b = 0; b < sb.nbins; ++b) {
+                const uint32_t c = std::min(counts[b], sb.slot_cap_h[b / sb.bins_per_pattern]);
+                if (c > LDS_SORT_CAP_HUGE) {
+                    huge.push_back({b, c, nhuge, at});
+                    nhuge += c;
+                } else if (c > LDS_SORT_CAP_MAX) {
+                    big.push_back(b);
+                }
+                if (c > LDS_SORT_SMALL) nlarge += c;
+                at += c;
+            }
+        }
+        // with a huge bin and most keys in large bins (configs[4]: 29 of 31 M)
+        // one radix sort of the whole list: every per-bin form sorts at about
+        // the same keys/s (block radix 27-32, huge-bin radix ~26 Gkeys/s,
+        // r05k) and the whole list is one pass of kernels
+        const bool whole = !huge.empty() && 2 * nlarge > total;
+        if (whole) {
+            big.clear();
+            huge.clear();
+            nhuge = 0;
+        }
         const BinShape sh{sb.slot_base, sb.slot_cap, sb.bins_per_pattern};
         // up to 4096 bins each sort block sums the counts before it itself
-        const bool inline_off = lds && sb.nbins <= 4096 && big.empty();
+        const bool inline_off = !whole && sb.nbins <= 4096 && big.empty() && huge.empty();
         auto counted = hipcub::TransformInputIterator<uint64_t, BinCount, hipcub::CountingInputIterator<uint32_t>>(
             hipcub::CountingInputIterator<uint32_t>(0u), BinCount{sb.cnt, sh});
-        size_t sort_bytes = 0, scan_bytes = 0;
-        if (!lds)
+        size_t scan_bytes = 0, sort_bytes = 0;
+        // sort only the significant bits: positions < 2^pos_bits, pattern
+        // slots < 2^slot_bits
+        uint32_t pos_bits = 1, slot_bits = 1;
+        while (pos_bits < 48 && (db->n >> pos_bits)) ++pos_bits;
+        while (slot_bits < 16 && ((uint64_t)(sb.nbins / sb.bins_per_pattern - 1) >> slot_bits)) ++slot_bits;
+        const bool pack = pos_bits + slot_bits < 56;
+        size_t hsort_bytes = 0;
+        if (!huge.empty())
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, hsort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                     (int)nhuge, 0, pack ? (int)(pos_bits + slot_bits) : 64, s));
+        if (whole)
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                     (int)total, 0, 64, s));
+                                                     (int)total, 0, pack ? (int)(pos_bits + slot_bits) : 64, s));
         if (!inline_off)
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)sb.nbins, s));
         (void)hipGetLastError();   // rocPRIM's stale capture status, size queries too (see the scan below)
         Carve c;
         const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
-        const size_t o_uns = lds ? 0 : c.take(total * sizeof(uint64_t));
-        const size_t o_tmp = lds ? 0 : c.take(sort_bytes);
         const size_t o_scan = c.take(scan_bytes);
         const size_t o_big = c.take(inline_off ? 0 : (size_t)sb.nbins * sizeof(uint32_t));   // bin lists
+        const size_t o_hb = c.take(huge.size() * sizeof(HugeBin));
+        const size_t o_hin = c.take(nhuge * sizeof(uint64_t));
+        const size_t o_hout = c.take(nhuge * sizeof(uint64_t));
+        const size_t o_hsort = c.take(hsort_bytes);
+        const size_t o_uns = c.take(whole ? total * sizeof(uint64_t) : 0);
+        const size_t o_tmp = c.take(sort_bytes);
         uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
         if (!inline_off) {
@@ -461,13 +616,26 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             // the next launch check does not report it
             (void)hipGetLastError();
         }
-        if (lds && inline_off) {
+        if (whole) {
+            uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
+            hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh, unsorted,
+                               pack ? pos_bits : 0u);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
+                                                     pack ? (int)(pos_bits + slot_bits) : 64, s));
+            (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
+            if (pack) {
+                hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
+                                   pos_bits);
+                HIPCHK(hipGetLastError());
+            }
+        } else if (inline_off) {
             auto kern = maxc > LDS_SORT_CAP ? k_sort_bins<LDS_SORT_CAP_MAX> : k_sort_bins<LDS_SORT_CAP>;
             hipLaunchKernelGGL(kern, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, (const uint64_t*)nullptr, sh,
                                h->keys, slot_len, h->lens, (uint32_t*)nullptr, 0u, (uint64_t*)nullptr,
                                (const uint32_t*)nullptr, sb.nbins);
             HIPCHK(hipGetLastError());
-        } else if (lds) {
+        } else {
             // many bins (a large batch: patterns x segments), each pass a
             // size class: a bin's sort is a short chain of dependent loads, so
             // the small-bin pass (most bins, 2 KB of LDS) keeps many blocks
@@ -484,42 +652,38 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             HIPCHK(hipGetLastError());
             std::vector<uint32_t> lists(mid);
             lists.insert(lists.end(), big.begin(), big.end());
+            if (!huge.empty()) {
+                HugeBin* d_hb = reinterpret_cast<HugeBin*>(base + o_hb);
+                uint64_t* hin = reinterpret_cast<uint64_t*>(base + o_hin);
+                uint64_t* hout = reinterpret_cast<uint64_t*>(base + o_hout);
+                const uint32_t pb = pack ? pos_bits : 0u;
+                HIPCHK(hipMemcpyAsync(d_hb, huge.data(), huge.size() * sizeof(HugeBin), hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(k_gather_huge, dim3((uint32_t)huge.size()), dim3(1024), 0, s, sb.out, sh, d_hb, hin, pb);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_hsort, hsort_bytes, hin, hout, (int)nhuge, 0,
+                                                         pack ? (int)(pos_bits + slot_bits) : 64, s));
+                (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
+                hipLaunchKernelGGL(k_scatter_huge, dim3((uint32_t)huge.size()), dim3(1024), 0, s, hout, sh, d_hb,
+                                   h->keys, slot_len, h->lens, pb);
+                HIPCHK(hipGetLastError());
+                if (lists.empty()) HIPCHK(hipStreamSynchronize(s));   // `huge` (pageable) was read by the copy
+            }
             if (!lists.empty()) {
                 uint32_t* d_lists = reinterpret_cast<uint32_t*>(base + o_big);
                 HIPCHK(hipMemcpyAsync(d_lists, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, s));
+                static_assert(256 * 16 == LDS_SORT_CAP_MAX && 512 * 32 == LDS_SORT_CAP_HUGE, "radix bin shapes");
                 if (!mid.empty())
-                    hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_MAX, 256>), dim3((uint32_t)mid.size()), dim3(256), 0, s,
-                                       sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
-                                       (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_lists,
-                                       (uint32_t)mid.size());
+                    hipLaunchKernelGGL((k_radix_bins<256, 16>), dim3((uint32_t)mid.size()), dim3(256), 0, s, sb.out,
+                                       sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
+                                       (const uint32_t*)d_lists, (uint32_t)mid.size());
                 if (!big.empty())
-                    hipLaunchKernelGGL((k_sort_bins<LDS_SORT_CAP_HUGE, 1024>), dim3((uint32_t)big.size()), dim3(1024), 0,
-                                       s, sb.out, sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
-                                       (uint32_t*)nullptr, 0u, (uint64_t*)nullptr, (const uint32_t*)d_lists + mid.size(),
-                                       (uint32_t)big.size());
+                    hipLaunchKernelGGL((k_radix_bins<512, 32>), dim3((uint32_t)big.size()), dim3(512), 0, s, sb.out,
+                                       sb.cnt, (const uint64_t*)d_off, sh, h->keys, slot_len, h->lens,
+                                       (const uint32_t*)d_lists + mid.size(), (uint32_t)big.size());
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipStreamSynchronize(s));   // `lists` (pageable) was read by the copy
             }
             if (lens_done) *lens_done = slot_len != nullptr;
-        } else {
-            uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
-            // sort only the significant bits: positions < 2^pos_bits, pattern
-            // slots < 2^slot_bits
-            uint32_t pos_bits = 1, slot_bits = 1;
-            while (pos_bits < 48 && (db->n >> pos_bits)) ++pos_bits;
-            while (slot_bits < 16 && ((uint64_t)(sb.nbins / sb.bins_per_pattern - 1) >> slot_bits)) ++slot_bits;
-            const bool pack = pos_bits + slot_bits < 56;
-            hipLaunchKernelGGL(k_gather_bins, dim3(sb.nbins), dim3(256), 0, s, sb.out, sb.cnt, d_off, sh,
-                               unsorted, pack ? pos_bits : 0u);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
-                                                     pack ? (int)(pos_bits + slot_bits) : 64, s));
-            (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
-            if (pack) {
-                hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
-                                   pos_bits);
-                HIPCHK(hipGetLastError());
-            }
         }
     } catch (...) {
         pool_put(h->device, h->keys, h->keys_cap);
@@ -632,6 +796,14 @@ __device__ inline bool rep_keep(const RepArgs& a, uint64_t key) {
     return !(s > 0 && tv_header(a.tv, s - 1) && tv_raw(a.tv, s) == (uint8_t)'\n');
 }
 
+// region_near for a candidate's start, false past the text: a speculative
+// list that will be discarded holds stale keys, whose positions may lie
+// beyond the region tables
+__device__ inline bool rep_near(const RepArgs& a, uint64_t key) {
+    const uint64_t s = key & POS_MASK;
+    return s < a.tv.n && region_near(a.tv.reg, s);
+}
+
 // '^' passes at a line start or at R (recCheckLeftContext 0x402170): the
 // region start is R when a region's search begins
 __device__ inline bool rep_line_start(const RepArgs& a, uint64_t s) {
@@ -690,7 +862,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (len[u]) {
-                    const bool nr = region_near(a.tv.reg, key[u] & POS_MASK);
+                    const bool nr = rep_near(a, key[u]);
                     if (rep_valid(a, key[u], len[u], nr)) m = umax64(m, rep_val(a, key[u], len[u], nr));
                 }
         }
@@ -713,7 +885,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint64_t s = key & POS_MASK;
-            bool ok = rep_valid(a, key, a.lens[i], region_near(a.tv.reg, s));
+            bool ok = rep_valid(a, key, a.lens[i], rep_near(a, key));
             if (ok && (a.flags & PM_ANCHOR_START)) ok = rep_line_start(a, s);
             ok = ok && rep_keep(a, key);
             a.acc[i] = ok ? 1 : 0;
@@ -729,23 +901,52 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
     carry = block_max(carry, red);
     uint64_t own = 0;   // kept candidates of this chunk found by this thread's walks
-    for (uint64_t base = b0; base < b1; base += REP_T) {
-        const uint64_t i = base + threadIdx.x;
-        uint64_t key = 0, val = 0;
-        uint32_t len = 0;
-        bool valid = false;
-        if (i < b1) {
-            key = a.keys[i];
-            len = a.lens[i];
-            const bool nr = region_near(a.tv.reg, key & POS_MASK);
-            valid = rep_valid(a, key, len, nr);
-            if (valid) val = rep_val(a, key, len, nr);
-            else a.acc[i] = 0;
+    // A tile is REP_T * RW candidates, RW consecutive ones per thread: the
+    // block's serial chain of tiles (a load, the scan's exchange, two
+    // barriers each) is RW times shorter.  The next tile's loads are in
+    // flight while a tile is scanned.
+    constexpr int RW = 4;
+    constexpr uint64_t TT = (uint64_t)REP_T * RW;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t nkey[RW];
+    uint32_t nlen[RW];
+#pragma unroll
+    for (int u = 0; u < RW; ++u) {
+        const uint64_t i = b0 + (uint64_t)threadIdx.x * RW + u;
+        nkey[u] = i < b1 ? a.keys[i] : 0ull;
+        nlen[u] = i < b1 ? a.lens[i] : 0u;
+    }
+    for (uint64_t base = b0; base < b1; base += TT) {
+        const uint64_t i0 = base + (uint64_t)threadIdx.x * RW;
+        uint64_t key[RW], val[RW];
+        uint32_t len[RW];
+        bool valid[RW];
+#pragma unroll
+        for (int u = 0; u < RW; ++u) {
+            key[u] = nkey[u];
+            len[u] = nlen[u];
+            const uint64_t ni = i0 + TT + u;
+            nkey[u] = ni < b1 ? a.keys[ni] : 0ull;
+            nlen[u] = ni < b1 ? a.lens[ni] : 0u;
         }
-        // exclusive max-scan over the tile: within each wave by shuffles,
-        // then the maxima of the waves before it (one LDS exchange)
-        const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        uint64_t incl = val;
+        uint64_t tmax = 0;   // the thread's candidates' running maximum
+#pragma unroll
+        for (int u = 0; u < RW; ++u) {
+            val[u] = 0;
+            valid[u] = false;
+            if (i0 + u < b1) {
+                const bool nr = rep_near(a, key[u]);
+                valid[u] = rep_valid(a, key[u], len[u], nr);
+                if (valid[u]) val[u] = rep_val(a, key[u], len[u], nr);
+                else a.acc[i0 + u] = 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RW; ++u) tmax = umax64(tmax, val[u]);
+        // exclusive max-scan over the tile: the threads' maxima within each
+        // wave by shuffles, then the maxima of the waves before it (one LDS
+        // exchange)
+        uint64_t incl = tmax;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint64_t o = shfl_up64(incl, d);
@@ -761,7 +962,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         }
         __syncthreads();   // wmax is rewritten by the next tile
         const uint64_t below = shfl_up64(incl, 1);
-        const uint64_t excl = umax64(carry, lane ? umax64(below, pre) : pre);
+        uint64_t excl = umax64(carry, lane ? umax64(below, pre) : pre);
         carry = umax64(carry, tile_max);
         // '^': a start is reported only at a line start or exactly at the
         // resume point R (recCheckLeftContext 0x402170), so a candidate that
@@ -769,35 +970,51 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         // (with '^' a candidate at a region start is a head: R restarts
         // there -- the file's first position included, R = 0 before any
         // report, key == excl == 0 for pattern 0)
-        if (!valid ||
-            (anch ? key < excl || (key == excl && (key & POS_MASK) != 0 && !rep_region_start(a, key & POS_MASK))
-                  : key < excl))
-            continue;   // not a head: its head's walk writes it
-        // head: every earlier report ends before it (R < its start)
-        const uint64_t s0 = key & POS_MASK;
-        const bool first = !anch || rep_line_start(a, s0);
-        uint8_t kept = first && rep_keep(a, key) ? 1 : 0;
-        a.acc[i] = kept;
-        own += kept;
-        uint64_t R = first ? s0 + len : s0 - 1, run = val;   // s0 - 1: below every start of the cluster
-        for (uint64_t j = i + 1; j < total; ++j) {
-            const uint64_t kj = a.keys[j];
-            if (anch ? kj > run || (kj == run && rep_region_start(a, kj & POS_MASK)) : kj >= run) break;  // the next head
-            const uint32_t lj = a.lens[j];
-            kept = 0;
-            const bool nj = region_near(a.tv.reg, kj & POS_MASK);
-            if (rep_valid(a, kj, lj, nj)) {
-                const uint64_t sj = kj & POS_MASK;
-                if (sj >= R && (!anch || sj == R || rep_line_start(a, sj))) {
-                    R = sj + lj;
-                    kept = rep_keep(a, kj) ? 1 : 0;
+        bool head[RW];
+#pragma unroll
+        for (int u = 0; u < RW; ++u) {
+            head[u] = valid[u] && !(anch ? key[u] < excl || (key[u] == excl && (key[u] & POS_MASK) != 0 &&
+                                                              !rep_region_start(a, key[u] & POS_MASK))
+                                         : key[u] < excl);
+            excl = umax64(excl, val[u]);
+        }
+        // the next candidate a head: the walk below would stop at it (its
+        // running maximum is this head's end), so it is skipped -- the
+        // common case, the walk's dependent loads are not paid.  The next
+        // thread's first candidate comes by a shuffle (lane 63: the walk).
+        const bool nh0 = __shfl_down(head[0] ? 1 : 0, 1, 64) != 0 && lane < 63;
+#pragma unroll
+        for (int u = 0; u < RW; ++u) {
+            if (!head[u]) continue;   // not a head: its head's walk writes it
+            const uint64_t i = i0 + u;
+            // head: every earlier report ends before it (R < its start)
+            const uint64_t s0 = key[u] & POS_MASK;
+            const bool first = !anch || rep_line_start(a, s0);
+            uint8_t kept = first && rep_keep(a, key[u]) ? 1 : 0;
+            a.acc[i] = kept;
+            own += kept;
+            const bool next_head = u + 1 < RW ? head[u + 1 < RW ? u + 1 : u] : nh0;
+            if (!anch && next_head) continue;
+            uint64_t R = first ? s0 + len[u] : s0 - 1, run = val[u];   // s0 - 1: below every start of the cluster
+            for (uint64_t j = i + 1; j < total; ++j) {
+                const uint64_t kj = a.keys[j];
+                if (anch ? kj > run || (kj == run && rep_region_start(a, kj & POS_MASK)) : kj >= run) break;  // the next head
+                const uint32_t lj = a.lens[j];
+                kept = 0;
+                const bool nj = rep_near(a, kj);
+                if (rep_valid(a, kj, lj, nj)) {
+                    const uint64_t sj = kj & POS_MASK;
+                    if (sj >= R && (!anch || sj == R || rep_line_start(a, sj))) {
+                        R = sj + lj;
+                        kept = rep_keep(a, kj) ? 1 : 0;
+                    }
+                    run = umax64(run, rep_val(a, kj, lj, nj));
                 }
-                run = umax64(run, rep_val(a, kj, lj, nj));
-            }
-            a.acc[j] = kept;
-            if (kept) {
-                if (j < b1) ++own;
-                else atomicAdd(&a.bcnt[j / C], 1u);   // a cluster running into a later chunk (rare)
+                a.acc[j] = kept;
+                if (kept) {
+                    if (j < b1) ++own;
+                    else atomicAdd(&a.bcnt[j / C], 1u);   // a cluster running into a later chunk (rare)
+                }
             }
         }
     }
@@ -822,11 +1039,14 @@ __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
     }
     const uint64_t b0 = blockIdx.x * C, b1 = umin64(total, b0 + C);
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t nacc = b0 + threadIdx.x < b1 ? a.acc[b0 + threadIdx.x] : 0;   // the next tile's flags in flight
     for (uint64_t base = b0; base < b1; base += REP_T) {
         const uint64_t i = base + threadIdx.x;
-        const bool keep = i < b1 && (a.acc[i] & 1);   // bit 1: a cluster head (k_es_walk)
+        const bool keep = i < b1 && (nacc & 1);   // bit 1: a cluster head (k_es_walk)
+        nacc = i + REP_T < b1 ? a.acc[i + REP_T] : 0;
         // the kept entries before this one: a wave ballot, then the counts
-        // of the waves before it (one LDS exchange)
+        // of the waves before it (one LDS exchange).  (Four consecutive
+        // entries per thread measured slower: 251 vs 141 us on configs[4].)
         const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
         if (lane == 0) scan[w] = (uint32_t)__builtin_popcountll(m);
         __syncthreads();

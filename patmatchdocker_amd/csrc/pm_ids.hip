@@ -81,12 +81,15 @@ __device__ __forceinline__ void dma_dword(u64 ga, u32 lds) {
 // the line just fetched, so the exception plane costs HBM bytes only for
 // flagged rows while every step still issues 4 DMAs (the vmcnt waits count
 // them).
-__device__ __forceinline__ void dma_word(const uint2* p, long dbo, u32 lds, bool ex) {
-    const u64 ga = (u64)p, ge = ex ? (u64)(p + dbo) : ga;
-    dma_dword(ga, lds);
-    dma_dword(ga + 4ull, lds + 256u);
-    dma_dword(ge, lds + 512u);
-    dma_dword(ge + 4ull, lds + 768u);
+// The planes' {hi, lo} may come from another address (ph, the lane-0 word
+// every lane loads when only lane 0 needs it) and land elsewhere (lhl, a
+// keep slot: same {hi, lo} offsets) than the exception dwords (lex).
+__device__ __forceinline__ void dma_word(const uint2* ph, const uint2* p, long dbo, u32 lhl, u32 lex, bool ex) {
+    const u64 ga = (u64)ph, ge = ex ? (u64)(p + dbo) : ga;
+    dma_dword(ga, lhl);
+    dma_dword(ga + 4ull, lhl + 256u);
+    dma_dword(ge, lex);
+    dma_dword(ge + 4ull, lex + 256u);
 }
 __device__ inline void push(const IArgs& a, u64 pos) {
     const u32 bin = (u32)(pos >> a.pos_shift);
@@ -147,6 +150,17 @@ int subset_table(int s) {
 // at 32 / 64 / 128 (round 4, tools/gpu_idsab.sh).
 int ids_wpl(int) { return 32; }
 
+// PM_IDS_KEEP=1: the warm-up words stay in LDS for the lane that owns them
+// (WPL = 32: lane c's warm-up column is lane c + 1's own, read 32 steps
+// later) instead of being read again from memory.  Measured slower and off
+// by default: its 8 KB of LDS per wave leave 3 workgroups per CU instead of
+// 4, and the kernel took 1.84 vs 1.58 ms per strand (-k 2ids 2,056 vs 2,262
+// Gbases/s, profiles/r05k_ids_keep.txt).
+bool ids_keep() {
+    const char* e = getenv("PM_IDS_KEEP");
+    return e && e[0] == '1';
+}
+
 // The kernel's source and its cache signature (everything the source
 // depends on); with want_source false only the signature (a query's cache
 // lookup: generating the source cost ~0.1 ms per query).
@@ -172,7 +186,8 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     }
     std::ostringstream sg;
     const int WPL = ids_wpl(WU);
-    sg << "ids11:" << WPL << ":" << m << ":" << k << ":" << sp.errs << ":";
+    const bool keep = sp.keep && WPL == 32 && WU >= 1;   // lane c's warm-up column is lane c + 1's
+    sg << "ids12:" << WPL << ":" << (keep ? 1 : 0) << ":" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) {
         sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
         if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
@@ -246,6 +261,8 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     // one step over word t = `tv` of the lane's stream column, whose plane /
     // exception words are `vv` / `ev` and whose plane word is at pointer `pv`;
     // `emit`: t < 32 (the lane's own column) -- report starts
+    // kept_phase: own words t < WU, which the lane to the left kept (keep)
+    bool kept_phase = false;
     auto step = [&](std::ostringstream& o, char src, char dst, const std::string& tv, const std::string& vv,
                     const std::string& pv, bool emit) {
         const std::string in = "            ";
@@ -255,7 +272,17 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
         // still be in flight), then the DMA DEPTH steps ahead goes into the
         // slot the previous step read
         o << in << "    asm volatile(\"s_waitcnt vmcnt(" << 4 * (IDS_DEPTH - 1) << ")\" ::: \"memory\");\n";
-        o << in << "    const uint2 v = make_uint2(ring[sl * 256u + col], ring[sl * 256u + 64u + col]);\n";
+        // the word's planes: the ring slot, or (keep) the warm-up word's keep
+        // slot / the kept own word of the lane to the left
+        if (!keep)
+            o << in << "    const u32* vs_ = ring + sl * 256u + col;\n";
+        else if (!emit)
+            o << in << "    const u32* vs_ = keep + ((u32)(" << tv << ") - WPL) * 128u + col;\n";
+        else if (kept_phase)
+            o << in << "    const u32* vs_ = col ? keep + (u32)(" << tv << ") * 128u + col - 1u : ring + sl * 256u;\n";
+        else
+            o << in << "    const u32* vs_ = ring + sl * 256u + col;\n";
+        o << in << "    const uint2 v = make_uint2(vs_[0], vs_[64]);\n";
         o << in << "    issue(qs + IDS_DEPTH, snx);\n";
         if (emit)
             o << in << "    const uint2* " << pv << " = pm + (long)(((" << tv << ") & 31) * 64 + ((" << tv << ") >> 5));\n";
@@ -313,9 +340,14 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     std::ostringstream o;
     o << kIdsCommon;
     o << "#define WU " << WU << "\n";
-    // 4 workgroups per CU: <= 128 VGPRs, 4 waves per SIMD (staging each
-    // tile in LDS by LDS-DMA first measured no faster, round 2)
-    o << "#define IDS_WG 4\n#define IDS_DEPTH " << IDS_DEPTH << "\n#define IDS_SLOTS " << IDS_DEPTH + 1 << "\n";
+    // keep: the warm-up words' planes stay in LDS for the lane that owns
+    // them (ids_keep_ok); 4 workgroups per CU without it (<= 128 VGPRs, 4
+    // waves per SIMD; staging each tile in LDS by LDS-DMA first measured no
+    // faster, round 2), as many as the keep slots leave LDS for with it
+    const int per_wg = 4 * ((IDS_DEPTH + 1) * 1024 + (keep ? WU * 512 : 0));
+    const int wg = keep ? std::max(1, std::min(4, (160 << 10) / per_wg)) : 4;
+    o << "#define IDS_KEEP " << (keep ? 1 : 0) << "\n#define IDS_KEEP_WORDS " << (keep ? WU : 1) << "\n";
+    o << "#define IDS_WG " << wg << "\n#define IDS_DEPTH " << IDS_DEPTH << "\n#define IDS_SLOTS " << IDS_DEPTH + 1 << "\n";
     o << "#define WPL " << WPL << "u\n#define TPW " << WPL / 32 << "u\n#define LPT " << 2048 / WPL << "u\n";
     o << "#define STRIDE_MASK " << (WPL == 32 ? "0xffffffffffffffffull" : WPL == 64 ? "0x5555555555555555ull"
                                                                                       : "0x1111111111111111ull") << "\n";
@@ -332,10 +364,16 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
 // adds the halo's bit u).
 extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) {   // IDS_WG workgroups per CU
     __shared__ __attribute__((aligned(16))) u32 ids_ring[4][IDS_SLOTS * 256];   // per wave: {hi, lo, brk, oth} x 64 lanes per slot
+    // per wave (IDS_KEEP): the warm-up words' {hi, lo} x 64 lanes, slot u =
+    // warm-up word u -- lane c's warm-up word u is lane c + 1's own word u,
+    // which lane c + 1 reads here 32 steps later instead of from memory
+    __shared__ __attribute__((aligned(16))) u32 ids_keep[4][IDS_KEEP_WORDS * 128];
     const u32 col = threadIdx.x & 63;
     const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     u32* const ring = ids_ring[wid];
     const u32 rbase = __builtin_amdgcn_readfirstlane((u32)reinterpret_cast<u64>(ring));   // its LDS byte address
+    u32* const keep = ids_keep[wid];
+    const u32 kbase = __builtin_amdgcn_readfirstlane((u32)reinterpret_cast<u64>(keep));
     const u64 wave = (u64)blockIdx.x * 4u + wid, nwaves = gridDim.x * 4ull;
     const long dbo = a.bo - a.hl;   // the exception plane has the planes' layout
     const u64 ngroups = (a.ntiles + TPW - 1) / TPW;
@@ -382,7 +420,18 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
             const bool ex2 = w2 ? exw(u2) : (o2 && exo((u32)t2));
             const uint2* g2 = w2 ? pn + (long)((u2 & 31u) * s1 + (u2 >> 5) * s2)
                                  : o2 ? pm + (long)((t2 & 31) * 64 + (t2 >> 5)) : tb;
-            dma_word(g2, dbo, rbase + slot * 1024u, ex2);
+            const u32 lr = rbase + slot * 1024u;
+            if (IDS_KEEP && w2) {            // a warm-up word: its planes into keep slot u2
+                dma_word(g2, g2, dbo, kbase + u2 * 512u, lr + 512u, ex2);
+            } else if (IDS_KEEP && o2 && t2 < WU) {
+                // an own word the lane to the left kept: only lane 0 (whose
+                // word nobody kept) needs the planes, the others load lane
+                // 0's word (one line)
+                const uint2* g0 = tb + (long)((t2 & 31) * 64 + (t2 >> 5));
+                dma_word(col ? g0 : g2, g2, dbo, lr, lr + 512u, ex2);
+            } else {
+                dma_word(g2, g2, dbo, lr, lr + 512u, ex2);
+            }
         };
         // the first IDS_DEPTH words go in flight now (the previous group's
         // DMAs have all landed: the slots are free)
@@ -416,7 +465,13 @@ extern "C" __global__ __launch_bounds__(256, IDS_WG) void pm_ids_rev(IArgs a) { 
         o << "        }\n";
     };
     phase(WPL - 1 + WU, WU, false);   // warm-up: t = WPL + WU - 1 .. WPL
-    phase(WPL - 1, WPL, true);        // own column: t = WPL - 1 .. 0
+    if (keep) {                       // own column: t = WPL - 1 .. WU, then the kept words WU - 1 .. 0
+        phase(WPL - 1, WPL - WU, true);
+        kept_phase = true;
+        phase(WU - 1, WU, true);
+    } else {
+        phase(WPL - 1, WPL, true);    // own column: t = WPL - 1 .. 0
+    }
     // the last tile's look-ahead DMAs land before the wave ends (its LDS is
     // released with the workgroup)
     o << "    }\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}\n";
@@ -436,15 +491,17 @@ bool ids_rev_scan(pm_db* db, const IdsSpec& sp, const Sink& sink, hipStream_t s,
     if (db->alphabet != PM_ALPHA_NUC || sp.m * (sp.k + 1) > IDS_MAX_REGS || sp.m > 64) return false;
     const int WU = sp.m + ((sp.errs & PM_ERR_INS) ? sp.k : 0) - 1;
     if (WU > std::min(HALO - 1, ids_wpl(WU))) return false;   // the warm-up must fit the next lane column or the halo
+    IdsSpec spk = sp;
+    spk.keep = ids_keep();
     std::string sig;
-    gen_ids_source(sp, &sig, false);
+    gen_ids_source(spk, &sig, false);
     hipFunction_t fn;
     {
         std::lock_guard<std::mutex> lk(g_ids_mu);
         auto key = std::make_pair(db->device, sig);
         auto it = g_ids_cache.find(key);
         if (it == g_ids_cache.end()) {
-            std::vector<char> code = hiprtc_compile(gen_ids_source(sp, &sig));
+            std::vector<char> code = hiprtc_compile(gen_ids_source(spk, &sig));
             IdsKernel kk;
             HIPCHK(hipModuleLoadData(&kk.module, code.data()));
             HIPCHK(hipModuleGetFunction(&kk.fn, kk.module, "pm_ids_rev"));
@@ -484,6 +541,7 @@ extern "C" int pm_ids_jit_compile(int m, const uint64_t* byte_mask, int k, int e
         require((errs & ~(PM_ERR_INS | PM_ERR_DEL | PM_ERR_SUB)) == 0, "bad error-type mask");
         // the start configuration of a plain class sequence, as scan_nfa builds it
         IdsSpec sp{m, k, errs, byte_mask, nullptr, {}, {}, 0};
+        sp.keep = ids_keep();
         const uint64_t last = 1ull << (m - 1);
         uint64_t S = 0;
         for (int j = 0; j <= k; ++j) {

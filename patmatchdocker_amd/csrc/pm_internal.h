@@ -504,6 +504,7 @@ struct IdsSpec {
     const uint64_t* d_bmask;     // the same table on the device ('\n' accepted by none)
     uint64_t rev_pre[PM_MAX_K + 1], rev_ins[PM_MAX_K + 1];   // the injected start config (scan_nfa)
     int pattern_id;
+    bool keep = false;           // (set by ids_rev_scan) the warm-up words' planes kept in LDS
 };
 bool ids_rev_scan(pm_db* db, const IdsSpec& spec, const Sink& sink, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b);
 

@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 
 MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
-ROUND = "r04"   # committed PMC traffic run (profiles/r04_traffic.json)
+ROUND = "r05"   # committed PMC traffic run (profiles/r05_traffic.json)
 
 
 def parse_args():

@@ -2004,9 +2004,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // configs[4] at 12.5 Gbp: 16 waves, 256 segments -- one round of
             // verify blocks and 64 Ki (pattern, segment) bins; measured 9.25,
             // 8.73, 10.6 ms per step at 8, 16, 32 waves)
-            // (PM_BATCH_SEG_TILES: the segment size in tiles, for A/B runs)
-            static const uint64_t seg_tiles = getenv("PM_BATCH_SEG_TILES") ? strtoull(getenv("PM_BATCH_SEG_TILES"), nullptr, 10) : 752;
-            const uint64_t wpo = std::min<uint64_t>(BATCH_MAX_WPO, std::max<uint64_t>(1, (seg_tiles + tpw / 2) / tpw));
+            // (round 5: ~376-tile segments, two verify blocks per CU,
+            // measured the same, 8.67 vs 8.69 ms)
+            const uint64_t wpo = std::min<uint64_t>(BATCH_MAX_WPO, std::max<uint64_t>(1, (752 + tpw / 2) / tpw));
             const uint64_t nout = (nwaves + wpo - 1) / wpo;
             std::vector<uint32_t> slot_caps(n_patterns, 64);
             // candidates per wave: ~1 % of the positions at configs[4]

@@ -44,6 +44,9 @@ for name in ("bench", "bench100", "bench_ids", "bench_cfg4", "configs"):
 for d in ("prof", "prof100", "prof_ids", "prof_cfg4"):
     copy(os.path.join(root, d, "run_kernel_stats.csv"), "%s_%s_kernel_stats.csv" % (rnd, d))
 copy(os.path.join(root, "prof", "run_kernel_trace.csv"), "%s_prof_kernel_trace.csv" % rnd)
+copy(os.path.join(root, "cfg3", "run_kernel_stats.csv"), "%s_cfg3_kernel_stats.csv" % rnd)
+copy(os.path.join(root, "cfg3", "run_kernel_trace.csv"), "%s_cfg3_kernel_trace.csv" % rnd)
+copy(os.path.join(root, "cfg3.log"), "%s_cfg3_query_ms.txt" % rnd)
 
 lin = pmc(["p1", "p2", "p3", "p4"], "pm_linear_jit")
 ids = pmc(["q1", "q2", "q3", "q4"], "pm_ids_rev")

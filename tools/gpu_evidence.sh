@@ -5,6 +5,7 @@
 #   PMC passes (one counter group per run) on pm_linear_jit and pm_ids_rev
 #   FETCH_SIZE calibration on known-byte reads (tools/micro/calib_read)
 #   configs[0]/[1]/[3] timings with bit-exact checks (tools/config_times.py)
+#   a kernel trace of configs[3]'s queries (tools/cfg3_prof.py)
 # then: python3 tools/evidence_summary.py gpurun_out/<tag> <round> (host side)
 # Usage: bash tools/gpu_evidence.sh <tag>
 set -o pipefail
@@ -38,4 +39,5 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
 done
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/cal" -o run -- ./tools/micro/calib_read 4096 > "$out/cal.json" 2> "$out/cal.err" || die calibration "$out/cal.err"
 timeout -k 10 300 python tools/config_times.py > "$out/configs.json" 2> "$out/configs.err" || die configs "$out/configs.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/cfg3" -o run -- python3 tools/cfg3_prof.py > "$out/cfg3.log" 2>&1 || die cfg3 "$out/cfg3.log"
 echo evidence-done

@@ -440,7 +440,18 @@ struct EeWalk {
         uint64_t fin, alive;
         uint64_t R[KR + 1][WB];
         uint64_t t1[WB], t2[WB];
+        uint64_t Bc[WB], Ac[WB];   // the step character's table words (ba)
     };
+    // the table words of character c (loaded a step ahead by the phases)
+    __device__ __forceinline__ void ba(const EePart& V, uint8_t c, uint64_t (&B)[WB], uint64_t (&A)[WB]) const {
+        const uint64_t* pB = tab + V.o_B + (size_t)c * V.pw;
+        const uint64_t* pA = tab + V.o_A + (size_t)c * V.pw;
+#pragma unroll
+        for (int w = 0; w < WB; ++w) {
+            B[w] = w < V.pw ? pB[w] : 0ull;
+            A[w] = w < V.pw ? pA[w] : 0ull;
+        }
+    }
 
     __device__ __forceinline__ void rows_init(Rows& s, const EePart& V, int kmax) const {
         s.W = V.pw;
@@ -461,9 +472,9 @@ struct EeWalk {
             if (S->errs & PM_ERR_DEL) close(s.R[j], s.W, V);
         }
     }
-    __device__ __forceinline__ void row0(Rows& s, const EePart& V, uint8_t c, uint64_t inj) const {
-        const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
-        const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
+    __device__ __forceinline__ void row0(Rows& s, const EePart& V, uint64_t inj) const {
+        const uint64_t* B = s.Bc;
+        const uint64_t* A = s.Ac;
         uint64_t carry = inj;
 #pragma unroll
         for (int w = 0; w < WB; ++w) {
@@ -477,9 +488,9 @@ struct EeWalk {
 #pragma unroll
         for (int w = 0; w < WB; ++w) s.R[0][w] = w < s.W ? s.t2[w] : 0ull;
     }
-    __device__ __forceinline__ void rowj(Rows& s, const EePart& V, int j, uint8_t c, uint64_t inj) const {
-        const uint64_t* B = tab + V.o_B + (size_t)c * V.pw;
-        const uint64_t* A = tab + V.o_A + (size_t)c * V.pw;
+    __device__ __forceinline__ void rowj(Rows& s, const EePart& V, int j, uint64_t inj) const {
+        const uint64_t* B = s.Bc;
+        const uint64_t* A = s.Ac;
         uint64_t dc = 0, sc = inj, mc = inj;
         uint64_t nw[WB];
 #pragma unroll
@@ -562,9 +573,14 @@ struct EeWalk {
         if (pos != recbeg) {
             uint64_t inj = 1;
             uint8_t c = at(pos - 1);
+            ba(V, c, s.Bc, s.Ac);
             for (int64_t X = pos - 2; X != recbeg - 2; --X) {
+                // the next step's character and table words, read before
+                // this step's rows (off the rows' dependency chain)
                 const uint8_t look = X + 1 != recbeg ? at(X) : (uint8_t)0;
-                row0(s, V, c, inj);
+                uint64_t Bn[WB], An[WB];
+                ba(V, look, Bn, An);
+                row0(s, V, inj);
                 if (fin_of(s.t2, s) && left_ok(X, recbeg)) {
                     start = X;
                     nerr = 0;
@@ -573,7 +589,7 @@ struct EeWalk {
 #pragma unroll
                 for (int j = 1; j <= KR; ++j) {
                     if (j > maxk) break;
-                    rowj(s, V, j, c, inj);
+                    rowj(s, V, j, inj);
                     if (fin_of(s.t2, s) && left_ok(X, recbeg)) {
                         int cc = j;                      // 0x40ec54: walk down
 #pragma unroll
@@ -593,7 +609,11 @@ struct EeWalk {
                 }
                 if (!rows_alive(s, maxk)) break;
                 inj = 0;
-                c = look;
+#pragma unroll
+                for (int w = 0; w < WB; ++w) {
+                    s.Bc[w] = Bn[w];
+                    s.Ac[w] = An[w];
+                }
             }
         }
         if (!found) return false;
@@ -631,11 +651,13 @@ struct EeWalk {
         }
         if (pos != recend) {
             uint64_t inj = 1;
-            uint8_t c = at(pos);
+            ba(V, at(pos), s.Bc, s.Ac);
             for (int64_t Y = pos + 1;; ++Y) {
                 const int64_t q = Y - 1;
                 const uint8_t look = q != recend - 1 ? at(Y) : (uint8_t)0;
-                row0(s, V, c, inj);
+                uint64_t Bn[WB], An[WB];
+                ba(V, look, Bn, An);
+                row0(s, V, inj);
                 if (fin_of(s.t2, s) && right_ok(Y + 1, recend)) {
                     end = Y + 1;
                     return true;
@@ -643,7 +665,7 @@ struct EeWalk {
 #pragma unroll
                 for (int j = 1; j <= KR; ++j) {
                     if (j > maxk) break;
-                    rowj(s, V, j, c, inj);
+                    rowj(s, V, j, inj);
                     if (fin_of(s.t2, s) && right_ok(Y + 1, recend)) {
                         int cc = j;
 #pragma unroll
@@ -662,7 +684,11 @@ struct EeWalk {
                 if (!rows_alive(s, maxk)) break;
                 if (q == recend - 1) break;
                 inj = 0;
-                c = look;
+#pragma unroll
+                for (int w = 0; w < WB; ++w) {
+                    s.Bc[w] = Bn[w];
+                    s.Ac[w] = An[w];
+                }
             }
         }
         if (!found) return false;
@@ -905,30 +931,33 @@ struct EeWalk {
             }
             int64_t nxt = p;
             bool restart = false;
+            // a step's character and its table words come from the step
+            // before (`look` then was the look-ahead), and the next step's
+            // look-ahead is read before this step's arithmetic: the text and
+            // table reads leave the rows' dependency chain
+            uint8_t look = nxt < n ? at(nxt) : c;
+            uint64_t Tc = T[c], TAc = TA[c];
             for (;;) {
                 if (nxt > stop + 1) return false;   // the candidate nxt is past stop
-                uint8_t look = c;
-                if (nxt < n) {
-                    look = at(nxt);
-                    if (look == (uint8_t)'\n') {
-                        p = nxt + 1;
-                        restart = true;
-                        break;
-                    }
+                if (nxt < n && look == (uint8_t)'\n') {
+                    p = nxt + 1;
+                    restart = true;
+                    break;
                 }
+                const uint8_t look2 = nxt + 1 < n ? at(nxt + 1) : look;   // the next step's look-ahead
+                const uint64_t Tl = T[look], TAl = TA[look];
                 uint64_t pold = Rr[0];
-                uint64_t raw0 = ((Rr[0] << 1) | 1) & T[c];
-                if (ta0) raw0 |= Rr[0] & TA[c];
+                uint64_t raw0 = ((Rr[0] << 1) | 1) & Tc;
+                if (ta0) raw0 |= Rr[0] & TAc;
                 uint64_t pnew = xclose(raw0);
                 Rr[0] = pnew;
 #pragma unroll
                 for (int j = 1; j <= KR; ++j) {
                     if (j > k) break;
                     const uint64_t old = Rr[j];
-                    const uint64_t v = (((old << 1) | 1) & T[c]) | (old & TA[c]) | ((pnew | pold) << 1) | pold | 1ull |
-                                       Tr[j];
-                    const uint64_t u = xclose((pold & TA[look]) | (((pold << 1) | 1) & T[look]));
-                    Tr[j] = (u & TA[c]) | ((u << 1) & T[c]);
+                    const uint64_t v = (((old << 1) | 1) & Tc) | (old & TAc) | ((pnew | pold) << 1) | pold | 1ull | Tr[j];
+                    const uint64_t u = xclose((pold & TAl) | (((pold << 1) | 1) & Tl));
+                    Tr[j] = (u & TAc) | ((u << 1) & Tc);
                     Rr[j] = xclose(v);
                     pold = old;
                     pnew = Rr[j];
@@ -936,6 +965,9 @@ struct EeWalk {
                 if ((pick(Rr, k) & fin) && nxt <= stop && check(0, nxt, mb, me)) return true;
                 if (n < nxt + 1) return false;
                 c = look;
+                Tc = Tl;
+                TAc = TAl;
+                look = look2;
                 ++nxt;
             }
             if (!restart) return false;

@@ -240,7 +240,11 @@ __device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t 
 // (6 candidates per thread measured no faster: 8.46 vs 8.39 ms per
 // configs[4] step, round 5)
 constexpr int VU = 4;
+// HASH: the codes' first entry and count from an LDS hash table (one global
+// stage less per candidate than the 4 MB code_off array)
+template <bool HASH>
 __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
+    __shared__ uint64_t s_hash[HASH ? BQ_HASH_SLOTS : 1];
     __shared__ uint32_t cnt_p[BATCH_MAX_P];
     __shared__ uint32_t cap_p[BATCH_MAX_P];
     __shared__ uint64_t base_p[BATCH_MAX_P];
@@ -251,6 +255,8 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
         cap_p[p] = a.slot_cap[p];
         base_p[p] = a.slot_base[p] + (uint64_t)og * a.slot_cap[p];
     }
+    if constexpr (HASH)
+        for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
     const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
     if (threadIdx.x == 0) {
         uint32_t run = 0;
@@ -288,7 +294,21 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             const bool ok = base + u * blockDim.x + threadIdx.x < total;
-            co[u] = ok ? a.code_off[alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u)] : 0u;
+            const uint32_t code = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
+            if constexpr (HASH) {
+                co[u] = 0u;
+                if (ok)   // a candidate's code is present: the probe ends there (an empty slot: none)
+                    for (uint32_t h = bq_hash(code);; h = (h + 1) & (BQ_HASH_SLOTS - 1)) {
+                        const uint64_t sl = s_hash[h];
+                        if (sl == ~0ull) break;
+                        if ((uint32_t)(sl & 0xFFFFFu) == code) {
+                            co[u] = (uint32_t)((sl >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl >> 44);
+                            break;
+                        }
+                    }
+            } else {
+                co[u] = ok ? a.code_off[code] : 0u;
+            }
             lf[u] = ok && e[u].x < a.ntiles ? a.lflag[e[u].x] : 0ull;
         }
 #pragma unroll
@@ -428,12 +448,28 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
         e[1] = plen[p];
         for (int b = 0; b < 4; ++b) e[4 + b] = bi.pmask[(size_t)4 * p + b];   // the second uint4
     }
+    // the verify's hash table of the codes present (LDS): first entry and
+    // count per code, open addressing
+    {
+        std::vector<std::pair<uint32_t, uint32_t>> codes;   // (code, first entry)
+        for (size_t i = 0; i < ents.size(); ++i)
+            if (i == 0 || ents[i].code != ents[i - 1].code) codes.push_back({ents[i].code, (uint32_t)i});
+        if (codes.size() <= BQ_HASH_MAX_CODES && ents.size() < (1u << 24)) {
+            bi.hash.assign(BQ_HASH_SLOTS, ~0ull);
+            for (const auto& cf : codes) {
+                uint32_t h = bq_hash(cf.first);
+                while (bi.hash[h] != ~0ull) h = (h + 1) & (BQ_HASH_SLOTS - 1);
+                bi.hash[h] = (uint64_t)cf.first | (uint64_t)cf.second << 20 | (uint64_t)(bi.code_off[cf.first] & 255u) << 44;
+            }
+        }
+    }
     Carve cv;
     bi.o_table = cv.take(bi.table.size() * 4);
     bi.o_code = cv.take(bi.code_off.size() * 4);
     bi.o_ents = cv.take(std::max<size_t>(bi.ents.size(), BATCH_ENT_WORDS) * 4);
     bi.o_pmask = cv.take(bi.pmask.size() * 4);
     bi.o_popt = cv.take(bi.popt.size() * 4);
+    bi.o_hash = cv.take(bi.hash.size() * 8);
     bi.bytes = cv.off;
     return true;
 }
@@ -443,7 +479,10 @@ void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t n
     // the kernel's own dispatch timestamps (no marker packets)
     hipExtLaunchKernelGGL(k_batch_scan, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_batch_verify, dim3(va.nout), dim3(1024), 0, s, va);
+    // PM_BATCH_HASH=0: the code_off array (A/B)
+    static const bool hash_on = !(getenv("PM_BATCH_HASH") && getenv("PM_BATCH_HASH")[0] == '0');
+    if (va.hash && hash_on) hipLaunchKernelGGL(k_batch_verify<true>, dim3(va.nout), dim3(1024), 0, s, va);
+    else hipLaunchKernelGGL(k_batch_verify<false>, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_batch_fixup, dim3(64), dim3(256), 0, s, va);
     HIPCHK(hipGetLastError());

@@ -282,6 +282,9 @@ __global__ __launch_bounds__(XT_T) void k_xt_heads(XtPrep X, const uint64_t* __r
 
 // one walk: nrgrep's scanner and checkMatch over [R, n), candidates up to
 // `stop`
+// WB: the verify parts' words; SC: the scanner (xt_scanner: one scanner and
+// one inlined checkMatch per kernel)
+template <int WB, int SC>
 struct XtWalk {
     const XtSlot* S;
     const uint64_t* tab;
@@ -313,9 +316,9 @@ struct XtWalk {
     }
 
     // one phase of checkMatch: D from X, then (D << 1 | carry) & B | D & A
-    // and the closure per character (0x411c98 / 0x411eb0)
-    template <int WB>
-    __device__ bool phase(int side, uint64_t pos, uint64_t bound, bool left, uint64_t& out) const {
+    // and the closure per character (0x411c98 / 0x411eb0); the next step's
+    // character and table words are read before the step's arithmetic
+    __device__ __forceinline__ bool phase(int side, uint64_t pos, uint64_t bound, bool left, uint64_t& out) const {
         const int W = S->pw[side], len = S->plen[side];
         const uint64_t fin = 1ull << ((len - 1) & 63);
         const uint64_t* vB = tab + S->o_vB[side];
@@ -325,21 +328,42 @@ struct XtWalk {
         for (int w = 0; w < WB; ++w) D[w] = w < W ? S->vX[side][w] : 0ull;
         uint64_t carry = 1;
         uint64_t p = pos;   // left: the boundary is p; right: p is the last character read + 1
+        uint64_t Bc[WB], Ac[WB];
+        {
+            const uint8_t c0 = p != bound ? (left ? at(p - 1) : at(p)) : (uint8_t)0;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) {
+                Bc[w] = w < W ? vB[(size_t)c0 * W + w] : 0ull;
+                Ac[w] = w < W ? vA[(size_t)c0 * W + w] : 0ull;
+            }
+        }
         for (;;) {
             const bool ok = left ? left_ok(p, bound) : right_ok(p, bound);
-            if ((D[W - 1] & fin) && ok) {
+            uint64_t dl = 0;   // D[W - 1] without a run-time index (no scratch)
+#pragma unroll
+            for (int w = 0; w < WB; ++w)
+                if (w == W - 1) dl = D[w];
+            if ((dl & fin) && ok) {
                 out = p;
                 return true;
             }
             if (p == bound) return false;
-            const uint8_t c = left ? at(p - 1) : at(p);
             p = left ? p - 1 : p + 1;
+            uint64_t Bn[WB], An[WB];
+            {
+                const uint8_t cn = p != bound ? (left ? at(p - 1) : at(p)) : (uint8_t)0;
+#pragma unroll
+                for (int w = 0; w < WB; ++w) {
+                    Bn[w] = w < W ? vB[(size_t)cn * W + w] : 0ull;
+                    An[w] = w < W ? vA[(size_t)cn * W + w] : 0ull;
+                }
+            }
             bool any = false;
 #pragma unroll
             for (int w = 0; w < WB; ++w) {
                 if (w >= W) break;
                 const uint64_t old = D[w];
-                D[w] = (((old << 1) | carry) & vB[(size_t)c * W + w]) | (old & vA[(size_t)c * W + w]);
+                D[w] = (((old << 1) | carry) & Bc[w]) | (old & Ac[w]);
                 any |= D[w] != 0;
                 carry = old >> 63;
             }
@@ -355,11 +379,15 @@ struct XtWalk {
                 borrow = (bi < borrow) | (xx < bi);
             }
             carry = 0;
+#pragma unroll
+            for (int w = 0; w < WB; ++w) {
+                Bc[w] = Bn[w];
+                Ac[w] = An[w];
+            }
         }
     }
 
-    template <int WB>
-    __device__ bool check(uint64_t pos, uint64_t& mb, uint64_t& me) {
+    __device__ __forceinline__ bool check(uint64_t pos, uint64_t& mb, uint64_t& me) {
         const uint64_t rp = S->type == 3 ? pos - 1 : pos;   // 0x411b90
         if (pos == 0 && S->type == 3) return false;
         uint64_t recbeg, recend;
@@ -368,13 +396,13 @@ struct XtWalk {
         uint64_t start = pos;
         if (S->plen[0] == 0) {
             if (!left_ok(pos, recbeg)) return false;
-        } else if (!phase<WB>(0, pos, recbeg, true, start)) {
+        } else if (!phase(0, pos, recbeg, true, start)) {
             return false;
         }
         uint64_t end = pos;
         if (S->plen[1] == 0) {
             if (!right_ok(pos, recend)) return false;
-        } else if (!phase<WB>(1, pos, recend, false, end)) {
+        } else if (!phase(1, pos, recend, false, end)) {
             return false;
         }
         mb = start;
@@ -383,11 +411,10 @@ struct XtWalk {
     }
 
     // the scanners (pm_nrgrep_ext.c); false when no candidate <= stop verifies
-    template <int WB>
     __device__ bool scan(uint64_t stop, uint64_t& mb, uint64_t& me) {
         const uint64_t* T = tab + S->o_T;
         const uint64_t* TA = tab + S->o_TA;
-        if (S->type == 2 && !S->simple) {                // extendedScan 0x4116f0, window
+        if constexpr (SC == 0) {                         // extendedScan 0x4116f0, window
             const uint64_t len = (uint64_t)S->fwd;
             if (n < len) return false;
             const uint64_t limit = n - len;
@@ -414,12 +441,12 @@ struct XtWalk {
                     }
                 }
                 if (dead) continue;
-                if ((D >> 63) && check<WB>(r11, mb, me)) return true;
+                if ((D >> 63) && check(r11, mb, me)) return true;
                 ++r11;
             }
             return false;
         }
-        if (S->type == 2) {                              // simpleScan 0x4166d2, window
+        if constexpr (SC == 1) {                         // simpleScan 0x4166d2, window
             const uint64_t len = (uint64_t)S->len;
             if (n < len) return false;
             const uint64_t r8 = n - len;
@@ -433,16 +460,20 @@ struct XtWalk {
                 }
                 uint64_t c = s0 + len - 1;
                 uint64_t e = len;
+                // the table word of the next character read, a step ahead
+                uint64_t Tn = c > s0 ? T[at(c - 1)] : 0ull;
                 for (;;) {
                     const uint64_t sh = D << 1;
                     --e;
                     --c;
+                    const uint64_t Tc = Tn;
+                    Tn = c > s0 ? T[at(c - 1)] : 0ull;
                     // reading s0 - 1 only meets a shifted-out state
-                    D = sh ? sh & T[at(c)] : 0ull;
+                    D = sh ? sh & Tc : 0ull;
                     if (!D) break;
                 }
                 if (e == 0) {
-                    if (check<WB>(s0, mb, me)) return true;
+                    if (check(s0, mb, me)) return true;
                     ++s0;
                 } else {
                     s0 = c + 1;
@@ -451,7 +482,7 @@ struct XtWalk {
             return false;
         }
         const uint64_t fin = 1ull << (S->len - 1);
-        if (S->simple) {                                 // simpleScan 0x41663d, prefix: the START goes on
+        if constexpr (SC == 2) {                         // simpleScan 0x41663d, prefix: the START goes on
             const uint64_t len = (uint64_t)S->len;
             uint64_t D = ~0ull;
             for (uint64_t q = R; q < n; ++q) {
@@ -459,16 +490,23 @@ struct XtWalk {
                 if (!(D & fin)) {
                     const uint64_t c = q + 1 - len;
                     if (c > stop) return false;
-                    if (check<WB>(c, mb, me)) return true;
+                    if (check(c, mb, me)) return true;
                 }
             }
             return false;
         }
         uint64_t D = 0;                                  // extendedScan 0x41184f, prefix
         bool fresh = true;
+        // the next character and its table words are read a step ahead
+        uint8_t cn = R < n ? at(R) : (uint8_t)0;
+        uint64_t Tn = T[cn], TAn = TA[cn];
         for (uint64_t p = R; p < n; ++p) {
             if (p >= stop) return false;   // the candidate p + 1 is past it
-            const uint8_t c = at(p);
+            const uint8_t c = cn;
+            const uint64_t Tc = Tn, TAc = TAn;
+            cn = p + 1 < n ? at(p + 1) : (uint8_t)0;
+            Tn = T[cn];
+            TAn = TA[cn];
             if (c == (uint8_t)'\n') {
                 fresh = true;
                 continue;
@@ -477,10 +515,10 @@ struct XtWalk {
                 D = 0;
                 fresh = false;
             }
-            D = (D & TA[c]) | (((D << 1) | 1ull) & T[c]);
+            D = (D & TAc) | (((D << 1) | 1ull) & Tc);
             const uint64_t xx = D | S->fF;
             D |= (~(xx - S->fI) ^ xx) & S->fS;
-            if ((D & fin) && check<WB>(p + 1, mb, me)) return true;
+            if ((D & fin) && check(p + 1, mb, me)) return true;
         }
         return false;
     }
@@ -488,7 +526,7 @@ struct XtWalk {
 
 // One thread per cluster head: the printed matches are written in place
 // from the head on (acc bit 0), every other entry of the cluster is cleared.
-template <int WB>
+template <int WB, int SC>
 __global__ __launch_bounds__(WALK_T) void k_xt_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
                                                     const uint64_t* total_d, uint64_t total_h,
                                                     uint8_t* __restrict__ acc, TextView tv) {
@@ -520,7 +558,7 @@ __global__ __launch_bounds__(WALK_T) void k_xt_walk(XtPrep X, uint64_t* __restri
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            XtWalk w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
+            XtWalk<WB, SC> w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             uint64_t stop;
             if (S->max_len >= 0) {
                 // candidates in [first, last + max_len] can print the
@@ -538,7 +576,7 @@ __global__ __launch_bounds__(WALK_T) void k_xt_walk(XtPrep X, uint64_t* __restri
             w.nl_hi = w.next_nl(w.R);
             for (;;) {
                 uint64_t mb = 0, me = 0;
-                if (!w.scan<WB>(stop, mb, me)) break;
+                if (!w.scan(stop, mb, me)) break;
                 if (!xt_header(tv, mb) && nout < nmax) {   // a printed start is one of the cluster's
                     keys[i + nout] = (pid << 48) | mb;
                     lens[i + nout] = (uint32_t)(me - mb);
@@ -571,6 +609,13 @@ __global__ __launch_bounds__(256) void k_xt_count(const uint64_t* total_d, uint6
 
 }  // namespace
 
+int xt_scanner(const Upload& up, size_t o_slot) {
+    XtSlot S;
+    memcpy(&S, up.blob.data() + o_slot, sizeof(S));
+    if (S.type == 2) return S.simple ? 1 : 0;
+    return S.simple ? 2 : 3;
+}
+
 void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* total_d, uint64_t total_h,
                uint8_t* acc, uint32_t* bcnt, uint32_t G, const TextView& tv, hipStream_t s) {
     const uint32_t blocks = 1024;
@@ -580,8 +625,22 @@ void xt_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
         ee_launch(X, keys, lens, total_d, total_h, acc, tv, X.words, s);
     } else {
         hipLaunchKernelGGL(k_xt_heads, dim3(blocks), dim3(XT_T), 0, s, X, keys, total_d, total_h, acc, tv);
-        hipLaunchKernelGGL(k_xt_walk<4>, dim3(blocks), dim3(WALK_T), walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN, s, X,
-                           keys, lens, total_d, total_h, acc, tv);
+        // the verify parts' words and the scanner are template arguments
+        const size_t lds = walk_tab_bytes(X.tab_words) + WALK_T * TC_WIN;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
+        };
+        auto by_sc = [&](auto wb) {
+            constexpr int WB = decltype(wb)::value;
+            switch (X.scanner) {
+                case 0: go(k_xt_walk<WB, 0>); break;
+                case 1: go(k_xt_walk<WB, 1>); break;
+                case 2: go(k_xt_walk<WB, 2>); break;
+                default: go(k_xt_walk<WB, 3>); break;
+            }
+        };
+        if (X.words <= 1) by_sc(std::integral_constant<int, 1>{});
+        else by_sc(std::integral_constant<int, 4>{});
     }
     hipLaunchKernelGGL(k_xt_count, dim3(G), dim3(256), 0, s, total_d, total_h, acc, bcnt);
     HIPCHK(hipGetLastError());

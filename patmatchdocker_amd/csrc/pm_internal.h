@@ -529,9 +529,17 @@ struct BatchIndex {
     std::vector<uint32_t> ents;       // BATCH_ENT_WORDS per (code, pattern) entry, in increasing code order
     std::vector<uint32_t> pmask;      // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
     std::vector<uint32_t> popt;       // [P]: o_p, the indexed piece's offset
-    // device image (ws_batch): table | code_off | ents | pmask | popt
-    size_t o_table = 0, o_code = 0, o_ents = 0, o_pmask = 0, o_popt = 0, bytes = 0;
+    // [BQ_HASH_SLOTS] open-addressing table of the codes present, for the
+    // verify's LDS (empty when there are too many codes): code | first entry
+    // << 20 | entries << 44, ~0 = empty slot
+    std::vector<uint64_t> hash;
+    // device image (ws_batch): table | code_off | ents | pmask | popt | hash
+    size_t o_table = 0, o_code = 0, o_ents = 0, o_pmask = 0, o_popt = 0, o_hash = 0, bytes = 0;
 };
+constexpr uint32_t BQ_HASH_BITS = 14;                      // 16 Ki slots: 128 KB of LDS
+constexpr uint32_t BQ_HASH_SLOTS = 1u << BQ_HASH_BITS;
+constexpr uint32_t BQ_HASH_MAX_CODES = BQ_HASH_SLOTS * 7 / 10;
+__host__ __device__ inline uint32_t bq_hash(uint32_t code) { return (code * 0x9E3779B1u) >> (32 - BQ_HASH_BITS); }
 // one verification entry (two uint4): {p | o_p << 16 | len << 24, length mask
 // (bits 2j + 1), 0, 0}, {mA, mC, mG, mT}
 constexpr int BATCH_ENT_WORDS = 8;
@@ -555,6 +563,7 @@ struct BatchVerifyArgs {
     uint32_t ccap;
     uint32_t* aux;          // the largest candidate count above ccap (0: none)
     const uint32_t* code_off;
+    const uint64_t* hash;   // BatchIndex::hash (null: code_off)
     const uint4* ents;      // two uint4 per entry
     const uint4* pmask;
     const uint32_t* popt;
@@ -1092,7 +1101,7 @@ struct XtPrep {
     int32_t words = 1;            // eextended: the verify parts' widest word count
     int32_t eregular = 0;         // rg: k > 0 (pm_regular.hip k_erg_walk)
     int32_t k = 0;                // errors (the walks' row count template argument)
-    int32_t scanner = 0;          // ee / eregular: ee_scanner / erg_scanner of the slot (a template argument of the walk)
+    int32_t scanner = 0;          // xt / ee / eregular: xt_scanner / ee_scanner / erg_scanner of the slot (a template argument of the walk)
     uint32_t tab_words = 0;       // words of the table blob at tab (copied to LDS when small)
 };
 // eextended heads + walk on s (keys/lens rewritten in place, acc bit 0 =
@@ -1104,6 +1113,9 @@ uint64_t ee_add_headers(pm_db* db, pm_hits* h, uint64_t total, int32_t pid);
 // the eextended walk's scanner kind: 0..2 esimpleScan pieces / window /
 // prefix, 3..5 eextendedScan pieces / window / prefix
 int ee_scanner(const Upload& up, size_t o_slot);
+// the extended walk's scanner kind (k = 0): 0 extendedScan window, 1
+// simpleScan window, 2 simpleScan prefix, 3 extendedScan prefix
+int xt_scanner(const Upload& up, size_t o_slot);
 // the eregular walk's scanner kind: 0..1 esimpleScan pieces / window,
 // 2 the pieces exactly, 3 bwdScanrk, 4 fwdScanrk
 int erg_scanner(const Upload& up, size_t o_slot);

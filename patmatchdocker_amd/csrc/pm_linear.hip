@@ -1634,6 +1634,7 @@ uint8_t* batch_tables(pm_db* db, const BatchIndex& bi, const std::string& sig) {
     memcpy(img.data() + bi.o_ents, bi.ents.data(), bi.ents.size() * 4);
     memcpy(img.data() + bi.o_pmask, bi.pmask.data(), bi.pmask.size() * 4);
     memcpy(img.data() + bi.o_popt, bi.popt.data(), bi.popt.size() * 4);
+    if (!bi.hash.empty()) memcpy(img.data() + bi.o_hash, bi.hash.data(), bi.hash.size() * 8);
     HIPCHK(hipMemcpyAsync(d, img.data(), img.size(), hipMemcpyHostToDevice, db->stream));
     HIPCHK(hipStreamSynchronize(db->stream));
     db->batch_sig = sig;
@@ -2042,6 +2043,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 BatchVerifyArgs va{reinterpret_cast<const uint4*>(rbase + o_cand),
                                    reinterpret_cast<const uint32_t*>(rbase + o_ccnt), ccap, sb.cnt + sb.nbins,
                                    reinterpret_cast<const uint32_t*>(d_batch + bi.o_code),
+                                   bi.hash.empty() ? nullptr : reinterpret_cast<const uint64_t*>(d_batch + bi.o_hash),
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_ents),
                                    reinterpret_cast<const uint4*>(d_batch + bi.o_pmask),
                                    reinterpret_cast<const uint32_t*>(d_batch + bi.o_popt),

@@ -682,6 +682,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     }
     if (extended) {
         if (k == 0) xtp.slot = reinterpret_cast<const XtSlot*>(d_up + o_xslot);
+        if (k == 0) xtp.scanner = xt_scanner(up, o_xslot);
         else xtp.ee = reinterpret_cast<const EeSlot*>(d_up + o_xslot);
         if (k > 0) xtp.scanner = ee_scanner(up, o_xslot);
         xtp.tab = reinterpret_cast<const uint64_t*>(d_up + o_xtab);

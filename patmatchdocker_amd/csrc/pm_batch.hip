@@ -151,25 +151,35 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
                 acc = alignb(tw >> (code & 31u), acc, 1u);
             }
             // candidates: probe i -> 16-byte entry {tile, lane << 11 | s << 6
-            // | i, the 32 bases from position i of the block}
+            // | i, the 32 bases from position i of the block}, written in
+            // position order (stream, then lane, then i): each lane's at its
+            // exclusive prefix of the wave's counts, so the verify's ordered
+            // form reads every segment's candidates in increasing position.
+            // The prefix is bit-sliced: per bit b of the counts a ballot and
+            // mbcnt (VALU/SALU; a shuffle scan is 7 ds_bpermute per stream in
+            // this LDS-bound kernel, measured 3.0 -> 3.48 ms; an LDS staging
+            // of the entries 3.67 ms), a round or two at ~0.26 per lane
             uint32_t m = acc;
-            while (__builtin_amdgcn_ballot_w64(m != 0u)) {
-                const bool has = m != 0u;
-                uint4 e = make_uint4(0u, 0u, 0u, 0u);
-                if (has) {
+            if (__builtin_amdgcn_ballot_w64(m != 0u)) {   // wave-uniform
+                const uint32_t cnt = (uint32_t)__builtin_popcount(m);
+                uint32_t q = 0, tot = 0;
+                for (uint32_t b = 0; __builtin_amdgcn_ballot_w64((cnt >> b) != 0u); ++b) {
+                    const uint64_t bb = __builtin_amdgcn_ballot_w64((cnt >> b) & 1u);
+                    q += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+                    tot += (uint32_t)__builtin_popcountll(bb) << b;
+                }
+                while (m) {
                     const uint32_t i = (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
                     const bool up = i >= 16u;
                     const uint32_t r = (2u * i) & 31u;
                     const uint32_t w0 = up ? c1 : c0, w1 = up ? c2 : c1, w2 = up ? c3 : c2;
-                    e = make_uint4((uint32_t)tile, ((uint32_t)lane << 11) | ((uint32_t)s << 6) | i, alignb(w1, w0, r),
-                                   alignb(w2, w1, r));
+                    const uint4 e = make_uint4((uint32_t)tile, ((uint32_t)lane << 11) | ((uint32_t)s << 6) | i,
+                                               alignb(w1, w0, r), alignb(w2, w1, r));
+                    if (ccnt + q < a.ccap) cseg[ccnt + q] = e;
+                    ++q;
                 }
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(has);
-                const uint32_t below =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                if (has && ccnt + below < a.ccap) cseg[ccnt + below] = e;
-                ccnt += (uint32_t)__builtin_popcountll(bal);
+                ccnt += tot;
             }
         }
     }
@@ -183,11 +193,11 @@ struct VerifySlots {
     uint32_t* cnt;    // [P] keys so far
 };
 
-// One entry (h, mk) of a candidate: on a match, its key into this segment's
-// list (LDS counter) or the next segment's list (xkeys).  lf: the lane flags
-// of the candidate's tile (prefetched).
-__device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t og, const VerifySlots& vs, uint4 e,
-                                             uint64_t lf, uint4 h, uint4 mk) {
+// One entry (h, mk) of a candidate: 0 no match, 1 a match of this segment
+// (its key in `key`), 2 a match whose start lies in the next segment (its key
+// already in xkeys).  lf: the lane flags of the candidate's tile (prefetched).
+__device__ __forceinline__ int verify_key(const BatchVerifyArgs& a, uint32_t og, uint4 e, uint64_t lf, uint4 h, uint4 mk,
+                                          uint64_t& key) {
     const uint32_t x0 = e.z, x1 = e.w;
     const uint32_t i = e.y & 63u, st0 = (e.y >> 6) & 31u, bl = e.y >> 11;
     const uint32_t p = h.x & 0xFFFFu, op = (h.x >> 16) & 255u;
@@ -199,7 +209,7 @@ __device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t 
     const uint32_t s1 = (lsh & mk.y) | (~lsh & mk.x);
     const uint32_t s2 = (lsh & mk.w) | (~lsh & mk.z);
     const uint32_t res = (wc & s2) | (~wc & s1);
-    if ((res & h.y) != h.y) return;
+    if ((res & h.y) != h.y) return 0;
     uint64_t tile = e.x;
     uint32_t w = 32u * bl + a.omax + i - op, st = st0;
     if (w >= STREAM) {   // the start lies in the next stream (or tile)
@@ -211,7 +221,7 @@ __device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t 
         }
     }
     const uint64_t pos = pos_of(tile, w, st);
-    if (tile >= a.ntiles || pos + (uint64_t)len > a.n) return;
+    if (tile >= a.ntiles || pos + (uint64_t)len > a.n) return 0;
     if ((lf >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
         uint32_t kill = 0;
         for (int j = 0; j < len; ++j) {
@@ -219,16 +229,24 @@ __device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t 
             const uint2 b = a.bo[l.word];
             kill |= ((b.x | b.y) >> l.bit) & 1u;
         }
-        if (kill) return;
+        if (kill) return 0;
     }
-    const uint64_t key = ((uint64_t)p << 48) | pos;
+    key = ((uint64_t)p << 48) | pos;
     const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
-    if (ogr == og) {
+    if (ogr == og) return 1;
+    const uint32_t o = atomicAdd(a.xcnt, 1u);
+    if (o < a.xcap) a.xkeys[o] = key;
+    return 2;
+}
+// the unordered form: a match of this segment into its (pattern, segment)
+// list by an LDS counter
+__device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t og, const VerifySlots& vs, uint4 e,
+                                             uint64_t lf, uint4 h, uint4 mk) {
+    uint64_t key;
+    if (verify_key(a, og, e, lf, h, mk, key) == 1) {
+        const uint32_t p = (uint32_t)(key >> 48);
         const uint32_t o = atomicAdd(&vs.cnt[p], 1u);
         if (o < vs.cap[p]) a.out[vs.base[p] + o] = key;
-    } else {
-        const uint32_t o = atomicAdd(a.xcnt, 1u);
-        if (o < a.xcap) a.xkeys[o] = key;
     }
 }
 
@@ -327,6 +345,136 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
     }
     __syncthreads();
     for (int p = threadIdx.x; p < a.P; p += blockDim.x) a.seg_cnt[(uint64_t)p * a.nout + og] = cnt_p[p];
+}
+
+// The ordered form (BatchVerifyArgs::ord set): a segment's matches leave in
+// position order, so no sort by position follows, only a stable one by
+// pattern (pm_hits.hip ordered_to_hits).  Wave wv of the segment's block
+// takes the contiguous wv-th sixteenth of its candidates (the scan writes
+// them in position order), VU * 64 per round; each candidate's matches go to
+// the wave's own list at the lanes' exclusive prefix (no barrier).  A
+// candidate with more than VH matches sets ord_bad (the host then runs the
+// unordered form); matches of the next segment go to xkeys and those keys,
+// like the exception pass's, to the (pattern, segment) bins.
+constexpr int VH = 8;
+template <bool HASH>
+__global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
+    __shared__ uint64_t s_hash[HASH ? BQ_HASH_SLOTS : 1];
+    __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
+    const uint32_t og = blockIdx.x;
+    if constexpr (HASH)
+        for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
+    // the bins (exception pass, xkeys, first starts) start empty
+    for (int p = threadIdx.x; p < a.P; p += blockDim.x) a.seg_cnt[(uint64_t)p * a.nout + og] = 0u;
+    const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < nw; ++k) {
+            uint32_t c = a.cand_cnt[w0 + k];
+            if (c > a.ccap) {
+                atomicMax(a.aux, c);
+                c = a.ccap;
+            }
+            s_n[k] = run;
+            run += c;
+        }
+        s_n[nw] = run;
+    }
+    __syncthreads();
+    const uint32_t total = s_n[nw];
+    auto at = [&](uint32_t q) {
+        uint32_t k = 0;
+        while (q >= s_n[k + 1]) ++k;
+        return a.cand + (uint64_t)(w0 + k) * a.ccap + (q - s_n[k]);
+    };
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr uint32_t NWV = BATCH_VERIFY_WAVES;
+    static_assert(NWV * 64 == 1024, "one verify block: 1024 threads");
+    const uint32_t per = (total + NWV - 1) / NWV;
+    const uint32_t q0 = min(total, wv * per), q1 = min(total, q0 + per);
+    const uint64_t list = (uint64_t)og * NWV + wv;
+    uint64_t* out = a.ord_out + list * a.ord_cap;
+    uint32_t wcnt = 0;   // wave-uniform
+    // the scan wave a lane's next candidate lies in (its candidates increase)
+    uint32_t kk = 0;
+    auto at_k = [&](uint32_t q) {
+        while (q >= s_n[kk + 1]) ++kk;
+        return a.cand + (uint64_t)(w0 + kk) * a.ccap + (q - s_n[kk]);
+    };
+    (void)at;
+    // a round: candidate base + u * 64 + lane (coalesced loads); its matches
+    // leave per u, in (u, lane) order = position order
+    for (uint32_t base = q0; base < q1; base += 64 * VU) {
+        uint4 e[VU], h[VU], mk[VU];
+        uint32_t co[VU];
+        uint64_t lf[VU];
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            const uint32_t q = base + u * 64 + lane;
+            e[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            const bool ok = base + u * 64 + lane < q1;
+            const uint32_t code = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
+            co[u] = 0u;
+            if constexpr (HASH) {
+                if (ok)
+                    for (uint32_t hh = bq_hash(code);; hh = (hh + 1) & (BQ_HASH_SLOTS - 1)) {
+                        const uint64_t sl = s_hash[hh];
+                        if (sl == ~0ull) break;
+                        if ((uint32_t)(sl & 0xFFFFFu) == code) {
+                            co[u] = (uint32_t)((sl >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl >> 44);
+                            break;
+                        }
+                    }
+            } else {
+                co[u] = ok ? a.code_off[code] : 0u;
+            }
+            lf[u] = ok && e[u].x < a.ntiles ? a.lflag[e[u].x] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            const uint32_t lo = co[u] >> 8;
+            h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
+            mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            uint64_t hk[VH];
+            uint32_t nh = 0;
+            bool bad = false;
+            auto take = [&](uint4 h1, uint4 m1) {
+                uint64_t key;
+                if (verify_key(a, og, e[u], lf[u], h1, m1, key) == 1) {
+#pragma unroll
+                    for (int t = 0; t < VH; ++t)
+                        if (t == (int)nh) hk[t] = key;
+                    if (nh < VH) ++nh;
+                    else bad = true;
+                }
+            };
+            if (co[u]) {
+                take(h[u], mk[u]);
+                const uint32_t lo = co[u] >> 8, hi = lo + (co[u] & 255u);
+                for (uint32_t t = lo + 1; t < hi; ++t) take(a.ents[2 * t], a.ents[2 * t + 1]);
+            }
+            if (bad) atomicOr(a.ord_bad, 1u);
+            // the lanes' exclusive prefix of their match counts, bit-sliced
+            // (ballot + mbcnt per bit, as in k_batch_scan)
+            uint32_t at0 = wcnt, tot = 0;
+            for (uint32_t b = 0; __builtin_amdgcn_ballot_w64((nh >> b) != 0u); ++b) {
+                const uint64_t bb = __builtin_amdgcn_ballot_w64((nh >> b) & 1u);
+                at0 += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+                tot += (uint32_t)__builtin_popcountll(bb) << b;
+            }
+#pragma unroll
+            for (int t = 0; t < VH; ++t)
+                if ((uint32_t)t < nh && at0 + t < a.ord_cap) out[at0 + t] = hk[t];
+            wcnt += tot;
+        }
+    }
+    if (lane == 0) a.ord_cnt[list] = wcnt;
 }
 
 __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
@@ -481,8 +629,12 @@ void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t n
     HIPCHK(hipGetLastError());
     // PM_BATCH_HASH=0: the code_off array (A/B)
     static const bool hash_on = !(getenv("PM_BATCH_HASH") && getenv("PM_BATCH_HASH")[0] == '0');
-    if (va.hash && hash_on) hipLaunchKernelGGL(k_batch_verify<true>, dim3(va.nout), dim3(1024), 0, s, va);
-    else hipLaunchKernelGGL(k_batch_verify<false>, dim3(va.nout), dim3(1024), 0, s, va);
+    const bool hash = va.hash && hash_on;
+    if (va.ord_out)
+        hipLaunchKernelGGL(hash ? k_batch_verify_ord<true> : k_batch_verify_ord<false>, dim3(va.nout), dim3(1024), 0, s,
+                           va);
+    else
+        hipLaunchKernelGGL(hash ? k_batch_verify<true> : k_batch_verify<false>, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_batch_fixup, dim3(64), dim3(256), 0, s, va);
     HIPCHK(hipGetLastError());

@@ -568,6 +568,7 @@ void free_db(pm_db* db) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
+    if (db->pin_ord.p) (void)hipHostFree(db->pin_ord.p);
     for (pm_lane* l : {static_cast<pm_lane*>(db), &db->alt}) {
         for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p, l->ws_rep.p, l->ws_oth.p})
             if (p) (void)hipFree(p);

@@ -12,6 +12,7 @@
 // sorted by themselves, then copied to their offsets.
 #include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_merge.hpp>
 
 #include <map>
 #include <mutex>
@@ -253,6 +254,21 @@ __global__ void k_gather_bins(const uint64_t* __restrict__ out, const uint32_t* 
         dst[o + i] = pos_bits ? ((k >> 48) << pos_bits) | (k & ((1ull << 48) - 1)) : k;
     }
 }
+// the ordered batch verify's lists gathered at their offsets (list order =
+// position order)
+__global__ void k_gather_lists(const uint64_t* __restrict__ ord, uint32_t cap, const uint32_t* __restrict__ cnt,
+                               const uint64_t* __restrict__ off, uint64_t* __restrict__ dst) {
+    const uint32_t l = blockIdx.x;
+    const uint32_t c = min(cnt[l], cap);
+    const uint64_t o = off[l];
+    const uint64_t* src = ord + (uint64_t)l * cap;
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = src[i];
+}
+struct ListCount {
+    const uint32_t* cnt;
+    uint32_t cap;
+    __device__ uint64_t operator()(uint32_t l) const { return min(cnt[l], cap); }
+};
 __global__ void k_unpack_keys(uint64_t* __restrict__ keys, uint64_t n, uint32_t pos_bits) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -694,6 +710,74 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
     return h;
 }
 
+pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t sink_total,
+                         const uint64_t* ord, uint32_t ord_cap, const uint32_t* d_cnt, const uint32_t* cnt,
+                         uint32_t nlists, int n_patterns) {
+    uint64_t t1 = 0;
+    for (uint32_t l = 0; l < nlists; ++l) t1 += std::min(cnt[l], ord_cap);
+    // the sink first (its sort reserves ws_post itself)
+    pm_hits* hs = sink_total ? sink_to_hits(db, sb, counts, sink_total, nullptr, nullptr) : nullptr;
+    if (t1 == 0 && hs) return hs;
+    hipStream_t s = db->stream;
+    const uint64_t total = t1 + sink_total;
+    pm_hits* h = new pm_hits();
+    h->device = db->device;
+    h->count = total;
+    try {
+        h->keys = static_cast<uint64_t*>(pool_get(db->device, std::max<uint64_t>(total, 1) * 8, &h->keys_cap));
+        h->lens = static_cast<uint32_t*>(pool_get(db->device, std::max<uint64_t>(total, 1) * 4, &h->lens_cap));
+        if (total) {
+            // the lists hold every pattern's keys in increasing position: one
+            // stable radix sort over the pattern bits (48 + slot_bits) orders
+            // them by (pattern, position)
+            uint32_t slot_bits = 1;
+            while (slot_bits < 16 && ((uint64_t)(n_patterns - 1) >> slot_bits)) ++slot_bits;
+            auto counted = hipcub::TransformInputIterator<uint64_t, ListCount, hipcub::CountingInputIterator<uint32_t>>(
+                hipcub::CountingInputIterator<uint32_t>(0u), ListCount{d_cnt, ord_cap});
+            size_t scan_bytes = 0, sort_bytes = 0, merge_bytes = 0;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)nlists, s));
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                     (int)t1, 48, 48 + (int)slot_bits, s));
+            if (hs)
+                HIPCHK(rocprim::merge(nullptr, merge_bytes, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
+                                      (uint64_t*)nullptr, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
+            (void)hipGetLastError();   // rocPRIM's stale capture status (sink_to_hits)
+            Carve c;
+            const size_t o_off = c.take(nlists * sizeof(uint64_t));
+            const size_t o_scan = c.take(scan_bytes);
+            const size_t o_in = c.take(t1 * sizeof(uint64_t));
+            const size_t o_mid = c.take(hs ? t1 * sizeof(uint64_t) : 0);
+            const size_t o_tmp = c.take(std::max(sort_bytes, merge_bytes));
+            uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
+            uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
+            uint64_t* in = reinterpret_cast<uint64_t*>(base + o_in);
+            uint64_t* sorted = hs ? reinterpret_cast<uint64_t*>(base + o_mid) : h->keys;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)nlists, s));
+            (void)hipGetLastError();
+            hipLaunchKernelGGL(k_gather_lists, dim3(nlists), dim3(256), 0, s, ord, ord_cap, d_cnt, d_off, in);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, in, sorted, (int)t1, 48,
+                                                     48 + (int)slot_bits, s));
+            (void)hipGetLastError();
+            if (hs) {
+                HIPCHK(rocprim::merge(base + o_tmp, merge_bytes, (const uint64_t*)sorted, (const uint64_t*)hs->keys,
+                                      h->keys, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
+                (void)hipGetLastError();
+            }
+        }
+    } catch (...) {
+        discard_hits(h);
+        if (hs) discard_hits(hs);
+        throw;
+    }
+    if (hs) {
+        // its buffers go back to the pool once the merge has read them
+        HIPCHK(hipStreamSynchronize(s));
+        discard_hits(hs);
+    }
+    return h;
+}
+
 // ---------------------------------------------------------------------------
 // nrgrep report selection (see pm_internal.h and DESIGN.md §1)
 // ---------------------------------------------------------------------------
@@ -848,16 +932,27 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
     uint64_t m = 0;
     if (a.flags & PM_REPORT_NRGREP) {
         // 4 candidates per round: their loads (and the region lookups that
-        // depend on them) are in flight together
+        // depend on them) are in flight together, the next round's loads
+        // while this one's lookups run
         constexpr int U = 4;
+        uint64_t nkey[U];
+        uint32_t nlen[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = b0 + threadIdx.x + (uint64_t)u * REP_T;
+            nkey[u] = i < b1 ? a.keys[i] : 0ull;
+            nlen[u] = i < b1 ? a.lens[i] : 0u;
+        }
         for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += U * REP_T) {
             uint64_t key[U];
             uint32_t len[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint64_t i = i0 + (uint64_t)u * REP_T;
-                key[u] = i < b1 ? a.keys[i] : 0ull;
-                len[u] = i < b1 ? a.lens[i] : 0u;
+                key[u] = nkey[u];
+                len[u] = nlen[u];
+                const uint64_t i = i0 + (uint64_t)(U + u) * REP_T;
+                nkey[u] = i < b1 ? a.keys[i] : 0ull;
+                nlen[u] = i < b1 ? a.lens[i] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)

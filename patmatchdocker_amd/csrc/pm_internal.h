@@ -360,6 +360,7 @@ struct pm_db : pm_lane {
     pm_devbuf ws_batch;
     std::string batch_sig;
     pm_hostbuf pin_down;
+    pm_hostbuf pin_ord;   // the ordered batch verify's list counts
     // pipelined scans: record expansion + sort of scan i run on `post` while
     // scan i+1's kernel runs on `stream`, each on its own workspace lane (the
     // inherited pm_lane is the active one, `alt` the other; switch_lane swaps)
@@ -517,6 +518,7 @@ constexpr int BATCH_THREADS = 64 * BATCH_WAVES;
 constexpr int BATCH_MAX_P = 1024;
 constexpr int BATCH_MAX_LEN = 16;                          // a window's bases fit one 32-bit code word
 constexpr uint32_t BATCH_MAX_WPO = 64;                     // scan waves per output segment
+constexpr uint32_t BATCH_VERIFY_WAVES = 16;                // waves per verify block (one per segment)
 constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a quarter of the table)
 
 struct BatchIndex {
@@ -580,6 +582,13 @@ struct BatchVerifyArgs {
     uint64_t* xkeys;        // keys of the next segment
     uint32_t* xcnt;
     uint32_t xcap;
+    // the ordered form (null: the unordered one): per (segment, verify wave)
+    // list of ord_cap keys in position order, their counts, and a flag set
+    // when a lane's round held more matches than it keeps
+    uint64_t* ord_out = nullptr;
+    uint32_t* ord_cnt = nullptr;
+    uint32_t* ord_bad = nullptr;
+    uint32_t ord_cap = 0;
 };
 // k_batch_scan (timed by ev_a / ev_b), k_batch_verify, k_batch_fixup on s
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
@@ -652,6 +661,15 @@ pm_hits* sink_sort_speculative(pm_db* db, const SinkBuffers& sb, const int32_t* 
 void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // slot_len (device, per slot, optional): fixed match length of every key of
 // a slot -- the LDS sort writes h->lens with the keys.
+// The ordered batch verify's result: nlists lists of position-ordered keys
+// (list l at ord + l * ord_cap, cnt[l] <= ord_cap keys; d_cnt on the device)
+// and the sink's bins (counts, sink_total keys: the exception pass, keys of
+// the next segment, the first starts) into one (pattern, position)-sorted
+// list: one stable radix pass over the pattern bits, the sink sorted by
+// sink_to_hits, a merge of the two.  Lens are the caller's.
+pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t sink_total,
+                         const uint64_t* ord, uint32_t ord_cap, const uint32_t* d_cnt, const uint32_t* cnt,
+                         uint32_t nlists, int n_patterns);
 pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,
                       const int32_t* slot_len = nullptr, bool* lens_done = nullptr);
 // records h->ready on the db stream: call after the last kernel filling h

@@ -1578,6 +1578,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
 // last time.
 std::mutex g_cap_mu;
 std::map<std::pair<const pm_db*, std::string>, std::pair<std::vector<uint32_t>, uint32_t>> g_cap_hint;
+std::map<std::pair<const pm_db*, std::string>, uint32_t> g_ord_hint;   // the ordered batch verify's list capacity
 
 // PM_JIT: "0" never, "1" always, default: databases of >= 64 Mi positions
 bool use_jit(const pm_db* db) {
@@ -2026,12 +2027,26 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // starts per pattern and segment boundary
             const uint64_t xcap = std::max<uint64_t>(4096, nout * n_patterns * (bip->omax + 1));
             const bool exc = db->nflag && (db->n_oth_words || cross);
-            for (int attempt = 0; attempt < 4 && !done; ++attempt) {
+            // the ordered verify (PM_BATCH_ORDERED=0: off, A/B): per (segment,
+            // verify wave) a position-ordered list of ord_cap keys
+            const bool ord_env = !(getenv("PM_BATCH_ORDERED") && getenv("PM_BATCH_ORDERED")[0] == '0');
+            bool ordered = ord_env;
+            const uint32_t nlists = (uint32_t)nout * BATCH_VERIFY_WAVES;
+            uint32_t ord_cap = 1024;
+            {
+                std::lock_guard<std::mutex> lk(g_cap_mu);
+                auto it = g_ord_hint.find({db, cap_key});
+                if (it != g_ord_hint.end()) ord_cap = it->second;
+            }
+            const uint32_t* ord_h = nullptr;   // the lists' counts (pinned)
+            for (int attempt = 0; attempt < 6 && !done; ++attempt) {
                 Carve cv;
                 const size_t o_cand = cv.take(nwaves * ccap * sizeof(uint4));
                 const size_t o_ccnt = cv.take(nwaves * sizeof(uint32_t));
                 const size_t o_xcnt = cv.take(sizeof(uint32_t));
                 const size_t o_x = cv.take(xcap * sizeof(uint64_t));
+                const size_t o_ocnt = cv.take((nlists + 1) * sizeof(uint32_t));   // + the overflow flag
+                const size_t o_ord = cv.take(ordered ? (uint64_t)nlists * ord_cap * sizeof(uint64_t) : 0);
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
                 // k_batch_verify stores every (pattern, segment) count
                 sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
@@ -2052,18 +2067,57 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                    db->lflag, db->ntiles, db->n, sb.out, sb.cnt, sb.slot_base, sb.slot_cap,
                                    reinterpret_cast<uint64_t*>(rbase + o_x), reinterpret_cast<uint32_t*>(rbase + o_xcnt),
                                    (uint32_t)xcap};
+                uint32_t* d_ocnt = reinterpret_cast<uint32_t*>(rbase + o_ocnt);
+                if (ordered) {
+                    va.ord_out = reinterpret_cast<uint64_t*>(rbase + o_ord);
+                    va.ord_cnt = d_ocnt;
+                    va.ord_bad = d_ocnt + nlists;
+                    va.ord_cap = ord_cap;
+                    HIPCHK(hipMemsetAsync(va.ord_bad, 0, sizeof(uint32_t), s));
+                }
                 jev.clear();
                 jev.emplace_back(new EventPair());
                 batch_launch(sa, va, nblocks, s, jev.back()->a, jev.back()->b);
                 if (exc) launch_others(chunks[0], s, sb, nout, tpw * wpo);
+                if (ordered) {
+                    uint32_t* hp = static_cast<uint32_t*>(reserve_host(db, db->pin_ord, (nlists + 1) * sizeof(uint32_t)));
+                    HIPCHK(hipMemcpyAsync(hp, d_ocnt, (nlists + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+                    ord_h = hp;
+                }
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
                 const uint32_t cneed = sb.aux;
-                if (!overflow && cneed == 0) {
+                bool ord_retry = false;
+                if (ordered) {
+                    if (ord_h[nlists]) {   // a lane's round held more matches than it keeps
+                        ordered = false;
+                        ord_retry = true;
+                    } else {
+                        const uint32_t m = *std::max_element(ord_h, ord_h + nlists);
+                        if (m > ord_cap) {
+                            while (ord_cap < m) ord_cap *= 2;
+                            ord_retry = true;
+                        }
+                    }
+                }
+                if (!overflow && cneed == 0 && !ord_retry) {
                     done = true;
                     std::lock_guard<std::mutex> lk(g_cap_mu);
                     if (g_cap_hint.size() > 256) g_cap_hint.clear();
                     g_cap_hint[{db, cap_key}] = {slot_caps, ccap};
+                    if (g_ord_hint.size() > 256) g_ord_hint.clear();
+                    g_ord_hint[{db, cap_key}] = ord_cap;
+                    if (ordered) {
+                        hit_list = ordered_to_hits(db, sb, counts, total, va.ord_out, ord_cap, d_ocnt, ord_h, nlists,
+                                                   n_patterns);
+                        total = hit_list->count;
+                        if (total) {
+                            hipLaunchKernelGGL(k_linear_lens, dim3(blocks_for(total, 256)), dim3(256), 0, s,
+                                               hit_list->keys, total, reinterpret_cast<const int32_t*>(d_up + o_len),
+                                               hit_list->lens);
+                            HIPCHK(hipGetLastError());
+                        }
+                    }
                     break;
                 }
                 if (cneed) ccap = std::max<uint32_t>(ccap, cneed + cneed / 8 + 64);

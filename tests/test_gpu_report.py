@@ -277,7 +277,8 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
     positions) on a multi-tile database full of exceptions, patterns of
     every length 10..16 (different piece offsets o_p) + configs[4]'s motifs,
     every pattern's report list vs the oracle; and the same query with the
-    filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks).
+    filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks) and
+    with the unordered verify (PM_BATCH_ORDERED=0).
     minlen 11 also runs the stride-2 probes (PM_BATCH_STRIDE=2: every other
     position, two indexed pieces per pattern)."""
     import bench
@@ -299,6 +300,9 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
             monkeypatch.setenv("PM_BATCH_STRIDE", "2")
             res_s2, _ = engine.scan(db, progs, k=0, types="s")
             monkeypatch.delenv("PM_BATCH_STRIDE")
+        # the unordered verify (per-(pattern, segment) bins + sort)
+        monkeypatch.setenv("PM_BATCH_ORDERED", "0")
+        res_unord, _ = engine.scan(db, progs, k=0, types="s")
         monkeypatch.setenv("PM_BATCH", "0")
         res_chunks, _ = engine.scan(db, progs, k=0, types="s")
     finally:
@@ -308,6 +312,7 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
         want = oracle_mod.scan_threads(text, prog, 0, "s", skip_headers=True, threads=16, report="nrgrep")
         assert _pairs(r) == want, prog.source
         assert _pairs(rc) == want, prog.source
+        assert _pairs(res_unord[i]) == want, prog.source
         if res_s2 is not None:
             assert _pairs(res_s2[i]) == want, prog.source
         total += len(want)

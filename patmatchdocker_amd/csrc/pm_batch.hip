@@ -196,8 +196,10 @@ struct VerifySlots {
 // One entry (h, mk) of a candidate: 0 no match, 1 a match of this segment
 // (its key in `key`), 2 a match whose start lies in the next segment (its key
 // already in xkeys).  lf: the lane flags of the candidate's tile (prefetched).
-__device__ __forceinline__ int verify_key(const BatchVerifyArgs& a, uint32_t og, uint4 e, uint64_t lf, uint4 h, uint4 mk,
-                                          uint64_t& key) {
+// tend: the segment's end tile (a start never lies before its candidate's
+// segment, so tile < tend is this segment -- no 64-bit division)
+__device__ __forceinline__ int verify_key(const BatchVerifyArgs& a, uint64_t tend, uint4 e, uint64_t lf, uint4 h,
+                                          uint4 mk, uint64_t& key) {
     const uint32_t x0 = e.z, x1 = e.w;
     const uint32_t i = e.y & 63u, st0 = (e.y >> 6) & 31u, bl = e.y >> 11;
     const uint32_t p = h.x & 0xFFFFu, op = (h.x >> 16) & 255u;
@@ -232,18 +234,17 @@ __device__ __forceinline__ int verify_key(const BatchVerifyArgs& a, uint32_t og,
         if (kill) return 0;
     }
     key = ((uint64_t)p << 48) | pos;
-    const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
-    if (ogr == og) return 1;
+    if (tile < tend) return 1;
     const uint32_t o = atomicAdd(a.xcnt, 1u);
     if (o < a.xcap) a.xkeys[o] = key;
     return 2;
 }
 // the unordered form: a match of this segment into its (pattern, segment)
 // list by an LDS counter
-__device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint32_t og, const VerifySlots& vs, uint4 e,
+__device__ __forceinline__ void verify_entry(const BatchVerifyArgs& a, uint64_t tend, const VerifySlots& vs, uint4 e,
                                              uint64_t lf, uint4 h, uint4 mk) {
     uint64_t key;
-    if (verify_key(a, og, e, lf, h, mk, key) == 1) {
+    if (verify_key(a, tend, e, lf, h, mk, key) == 1) {
         const uint32_t p = (uint32_t)(key >> 48);
         const uint32_t o = atomicAdd(&vs.cnt[p], 1u);
         if (o < vs.cap[p]) a.out[vs.base[p] + o] = key;
@@ -276,6 +277,7 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
     if constexpr (HASH)
         for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
     const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
+    const uint64_t tend = (uint64_t)(w0 + a.wpo) * a.tiles_per_wave;
     if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t k = 0; k < nw; ++k) {
@@ -338,9 +340,9 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             if (!co[u]) continue;
-            verify_entry(a, og, vs, e[u], lf[u], h[u], mk[u]);
+            verify_entry(a, tend, vs, e[u], lf[u], h[u], mk[u]);
             const uint32_t lo = co[u] >> 8, hi = lo + (co[u] & 255u);
-            for (uint32_t t = lo + 1; t < hi; ++t) verify_entry(a, og, vs, e[u], lf[u], a.ents[2 * t], a.ents[2 * t + 1]);
+            for (uint32_t t = lo + 1; t < hi; ++t) verify_entry(a, tend, vs, e[u], lf[u], a.ents[2 * t], a.ents[2 * t + 1]);
         }
     }
     __syncthreads();
@@ -364,9 +366,10 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     const uint32_t og = blockIdx.x;
     if constexpr (HASH)
         for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
-    // the bins (exception pass, xkeys, first starts) start empty
-    for (int p = threadIdx.x; p < a.P; p += blockDim.x) a.seg_cnt[(uint64_t)p * a.nout + og] = 0u;
+    // (the bins of the exception pass, xkeys and first starts are zeroed by
+    // the host: the exception pass may run concurrently)
     const uint32_t w0 = og * a.wpo, nw = min(a.nwaves, w0 + a.wpo) - w0;
+    const uint64_t tend = (uint64_t)(w0 + a.wpo) * a.tiles_per_wave;
     if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t k = 0; k < nw; ++k) {
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
             bool bad = false;
             auto take = [&](uint4 h1, uint4 m1) {
                 uint64_t key;
-                if (verify_key(a, og, e[u], lf[u], h1, m1, key) == 1) {
+                if (verify_key(a, tend, e[u], lf[u], h1, m1, key) == 1) {
 #pragma unroll
                     for (int t = 0; t < VH; ++t)
                         if (t == (int)nh) hk[t] = key;

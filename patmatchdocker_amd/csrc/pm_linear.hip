@@ -2030,6 +2030,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // the ordered verify (PM_BATCH_ORDERED=0: off, A/B): per (segment,
             // verify wave) a position-ordered list of ord_cap keys
             const bool ord_env = !(getenv("PM_BATCH_ORDERED") && getenv("PM_BATCH_ORDERED")[0] == '0');
+            const bool exc_conc = !(getenv("PM_BATCH_EXC_CONC") && getenv("PM_BATCH_EXC_CONC")[0] == '0');
             bool ordered = ord_env;
             const uint32_t nlists = (uint32_t)nout * BATCH_VERIFY_WAVES;
             uint32_t ord_cap = 1024;
@@ -2048,8 +2049,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 const size_t o_ocnt = cv.take((nlists + 1) * sizeof(uint32_t));   // + the overflow flag
                 const size_t o_ord = cv.take(ordered ? (uint64_t)nlists * ord_cap * sizeof(uint64_t) : 0);
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
-                // k_batch_verify stores every (pattern, segment) count
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/false);
+                // k_batch_verify stores every (pattern, segment) count; the
+                // ordered form only adds to the bins (zeroed here)
+                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/ordered);
                 const BatchIndex& bi = *bip;
                 const uint32_t* d_tab = reinterpret_cast<const uint32_t*>(d_batch + bi.o_table);
                 BatchScanArgs sa{db->hl, db->ntiles, d_tab, bi.omax, (uint32_t)tpw, (uint32_t)nwaves, ccap,
@@ -2077,8 +2079,23 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 }
                 jev.clear();
                 jev.emplace_back(new EventPair());
+                // the ordered form's exception pass runs on its own stream,
+                // beside the scan and verify (its bins are atomic adds;
+                // PM_BATCH_EXC_CONC=0: after them, A/B)
+                const bool conc = exc && ordered && exc_conc;
+                if (conc) {
+                    hipStream_t es2 = exc_stream(db);
+                    HIPCHK(hipEventRecord(db->exc_fork, s));
+                    HIPCHK(hipStreamWaitEvent(es2, db->exc_fork, 0));
+                }
                 batch_launch(sa, va, nblocks, s, jev.back()->a, jev.back()->b);
-                if (exc) launch_others(chunks[0], s, sb, nout, tpw * wpo);
+                if (conc) {
+                    launch_others(chunks[0], db->exc, sb, nout, tpw * wpo);
+                    HIPCHK(hipEventRecord(db->exc_join, db->exc));
+                    HIPCHK(hipStreamWaitEvent(s, db->exc_join, 0));
+                } else if (exc) {
+                    launch_others(chunks[0], s, sb, nout, tpw * wpo);
+                }
                 if (ordered) {
                     uint32_t* hp = static_cast<uint32_t*>(reserve_host(db, db->pin_ord, (nlists + 1) * sizeof(uint32_t)));
                     HIPCHK(hipMemcpyAsync(hp, d_ocnt, (nlists + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_report.py tests/test_gpu_pa
 tail -2 $out/t.log
 timeout -k 10 300 python3 bench.py --config 4 --steps 10 --warmup 3 --no-cpu-baseline > $out/bench4.json 2> $out/bench4.err || { tail -20 $out/bench4.err; exit 1; }
 cut -c1-300 $out/bench4.json
-PM_BATCH_ORDERED=0 timeout -k 10 300 python3 bench.py --config 4 --steps 10 --warmup 3 --no-cpu-baseline > $out/bench4_off.json 2> $out/bench4_off.err || { tail -20 $out/bench4_off.err; exit 1; }
+PM_BATCH_EXC_CONC=0 timeout -k 10 300 python3 bench.py --config 4 --steps 10 --warmup 3 --no-cpu-baseline > $out/bench4_off.json 2> $out/bench4_off.err || { tail -20 $out/bench4_off.err; exit 1; }
 cut -c1-300 $out/bench4_off.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof4 -o run -- python3 bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline > $out/prof4.json 2> $out/prof4.err || { tail -20 $out/prof4.err; exit 1; }
 python3 tools/kstats.py $out/prof4/run_kernel_stats.csv | head -30

@@ -484,12 +484,13 @@ __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     // keys whose start fell into the next segment (the next tile's first positions)
     const uint32_t nx = min(*a.xcnt, a.xcap);
+    const uint32_t ns = a.sink_segs ? a.sink_segs : a.nout;
     for (uint32_t q = tid; q < nx; q += nth) {
         const uint64_t key = a.xkeys[q];
         const uint32_t p = (uint32_t)(key >> 48);
         const uint64_t tile = (key & 0xFFFFFFFFFFFFull) / TILE_POS;
-        const uint32_t ogr = (uint32_t)((tile / a.tiles_per_wave) / a.wpo);
-        const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)p * a.nout + ogr], 1u);
+        const uint32_t ogr = ns == 1 ? 0u : (uint32_t)tile / a.tiles_per_wave / a.wpo;   // 32-bit division
+        const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)p * ns + ogr], 1u);
         if (o < a.slot_cap[p]) a.out[a.slot_base[p] + (uint64_t)ogr * a.slot_cap[p] + o] = key;
     }
     // the file's first starts st < o_max - o_p: probed by no block
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
             ok = (m >> (2 * j + 1)) & 1u;
         }
         if (!ok) continue;
-        const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)p * a.nout], 1u);
+        const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)p * ns], 1u);
         if (o < a.slot_cap[p]) a.out[a.slot_base[p] + o] = ((uint64_t)p << 48) | st;
     }
 }

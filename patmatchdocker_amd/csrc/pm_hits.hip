@@ -710,6 +710,10 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
     return h;
 }
 
+namespace {
+void retire_buffers(pm_hits* h, hipStream_t s);   // below (report pass)
+}
+
 pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t sink_total,
                          const uint64_t* ord, uint32_t ord_cap, const uint32_t* d_cnt, const uint32_t* cnt,
                          uint32_t nlists, int n_patterns) {
@@ -771,8 +775,11 @@ pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uin
         throw;
     }
     if (hs) {
-        // its buffers go back to the pool once the merge has read them
-        HIPCHK(hipStreamSynchronize(s));
+        // its buffers go back to the pool once the merge has read them (an
+        // event-tracked shell, no host sync)
+        retire_buffers(hs, s);
+        hs->keys = nullptr;
+        hs->lens = nullptr;
         discard_hits(hs);
     }
     return h;
@@ -812,6 +819,7 @@ __device__ inline bool tv_header(const TextView& tv, uint64_t p) {
 struct RepArgs {
     const uint64_t* keys;
     const uint32_t* lens;
+    const int32_t* plen;    // non-null: lens by pattern (lens unread)
     uint64_t* okeys;
     uint32_t* olens;
     uint8_t* acc;           // per candidate: 1 = reported and kept (written exactly once, or twice with 0)
@@ -827,6 +835,10 @@ struct RepArgs {
 };
 
 __device__ inline uint64_t rep_total(const RepArgs& a) { return a.total_d ? *a.total_d : a.total_h; }
+// candidate i's length (key: its key)
+__device__ inline uint32_t rep_len(const RepArgs& a, uint64_t i, uint64_t key) {
+    return a.plen ? (uint32_t)a.plen[key >> 48] : a.lens[i];
+}
 __device__ inline uint64_t rep_chunk(uint64_t total, uint32_t G) { return (total + G - 1) / G; }
 
 // '$': the match must end at a line end or at the end of the text (the
@@ -941,7 +953,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
         for (int u = 0; u < U; ++u) {
             const uint64_t i = b0 + threadIdx.x + (uint64_t)u * REP_T;
             nkey[u] = i < b1 ? a.keys[i] : 0ull;
-            nlen[u] = i < b1 ? a.lens[i] : 0u;
+            nlen[u] = i < b1 && !a.plen ? a.lens[i] : 0u;
         }
         for (uint64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += U * REP_T) {
             uint64_t key[U];
@@ -949,10 +961,10 @@ __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 key[u] = nkey[u];
-                len[u] = nlen[u];
+                len[u] = !a.plen ? nlen[u] : i0 + (uint64_t)u * REP_T < b1 ? (uint32_t)a.plen[key[u] >> 48] : 0u;
                 const uint64_t i = i0 + (uint64_t)(U + u) * REP_T;
                 nkey[u] = i < b1 ? a.keys[i] : 0ull;
-                nlen[u] = i < b1 ? a.lens[i] : 0u;
+                nlen[u] = i < b1 && !a.plen ? a.lens[i] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -980,7 +992,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
         for (uint64_t i = b0 + threadIdx.x; i < b1; i += REP_T) {
             const uint64_t key = a.keys[i];
             const uint64_t s = key & POS_MASK;
-            bool ok = rep_valid(a, key, a.lens[i], rep_near(a, key));
+            bool ok = rep_valid(a, key, rep_len(a, i, key), rep_near(a, key));
             if (ok && (a.flags & PM_ANCHOR_START)) ok = rep_line_start(a, s);
             ok = ok && rep_keep(a, key);
             a.acc[i] = ok ? 1 : 0;
@@ -1009,7 +1021,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     for (int u = 0; u < RW; ++u) {
         const uint64_t i = b0 + (uint64_t)threadIdx.x * RW + u;
         nkey[u] = i < b1 ? a.keys[i] : 0ull;
-        nlen[u] = i < b1 ? a.lens[i] : 0u;
+        nlen[u] = i < b1 && !a.plen ? a.lens[i] : 0u;
     }
     for (uint64_t base = b0; base < b1; base += TT) {
         const uint64_t i0 = base + (uint64_t)threadIdx.x * RW;
@@ -1019,10 +1031,10 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
 #pragma unroll
         for (int u = 0; u < RW; ++u) {
             key[u] = nkey[u];
-            len[u] = nlen[u];
+            len[u] = !a.plen ? nlen[u] : i0 + u < b1 ? (uint32_t)a.plen[key[u] >> 48] : 0u;
             const uint64_t ni = i0 + TT + u;
             nkey[u] = ni < b1 ? a.keys[ni] : 0ull;
-            nlen[u] = ni < b1 ? a.lens[ni] : 0u;
+            nlen[u] = ni < b1 && !a.plen ? a.lens[ni] : 0u;
         }
         uint64_t tmax = 0;   // the thread's candidates' running maximum
 #pragma unroll
@@ -1094,7 +1106,7 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
             for (uint64_t j = i + 1; j < total; ++j) {
                 const uint64_t kj = a.keys[j];
                 if (anch ? kj > run || (kj == run && rep_region_start(a, kj & POS_MASK)) : kj >= run) break;  // the next head
-                const uint32_t lj = a.lens[j];
+                const uint32_t lj = rep_len(a, j, kj);
                 kept = 0;
                 const bool nj = rep_near(a, kj);
                 if (rep_valid(a, kj, lj, nj)) {
@@ -1154,8 +1166,9 @@ __global__ __launch_bounds__(REP_T) void k_rep_scatter(RepArgs a) {
         __syncthreads();
         if (keep) {
             const uint64_t o = base_out + pre + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            a.okeys[o] = a.keys[i];
-            a.olens[o] = a.lens[i];
+            const uint64_t k = a.keys[i];
+            a.okeys[o] = k;
+            a.olens[o] = rep_len(a, i, k);
         }
         base_out += tile;
     }
@@ -1217,6 +1230,8 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     RepArgs a{};
     a.keys = h->keys;
     a.lens = h->lens;
+    a.plen = h->plen;
+    require(!h->plen || (!es && !xt), "internal: lens by pattern only for the generic report");
     size_t kc = 0, lc = 0;
     a.okeys = static_cast<uint64_t*>(pool_get(h->device, h->keys_cap, &kc));
     a.olens = static_cast<uint32_t*>(pool_get(h->device, h->lens_cap, &lc));
@@ -1266,6 +1281,7 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
     }
     h->keys = a.okeys;
     h->lens = a.olens;
+    h->plen = nullptr;   // the pass wrote every kept length
     h->keys_cap = kc;
     h->lens_cap = lc;
 }
@@ -1274,6 +1290,7 @@ void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr
                  const XtPrep* xt) {
     if (total == 0) {
         h->count = 0;
+        h->plen = nullptr;
         return;
     }
     const ReportWs ws = report_ws(db, h->keys_cap / 8);

@@ -417,6 +417,9 @@ struct pm_hits {
     uint64_t* keys = nullptr;   // sorted, pattern << 48 | beg
     uint32_t* lens = nullptr;
     size_t keys_cap = 0, lens_cap = 0;
+    // set: lens[] is unwritten and a key's length is plen[pattern] (a batch
+    // of exact patterns; the report pass reads it and writes its own lens)
+    const int32_t* plen = nullptr;
     double kernel_ms = 0.0;
     hipEvent_t ready = nullptr;     // recorded after the last kernel writing keys/lens
     hipEvent_t last_use = nullptr;  // recorded by pm_hits_copy_device on the caller's stream
@@ -589,6 +592,7 @@ struct BatchVerifyArgs {
     uint32_t* ord_cnt = nullptr;
     uint32_t* ord_bad = nullptr;
     uint32_t ord_cap = 0;
+    uint32_t sink_segs = 0;   // segments per pattern of the bins k_batch_fixup fills (0: nout)
 };
 // k_batch_scan (timed by ev_a / ev_b), k_batch_verify, k_batch_fixup on s
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,

@@ -351,7 +351,7 @@ __device__ inline void other_windows(const OthersArgs& a, const Memb& memb, uint
             }
             if (ok) {
                 const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                const uint64_t og = (s / TILE_POS) / a.tiles_per_wg;
+                const uint64_t og = (uint32_t)(s / TILE_POS) / (uint32_t)a.tiles_per_wg;   // 32-bit division
                 const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
                 if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
             }
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void k_others_lane(LaneArgs a) {
             for (; live; live &= live - 1) {
                 const uint64_t s = (uint64_t)(q0 + __builtin_ctzll(live));
                 const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                const uint64_t og = (s / TILE_POS) / a.tiles_per_out;
+                const uint64_t og = (uint32_t)(s / TILE_POS) / (uint32_t)a.tiles_per_out;   // 32-bit division
                 const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nout + og], 1u);
                 if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s;
             }
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
                 for (; alive; alive &= alive - 1) {
                     const uint64_t s0 = (uint64_t)(q0 + __builtin_ctzll(alive));
                     const uint32_t slot = (uint32_t)(a.pattern_base + p);
-                    const uint64_t og = (s0 / TILE_POS) / a.tiles_per_wg;
+                    const uint64_t og = (uint32_t)(s0 / TILE_POS) / (uint32_t)a.tiles_per_wg;   // 32-bit division
                     const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
                     if (o < a.slot_cap[slot]) a.out[a.slot_base[slot] + og * a.slot_cap[slot] + o] = ((uint64_t)slot << 48) | s0;
                 }
@@ -2040,7 +2040,21 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 if (it != g_ord_hint.end()) ord_cap = it->second;
             }
             const uint32_t* ord_h = nullptr;   // the lists' counts (pinned)
+            // the ordered form's bins (exception pass, next-segment keys,
+            // first starts) are one per pattern: a few keys each, so the
+            // host's per-bin work after the sync is 256 bins, not 64 Ki
+            std::vector<uint32_t> caps_ord(n_patterns, 256);
+            {
+                std::lock_guard<std::mutex> lk(g_cap_mu);
+                auto it = g_cap_hint.find({db, cap_key + "|ord"});
+                if (it != g_cap_hint.end() && it->second.first.size() == caps_ord.size()) {
+                    caps_ord = it->second.first;
+                    ccap = std::max(ccap, it->second.second);
+                }
+            }
             for (int attempt = 0; attempt < 6 && !done; ++attempt) {
+                const uint64_t snout = ordered ? 1 : nout;   // sink segments per pattern
+                std::vector<uint32_t>& caps = ordered ? caps_ord : slot_caps;
                 Carve cv;
                 const size_t o_cand = cv.take(nwaves * ccap * sizeof(uint4));
                 const size_t o_ccnt = cv.take(nwaves * sizeof(uint32_t));
@@ -2051,7 +2065,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
                 // k_batch_verify stores every (pattern, segment) count; the
                 // ordered form only adds to the bins (zeroed here)
-                sb = make_sink_segments(db, n_patterns, (uint32_t)nout, slot_caps, /*zero_counts=*/ordered);
+                sb = make_sink_segments(db, n_patterns, (uint32_t)snout, caps, /*zero_counts=*/ordered);
                 const BatchIndex& bi = *bip;
                 const uint32_t* d_tab = reinterpret_cast<const uint32_t*>(d_batch + bi.o_table);
                 BatchScanArgs sa{db->hl, db->ntiles, d_tab, bi.omax, (uint32_t)tpw, (uint32_t)nwaves, ccap,
@@ -2070,6 +2084,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                    reinterpret_cast<uint64_t*>(rbase + o_x), reinterpret_cast<uint32_t*>(rbase + o_xcnt),
                                    (uint32_t)xcap};
                 uint32_t* d_ocnt = reinterpret_cast<uint32_t*>(rbase + o_ocnt);
+                va.sink_segs = (uint32_t)snout;
+                // the exception pass's segment of a start: all in one with snout 1
+                const uint64_t oth_tiles = ordered ? (uint64_t)UINT32_MAX : tpw * wpo;
                 if (ordered) {
                     va.ord_out = reinterpret_cast<uint64_t*>(rbase + o_ord);
                     va.ord_cnt = d_ocnt;
@@ -2090,11 +2107,11 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 }
                 batch_launch(sa, va, nblocks, s, jev.back()->a, jev.back()->b);
                 if (conc) {
-                    launch_others(chunks[0], db->exc, sb, nout, tpw * wpo);
+                    launch_others(chunks[0], db->exc, sb, snout, oth_tiles);
                     HIPCHK(hipEventRecord(db->exc_join, db->exc));
                     HIPCHK(hipStreamWaitEvent(s, db->exc_join, 0));
                 } else if (exc) {
-                    launch_others(chunks[0], s, sb, nout, tpw * wpo);
+                    launch_others(chunks[0], s, sb, snout, oth_tiles);
                 }
                 if (ordered) {
                     uint32_t* hp = static_cast<uint32_t*>(reserve_host(db, db->pin_ord, (nlists + 1) * sizeof(uint32_t)));
@@ -2121,14 +2138,18 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     done = true;
                     std::lock_guard<std::mutex> lk(g_cap_mu);
                     if (g_cap_hint.size() > 256) g_cap_hint.clear();
-                    g_cap_hint[{db, cap_key}] = {slot_caps, ccap};
+                    g_cap_hint[{db, ordered ? cap_key + "|ord" : cap_key}] = {caps, ccap};
                     if (g_ord_hint.size() > 256) g_ord_hint.clear();
                     g_ord_hint[{db, cap_key}] = ord_cap;
                     if (ordered) {
                         hit_list = ordered_to_hits(db, sb, counts, total, va.ord_out, ord_cap, d_ocnt, ord_h, nlists,
                                                    n_patterns);
                         total = hit_list->count;
-                        if (total) {
+                        if (report) {
+                            // the report pass reads each key's length by pattern
+                            // and writes the kept ones' (no lens pass)
+                            hit_list->plen = reinterpret_cast<const int32_t*>(d_up + o_len);
+                        } else if (total) {
                             hipLaunchKernelGGL(k_linear_lens, dim3(blocks_for(total, 256)), dim3(256), 0, s,
                                                hit_list->keys, total, reinterpret_cast<const int32_t*>(d_up + o_len),
                                                hit_list->lens);
@@ -2141,10 +2162,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 if (overflow) {
                     uint64_t keys_total = 0;
                     for (int p = 0; p < n_patterns; ++p) {
-                        const uint32_t* c = counts.data() + (uint64_t)p * nout;
-                        const uint32_t m = *std::max_element(c, c + nout);
-                        while (slot_caps[p] < m) slot_caps[p] *= 2;
-                        keys_total += (uint64_t)slot_caps[p] * nout;
+                        const uint32_t* c = counts.data() + (uint64_t)p * snout;
+                        const uint32_t m = *std::max_element(c, c + snout);
+                        while (caps[p] < m) caps[p] *= 2;
+                        keys_total += (uint64_t)caps[p] * snout;
                     }
                     require(keys_total * 8 <= (16ull << 30), "hit list larger than 16 GB of segments",
                             PM_E_UNSUPPORTED);

@@ -935,6 +935,13 @@ __device__ inline uint64_t block_sum(uint64_t v, uint64_t* red) {
     return r;
 }
 
+// fixed lengths by pattern, no anchors: a valid candidate's rep_val is
+// monotone along the (pattern, start)-sorted list (the end grows with the
+// start; a region's cap of it too)
+__device__ inline bool rep_monotone(const RepArgs& a) {
+    return a.plen && !(a.flags & (PM_ANCHOR_START | PM_ANCHOR_END));
+}
+
 // per chunk: the largest (pattern, end) of a valid candidate; the kept
 // counters start at 0
 __global__ __launch_bounds__(REP_T) void k_rep_max(RepArgs a) {
@@ -1005,8 +1012,30 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     const bool anch = (a.flags & PM_ANCHOR_START) != 0;
     // running maximum of every chunk before this one
     uint64_t carry = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
-    carry = block_max(carry, red);
+    if (rep_monotone(a)) {
+        // lengths by pattern and no anchors: a valid candidate's (pattern,
+        // end) never decreases along the list, so the running maximum is the
+        // last valid candidate's (no k_rep_max pass)
+        if (threadIdx.x == 0) {
+            uint64_t c = 0;
+            for (uint64_t j = b0; j-- > 0;) {
+                const uint64_t kj = a.keys[j];
+                const uint32_t lj = rep_len(a, j, kj);
+                const bool nj = rep_near(a, kj);
+                if (rep_valid(a, kj, lj, nj)) {
+                    c = rep_val(a, kj, lj, nj);
+                    break;
+                }
+            }
+            red[0] = c;
+        }
+        __syncthreads();
+        carry = red[0];
+        __syncthreads();
+    } else {
+        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
+        carry = block_max(carry, red);
+    }
     uint64_t own = 0;   // kept candidates of this chunk found by this thread's walks
     // A tile is REP_T * RW candidates, RW consecutive ones per thread: the
     // block's serial chain of tiles (a load, the scan's exchange, two
@@ -1261,7 +1290,10 @@ void report_enqueue_ws(pm_db* db, pm_hits* h, uint32_t flags, const ReportWs& ws
         // reads the file's own bytes, regions included
         xt_launch(*xt, h->keys, h->lens, a.total_d, a.total_h, a.acc, a.bcnt, G, text_view(db), s);
     } else {
-        hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
+        if (h->plen && !(flags & (PM_ANCHOR_START | PM_ANCHOR_END)) && (flags & PM_REPORT_NRGREP))
+            HIPCHK(hipMemsetAsync(a.bcnt, 0, G * sizeof(uint32_t), s));   // rep_monotone: no k_rep_max
+        else
+            hipLaunchKernelGGL(k_rep_max, dim3(G), dim3(REP_T), 0, s, a);
         hipLaunchKernelGGL(k_rep_walk, dim3(G), dim3(REP_T), 0, s, a);
     }
     if (done)

@@ -275,10 +275,13 @@ def main():
 
     def collect(h):
         try:
-            keys, lens = shards.hits_to_tensors(h, device)
             ms = engine.kernel_ms(h)
-        finally:
+        except BaseException:
             engine.destroy_hits(h)
+            raise
+        # the list's own device buffers become the tensors (no copy; they
+        # destroy the list when freed)
+        keys, lens = shards.hits_as_tensors(h, device)
         keys = shards.to_global(keys, offset)
         # substitutions only: every hit of pattern p is prog.m long, so only
         # the keys travel (to rank 0, which rebuilds the lengths)

@@ -318,6 +318,12 @@ int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst
  * uint32 lengths), for a caller that gathers hits across GPUs itself.   */
 int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count);
 
+/* The caller's last use of the buffers pm_hits_device returned: work queued
+ * on `stream` (hipStream_t) up to now.  pm_hits_destroy then recycles the
+ * buffers only after that work (e.g. tensors wrapping them, freed while a
+ * framework's kernels still read them).  Like pm_hits_copy_device's use. */
+int pm_hits_record_use(const pm_hits* h, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,7 +33,7 @@ EXPORTED = (
     "pm_last_error", "pm_version", "pm_device_count", "pm_db_create",
     "pm_db_create_synthetic", "pm_db_destroy", "pm_db_info", "pm_db_decode",
     "pm_scan_linear", "pm_scan_nfa", "pm_hits_count", "pm_hits_copy",
-    "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device",
+    "pm_hits_kernel_ms", "pm_hits_destroy", "pm_hits_device", "pm_hits_copy_device", "pm_hits_record_use",
     "pm_linear_jit_compile", "pm_scan_nfa_errs", "pm_scan_linear_async", "pm_scan_nfa_wide",
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
     "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes", "pm_scan_nfa_tree",
@@ -96,6 +96,7 @@ def _declare(lib):
     lib.pm_hits_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_double)]
     lib.pm_hits_destroy.argtypes = [P]
     lib.pm_hits_device.argtypes = [P, PP, PP, pu64]
+    lib.pm_hits_record_use.argtypes = [P, P]
     lib.pm_hits_copy_device.argtypes = [P, P, P, u64, P]
     lib.pm_esimple_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
     lib.pm_linear_jit_compile.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, P, ctypes.c_int, pu64]

@@ -1396,6 +1396,16 @@ int pm_hits_copy_device(const pm_hits* h, uint64_t* keys_dst, uint32_t* lens_dst
     });
 }
 
+int pm_hits_record_use(const pm_hits* h, void* stream) {
+    return guarded([&] {
+        require(h != nullptr, "hits is NULL");
+        DeviceGuard g(h->device);
+        pm_hits* hm = const_cast<pm_hits*>(h);
+        if (!hm->last_use) HIPCHK(hipEventCreateWithFlags(&hm->last_use, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(hm->last_use, (hipStream_t)stream));
+    });
+}
+
 int pm_hits_kernel_ms(const pm_hits* h, double* ms) {
     return guarded([&] {
         require(h != nullptr && ms != nullptr, "null argument");

@@ -32,6 +32,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 import torch.distributed as dist
+import torch.utils.dlpack
 
 POS_BITS = 48
 POS_MASK = (1 << POS_BITS) - 1
@@ -152,6 +153,100 @@ def _merge(parts, k, ln):
     out_k[dest] = k
     out_l[dest] = ln
     return out_k, out_l
+
+
+# --- zero-copy hand-over of a hit list (DLPack) ------------------------------
+import ctypes as _ct
+
+
+class _DLDevice(_ct.Structure):
+    _fields_ = [("device_type", _ct.c_int32), ("device_id", _ct.c_int32)]
+
+
+class _DLDataType(_ct.Structure):
+    _fields_ = [("code", _ct.c_uint8), ("bits", _ct.c_uint8), ("lanes", _ct.c_uint16)]
+
+
+class _DLTensor(_ct.Structure):
+    _fields_ = [("data", _ct.c_void_p), ("device", _DLDevice), ("ndim", _ct.c_int32), ("dtype", _DLDataType),
+                ("shape", _ct.POINTER(_ct.c_int64)), ("strides", _ct.POINTER(_ct.c_int64)),
+                ("byte_offset", _ct.c_uint64)]
+
+
+_DL_DELETER = _ct.CFUNCTYPE(None, _ct.c_void_p)
+
+
+class _DLManagedTensor(_ct.Structure):
+    _fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", _ct.c_void_p), ("deleter", _DL_DELETER)]
+
+
+_KDL_ROCM, _KDL_INT, _KDL_UINT = 10, 0, 1
+_LIVE = {}    # DLManagedTensor address -> (struct, shape, owner, device)
+_OWNERS = {}  # hit-list handle -> tensors still alive
+
+
+@_DL_DELETER
+def _dl_release(addr):
+    entry = _LIVE.pop(addr, None)
+    if entry is None:
+        return
+    h, dev = entry[2], entry[3]
+    _OWNERS[h] -= 1
+    if _OWNERS[h] == 0:
+        del _OWNERS[h]
+        from . import _lib
+        lib = _lib.load()
+        try:
+            # torch frees external memory at once: the buffers go back to
+            # the pool only after the work queued on torch's stream so far
+            lib.pm_hits_record_use(_ct.c_void_p(h), _ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        finally:
+            lib.pm_hits_destroy(_ct.c_void_p(h))
+
+
+_capsule_new = _ct.pythonapi.PyCapsule_New
+_capsule_new.restype = _ct.py_object
+_capsule_new.argtypes = [_ct.c_void_p, _ct.c_char_p, _ct.c_void_p]
+
+
+def _dl_tensor(h: int, ptr: int, n: int, bits: int, device: torch.device) -> torch.Tensor:
+    shape = (_ct.c_int64 * 1)(n)
+    mt = _DLManagedTensor()
+    mt.dl_tensor.data = ptr
+    mt.dl_tensor.device = _DLDevice(_KDL_ROCM, device.index if device.index is not None else 0)
+    mt.dl_tensor.ndim = 1
+    mt.dl_tensor.dtype = _DLDataType(_KDL_INT, bits, 1)
+    mt.dl_tensor.shape = shape
+    mt.dl_tensor.strides = None
+    mt.dl_tensor.byte_offset = 0
+    mt.deleter = _dl_release
+    addr = _ct.addressof(mt)
+    _LIVE[addr] = (mt, shape, h, device)
+    _OWNERS[h] = _OWNERS.get(h, 0) + 1
+    try:
+        return torch.utils.dlpack.from_dlpack(_capsule_new(addr, b"dltensor", None))
+    except Exception:
+        _dl_release(addr)
+        raise
+
+
+def hits_as_tensors(hits_handle, device: torch.device):
+    """A ``pm_hits`` list's own device buffers as torch tensors (keys int64,
+    lens int32), no copy: the tensors take the list over and destroy it
+    (``pm_hits_destroy``) when both are freed -- the caller must not destroy
+    it.  An empty list is destroyed at once."""
+    from . import _lib
+    lib = _lib.load()
+    keys_p, lens_p, n = _ct.c_void_p(), _ct.c_void_p(), _ct.c_uint64()
+    # waits for the list's producing work (the pointers are read by torch's streams)
+    _lib.check(lib.pm_hits_device(hits_handle, _ct.byref(keys_p), _ct.byref(lens_p), _ct.byref(n)))
+    h = hits_handle.value if isinstance(hits_handle, _ct.c_void_p) else int(hits_handle)
+    if n.value == 0:
+        _lib.check(lib.pm_hits_destroy(_ct.c_void_p(h)))
+        return (torch.empty(0, dtype=torch.int64, device=device), torch.empty(0, dtype=torch.int32, device=device))
+    keys = _dl_tensor(h, keys_p.value, n.value, 64, device)
+    lens = _dl_tensor(h, lens_p.value, n.value, 32, device)
+    return keys, lens
 
 
 def hits_to_tensors(hits_handle, device: torch.device):

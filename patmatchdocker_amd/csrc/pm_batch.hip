@@ -358,8 +358,8 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
 // candidate with more than VH matches sets ord_bad (the host then runs the
 // unordered form); matches of the next segment go to xkeys and those keys,
 // like the exception pass's, to the (pattern, segment) bins.
-constexpr int VH = 8;
-template <bool HASH>
+constexpr int VH = 4;
+template <bool HASH, bool PF>
 __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     __shared__ uint64_t s_hash[HASH ? BQ_HASH_SLOTS : 1];
     __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
@@ -406,15 +406,33 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     };
     (void)at;
     // a round: candidate base + u * 64 + lane (coalesced loads); its matches
-    // leave per u, in (u, lane) order = position order
+    // leave per u, in (u, lane) order = position order.  The next round's
+    // candidates are loaded while this round's lookups run (PF).
+    uint4 ne[VU];
+    if constexpr (PF) {
+#pragma unroll
+        for (int u = 0; u < VU; ++u) {
+            const uint32_t q = q0 + u * 64 + lane;
+            ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
     for (uint32_t base = q0; base < q1; base += 64 * VU) {
         uint4 e[VU], h[VU], mk[VU];
         uint32_t co[VU];
         uint64_t lf[VU];
+        if constexpr (PF) {
 #pragma unroll
-        for (int u = 0; u < VU; ++u) {
-            const uint32_t q = base + u * 64 + lane;
-            e[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
+            for (int u = 0; u < VU; ++u) {
+                e[u] = ne[u];
+                const uint32_t q = base + 64 * VU + u * 64 + lane;
+                ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < VU; ++u) {
+                const uint32_t q = base + u * 64 + lane;
+                e[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
+            }
         }
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
@@ -635,8 +653,13 @@ void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t n
     static const bool hash_on = !(getenv("PM_BATCH_HASH") && getenv("PM_BATCH_HASH")[0] == '0');
     const bool hash = va.hash && hash_on;
     if (va.ord_out)
-        hipLaunchKernelGGL(hash ? k_batch_verify_ord<true> : k_batch_verify_ord<false>, dim3(va.nout), dim3(1024), 0, s,
-                           va);
+    {
+        // PM_BATCH_VPF=0: no prefetch of the next round's candidates (A/B)
+        static const bool pf = !(getenv("PM_BATCH_VPF") && getenv("PM_BATCH_VPF")[0] == '0');
+        auto kern = hash ? (pf ? k_batch_verify_ord<true, true> : k_batch_verify_ord<true, false>)
+                         : (pf ? k_batch_verify_ord<false, true> : k_batch_verify_ord<false, false>);
+        hipLaunchKernelGGL(kern, dim3(va.nout), dim3(1024), 0, s, va);
+    }
     else
         hipLaunchKernelGGL(hash ? k_batch_verify<true> : k_batch_verify<false>, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());

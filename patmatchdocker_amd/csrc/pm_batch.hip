@@ -434,25 +434,33 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
                 e[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
             }
         }
+        // the candidates' first hash slots read together (their tiles' lane
+        // flags in flight meanwhile), then the rare further probes
+        uint32_t hh[VU], code[VU];
+        uint64_t sl[VU];
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             const bool ok = base + u * 64 + lane < q1;
-            const uint32_t code = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
+            code[u] = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
             co[u] = 0u;
             if constexpr (HASH) {
-                if (ok)
-                    for (uint32_t hh = bq_hash(code);; hh = (hh + 1) & (BQ_HASH_SLOTS - 1)) {
-                        const uint64_t sl = s_hash[hh];
-                        if (sl == ~0ull) break;
-                        if ((uint32_t)(sl & 0xFFFFFu) == code) {
-                            co[u] = (uint32_t)((sl >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl >> 44);
-                            break;
-                        }
-                    }
+                hh[u] = bq_hash(code[u]);
+                sl[u] = ok ? s_hash[hh[u]] : ~0ull;
             } else {
-                co[u] = ok ? a.code_off[code] : 0u;
+                co[u] = ok ? a.code_off[code[u]] : 0u;
             }
             lf[u] = ok && e[u].x < a.ntiles ? a.lflag[e[u].x] : 0ull;
+        }
+        if constexpr (HASH) {
+#pragma unroll
+            for (int u = 0; u < VU; ++u) {
+                // a candidate's code is present: the probe ends there (an empty slot: none)
+                while (sl[u] != ~0ull && (uint32_t)(sl[u] & 0xFFFFFu) != code[u]) {
+                    hh[u] = (hh[u] + 1) & (BQ_HASH_SLOTS - 1);
+                    sl[u] = s_hash[hh[u]];
+                }
+                if (sl[u] != ~0ull) co[u] = (uint32_t)((sl[u] >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl[u] >> 44);
+            }
         }
 #pragma unroll
         for (int u = 0; u < VU; ++u) {

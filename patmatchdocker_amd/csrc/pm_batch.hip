@@ -359,11 +359,17 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
 // unordered form); matches of the next segment go to xkeys and those keys,
 // like the exception pass's, to the (pattern, segment) bins.
 constexpr int VH = 4;
-template <bool HASH, bool PF>
+// HIST: each wave also counts its list's keys per pattern (LDS), stored as
+// ord_hist[p][list]: the host's stable scatter by pattern needs no
+// histogram pass (patterns <= ORD_HIST_MAX_P).
+template <bool HASH, bool HIST>
 __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     __shared__ uint64_t s_hash[HASH ? BQ_HASH_SLOTS : 1];
     __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
+    __shared__ uint32_t s_hist[HIST ? BATCH_VERIFY_WAVES : 1][HIST ? ORD_HIST_MAX_P : 1];
     const uint32_t og = blockIdx.x;
+    if constexpr (HIST)
+        for (uint32_t i = threadIdx.x; i < BATCH_VERIFY_WAVES * ORD_HIST_MAX_P; i += blockDim.x) (&s_hist[0][0])[i] = 0u;
     if constexpr (HASH)
         for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
     // (the bins of the exception pass, xkeys and first starts are zeroed by
@@ -407,32 +413,23 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     (void)at;
     // a round: candidate base + u * 64 + lane (coalesced loads); its matches
     // leave per u, in (u, lane) order = position order.  The next round's
-    // candidates are loaded while this round's lookups run (PF).
+    // candidates are loaded while this round's lookups run (verify 2.14 ->
+    // 2.00 ms on configs[4]).
     uint4 ne[VU];
-    if constexpr (PF) {
 #pragma unroll
-        for (int u = 0; u < VU; ++u) {
-            const uint32_t q = q0 + u * 64 + lane;
-            ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
-        }
+    for (int u = 0; u < VU; ++u) {
+        const uint32_t q = q0 + u * 64 + lane;
+        ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
     }
     for (uint32_t base = q0; base < q1; base += 64 * VU) {
         uint4 e[VU], h[VU], mk[VU];
         uint32_t co[VU];
         uint64_t lf[VU];
-        if constexpr (PF) {
 #pragma unroll
-            for (int u = 0; u < VU; ++u) {
-                e[u] = ne[u];
-                const uint32_t q = base + 64 * VU + u * 64 + lane;
-                ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < VU; ++u) {
-                const uint32_t q = base + u * 64 + lane;
-                e[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
-            }
+        for (int u = 0; u < VU; ++u) {
+            e[u] = ne[u];
+            const uint32_t q = base + 64 * VU + u * 64 + lane;
+            ne[u] = q < q1 ? *at_k(q) : make_uint4(0u, 0u, 0u, 0u);
         }
         // the candidates' first hash slots read together (their tiles' lane
         // flags in flight meanwhile), then the rare further probes
@@ -500,10 +497,19 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
 #pragma unroll
             for (int t = 0; t < VH; ++t)
                 if ((uint32_t)t < nh && at0 + t < a.ord_cap) out[at0 + t] = hk[t];
+            if constexpr (HIST) {
+#pragma unroll
+                for (int t = 0; t < VH; ++t)
+                    if ((uint32_t)t < nh) atomicAdd(&s_hist[wv][(uint32_t)(hk[t] >> 48)], 1u);
+            }
             wcnt += tot;
         }
     }
     if (lane == 0) a.ord_cnt[list] = wcnt;
+    if constexpr (HIST) {
+        const uint64_t nl = (uint64_t)a.nout * NWV;
+        for (uint32_t p = lane; p < (uint32_t)a.P; p += 64) a.ord_hist[p * nl + list] = s_hist[wv][p];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_batch_fixup(BatchVerifyArgs a) {
@@ -660,15 +666,12 @@ void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t n
     // PM_BATCH_HASH=0: the code_off array (A/B)
     static const bool hash_on = !(getenv("PM_BATCH_HASH") && getenv("PM_BATCH_HASH")[0] == '0');
     const bool hash = va.hash && hash_on;
-    if (va.ord_out)
-    {
-        // PM_BATCH_VPF=0: no prefetch of the next round's candidates (A/B)
-        static const bool pf = !(getenv("PM_BATCH_VPF") && getenv("PM_BATCH_VPF")[0] == '0');
-        auto kern = hash ? (pf ? k_batch_verify_ord<true, true> : k_batch_verify_ord<true, false>)
-                         : (pf ? k_batch_verify_ord<false, true> : k_batch_verify_ord<false, false>);
+    if (va.ord_out) {
+        const bool hist = va.ord_hist != nullptr;
+        auto kern = hash ? (hist ? k_batch_verify_ord<true, true> : k_batch_verify_ord<true, false>)
+                         : (hist ? k_batch_verify_ord<false, true> : k_batch_verify_ord<false, false>);
         hipLaunchKernelGGL(kern, dim3(va.nout), dim3(1024), 0, s, va);
-    }
-    else
+    } else
         hipLaunchKernelGGL(hash ? k_batch_verify<true> : k_batch_verify<false>, dim3(va.nout), dim3(1024), 0, s, va);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_batch_fixup, dim3(64), dim3(256), 0, s, va);

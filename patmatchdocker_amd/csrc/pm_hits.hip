@@ -264,6 +264,52 @@ __global__ void k_gather_lists(const uint64_t* __restrict__ ord, uint32_t cap, c
     const uint64_t* src = ord + (uint64_t)l * cap;
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[o + i] = src[i];
 }
+// The lists' keys to their (pattern, position) places: one wave per list,
+// its keys in list order (= position order), 4 x 64 per round.  Per
+// sub-round the lanes holding the same pattern find each other (a ballot
+// per pattern bit), take base[p] + their rank among them, and the group's
+// last lane advances base[p] (LDS, this wave's alone): a stable scatter, no
+// sort.  base[p] starts at the exclusive scan of keys per (pattern, list)
+// in pattern-major order.
+constexpr uint32_t SCAT_U = 4;
+__global__ __launch_bounds__(64) void k_list_scatter(const uint64_t* __restrict__ ord, uint32_t cap,
+                                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                                                     uint32_t nlists, uint32_t P, uint32_t pbits,
+                                                     uint64_t* __restrict__ dst) {
+    __shared__ uint32_t base[ORD_HIST_MAX_P];
+    const uint32_t l = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t p = lane; p < P; p += 64) base[p] = off[(uint64_t)p * nlists + l];
+    __syncthreads();
+    const uint32_t c = min(cnt[l], cap);
+    const uint64_t* src = ord + (uint64_t)l * cap;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;   // lanes under this one
+    uint64_t nk[SCAT_U];
+#pragma unroll
+    for (uint32_t u = 0; u < SCAT_U; ++u) nk[u] = u * 64 + lane < c ? src[u * 64 + lane] : 0ull;
+    for (uint32_t i0 = 0; i0 < c; i0 += 64 * SCAT_U) {
+        uint64_t k[SCAT_U];
+#pragma unroll
+        for (uint32_t u = 0; u < SCAT_U; ++u) {   // this round's keys; the next round's in flight
+            k[u] = nk[u];
+            const uint32_t i = i0 + 64 * SCAT_U + u * 64 + lane;
+            nk[u] = i < c ? src[i] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < SCAT_U; ++u) {
+            const bool valid = i0 + u * 64 + lane < c;
+            const uint32_t p = (uint32_t)(k[u] >> 48);
+            uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+            for (uint32_t b = 0; b < pbits; ++b) {
+                const uint64_t bb = __builtin_amdgcn_ballot_w64((p >> b) & 1u);
+                peers &= ((p >> b) & 1u) ? bb : ~bb;
+            }
+            if (valid) {
+                dst[base[p] + (uint32_t)__builtin_popcountll(peers & below)] = k[u];
+                if (!(peers >> lane >> 1)) base[p] += (uint32_t)__builtin_popcountll(peers);   // the group's last lane
+            }
+        }
+    }
+}
 struct ListCount {
     const uint32_t* cnt;
     uint32_t cap;
@@ -716,7 +762,7 @@ void retire_buffers(pm_hits* h, hipStream_t s);   // below (report pass)
 
 pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t sink_total,
                          const uint64_t* ord, uint32_t ord_cap, const uint32_t* d_cnt, const uint32_t* cnt,
-                         uint32_t nlists, int n_patterns) {
+                         uint32_t nlists, int n_patterns, const uint32_t* d_hist) {
     uint64_t t1 = 0;
     for (uint32_t l = 0; l < nlists; ++l) t1 += std::min(cnt[l], ord_cap);
     // the sink first (its sort reserves ws_post itself)
@@ -739,30 +785,44 @@ pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uin
             auto counted = hipcub::TransformInputIterator<uint64_t, ListCount, hipcub::CountingInputIterator<uint32_t>>(
                 hipcub::CountingInputIterator<uint32_t>(0u), ListCount{d_cnt, ord_cap});
             size_t scan_bytes = 0, sort_bytes = 0, merge_bytes = 0;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)nlists, s));
-            HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                     (int)t1, 48, 48 + (int)slot_bits, s));
+            const uint64_t nh = d_hist ? (uint64_t)n_patterns * nlists : 0;
+            if (d_hist) {   // keys per (pattern, list) -> their first places
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_hist, (uint32_t*)nullptr, (int)nh, s));
+            } else {
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)nlists, s));
+                HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                         (int)t1, 48, 48 + (int)slot_bits, s));
+            }
             if (hs)
                 HIPCHK(rocprim::merge(nullptr, merge_bytes, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
                                       (uint64_t*)nullptr, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
             (void)hipGetLastError();   // rocPRIM's stale capture status (sink_to_hits)
             Carve c;
-            const size_t o_off = c.take(nlists * sizeof(uint64_t));
+            const size_t o_off = c.take(d_hist ? nh * sizeof(uint32_t) : nlists * sizeof(uint64_t));
             const size_t o_scan = c.take(scan_bytes);
-            const size_t o_in = c.take(t1 * sizeof(uint64_t));
+            const size_t o_in = c.take(d_hist ? 0 : t1 * sizeof(uint64_t));
             const size_t o_mid = c.take(hs ? t1 * sizeof(uint64_t) : 0);
             const size_t o_tmp = c.take(std::max(sort_bytes, merge_bytes));
             uint8_t* base = static_cast<uint8_t*>(reserve(db, db->ws_post, c.off));
             uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
             uint64_t* in = reinterpret_cast<uint64_t*>(base + o_in);
             uint64_t* sorted = hs ? reinterpret_cast<uint64_t*>(base + o_mid) : h->keys;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)nlists, s));
-            (void)hipGetLastError();
-            hipLaunchKernelGGL(k_gather_lists, dim3(nlists), dim3(256), 0, s, ord, ord_cap, d_cnt, d_off, in);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, in, sorted, (int)t1, 48,
-                                                     48 + (int)slot_bits, s));
-            (void)hipGetLastError();
+            if (d_hist) {
+                uint32_t* d_poff = reinterpret_cast<uint32_t*>(base + o_off);
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, d_hist, d_poff, (int)nh, s));
+                (void)hipGetLastError();
+                hipLaunchKernelGGL(k_list_scatter, dim3(nlists), dim3(64), 0, s, ord, ord_cap, d_cnt, d_poff, nlists,
+                                   (uint32_t)n_patterns, slot_bits, sorted);
+                HIPCHK(hipGetLastError());
+            } else {
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)nlists, s));
+                (void)hipGetLastError();
+                hipLaunchKernelGGL(k_gather_lists, dim3(nlists), dim3(256), 0, s, ord, ord_cap, d_cnt, d_off, in);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, in, sorted, (int)t1, 48,
+                                                         48 + (int)slot_bits, s));
+                (void)hipGetLastError();
+            }
             if (hs) {
                 HIPCHK(rocprim::merge(base + o_tmp, merge_bytes, (const uint64_t*)sorted, (const uint64_t*)hs->keys,
                                       h->keys, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));

@@ -522,6 +522,7 @@ constexpr int BATCH_MAX_P = 1024;
 constexpr int BATCH_MAX_LEN = 16;                          // a window's bases fit one 32-bit code word
 constexpr uint32_t BATCH_MAX_WPO = 64;                     // scan waves per output segment
 constexpr uint32_t BATCH_VERIFY_WAVES = 16;                // waves per verify block (one per segment)
+constexpr uint32_t ORD_HIST_MAX_P = 256;                   // patterns counted per list by the ordered verify
 constexpr uint64_t BATCH_MAX_EXPANSIONS = 1ull << 18;      // indexed codes (a quarter of the table)
 
 struct BatchIndex {
@@ -593,6 +594,7 @@ struct BatchVerifyArgs {
     uint32_t* ord_bad = nullptr;
     uint32_t ord_cap = 0;
     uint32_t sink_segs = 0;   // segments per pattern of the bins k_batch_fixup fills (0: nout)
+    uint32_t* ord_hist = nullptr;   // [P][nout * BATCH_VERIFY_WAVES] keys per (pattern, list); null: none
 };
 // k_batch_scan (timed by ev_a / ev_b), k_batch_verify, k_batch_fixup on s
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
@@ -671,9 +673,11 @@ void discard_hits(pm_hits* h);   // buffers back to the pool (no event waits)
 // the next segment, the first starts) into one (pattern, position)-sorted
 // list: one stable radix pass over the pattern bits, the sink sorted by
 // sink_to_hits, a merge of the two.  Lens are the caller's.
+// d_hist (may be null): keys per (pattern, list), [P][nlists] -- then a
+// stable scatter by pattern replaces the radix sort.
 pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t sink_total,
                          const uint64_t* ord, uint32_t ord_cap, const uint32_t* d_cnt, const uint32_t* cnt,
-                         uint32_t nlists, int n_patterns);
+                         uint32_t nlists, int n_patterns, const uint32_t* d_hist = nullptr);
 pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32_t>& counts, uint64_t total,
                       const int32_t* slot_len = nullptr, bool* lens_done = nullptr);
 // records h->ready on the db stream: call after the last kernel filling h

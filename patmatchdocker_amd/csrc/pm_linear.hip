@@ -2031,6 +2031,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             // verify wave) a position-ordered list of ord_cap keys
             const bool ord_env = !(getenv("PM_BATCH_ORDERED") && getenv("PM_BATCH_ORDERED")[0] == '0');
             const bool exc_conc = !(getenv("PM_BATCH_EXC_CONC") && getenv("PM_BATCH_EXC_CONC")[0] == '0');
+            const bool scatter_env = !(getenv("PM_BATCH_SCATTER") && getenv("PM_BATCH_SCATTER")[0] == '0');
             bool ordered = ord_env;
             const uint32_t nlists = (uint32_t)nout * BATCH_VERIFY_WAVES;
             uint32_t ord_cap = 1024;
@@ -2062,6 +2063,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 const size_t o_x = cv.take(xcap * sizeof(uint64_t));
                 const size_t o_ocnt = cv.take((nlists + 1) * sizeof(uint32_t));   // + the overflow flag
                 const size_t o_ord = cv.take(ordered ? (uint64_t)nlists * ord_cap * sizeof(uint64_t) : 0);
+                // keys per (pattern, list): the stable scatter instead of a radix sort
+                // (PM_BATCH_SCATTER=0: the radix sort, A/B)
+                const bool hist = ordered && n_patterns <= (int)ORD_HIST_MAX_P && scatter_env;
+                const size_t o_hist = cv.take(hist ? (uint64_t)n_patterns * nlists * sizeof(uint32_t) : 0);
                 uint8_t* rbase = static_cast<uint8_t*>(reserve(db, db->ws_rec, cv.off));
                 // k_batch_verify stores every (pattern, segment) count; the
                 // ordered form only adds to the bins (zeroed here)
@@ -2092,6 +2097,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     va.ord_cnt = d_ocnt;
                     va.ord_bad = d_ocnt + nlists;
                     va.ord_cap = ord_cap;
+                    if (hist) va.ord_hist = reinterpret_cast<uint32_t*>(rbase + o_hist);
                     HIPCHK(hipMemsetAsync(va.ord_bad, 0, sizeof(uint32_t), s));
                 }
                 jev.clear();
@@ -2143,7 +2149,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     g_ord_hint[{db, cap_key}] = ord_cap;
                     if (ordered) {
                         hit_list = ordered_to_hits(db, sb, counts, total, va.ord_out, ord_cap, d_ocnt, ord_h, nlists,
-                                                   n_patterns);
+                                                   n_patterns, va.ord_hist);
                         total = hit_list->count;
                         if (report) {
                             // the report pass reads each key's length by pattern

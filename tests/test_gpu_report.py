@@ -278,7 +278,8 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
     every length 10..16 (different piece offsets o_p) + configs[4]'s motifs,
     every pattern's report list vs the oracle; and the same query with the
     filter off (PM_BATCH=0: the bit-sliced kernel in 8-pattern chunks) and
-    with the unordered verify (PM_BATCH_ORDERED=0).
+    with the unordered verify (PM_BATCH_ORDERED=0) and the ordered lists
+    radix sorted instead of scattered (PM_BATCH_SCATTER=0).
     minlen 11 also runs the stride-2 probes (PM_BATCH_STRIDE=2: every other
     position, two indexed pieces per pattern)."""
     import bench
@@ -300,6 +301,10 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
             monkeypatch.setenv("PM_BATCH_STRIDE", "2")
             res_s2, _ = engine.scan(db, progs, k=0, types="s")
             monkeypatch.delenv("PM_BATCH_STRIDE")
+        # the ordered lists sorted by a radix pass instead of the stable scatter
+        monkeypatch.setenv("PM_BATCH_SCATTER", "0")
+        res_radix, _ = engine.scan(db, progs, k=0, types="s")
+        monkeypatch.delenv("PM_BATCH_SCATTER")
         # the unordered verify (per-(pattern, segment) bins + sort)
         monkeypatch.setenv("PM_BATCH_ORDERED", "0")
         res_unord, _ = engine.scan(db, progs, k=0, types="s")
@@ -313,6 +318,7 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
         assert _pairs(r) == want, prog.source
         assert _pairs(rc) == want, prog.source
         assert _pairs(res_unord[i]) == want, prog.source
+        assert _pairs(res_radix[i]) == want, prog.source
         if res_s2 is not None:
             assert _pairs(res_s2[i]) == want, prog.source
         total += len(want)

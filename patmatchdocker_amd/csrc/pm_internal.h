@@ -70,6 +70,10 @@ void set_error(const std::string& msg);
 
 template <class F>
 int guarded(F&& f) {
+    // a status left on this thread by another library's call (a framework's,
+    // or rocPRIM's stale stream-capture query) is not this call's failure:
+    // the launch checks below report only what this call enqueues
+    (void)hipGetLastError();
     try {
         f();
         return PM_OK;

@@ -51,6 +51,13 @@ copy(os.path.join(root, "cfg3.log"), "%s_cfg3_query_ms.txt" % rnd)
 lin = pmc(["p1", "p2", "p3", "p4"], "pm_linear_jit")
 ids = pmc(["q1", "q2", "q3", "q4"], "pm_ids_rev")
 batch = pmc(["c1", "c2"], "k_batch_scan")
+# the same configs[4] passes hold every kernel of the step
+cfg4 = {"%s (configs[4], 256 patterns k=0)" % k: pmc(["c1", "c2"], k)
+        for k in ("k_batch_scan", "k_batch_verify_ord", "k_others_batch", "k_list_scatter", "k_rep_walk")}
+cfg4["note"] = ("medians per dispatch from tools/gpu_evidence.sh's configs[4] passes (two counter groups); "
+                "the exception pass runs beside the scan and verify on its own stream, so its and the verify's "
+                "cycles include that overlap")
+json.dump(cfg4, open(os.path.join(prof, "%s_cfg4_pmc.json" % rnd), "w"), indent=1)
 cal = pmc(["cal"], "k_read")
 bench = json.load(open(os.path.join(root, "bench.json")))
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]

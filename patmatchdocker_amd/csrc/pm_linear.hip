@@ -2034,7 +2034,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             const bool scatter_env = !(getenv("PM_BATCH_SCATTER") && getenv("PM_BATCH_SCATTER")[0] == '0');
             bool ordered = ord_env;
             const uint32_t nlists = (uint32_t)nout * BATCH_VERIFY_WAVES;
-            uint32_t ord_cap = 1024;
+            // (PM_BATCH_ORD_CAP: a smaller first capacity, for the tests of the
+            // grow-and-retry path)
+            uint32_t ord_cap = getenv("PM_BATCH_ORD_CAP") ? std::max(1, atoi(getenv("PM_BATCH_ORD_CAP"))) : 1024;
             {
                 std::lock_guard<std::mutex> lk(g_cap_mu);
                 auto it = g_ord_hint.find({db, cap_key});

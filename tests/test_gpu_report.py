@@ -323,3 +323,34 @@ def test_batch_filter_with_exceptions(engine, oracle_mod, monkeypatch, width, he
             assert _pairs(res_s2[i]) == want, prog.source
         total += len(want)
     assert total > 1000
+
+
+def test_ordered_batch_retries_and_falls_back(engine, oracle_mod, monkeypatch):
+    """The ordered batch verify's two escape paths, every pattern vs the
+    oracle: lists that overflow their first capacity (PM_BATCH_ORD_CAP=8:
+    grown and re-run), and a batch whose candidates match more patterns
+    than a lane keeps per candidate (the same motif eight times: the
+    unordered verify takes over)."""
+    import bench
+    monkeypatch.setenv("PM_JIT", "1")
+    text = _exception_rich_fasta(77, 2.0, 60, False)
+    motifs = bench.batch_patterns(24, seed=5)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        monkeypatch.setenv("PM_BATCH_ORD_CAP", "8")
+        progs = [compile_pattern(convert("-n", m)) for m in motifs]
+        res, _ = engine.scan(db, progs, k=0, types="s")
+        monkeypatch.delenv("PM_BATCH_ORD_CAP")
+        dup = [compile_pattern(convert("-n", motifs[0])) for _ in range(8)] + progs[1:12]
+        res_dup, _ = engine.scan(db, dup, k=0, types="s")
+    finally:
+        db.close()
+    total = 0
+    for prog, r in zip(progs, res):
+        want = oracle_mod.scan_threads(text, prog, 0, "s", skip_headers=True, threads=16, report="nrgrep")
+        assert _pairs(r) == want, prog.source
+        total += len(want)
+    assert total > 100   # ~16 lists of 8 keys: the first capacity overflows
+    for prog, r in zip(dup, res_dup):
+        want = oracle_mod.scan_threads(text, prog, 0, "s", skip_headers=True, threads=16, report="nrgrep")
+        assert _pairs(r) == want, prog.source

@@ -187,6 +187,13 @@ _OWNERS = {}  # hit-list handle -> tensors still alive
 
 @_DL_DELETER
 def _dl_release(addr):
+    try:
+        _dl_release_impl(addr)
+    except Exception:   # interpreter teardown: the module's globals may be gone
+        pass
+
+
+def _dl_release_impl(addr):
     entry = _LIVE.pop(addr, None)
     if entry is None:
         return
@@ -226,7 +233,7 @@ def _dl_tensor(h: int, ptr: int, n: int, bits: int, device: torch.device) -> tor
     try:
         return torch.utils.dlpack.from_dlpack(_capsule_new(addr, b"dltensor", None))
     except Exception:
-        _dl_release(addr)
+        _dl_release_impl(addr)
         raise
 
 

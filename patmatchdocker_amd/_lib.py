@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("PM_LIB_AB") or os.path.join(_HERE, "libpatmatch_hip.s
 
 PM_ALPHA_NUC = 0
 PM_ALPHA_BYTE = 1
+PM_E_ARG, PM_E_HIP, PM_E_NODEV = -1, -2, -3
 PM_E_UNSUPPORTED = -4
 PM_MAX_K = 15                 # errors, general patterns (<= 7 above 128 positions)
 PM_MAX_POSITIONS = 256        # automaton positions, general patterns

@@ -14,6 +14,14 @@ namespace pm {
 thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+void note_cleared_capture_status() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        fprintf(stderr, "patmatch_hip: cleared hipErrorStreamCaptureUnsupported left pending on the calling thread "
+                        "by an earlier call (not this library's)\n");
+    });
+}
+
 namespace {
 
 // code of a folded byte: 0..3 = A C G T, 4 = delimiter, 5 = other
@@ -462,10 +470,10 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipGetLastError());
     size_t tmp_bytes = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
-    (void)hipGetLastError();   // (rocPRIM's stale capture status, as below)
+    clear_stale_capture_status("rocPRIM call (pm_db)");   // (rocPRIM's stale capture status, as below)
     void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
-    (void)hipGetLastError();   // rocPRIM leaves a stale "stream is capturing" status behind
+    clear_stale_capture_status("rocPRIM call (pm_db)");   // rocPRIM leaves a stale "stream is capturing" status behind
     uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 16));
     HIPCHK(hipMemcpyAsync(h, db->sbbase + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h + 1, sbcnt + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
@@ -551,39 +559,41 @@ void free_db(pm_db* db) {
             db->pending.erase(h);   // the list stays unresolved (count 0)
         }
     }
-    if (db->stream) (void)hipStreamSynchronize(db->stream);
+    if (db->stream) quiet(hipStreamSynchronize(db->stream));
     if (db->post) {
-        (void)hipStreamSynchronize(db->post);
-        (void)hipStreamDestroy(db->post);
+        quiet(hipStreamSynchronize(db->post));
+        quiet(hipStreamDestroy(db->post));
     }
     if (db->exc) {
-        (void)hipStreamSynchronize(db->exc);
-        (void)hipStreamDestroy(db->exc);
+        quiet(hipStreamSynchronize(db->exc));
+        quiet(hipStreamDestroy(db->exc));
     }
     for (hipEvent_t e : {db->exc_fork, db->exc_join})
-        if (e) (void)hipEventDestroy(e);
+        if (e) quiet(hipEventDestroy(e));
     void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->hdr_end, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-    if (db->pin_down.p) (void)hipHostFree(db->pin_down.p);
-    if (db->pin_ord.p) (void)hipHostFree(db->pin_ord.p);
+        if (p) quiet(hipFree(p));
+    if (db->pin_down.p) quiet(hipHostFree(db->pin_down.p));
+    if (db->pin_ord.p) quiet(hipHostFree(db->pin_ord.p));
     for (pm_lane* l : {static_cast<pm_lane*>(db), &db->alt}) {
         for (void* p : {l->ws_tab.p, l->ws_sink.p, l->ws_rec.p, l->ws_rep.p, l->ws_oth.p})
-            if (p) (void)hipFree(p);
+            if (p) quiet(hipFree(p));
         for (void* p : {l->pin_up.p, l->pin_slots.p})
-            if (p) (void)hipHostFree(p);
+            if (p) quiet(hipHostFree(p));
         for (hipEvent_t e : {l->up_fence, l->slots_fence, l->free_ev})
-            if (e) (void)hipEventDestroy(e);
+            if (e) quiet(hipEventDestroy(e));
     }
-    if (db->own_stream && db->stream) (void)hipStreamDestroy(db->stream);
+    if (db->own_stream && db->stream) quiet(hipStreamDestroy(db->stream));
     delete db;
 }
 
 void check_device(int device) {
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw failure(PM_E_NODEV, "no HIP device");
+    const hipError_t e = hipGetDeviceCount(&ndev);
+    quiet(e);   // reported as PM_E_NODEV below, not left pending
+    if (e != hipSuccess || ndev == 0) throw failure(PM_E_NODEV, "no HIP device");
     require(device >= 0 && device < ndev, "device out of range");
 }
 
@@ -744,7 +754,7 @@ void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<ui
         HIPCHK(hipMemcpy(nt[3], near.data(), near.size() * 4, hipMemcpyHostToDevice));
     } catch (...) {
         for (void* p : nt)
-            if (p) (void)hipFree(p);
+            if (p) quiet(hipFree(p));
         throw;
     }
     HIPCHK(hipStreamSynchronize(db->stream));   // queued scans may still read the old table
@@ -772,7 +782,9 @@ int pm_device_count(int* count) {
     return guarded([&] {
         require(count != nullptr, "count is NULL");
         int c = 0;
-        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        const hipError_t e = hipGetDeviceCount(&c);
+        quiet(e);   // no device is an answer (0), not a status for the next call
+        if (e != hipSuccess) c = 0;
         *count = c;
     });
 }
@@ -839,8 +851,8 @@ int pm_db_create(const uint8_t* fasta, uint64_t n, int alphabet, int device, voi
         *out = db;
     });
     if (rc != PM_OK) {
-        if (db && db->stream) (void)hipStreamSynchronize(db->stream);
-        for (void* p : owned) (void)hipFree(p);
+        if (db && db->stream) quiet(hipStreamSynchronize(db->stream));
+        for (void* p : owned) quiet(hipFree(p));
         free_db(db);
     }
     return rc;
@@ -885,8 +897,8 @@ int pm_db_create_synthetic(uint64_t n_records, uint64_t rec_len, uint64_t seed, 
         *out = db;
     });
     if (rc != PM_OK) {
-        if (db && db->stream) (void)hipStreamSynchronize(db->stream);
-        for (void* p : owned) (void)hipFree(p);
+        if (db && db->stream) quiet(hipStreamSynchronize(db->stream));
+        for (void* p : owned) quiet(hipFree(p));
         free_db(db);
     }
     return rc;

@@ -360,15 +360,20 @@ std::map<size_t, std::vector<void*>> g_pinned;                 // capacity -> fr
 // events have completed, so pm_hits_destroy never blocks the host
 std::vector<pm_hits*> g_deferred;
 
-bool event_done(hipEvent_t e) { return !e || hipEventQuery(e) == hipSuccess; }
+bool event_done(hipEvent_t e) {
+    if (!e) return true;
+    const hipError_t q = hipEventQuery(e);
+    quiet(q);   // hipErrorNotReady is an answer, not a failure to leave pending
+    return q == hipSuccess;
+}
 
 bool hits_idle(const pm_hits* h) {
     return event_done(h->ready) && event_done(h->last_use) && (!h->pending || event_done(h->pending->counted));
 }
 
 void release_hits(pm_hits* h) {   // every event of h has completed
-    if (h->ready) (void)hipEventDestroy(h->ready);
-    if (h->last_use) (void)hipEventDestroy(h->last_use);
+    if (h->ready) quiet(hipEventDestroy(h->ready));
+    if (h->last_use) quiet(hipEventDestroy(h->last_use));
     delete h->pending;
     pool_put(h->device, h->keys, h->keys_cap);
     pool_put(h->device, h->lens, h->lens_cap);
@@ -425,7 +430,7 @@ void pinned_put(void* p, size_t cap) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     auto& v = g_pinned[cap];
     if (v.size() < 8) v.push_back(p);
-    else (void)hipHostFree(p);
+    else quiet(hipHostFree(p));
 }
 
 void* pool_get(int device, size_t bytes, size_t* cap) {
@@ -458,7 +463,7 @@ void pool_put(int device, void* p, size_t cap) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     auto& v = g_pool[{device, cap}];
     if (v.size() < 8) v.push_back(p);
-    else (void)hipFree(p);
+    else quiet(hipFree(p));
 }
 
 // Allocates out/cnt/slot arrays for n_slots slots of `per_slot` bins with
@@ -658,7 +663,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                                                      (int)total, 0, pack ? (int)(pos_bits + slot_bits) : 64, s));
         if (!inline_off)
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)sb.nbins, s));
-        (void)hipGetLastError();   // rocPRIM's stale capture status, size queries too (see the scan below)
+        clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status, size queries too (see the scan below)
         Carve c;
         const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
         const size_t o_scan = c.take(scan_bytes);
@@ -676,7 +681,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             // rocPRIM's scan leaves a stale "stream is capturing" status from
             // its capture query behind (the call itself succeeded): clear it so
             // the next launch check does not report it
-            (void)hipGetLastError();
+            clear_stale_capture_status("rocPRIM call (pm_hits)");
         }
         if (whole) {
             uint64_t* unsorted = reinterpret_cast<uint64_t*>(base + o_uns);
@@ -685,7 +690,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             HIPCHK(hipGetLastError());
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
                                                      pack ? (int)(pos_bits + slot_bits) : 64, s));
-            (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
+            clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (see the scan above)
             if (pack) {
                 hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
                                    pos_bits);
@@ -724,7 +729,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_hsort, hsort_bytes, hin, hout, (int)nhuge, 0,
                                                          pack ? (int)(pos_bits + slot_bits) : 64, s));
-                (void)hipGetLastError();   // rocPRIM's stale capture status (see the scan above)
+                clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (see the scan above)
                 hipLaunchKernelGGL(k_scatter_huge, dim3((uint32_t)huge.size()), dim3(1024), 0, s, hout, sh, d_hb,
                                    h->keys, slot_len, h->lens, pb);
                 HIPCHK(hipGetLastError());
@@ -796,7 +801,7 @@ pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uin
             if (hs)
                 HIPCHK(rocprim::merge(nullptr, merge_bytes, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
                                       (uint64_t*)nullptr, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
-            (void)hipGetLastError();   // rocPRIM's stale capture status (sink_to_hits)
+            clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (sink_to_hits)
             Carve c;
             const size_t o_off = c.take(d_hist ? nh * sizeof(uint32_t) : nlists * sizeof(uint64_t));
             const size_t o_scan = c.take(scan_bytes);
@@ -810,23 +815,23 @@ pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uin
             if (d_hist) {
                 uint32_t* d_poff = reinterpret_cast<uint32_t*>(base + o_off);
                 HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, d_hist, d_poff, (int)nh, s));
-                (void)hipGetLastError();
+                clear_stale_capture_status("rocPRIM call (pm_hits)");
                 hipLaunchKernelGGL(k_list_scatter, dim3(nlists), dim3(64), 0, s, ord, ord_cap, d_cnt, d_poff, nlists,
                                    (uint32_t)n_patterns, slot_bits, sorted);
                 HIPCHK(hipGetLastError());
             } else {
                 HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)nlists, s));
-                (void)hipGetLastError();
+                clear_stale_capture_status("rocPRIM call (pm_hits)");
                 hipLaunchKernelGGL(k_gather_lists, dim3(nlists), dim3(256), 0, s, ord, ord_cap, d_cnt, d_off, in);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, in, sorted, (int)t1, 48,
                                                          48 + (int)slot_bits, s));
-                (void)hipGetLastError();
+                clear_stale_capture_status("rocPRIM call (pm_hits)");
             }
             if (hs) {
                 HIPCHK(rocprim::merge(base + o_tmp, merge_bytes, (const uint64_t*)sorted, (const uint64_t*)hs->keys,
                                       h->keys, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
-                (void)hipGetLastError();
+                clear_stale_capture_status("rocPRIM call (pm_hits)");
             }
         }
     } catch (...) {
@@ -1396,7 +1401,7 @@ void report_sync(pm_db* db, pm_hits* h, uint32_t flags, uint64_t total, bool hdr
 }  // namespace pm
 
 pm_pending::~pm_pending() {
-    if (counted) (void)hipEventDestroy(counted);
+    if (counted) pm::quiet(hipEventDestroy(counted));
     pm::pinned_put(counts_h, counts_cap);
 }
 

@@ -68,12 +68,52 @@ struct failure : std::runtime_error {
 
 void set_error(const std::string& msg);
 
+// A HIP error stays on the thread until it is read: a successful call does
+// not reset it (tools/micro/status_probe.hip, round 6).  So a launch check
+// (HIPCHK(hipGetLastError())) also reports any earlier unchecked call's
+// failure on the same thread.  hipErrorStreamCaptureUnsupported is what a
+// capture-unsafe call (hipMalloc, a synchronize) returns while any thread
+// captures a stream in global mode; this library never captures, but a
+// caller's thread may carry that code from such a call of its own.  It is
+// the one code cleared without failing; every other pending status is an
+// error.  (Round 5 cleared after every rocPRIM call, on the theory that
+// rocPRIM leaves that code behind; the probe shows none of the rocPRIM /
+// hipCUB calls made here leaves any status, on a non-blocking stream or the
+// null stream.  The checks stay after those calls, now failing on any other
+// code.)
+inline void clear_stale_capture_status(const char* after) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess && e != hipErrorStreamCaptureUnsupported)
+        throw failure(PM_E_HIP, std::string(after) + ": " + hipGetErrorString(e));
+}
+
+// A call whose failure is deliberately ignored (teardown: frees, destroys,
+// a final synchronize; a query whose "no" is an answer) must not leave its
+// code pending for the next launch check on the thread: read it back.
+inline void quiet(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+}
+
+void note_cleared_capture_status();   // one stderr line per process (pm_db.hip)
+
 template <class F>
 int guarded(F&& f) {
-    // a status left on this thread by another library's call (a framework's,
-    // or rocPRIM's stale stream-capture query) is not this call's failure:
-    // the launch checks below report only what this call enqueues
-    (void)hipGetLastError();
+    // a C-ABI entry starts from a clean thread status: a pending capture
+    // code (above) is cleared and noted once on stderr; any other status
+    // pending from an earlier call (another library's, or a launch nobody
+    // checked) is reported as this entry's failure rather than thrown away,
+    // and is cleared by reading it, so the next call starts clean
+    // (hipErrorNoDevice is left by the runtime's own start-up on a host
+    // without a GPU; the host-only entries -- the hipRTC compile checks --
+    // run there, and every entry that needs a device reports PM_E_NODEV)
+    const hipError_t prior = hipGetLastError();
+    if (prior == hipErrorStreamCaptureUnsupported) {
+        note_cleared_capture_status();
+    } else if (prior != hipSuccess && prior != hipErrorNoDevice) {
+        set_error(std::string("a HIP error was pending on this thread before the call: ") +
+                  hipGetErrorString(prior));
+        return PM_E_HIP;
+    }
     try {
         f();
         return PM_OK;
@@ -259,8 +299,8 @@ struct EventPair {
         HIPCHK(hipEventCreate(&b));
     }
     ~EventPair() {
-        if (a) (void)hipEventDestroy(a);
-        if (b) (void)hipEventDestroy(b);
+        if (a) quiet(hipEventDestroy(a));
+        if (b) quiet(hipEventDestroy(b));
     }
     double ms() {
         float v = 0.f;
@@ -447,7 +487,7 @@ struct DeviceGuard {
         if (prev != dev) HIPCHK(hipSetDevice(dev));
     }
     ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (prev >= 0) quiet(hipSetDevice(prev));
     }
 };
 

@@ -2488,7 +2488,7 @@ void hits_finalize(pm_hits* h) {
     h->lens_cap = r->lens_cap;
     h->count = r->count;
     h->kernel_ms = r->kernel_ms;
-    if (h->ready) (void)hipEventDestroy(h->ready);
+    if (h->ready) quiet(hipEventDestroy(h->ready));
     h->ready = r->ready;
     delete r;
 }

@@ -1080,23 +1080,29 @@ __global__ __launch_bounds__(REP_T) void k_rep_walk(RepArgs a) {
     if (rep_monotone(a)) {
         // lengths by pattern and no anchors: a valid candidate's (pattern,
         // end) never decreases along the list, so the running maximum is the
-        // last valid candidate's (no k_rep_max pass)
-        if (threadIdx.x == 0) {
-            uint64_t c = 0;
-            for (uint64_t j = b0; j-- > 0;) {
+        // last valid candidate's (no k_rep_max pass).  The block looks back
+        // REP_T keys per round, nearest first: a long run of invalid keys
+        // (dropped at region ends) costs rounds of REP_T parallel loads, not
+        // one dependent load per key on one thread.  Values are monotone
+        // along the valid keys, so a round's maximum is its last valid one's
+        // (and a value is never 0: end > 0).
+        for (uint64_t top = b0; top > 0;) {
+            const uint64_t lo = top > REP_T ? top - REP_T : 0;
+            uint64_t v = 0;
+            if (threadIdx.x < top - lo) {
+                const uint64_t j = top - 1 - threadIdx.x;
                 const uint64_t kj = a.keys[j];
                 const uint32_t lj = rep_len(a, j, kj);
                 const bool nj = rep_near(a, kj);
-                if (rep_valid(a, kj, lj, nj)) {
-                    c = rep_val(a, kj, lj, nj);
-                    break;
-                }
+                if (rep_valid(a, kj, lj, nj)) v = rep_val(a, kj, lj, nj);
             }
-            red[0] = c;
+            v = block_max(v, red);   // uniform across the block
+            if (v) {
+                carry = v;
+                break;
+            }
+            top = lo;
         }
-        __syncthreads();
-        carry = red[0];
-        __syncthreads();
     } else {
         for (uint32_t b = threadIdx.x; b < blockIdx.x; b += REP_T) carry = umax64(carry, a.bmax[b]);
         carry = block_max(carry, red);

@@ -730,8 +730,12 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // dependent steps, so lanes (not the halo's re-read) set the time
     // (configs[3], 3.5 MB at k = 1: 64-position chunks left < 1 wave per
     // SIMD).  Unbounded patterns keep 64 (their carry rounds grow with the
-    // chunks per record).
+    // chunks per record).  The short chunks start at the halo's size (a
+    // lane re-reads halo positions per chunk, so a 200-position pattern in
+    // 16-position chunks would step ~14x per emitted position).
     uint64_t chunk = unbounded ? 64 : 16;
+    if (!unbounded)
+        while (chunk < 64 && chunk < (uint64_t)a.halo) chunk *= 2;
     while (chunk < (uint64_t)MAX_NFA_CHUNK && db->n / (chunk * 2) >= 256ull * 4 * 64 * 2) chunk *= 2;
     if (db->alphabet == PM_ALPHA_NUC) chunk = std::min<uint64_t>(chunk, STREAM);
     a.chunk = (int)chunk;

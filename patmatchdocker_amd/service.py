@@ -94,7 +94,11 @@ class _DatabaseCache:
             ent = self._dbs.get(key)
             stale = ent is None or (ent.stamp != stamp and mode != "cached") or mode == "reopen"
             if stale:
+                # the old entry leaves the table before the open: if the open
+                # raises (here, or on every rank when rank 0's shared_regions
+                # fails), the next request finds no entry and opens again
                 if ent is not None:
+                    del self._dbs[key]
                     self._retire(ent)
                 if shard is None:
                     db = engine.SequenceDatabase.from_file(path, device=device)
@@ -126,7 +130,7 @@ class _DatabaseCache:
             return False
         with self._lock:
             ent = self._dbs.get(key)
-            return ent is not None and ent.stamp == (st.st_mtime_ns, st.st_size)
+            return ent is not None and not ent.retired and ent.stamp == (st.st_mtime_ns, st.st_size)
 
     class _Lease:
         def __init__(self, cache, path, device, shard=None, mode=None):

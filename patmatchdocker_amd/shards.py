@@ -203,11 +203,17 @@ def _dl_release_impl(addr):
         del _OWNERS[h]
         from . import _lib
         lib = _lib.load()
+        recorded = False
         try:
             # torch frees external memory at once: the buffers go back to
             # the pool only after the work queued on torch's stream so far
-            lib.pm_hits_record_use(_ct.c_void_p(h), _ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+            rc = lib.pm_hits_record_use(_ct.c_void_p(h), _ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+            recorded = rc == 0
         finally:
+            if not recorded:
+                # no use recorded: wait for every stream of the device, so no
+                # queued reader sees the buffers reused
+                torch.cuda.synchronize(dev)
             lib.pm_hits_destroy(_ct.c_void_p(h))
 
 
@@ -241,7 +247,16 @@ def hits_as_tensors(hits_handle, device: torch.device):
     """A ``pm_hits`` list's own device buffers as torch tensors (keys int64,
     lens int32), no copy: the tensors take the list over and destroy it
     (``pm_hits_destroy``) when both are freed -- the caller must not destroy
-    it.  An empty list is destroyed at once."""
+    it.  An empty list is destroyed at once.
+
+    Stream contract: when the last tensor is freed, the buffers go back to
+    the library's pool after the work queued so far on torch's CURRENT
+    stream of ``device`` (``pm_hits_record_use``).  A caller that reads the
+    tensors on another stream (``with torch.cuda.stream(s2)``) must free them
+    while that stream is current, or synchronize it first (or
+    ``record_stream`` a clone) -- as with any tensor torch's caching
+    allocator hands back early.  If the use cannot be recorded, the release
+    synchronizes the device before the buffers are returned."""
     from . import _lib
     lib = _lib.load()
     keys_p, lens_p, n = _ct.c_void_p(), _ct.c_void_p(), _ct.c_uint64()

@@ -64,3 +64,35 @@ def test_threads_share_one_entry(svc, tmp_path):
     for t in ts:
         t.join()
     assert len(FakeDB.opened) == 1 and len(set(map(id, seen))) == 1
+
+
+def test_a_failed_open_is_retried_by_the_next_lease(svc, monkeypatch, tmp_path):
+    """"reopen" retires the entry before it opens the file again; an open
+    that raises leaves no entry behind, so the next lease opens again, and
+    resident() never reports a retired entry (a closed entry
+    stayed in the table and every later request got a database of None)."""
+    from patmatchdocker_amd import engine
+    _, cache = svc
+    f = tmp_path / "c.seq"
+    f.write_bytes(b">c\nACGT\n")
+    with cache.lease(str(f)) as db1:
+        pass
+    assert cache.resident(str(f))
+    calls = {"n": 0}
+
+    def flaky(cls, p, device=0):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise RuntimeError("open failed")
+        return FakeDB(p)
+
+    monkeypatch.setattr(engine.SequenceDatabase, "from_file", classmethod(flaky))
+    with pytest.raises(RuntimeError):
+        with cache.lease(str(f), mode="reopen"):
+            pass
+    assert db1.closed and not cache.resident(str(f))
+    with cache.lease(str(f), mode="cached") as db2:   # no entry: opens, whatever the mode
+        assert db2 is not db1 and not db2.closed
+    assert cache.resident(str(f)) and calls["n"] == 2
+    with cache.lease(str(f)) as db3:
+        assert db3 is db2

@@ -324,6 +324,25 @@ int pm_hits_device(const pm_hits* h, void** keys, void** lens, uint64_t* count);
  * framework's kernels still read them).  Like pm_hits_copy_device's use. */
 int pm_hits_record_use(const pm_hits* h, void* stream);
 
+/* The serving rank's merge of the ranks' hit lists (sharded scans, one rank
+ * per GPU: replaces the order of one nrgrep_coords process's output over
+ * the whole file, patmatch.py:733-743).  Part r = keys[part_beg[r] ..
+ * part_beg[r] + part_len[r]) (host arrays, up to 64 parts), each sorted by
+ * key (pattern << 48 | position) and covering its own position range, the
+ * ranges increasing with r; out_keys receives every key sorted by key (per
+ * pattern the parts' slices in part order: no sort).  out_lens (may be
+ * NULL) receives each key's length: lens[i] moved with its key, or, with
+ * lens NULL, len_of_pattern[pattern] (a device array of n_patterns entries:
+ * fixed-length patterns).  Every key's pattern must be < n_patterns.  All
+ * arrays but part_beg / part_len are device memory.  `work` (device,
+ * *work_bytes bytes; NULL = size query: *work_bytes is set) holds the
+ * slices' starts and destinations.  Enqueued on `stream` (hipStream_t;
+ * NULL = the null stream, synchronous).                                   */
+int pm_merge_parts(const uint64_t* keys, const int32_t* lens, const uint64_t* part_beg,
+                   const uint64_t* part_len, int nparts, int n_patterns,
+                   const int32_t* len_of_pattern, uint64_t* out_keys, int32_t* out_lens,
+                   void* work, uint64_t* work_bytes, int device, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,7 +39,7 @@ EXPORTED = (
     "pm_ids_jit_compile", "pm_esimple_plan", "pm_db_set_regions", "pm_db_regions",
     "pm_extended_plan", "pm_eextended_plan", "pm_db_residue_codes", "pm_scan_nfa_tree",
     "pm_regular_plan",
-    "pm_eregular_plan",
+    "pm_eregular_plan", "pm_merge_parts",
 )
 PM_NRGREP_BUFFER = 1600000    # nrgrep_coords -b 1600000 (bytes: patmatch.py:733-743)
 
@@ -99,6 +99,7 @@ def _declare(lib):
     lib.pm_hits_device.argtypes = [P, PP, PP, pu64]
     lib.pm_hits_record_use.argtypes = [P, P]
     lib.pm_hits_copy_device.argtypes = [P, P, P, u64, P]
+    lib.pm_merge_parts.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, P, P, P, P, pu64, ctypes.c_int, P]
     lib.pm_esimple_plan.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
     lib.pm_linear_jit_compile.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, P, ctypes.c_int, pu64]
     for name in EXPORTED:

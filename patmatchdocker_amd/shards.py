@@ -90,26 +90,76 @@ def gather_hits(keys: torch.Tensor, lens: Optional[torch.Tensor], group=None, ds
     if send_lens:
         pl = torch.zeros(width, dtype=lens.dtype, device=lens.device)
         pl[:lens.numel()] = lens
+    # the receive buffers are views of one allocation (rank r's list at
+    # r * width), so the merge reads the parts where they landed: no cat
+    recv = me == dst or dst is None
+    buf_k = torch.empty(world * width, dtype=keys.dtype, device=keys.device) if recv else None
+    all_k = list(buf_k.split(width)) if recv else None
+    if send_lens:
+        buf_l = torch.empty(world * width, dtype=pl.dtype, device=pl.device) if recv else None
+        all_l = list(buf_l.split(width)) if recv else None
     if dst is None:
-        all_k = [torch.empty_like(pk) for _ in range(world)]
         dist.all_gather(all_k, pk, group=group)
         if send_lens:
-            all_l = [torch.empty_like(pl) for _ in range(world)]
             dist.all_gather(all_l, pl, group=group)
     else:
-        all_k = [torch.empty_like(pk) for _ in range(world)] if me == dst else None
         dist.gather(pk, all_k, dst=gdst, group=group)
         if send_lens:
-            all_l = [torch.empty_like(pl) for _ in range(world)] if me == dst else None
             dist.gather(pl, all_l, dst=gdst, group=group)
         if me != dst:
             return None
+    if buf_k.is_cuda:
+        return merge_parts(buf_k, buf_l if send_lens else None, [r * width for r in range(world)], sizes,
+                           fixed_len if not send_lens else None)
     parts = [t[:n] for t, n in zip(all_k, sizes)]
     k = torch.cat(parts)
     ln = torch.cat([t[:n] for t, n in zip(all_l, sizes)]) if send_lens else _fixed_lens(k, fixed_len)
     if k.numel() == 0:
         return k, ln
     return _merge(parts, k, ln)
+
+
+def merge_parts(buf_k: torch.Tensor, buf_l: Optional[torch.Tensor], begs: Sequence[int], sizes: Sequence[int],
+                fixed_len: Optional[Sequence[int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The ranks' lists (part r = buf[begs[r] : begs[r] + sizes[r]] of a
+    device buffer, each sorted, position ranges increasing with r) ->
+    (keys, lens) sorted by key, on the device by ``pm_merge_parts`` (one
+    pass, no sort), ordered on torch's current stream.  Lengths move with
+    their keys (``buf_l``) or come from the pattern field (``fixed_len``)."""
+    from . import _lib
+    dev = buf_k.device
+    total = int(sum(sizes))
+    out_k = torch.empty(total, dtype=torch.int64, device=dev)
+    out_l = torch.empty(total, dtype=torch.int32, device=dev)
+    if total == 0:
+        return out_k, out_l
+    if buf_l is None:
+        table = torch.tensor(list(fixed_len), dtype=torch.int32, device=dev)
+        npat = table.numel()
+        lens_p = None
+    else:
+        npat = int((buf_k[begs[0]:begs[0] + sizes[0]] >> POS_BITS).max().item()) + 1 if sizes[0] else 1
+        for b, n in zip(begs[1:], sizes[1:]):
+            if n:
+                npat = max(npat, int((buf_k[b:b + n] >> POS_BITS).max().item()) + 1)
+        table = None
+        lens_p = buf_l.to(torch.int32) if buf_l.dtype != torch.int32 else buf_l
+    lib = _lib.load()
+    n = len(sizes)
+    beg_a = (_ct.c_uint64 * n)(*begs)
+    len_a = (_ct.c_uint64 * n)(*sizes)
+    wb = _ct.c_uint64()
+    stream = _ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(lib.pm_merge_parts(None, None, beg_a, len_a, n, npat, None, None, None, None, _ct.byref(wb),
+                                  dev.index or 0, stream))
+    work = torch.empty(max(1, wb.value), dtype=torch.uint8, device=dev)
+    _lib.check(lib.pm_merge_parts(_ct.c_void_p(buf_k.data_ptr()),
+                                  _ct.c_void_p(lens_p.data_ptr()) if lens_p is not None else None,
+                                  beg_a, len_a, n, npat,
+                                  _ct.c_void_p(table.data_ptr()) if table is not None else None,
+                                  _ct.c_void_p(out_k.data_ptr()), _ct.c_void_p(out_l.data_ptr()),
+                                  _ct.c_void_p(work.data_ptr()), _ct.byref(wb), dev.index or 0, stream))
+    return out_k, out_l
 
 
 def _fixed_lens(keys: torch.Tensor, fixed_len: Optional[Sequence[int]]) -> torch.Tensor:

@@ -263,9 +263,9 @@ int pm_scan_nfa_wide(pm_db* db, int m, int words, const uint64_t* byte_mask, con
  * parse-time nullable flag.  With PM_REGULAR (and PM_REPORT_NRGREP) the
  * report is the regular engine's at k = 0 and the eregular engine's at
  * k > 0 (eregularPreproc 0x406a20: k + 1 exact pieces, a window with k
- * errors or the automaton forward; checkMatch 0x406010; at most 63
- * positions, else PM_E_UNSUPPORTED; deletions with k >= min_len are
- * answered, every line walked).  A k > 0 plan whose first window is an
+ * errors or the automaton forward; checkMatch 0x406010; the sliced
+ * transition tables of fwdCheck / bwdCheck beyond 64 states restated;
+ * deletions with k >= min_len are answered, every line walked).  A k > 0 plan whose first window is an
  * extended sequence prints nothing (eregularPreproc dies, 0x4081ed).      */
 int pm_scan_nfa_tree(pm_db* db, int m, int words, const uint64_t* byte_mask, const uint64_t* follow,
                      const uint64_t* first, const uint64_t* last, int max_len, int min_len, int k,
@@ -286,9 +286,11 @@ int pm_regular_plan(int m, int words, const uint64_t* byte_mask, int nodes, cons
  * forward), out[2] = detClass of the first window (1: esimple's scanners,
  * 2: the binary dies, 3: eregularScan), out[3] = 0 when the binary would
  * read memory it never wrote for this plan, out[4] = the windows;
- * masks[3i .. 3i+2] = window i, its initial and its final states,
- * masks[48] = checkMatch's state word for class 1.  out: 5 ints, masks: 49
- * words.  At most 63 positions (PM_E_UNSUPPORTED above).                   */
+ * masks[(3i + j) * 5 .. + 4] = window i (j = 0), its initial (1) and its
+ * final (2) states, 5 words each; masks[48 * 5] = checkMatch's state word
+ * for class 1.  out: 5 ints, masks: 245 words.  PM_E_UNSUPPORTED when a
+ * window union exceeds 64 states or a transition-table slice would lie
+ * past the state set (regularMakeDet / SLICE, pm_regular.hip).           */
 int pm_eregular_plan(int m, int words, const uint64_t* byte_mask, int nodes, const int32_t* tree,
                      const int32_t* tree_nullable, int k, int32_t* out, uint64_t* masks);
 

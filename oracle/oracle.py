@@ -572,21 +572,24 @@ def eregular_plan(prog, k: int, types: str = "ids"):
     B = wide_masks(prog)
     tree, null, tp, np_ = _tree_arrays(prog)
     out = (ctypes.c_int * 6)()
-    masks = np.zeros(3 * 17 + 1, dtype=np.uint64)
+    nw = 5   # PMR_NW
+    masks = np.zeros((3 * 17 + 1) * nw, dtype=np.uint64)
     pu64 = ctypes.POINTER(ctypes.c_uint64)
     if lib().pmr_eplan(tp, np_, len(prog.tree), B.ctypes.data_as(pu64), prog.m, 1 if prog.ignore_case else 0, k,
                        err_flags(types), out, masks.ctypes.data_as(pu64)) < 0:
         raise ValueError("no eregular plan for %s at k=%d" % (prog.source, k))
-    wins = [(int(masks[3 * i]), int(masks[3 * i + 1]), int(masks[3 * i + 2])) for i in range(out[5])]
+    def word_set(j):
+        return sum(int(masks[j * nw + q]) << (64 * q) for q in range(nw))
+    wins = [(word_set(3 * i), word_set(3 * i + 1), word_set(3 * i + 2)) for i in range(out[5])]
     return {"type": out[0], "ell": out[1], "cls": out[2], "states": out[3], "defined": bool(out[4]),
-            "windows": wins, "match": int(masks[51])}
+            "windows": wins, "match": int(masks[51 * nw])}
 
 
 def scan_eregular(text: bytes, prog, k: int, types: str = "ids", skip_headers: bool = False,
                   bufsize: int = NRGREP_BUFFER, regs=None):
     """What nrgrep_coords prints for a class-3 pattern at k > 0 (pmr_eregular:
     nrgrep's eregular plan, its scanners, checkMatch and report rule), region
-    by region (``regions``).  Automata of at most 64 states."""
+    by region (``regions``).  Automata of up to 319 positions."""
     if prog.kind != "regular":
         raise ValueError("scan_eregular needs a regular pattern")
     if regs is not None or (bufsize and len(text) >= bufsize):

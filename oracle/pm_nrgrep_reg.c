@@ -753,8 +753,9 @@ int64_t pmr_regular(const uint8_t* text, int64_t n, const int32_t* tree, const i
 
 /* ========================================================================
  * eregular: the same patterns at k > 0 (searchPreproc: OptErrors != 0 and
- * detClass == 3 -> eregularPreproc 0x406a20).  Restated for automata of at
- * most 64 states (one word: every SLICE sees every state).
+ * detClass == 3 -> eregularPreproc 0x406a20).  Restated for automata of up
+ * to 319 positions (round 6: more than one word of states, the sliced
+ * transition tables of fwdCheck / bwdCheck included -- etab below).
  *
  *   eregularPreproc 0x406a20:
  *     regularFindBest 0x40a500 with K (its cost C carries + K) -> a window
@@ -819,24 +820,67 @@ typedef struct {
     int K, errs;
     int etype, ell, cls, npieces, pieces_computed, defined;
     double pbest, fbest;
-    uint64_t pwin[PME_MAXK + 1], pini[PME_MAXK + 1], pfin[PME_MAXK + 1];
+    rset pwin[PME_MAXK + 1], pini[PME_MAXK + 1], pfin[PME_MAXK + 1];
     int first[PME_MAXK + 1];
-    /* the automaton in one word */
     int m;
-    uint64_t arr[64], rev[64], B[256], final;
+    /* fwdCheck / bwdCheck's transition tables (regularMakeDet 0x40bfc0,
+     * called at 0x407c4c / 0x407c63): ntab tables, table t = the states
+     * t W .. t W + W - 1, W = ceil(m / ceil(m / OptDetWidth)) (0x407c1d;
+     * OptDetWidth .data 0x621920 = 16) */
+    int W, ntab;
     /* checkMatch */
     uint64_t match0;            /* class 1: P->0x28 */
     int nstates;                /* P->0x24 */
-    int unmap[64];              /* P->0x858 */
+    int unmap[PMR_MAXS];        /* P->0x858 */
 } ectx_t;
 
-static inline uint64_t etrans(const uint64_t* tab, uint64_t d) {
-    uint64_t r = 0;
-    while (d) {
-        r |= tab[__builtin_ctzll(d)];
-        d &= d - 1;
+/* eregularPreproc's successor sets (ISSET / OR over the arrows: exact) */
+static void ereach(const rctx_t* x, const rset* D, rset* out) {
+    memset(out, 0, sizeof(rset));
+    for (int s = 0; s < x->m; ++s)
+        if (rs_has(D, s)) rs_or(out, &x->arrows[s]);
+}
+
+/* fwdCheck / bwdCheck's transition (the seven slice loops of each, e.g.
+ * 0x403508 .. 0x40354f and 0x403fc8 .. 0x40400f): table t is indexed by
+ * SLICE(D, off, W) (0x41b8e0: W bits of ONE 64-bit word from bit off), off
+ * starting at 0 and moving on by W -- or, when the next slice would cross a
+ * word (0x403530: (off + W - 1) / 64 != off / 64), to the next word's first
+ * bit.  The tables are built for the states t W + b (no such jump), so after
+ * a jump the states off + b take the transitions of the states t W + b, and
+ * the states a jump skips take none (m <= 64: no slice crosses a word, the
+ * identity).  k = 0's fwdCheck (0x408c90) has no jump: rctx_t's vis. */
+static void etab(const ectx_t* e, const rset* tab, const rset* D, rset* out) {
+    memset(out, 0, sizeof(rset));
+    const uint64_t msk = e->W >= 64 ? ~0ull : (1ull << e->W) - 1;
+    int off = 0;
+    for (int t = 0; t < e->ntab; ++t) {
+        uint64_t sl = (D->w[off >> 6] >> (off & 63)) & msk;
+        while (sl) {
+            const int src = t * e->W + __builtin_ctzll(sl);
+            sl &= sl - 1;
+            if (src < e->m) rs_or(out, &tab[src]);
+        }
+        off += e->W;
+        if (((off + e->W - 1) >> 6) != (off >> 6)) off = (off & ~63) + 64;
     }
-    return r;
+}
+
+/* the table layout fwdCheck / bwdCheck read: -1 if a slice would read past
+ * the state set's words (SLICE on memory the binary never allocated) */
+static int etab_layout(ectx_t* e) {
+    const int m = e->m;
+    const int nt0 = (m + 16 - 1) / 16;
+    e->W = (m + nt0 - 1) / nt0;
+    e->ntab = (m + e->W - 1) / e->W;
+    const int words = (m + 63) / 64;
+    int off = 0;
+    for (int t = 0; t < e->ntab; ++t) {
+        if ((off >> 6) >= words || (off >> 6) >= PMR_NW) return -1;
+        off += e->W;
+        if (((off + e->W - 1) >> 6) != (off >> 6)) off = (off & ~63) + 64;
+    }
+    return 0;
 }
 
 /* eregularPreproc's plan (transpositions off: PatMatch's -k letters are
@@ -844,34 +888,33 @@ static inline uint64_t etrans(const uint64_t* tab, uint64_t d) {
 static int eplan(ectx_t* e, int K) {
     rctx_t* x = e->x;
     const int m = x->m;
-    if (m > 64 || K < 1 || K > PME_MAXK) return -1;
+    if (K < 1 || K > PME_MAXK) return -1;
     e->m = m;
     e->K = K;
-    for (int s = 0; s < m; ++s) {
-        e->arr[s] = x->arrows[s].w[0];
-        e->rev[s] = x->rev[s].w[0];
-    }
-    for (int c = 0; c < 256; ++c) e->B[c] = x->B[c].w[0];
-    e->final = x->final.w[0];
+    if (etab_layout(e) < 0) return -1;
     if (find_best(x, K) < 0) return -1;                     /* 0x406d39 */
     e->fbest = x->best;
     const int transp = 0;
     /* levels (0x406db8) */
-    uint64_t seen = 1;
+    rset seen, succ;
+    memset(&seen, 0, sizeof seen);
+    rs_set(&seen, 0);
     int nlev = 1;
-    while (!(seen & e->final)) {
+    while (!rs_inter(&seen, &x->final)) {
         ++nlev;
-        seen |= etrans(e->arr, seen);
+        ereach(x, &seen, &succ);
+        rs_or(&seen, &succ);
         if (nlev > m + 2) return -1;
     }
     const int minlen = nlev - 1;
-    uint64_t lev[66];
-    lev[0] = 1;
-    seen = 1;
+    rset* lev = calloc((size_t)nlev + 1, sizeof(rset));
+    rs_set(&lev[0], 0);
+    memset(&seen, 0, sizeof seen);
+    rs_set(&seen, 0);
     for (int i = 1; i <= minlen; ++i) {                    /* 0x406f69 */
-        const uint64_t succ = etrans(e->arr, seen);
-        lev[i] = succ & ~seen;
-        seen |= succ;
+        ereach(x, &seen, &succ);
+        for (int q = 0; q < PMR_NW; ++q) lev[i].w[q] = succ.w[q] & ~seen.w[q];
+        rs_or(&seen, &succ);
     }
     int pl0 = minlen - K * transp;                         /* 0x406e54 */
     if ((unsigned)pl0 > 64u) pl0 = 64;
@@ -879,14 +922,13 @@ static int eplan(ectx_t* e, int K) {
     const int PL1 = pl0 + 1;
     double best = 0.78;                                    /* .rodata 0x41d1e8 */
     int chosen = 0;
-    uint64_t pieces[PME_MAXK + 1];
+    rset pieces[PME_MAXK + 1];
     memset(pieces, 0, sizeof pieces);
     if (PL1 > 1 && pl0 != 1 && !(1.0 / (double)pl0 > 0.78)) {
-        double prob[64];
+        double* prob = calloc((size_t)m, sizeof(double));
         for (int i = 0; i < m; ++i) {                      /* 0x407031 */
-            prob[i] = 0.0;
             for (int c = 0; c < 256; ++c)
-                if ((e->B[c] >> i) & 1) prob[i] += pmn_letter_prob[c];
+                if (rs_has(&x->B[c], i)) prob[i] += pmn_letter_prob[c];
         }
         double* A = calloc((size_t)m * PL1, sizeof(double));
         for (int i = 0; i < m; ++i) {
@@ -897,7 +939,7 @@ static int eplan(ectx_t* e, int K) {
             for (int i = 0; i < m; ++i) {
                 double s = 0.0;
                 for (int j = 0; j < m; ++j)
-                    if ((e->arr[i] >> j) & 1) s += A[(size_t)j * PL1 + l - 1];
+                    if (rs_has(&x->arrows[i], j)) s += A[(size_t)j * PL1 + l - 1];
                 s *= prob[i];
                 A[(size_t)i * PL1 + l] = 1.0 < s ? 1.0 : s;
             }
@@ -911,7 +953,7 @@ static int eplan(ectx_t* e, int K) {
                     double v = A[(size_t)i * PL1 + a];
                     if (a < l)
                         for (int j = 0; j < m; ++j)
-                            if ((e->arr[i] >> j) & 1) v = 1.0 - (1.0 - v) * (1.0 - BT(j, l - 1, a));
+                            if (rs_has(&x->arrows[i], j)) v = 1.0 - (1.0 - v) * (1.0 - BT(j, l - 1, a));
                     BT(i, l, a) = v;
                 }
         double* C = calloc((size_t)nlev * PL1, sizeof(double));
@@ -919,7 +961,7 @@ static int eplan(ectx_t* e, int K) {
             for (int l = 0; l < PL1; ++l) {
                 double s = 1.0;
                 for (int i = 0; i < m; ++i)
-                    if (((lev[lv] >> i) & 1) && l != 0)
+                    if (rs_has(&lev[lv], i) && l != 0)
                         for (int a = 1; a <= l; ++a) s += BT(i, l, a);
                 C[(size_t)lv * PL1 + l] = s;
             }
@@ -964,21 +1006,24 @@ static int eplan(ectx_t* e, int K) {
             if (--pl == 1) break;                          /* 0x407ae0 */
             if (!(1.0 / (double)pl <= best)) break;
         }
+        free(prob);
         free(A);
         free(Bt);
         free(C);
         free(D);
         free(E);
     }
+    free(lev);
     e->pbest = best;
     int use_pieces = 0;
     if (best < 0.78) {                                     /* 0x4082c9 */
         e->pieces_computed = 1;
         for (int i = 0; i <= K; ++i) {
-            uint64_t w = pieces[i], last = 0;
+            rset w = pieces[i], last;
+            memset(&last, 0, sizeof last);
             for (int st = 0; st < chosen; ++st) {
-                last = etrans(e->arr, w);
-                w |= last;
+                ereach(x, &w, &last);
+                rs_or(&w, &last);
             }
             e->pwin[i] = w;
             e->pini[i] = pieces[i];
@@ -994,32 +1039,30 @@ static int eplan(ectx_t* e, int K) {
         e->etype = x->ell == 0 ? 3 : 2;
         e->ell = x->ell;
         e->npieces = 1;
-        e->pwin[0] = x->win.w[0];
-        e->pini[0] = x->winit.w[0];
-        e->pfin[0] = x->wfinal.w[0];
+        e->pwin[0] = x->win;
+        e->pini[0] = x->winit;
+        e->pfin[0] = x->wfinal;
     }
-    rset w0;
-    memset(&w0, 0, sizeof w0);
-    w0.w[0] = e->pwin[0];
-    e->cls = det_class1(x, 0, &w0);                        /* 0x407c97 */
+    e->cls = det_class1(x, 0, &e->pwin[0]);                /* 0x407c97 */
     e->defined = 1;
-    for (int i = 0; i < 64; ++i) e->unmap[i] = -1;
+    for (int i = 0; i < PMR_MAXS; ++i) e->unmap[i] = -1;
     if (e->cls == 1) {                                     /* 0x407e4b */
         const int nw = (e->etype == 1 || e->pieces_computed) ? K + 1 : 1;
         if (nw < K + 1) e->defined = 0;
         e->match0 = 0;
         for (int i = 0; i < nw; ++i) {
             int f = 0;
-            while (f < m && !((e->pwin[i] >> f) & 1)) ++f;
+            while (f < m && !rs_has(&e->pwin[i], f)) ++f;
             e->first[i] = f;
+            /* 0x407ef0 / 0x407f39: shl %cl (the count taken mod 64) */
             if (e->ell != 0) e->match0 |= 1ull << (f & 63);
             else {
                 int r = f + 1;
-                while (r < m && ((e->pwin[i] >> r) & 1)) ++r;
+                while (r < m && rs_has(&e->pwin[i], r)) ++r;
                 e->match0 |= 1ull << (r & 63);
             }
         }
-        e->nstates = m;
+        e->nstates = m;                                    /* P->0x858[i] = i, i < P->0x20 (0x407f67) */
         for (int i = 0; i < m; ++i) e->unmap[i] = i;
     } else if (e->cls == 3) {                              /* 0x407fe9 */
         rset uw, ui, uf;
@@ -1027,9 +1070,9 @@ static int eplan(ectx_t* e, int K) {
         memset(&ui, 0, sizeof ui);
         memset(&uf, 0, sizeof uf);
         for (int i = 0; i < e->npieces; ++i) {
-            uw.w[0] |= e->pwin[i];
-            ui.w[0] |= e->pini[i];
-            uf.w[0] |= e->pfin[i];
+            rs_or(&uw, &e->pwin[i]);
+            rs_or(&ui, &e->pini[i]);
+            rs_or(&uf, &e->pfin[i]);
         }
         x->win = uw;
         x->winit = ui;
@@ -1038,22 +1081,26 @@ static int eplan(ectx_t* e, int K) {
         if (load_fast(x) < 0) return -1;
         e->nstates = x->mp;
         for (int s = 0; s < m; ++s)
-            if ((uw.w[0] >> s) & 1) e->unmap[x->map[s]] = s;   /* 0x40807f */
+            if (rs_has(&uw, s)) e->unmap[x->map[s]] = s;   /* 0x40807f */
     }
     return 0;
 }
 
 /* ------------------------------------------------------------------------
- * fwdCheck 0x403310 / bwdCheck 0x403df0 with K + 1 rows; *kio: the budget
- * in, the errors used out.  -1: none.
+ * fwdCheck 0x403310 / bwdCheck 0x403df0 with K + 1 rows of state sets (the
+ * transitions through the sliced tables: etab); *kio: the budget in, the
+ * errors used out.  -1: none.
  * ---------------------------------------------------------------------- */
+
+static inline void rs_and(rset* d, const rset* s) { for (int q = 0; q < PMR_NW; ++q) d->w[q] &= s->w[q]; }
 
 static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     const rctx_t* x = e->x;
     const int K = *kio, ins = e->errs & PME_INS, del = e->errs & PME_DEL, sub = e->errs & PME_SUB;
-    uint64_t rows[PME_MAXK + 1];
-    rows[0] = 1ull << s;
-    if (rows[0] & e->final) {                              /* 0x40339d: insertions to the right context */
+    rset rows[PME_MAXK + 1], T;
+    memset(&rows[0], 0, sizeof(rset));
+    rs_set(&rows[0], s);
+    if (rs_inter(&rows[0], &x->final)) {                   /* 0x40339d: insertions to the right context */
         *kio = 0;
         for (int64_t q = p + 1;; ++q) {
             if (right_ok(x, q, lim + 1)) return q - 1;
@@ -1064,12 +1111,11 @@ static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     int kmax = K;
     int64_t best = -1;
     for (int j = 1; j <= kmax; ++j) {                      /* 0x4034c0 */
-        if (!del) {
-            rows[j] = rows[j - 1];                         /* (unset in the binary: see the header) */
-            continue;
-        }
-        rows[j] = rows[j - 1] | etrans(e->arr, rows[j - 1]);
-        if ((rows[j] & e->final) && right_ok(x, p + 1, lim + 1)) {   /* 0x403d82 */
+        rows[j] = rows[j - 1];                             /* (unset in the binary without OptDel: see the header) */
+        if (!del) continue;
+        etab(e, x->arrows, &rows[j - 1], &T);
+        rs_or(&rows[j], &T);
+        if (rs_inter(&rows[j], &x->final) && right_ok(x, p + 1, lim + 1)) {   /* 0x403d82 */
             *kio = j;
             kmax = j - 1;
             best = p;
@@ -1078,25 +1124,34 @@ static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     if (p == lim) return best;
     for (int64_t cur = p;;) {
         ++cur;
-        const uint64_t bc = e->B[x->t[cur]];
-        const uint64_t n0 = etrans(e->arr, rows[0]) & bc;
-        if ((n0 & e->final) && right_ok(x, cur + 1, lim + 1)) {
+        const rset* bc = &x->B[x->t[cur]];
+        rset n0;
+        etab(e, x->arrows, &rows[0], &n0);
+        rs_and(&n0, bc);
+        if (rs_inter(&n0, &x->final) && right_ok(x, cur + 1, lim + 1)) {
             *kio = 0;
             return cur;
         }
-        uint64_t oldp = rows[0], last = n0;
+        rset oldp = rows[0], last = n0;
         rows[0] = n0;
         for (int j = 1; j <= kmax; ++j) {                  /* 0x4037a0 */
-            uint64_t v = del ? etrans(e->arr, last) : 0;
-            if (ins) v |= oldp;
-            if (sub) v |= etrans(e->arr, oldp);
-            v |= etrans(e->arr, rows[j]) & bc;
-            const uint64_t oj = rows[j];
+            rset v;
+            memset(&v, 0, sizeof v);
+            if (del) etab(e, x->arrows, &last, &v);
+            if (ins) rs_or(&v, &oldp);
+            if (sub) {
+                etab(e, x->arrows, &oldp, &T);
+                rs_or(&v, &T);
+            }
+            etab(e, x->arrows, &rows[j], &T);
+            rs_and(&T, bc);
+            rs_or(&v, &T);
+            const rset oj = rows[j];
             rows[j] = v;
             last = v;
-            if ((v & e->final) && right_ok(x, cur + 1, lim + 1)) {   /* 0x403a01: the fewest errors */
+            if (rs_inter(&v, &x->final) && right_ok(x, cur + 1, lim + 1)) {   /* 0x403a01: the fewest errors */
                 int c = j;
-                while (c - 1 >= 0 && (rows[c - 1] & e->final)) --c;
+                while (c - 1 >= 0 && rs_inter(&rows[c - 1], &x->final)) --c;
                 if (c == 0) {
                     *kio = 0;
                     return cur;
@@ -1108,7 +1163,7 @@ static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
             }
             oldp = oj;
         }
-        if (!last) return best;                            /* 0x403afc */
+        if (!rs_any(&last)) return best;                   /* 0x403afc */
         if (cur == lim) return best;
     }
 }
@@ -1116,9 +1171,10 @@ static int64_t efwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
 static int64_t ebwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     const rctx_t* x = e->x;
     const int K = *kio, ins = e->errs & PME_INS, del = e->errs & PME_DEL, sub = e->errs & PME_SUB;
-    uint64_t rows[PME_MAXK + 1];
-    rows[0] = 1ull << s;
-    if (rows[0] & 1) {                                     /* 0x403e71: insertions to the left context */
+    rset rows[PME_MAXK + 1], T;
+    memset(&rows[0], 0, sizeof(rset));
+    rs_set(&rows[0], s);
+    if (rs_has(&rows[0], 0)) {                             /* 0x403e71: insertions to the left context */
         *kio = 0;
         for (int64_t q = p;;) {
             if (left_ok(x, q, lim)) return q;
@@ -1131,12 +1187,11 @@ static int64_t ebwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     int kmax = K;
     int64_t best = -1;
     for (int j = 1; j <= kmax; ++j) {                      /* 0x403f80 */
-        if (!del) {
-            rows[j] = rows[j - 1];
-            continue;
-        }
-        rows[j] = rows[j - 1] | etrans(e->rev, rows[j - 1]);
-        if ((rows[j] & 1) && left_ok(x, p, lim)) {         /* 0x40484e */
+        rows[j] = rows[j - 1];
+        if (!del) continue;
+        etab(e, x->rev, &rows[j - 1], &T);
+        rs_or(&rows[j], &T);
+        if (rs_has(&rows[j], 0) && left_ok(x, p, lim)) {   /* 0x40484e */
             *kio = j;
             kmax = j - 1;
             best = p;
@@ -1145,25 +1200,35 @@ static int64_t ebwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
     if (p == lim) return best;
     for (int64_t cur = p;;) {
         --cur;
-        const uint64_t bc = e->B[x->t[cur]];
-        const uint64_t n0 = etrans(e->rev, rows[0] & bc);
-        if ((n0 & 1) && left_ok(x, cur, lim)) {
+        const rset* bc = &x->B[x->t[cur]];
+        rset n0, a = rows[0];
+        rs_and(&a, bc);
+        etab(e, x->rev, &a, &n0);
+        if (rs_has(&n0, 0) && left_ok(x, cur, lim)) {
             *kio = 0;
             return cur;
         }
-        uint64_t oldp = rows[0], last = n0;
+        rset oldp = rows[0], last = n0;
         rows[0] = n0;
         for (int j = 1; j <= kmax; ++j) {                  /* 0x404230 */
-            uint64_t v = del ? etrans(e->rev, last) : 0;
-            if (ins) v |= oldp;
-            if (sub) v |= etrans(e->rev, oldp);
-            v |= etrans(e->rev, rows[j] & bc);
-            const uint64_t oj = rows[j];
+            rset v;
+            memset(&v, 0, sizeof v);
+            if (del) etab(e, x->rev, &last, &v);
+            if (ins) rs_or(&v, &oldp);
+            if (sub) {
+                etab(e, x->rev, &oldp, &T);
+                rs_or(&v, &T);
+            }
+            a = rows[j];
+            rs_and(&a, bc);
+            etab(e, x->rev, &a, &T);
+            rs_or(&v, &T);
+            const rset oj = rows[j];
             rows[j] = v;
             last = v;
-            if ((v & 1) && left_ok(x, cur, lim)) {         /* 0x404479 */
+            if (rs_has(&v, 0) && left_ok(x, cur, lim)) {   /* 0x404479 */
                 int c = j;
-                while (c - 1 >= 0 && (rows[c - 1] & 1)) --c;
+                while (c - 1 >= 0 && rs_has(&rows[c - 1], 0)) --c;
                 if (c == 0) {
                     *kio = 0;
                     return cur;
@@ -1175,7 +1240,7 @@ static int64_t ebwd(const ectx_t* e, int64_t p, int64_t lim, int s, int* kio) {
             }
             oldp = oj;
         }
-        if (!last) return best;                            /* 0x404579 */
+        if (!rs_any(&last)) return best;                   /* 0x404579 */
         if (cur == lim) return best;
     }
 }
@@ -1193,8 +1258,11 @@ static int echeck(const ectx_t* e, int64_t pos, int64_t R, uint64_t match, int64
     if (lo > 0 && x->nl[lo - 1] >= R) rb = x->nl[lo - 1] + 1;
     const int64_t re = lo < x->nnl ? x->nl[lo] : x->n;
     if (rp < rb || rp >= re) return 0;
-    for (int i = 0; i < e->nstates && i < 64; ++i) {       /* 0x4060b9 */
-        if (!((match >> i) & 1) || e->unmap[i] < 0) continue;
+    /* 0x4060b9: every i < P->0x24, its bit tested by `bt %rbx` (the bit
+     * number taken mod 64: class 1 over more than 64 states tries the states
+     * i, i + 64, ... of each set bit) */
+    for (int i = 0; i < e->nstates; ++i) {
+        if (!((match >> (i & 63)) & 1) || e->unmap[i] < 0) continue;
         const int s = e->unmap[i];
         int k1 = e->K, k2;
         int64_t st, en;
@@ -1376,7 +1444,7 @@ static int escan_pieces1(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
         for (int r = 0; r < np; ++r)
             for (int pp = 0; pp < mpc; ++pp) {
                 const int st = e->first[r] + mpc - 1 - pp;
-                if (st < 64 && ((e->B[c] >> st) & 1)) {
+                if (st < e->m && rs_has(&x->B[c], st)) {
                     const uint64_t bit = 1ull << (r * mpc + pp);
                     T0[c] |= bit;
                     if (pp > 0) T2[c] |= bit;
@@ -1421,7 +1489,7 @@ static int escan_window1(const ectx_t* e, int64_t R, int64_t* mb, int64_t* me) {
         T[c] = 0;
         for (int r = 0; r < Lw; ++r) {
             const int st = beg + Lw - 1 - r;
-            if (st < 64 && ((e->B[c] >> st) & 1)) T[c] |= 1ull << (64 - Lw + r);
+            if (st < e->m && rs_has(&x->B[c], st)) T[c] |= 1ull << (64 - Lw + r);
         }
     }
     const uint64_t top = ~0ull << (64 - Lw);
@@ -1492,8 +1560,9 @@ static void ectx_free(ectx_t* e) {
 /* out[0] = type (1 pieces, 2 backward window, 3 forward), out[1] = the
  * pieces' length or the window's ell, out[2] = detClass of windows[0],
  * out[3] = P->0x24, out[4] = 1 unless nrgrep reads memory it never wrote,
- * out[5] = the number of windows; masks[3 i .. 3 i + 2] = window i, its
- * initial and its final states; masks[51] = P->0x28 (class 1) */
+ * out[5] = the number of windows; masks[(3 i + j) PMR_NW ..] (PMR_NW words
+ * each) = window i, its initial and its final states (j = 0, 1, 2);
+ * masks[51 PMR_NW] = P->0x28 (class 1) */
 int pmr_eplan(const int32_t* tree, const int32_t* nullable, int nodes, const uint64_t* Bpos, int npos, int icase,
               int K, int errs, int* out, uint64_t* masks) {
     ectx_t* e = ectx_new(tree, nullable, nodes, Bpos, npos, icase, 0, K, errs);
@@ -1504,12 +1573,13 @@ int pmr_eplan(const int32_t* tree, const int32_t* nullable, int nodes, const uin
     out[3] = e->nstates;
     out[4] = e->defined;
     out[5] = e->npieces;
-    for (int i = 0; i < e->npieces; ++i) {
-        masks[3 * i] = e->pwin[i];
-        masks[3 * i + 1] = e->pini[i];
-        masks[3 * i + 2] = e->pfin[i];
-    }
-    masks[3 * (PME_MAXK + 1)] = e->match0;
+    for (int i = 0; i < e->npieces; ++i)
+        for (int q = 0; q < PMR_NW; ++q) {
+            masks[(3 * i) * PMR_NW + q] = e->pwin[i].w[q];
+            masks[(3 * i + 1) * PMR_NW + q] = e->pini[i].w[q];
+            masks[(3 * i + 2) * PMR_NW + q] = e->pfin[i].w[q];
+        }
+    masks[3 * (PME_MAXK + 1) * PMR_NW] = e->match0;
     ectx_free(e);
     return 0;
 }
@@ -1517,7 +1587,8 @@ int pmr_eplan(const int32_t* tree, const int32_t* nullable, int nodes, const uin
 /* What nrgrep_coords prints for a class-3 pattern at k = K > 0 over one
  * region (recSearchFile 0x402250).  errs: 1 insertions, 2 deletions, 4
  * substitutions.  Returns the number of matches (may exceed cap), -1 if
- * refused (more than 64 states). */
+ * refused (a window union of more than 64 states, or a table slice past the
+ * state set's words). */
 int64_t pmr_eregular(const uint8_t* text, int64_t n, const int32_t* tree, const int32_t* nullable, int nodes,
                      const uint64_t* Bpos, int npos, int icase, int mode, int K, int errs, int64_t* out_beg,
                      int64_t* out_end, int64_t cap) {

@@ -377,50 +377,76 @@ int window_states(const Plan& p, int ms) {
 }
 
 // ---------------------------------------------------------------------------
-// eregular (k > 0, at most 64 states: one word): eregularPreproc 0x406a20
+// eregular (k > 0): eregularPreproc 0x406a20
 // ---------------------------------------------------------------------------
 
-inline uint64_t trans1(const std::vector<Set>& tab, uint64_t d) {
-    uint64_t r = 0;
-    while (d) {
-        r |= tab[__builtin_ctzll(d)][0];
-        d &= d - 1;
-    }
+// eregularPreproc's successor sets (over the arrows, exact)
+inline Set reach_of(const Automaton& A, const Set& d) {
+    Set r{};
+    for (int s = 0; s < A.ms; ++s)
+        if (has(d, s)) join(r, A.arrows[s]);
     return r;
 }
 
 struct EPlan {
     int etype = 3, ell = 0, cls = 3, npieces = 1;
     bool pieces_computed = false, defined = true;
-    uint64_t pwin[PM_MAX_K + 1] = {}, pini[PM_MAX_K + 1] = {}, pfin[PM_MAX_K + 1] = {};
+    Set pwin[PM_MAX_K + 1] = {}, pini[PM_MAX_K + 1] = {}, pfin[PM_MAX_K + 1] = {};
     int first[PM_MAX_K + 1] = {};
     uint64_t match0 = 0;   // class 1: P->0x28
 };
+
+// fwdCheck / bwdCheck's transition tables (regularMakeDet 0x40bfc0 in slices
+// of W = ceil(m / ceil(m / 16)) states, OptDetWidth .data 0x621920): table t
+// holds the states t W + b, but the checks index it by SLICE(D, off, W)
+// (0x41b8e0, one word) with off moving on by W or, when the next slice would
+// cross a word, to the next word (0x403530).  src[q] = the state whose
+// transitions state q takes, -1 when no slice reads q (identity for m <=
+// 64).  False when a slice would read past the set's words.
+bool slice_map(int m, std::vector<int>& src) {
+    const int nt0 = (m + 16 - 1) / 16, W = (m + nt0 - 1) / nt0, ntab = (m + W - 1) / W;
+    src.assign(64 * RG_NW, -1);
+    int off = 0;
+    for (int t = 0; t < ntab; ++t) {
+        if ((off >> 6) >= (m + 63) / 64 || (off >> 6) >= RG_NW) return false;
+        for (int b = 0; b < W; ++b) {
+            const int q = off + b, from = t * W + b;
+            if ((q >> 6) == (off >> 6) && from < m && q < 64 * RG_NW) src[q] = from;
+        }
+        off += W;
+        if (((off + W - 1) >> 6) != (off >> 6)) off = (off & ~63) + 64;
+    }
+    return true;
+}
 
 // regularFindBest with K, the breadth-first levels, the piece DP against
 // 0.78 and (K + 1) 1.3 fb, detClass of windows[0] (oracle/pm_nrgrep_reg.c
 // eplan; transpositions off, PatMatch's letters are i/d/s)
 EPlan eplan_of(const Automaton& A, int K) {
-    require(A.ms <= 64, "eregular: more than 64 states", PM_E_UNSUPPORTED);
     require(K >= 1 && K <= PM_MAX_K, "eregular: k out of range");
+    {
+        std::vector<int> src;
+        require(slice_map(A.ms, src), "eregular: a transition table slice past the state set", PM_E_UNSUPPORTED);
+    }
     const Plan fb = plan_of(A, K);
     const int m = A.ms, transp = 0;
-    const uint64_t fin = A.final_[0];
-    uint64_t seen = 1;
+    Set seen{};
+    seen[0] = 1;
     int nlev = 1;
-    while (!(seen & fin)) {   // 0x406db8
+    while (!meets(seen, A.final_)) {   // 0x406db8
         ++nlev;
-        seen |= trans1(A.arrows, seen);
+        join(seen, reach_of(A, seen));
         require(nlev <= m + 2, "eregular: no final state reachable");
     }
     const int minlen = nlev - 1;
-    std::vector<uint64_t> lev(nlev, 0);
-    lev[0] = 1;
-    seen = 1;
+    std::vector<Set> lev(nlev + 1, Set{});
+    lev[0][0] = 1;
+    seen = Set{};
+    seen[0] = 1;
     for (int i = 1; i <= minlen; ++i) {   // 0x406f69
-        const uint64_t succ = trans1(A.arrows, seen);
-        lev[i] = succ & ~seen;
-        seen |= succ;
+        const Set succ = reach_of(A, seen);
+        for (int q = 0; q < RG_NW; ++q) lev[i][q] = succ[q] & ~seen[q];
+        join(seen, succ);
     }
     int pl0 = minlen - K * transp;   // 0x406e54
     if ((unsigned)pl0 > 64u) pl0 = 64;
@@ -428,14 +454,14 @@ EPlan eplan_of(const Automaton& A, int K) {
     const int PL1 = pl0 + 1;
     double best = 0.78;
     int chosen = 0;
-    uint64_t pieces[PM_MAX_K + 1] = {};
+    Set pieces[PM_MAX_K + 1] = {};
     if (PL1 > 1 && pl0 != 1 && !(1.0 / (double)pl0 > 0.78)) {
         double lp[256];
         letter_probs(lp);
         std::vector<double> prob(m, 0.0);
         for (int i = 0; i < m; ++i)
             for (int c = 0; c < 256; ++c)
-                if ((A.B[c][0] >> i) & 1) prob[i] += lp[c];
+                if (has(A.B[c], i)) prob[i] += lp[c];
         std::vector<double> Av((size_t)m * PL1, 0.0);
         for (int i = 0; i < m; ++i) {
             Av[(size_t)i * PL1] = 1.0;
@@ -445,7 +471,7 @@ EPlan eplan_of(const Automaton& A, int K) {
             for (int i = 0; i < m; ++i) {
                 double sum = 0.0;
                 for (int j = 0; j < m; ++j)
-                    if ((A.arrows[i][0] >> j) & 1) sum += Av[(size_t)j * PL1 + l - 1];
+                    if (has(A.arrows[i], j)) sum += Av[(size_t)j * PL1 + l - 1];
                 sum *= prob[i];
                 Av[(size_t)i * PL1 + l] = 1.0 < sum ? 1.0 : sum;
             }
@@ -459,7 +485,7 @@ EPlan eplan_of(const Automaton& A, int K) {
                     double v = Av[(size_t)i * PL1 + a];
                     if (a < l)
                         for (int j = 0; j < m; ++j)
-                            if ((A.arrows[i][0] >> j) & 1) v = 1.0 - (1.0 - v) * (1.0 - bt(j, l - 1, a));
+                            if (has(A.arrows[i], j)) v = 1.0 - (1.0 - v) * (1.0 - bt(j, l - 1, a));
                     bt(i, l, a) = v;
                 }
         std::vector<double> C((size_t)nlev * PL1, 0.0);
@@ -467,7 +493,7 @@ EPlan eplan_of(const Automaton& A, int K) {
             for (int l = 0; l < PL1; ++l) {
                 double sum = 1.0;
                 for (int i = 0; i < m; ++i)
-                    if (((lev[lv] >> i) & 1) && l != 0)
+                    if (has(lev[lv], i) && l != 0)
                         for (int a = 1; a <= l; ++a) sum += bt(i, l, a);
                 C[(size_t)lv * PL1 + l] = sum;
             }
@@ -517,10 +543,10 @@ EPlan eplan_of(const Automaton& A, int K) {
     if (best < 0.78) {   // 0x4082c9
         e.pieces_computed = true;
         for (int i = 0; i <= K; ++i) {
-            uint64_t w = pieces[i], last = 0;
+            Set w = pieces[i], last{};
             for (int st = 0; st < chosen; ++st) {
-                last = trans1(A.arrows, w);
-                w |= last;
+                last = reach_of(A, w);
+                join(w, last);
             }
             e.pwin[i] = w;
             e.pini[i] = pieces[i];
@@ -536,25 +562,23 @@ EPlan eplan_of(const Automaton& A, int K) {
         e.etype = fb.ell == 0 ? 3 : 2;
         e.ell = fb.ell;
         e.npieces = 1;
-        e.pwin[0] = fb.win[0];
-        e.pini[0] = fb.winit[0];
-        e.pfin[0] = fb.wfinal[0];
+        e.pwin[0] = fb.win;
+        e.pini[0] = fb.winit;
+        e.pfin[0] = fb.wfinal;
     }
-    Set w0{};
-    w0[0] = e.pwin[0];
-    e.cls = det_class(A, 0, w0);
+    e.cls = det_class(A, 0, e.pwin[0]);
     if (e.cls == 1) {   // 0x407e4b: the first state of each window (windows[1 .. K] unset for a window plan)
         const int nw = (e.etype == 1 || e.pieces_computed) ? K + 1 : 1;
         e.defined = nw == K + 1;
         for (int i = 0; i < nw; ++i) {
             int f = 0;
-            while (f < m && !((e.pwin[i] >> f) & 1)) ++f;
+            while (f < m && !has(e.pwin[i], f)) ++f;
             e.first[i] = f;
-            if (e.ell != 0) {
+            if (e.ell != 0) {   // shl %cl: the count mod 64 (0x407ef0)
                 e.match0 |= 1ull << (f & 63);
             } else {
                 int r = f + 1;
-                while (r < m && ((e.pwin[i] >> r) & 1)) ++r;
+                while (r < m && has(e.pwin[i], r)) ++r;
                 e.match0 |= 1ull << (r & 63);
             }
         }
@@ -639,7 +663,8 @@ bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_l
         // class 2: eregularPreproc stores through a null pointer (0x4081ed),
         // nrgrep_coords dies before the scan: nothing prints
         if (E.cls == 2) return false;
-        S.nw = 1;
+        const int nw = ms <= 64 ? 1 : RG_NW;
+        S.nw = nw;
         S.type = E.etype;
         S.ell = E.ell;
         S.cls = E.cls;
@@ -651,43 +676,52 @@ bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_l
         S.max_len = max_len < 0 ? -1 : max_len + k;
         S.gap = max_len < 0 ? -1 : 2 * S.max_len + 4;
         S.lines = 1;
-        S.final_[0] = A.final_[0];
-        S.o_arr = take(64);
-        S.o_rev = take(64);
-        S.o_B = take(256);
+        for (int q = 0; q < RG_NW; ++q) S.final_[q] = A.final_[q];
+        S.o_arr = take((size_t)ms * nw);
+        S.o_rev = take((size_t)ms * nw);
+        S.o_B = take((size_t)256 * nw);
         S.o_Bw = take(256);
         S.o_A = take(256);
         S.o_fw = take(64);
         S.o_rw = take(64);
         S.o_T0 = take(256);
         S.o_T2 = take(256);
-        for (int q = 0; q < ms; ++q) {
-            tab[S.o_arr + q] = A.arrows[q][0];
-            tab[S.o_rev + q] = A.rev[q][0];
-        }
-        for (int c = 0; c < 256; ++c) tab[S.o_B + c] = A.B[c][0];
+        // fwdCheck / bwdCheck's transitions with the slice layout baked in:
+        // row q = the arrows of the state whose table slot q's bit indexes
+        // (slice_map; the identity up to 64 states)
+        std::vector<int> src;
+        require(slice_map(ms, src), "eregular: a transition table slice past the state set", PM_E_UNSUPPORTED);
+        for (int q = 0; q < ms; ++q)
+            if (src[q] >= 0)
+                for (int w = 0; w < nw; ++w) {
+                    tab[S.o_arr + (size_t)q * nw + w] = A.arrows[src[q]][w];
+                    tab[S.o_rev + (size_t)q * nw + w] = A.rev[src[q]][w];
+                }
+        for (int c = 0; c < 256; ++c)
+            for (int w = 0; w < nw; ++w) tab[S.o_B + (size_t)c * nw + w] = A.B[c][w];
         if (E.cls == 3) {   // eregularLoadFast 0x406860: the union of the windows
             Set uw{}, ui{}, uf{};
             for (int i = 0; i < E.npieces; ++i) {
-                uw[0] |= E.pwin[i];
-                ui[0] |= E.pini[i];
-                uf[0] |= E.pfin[i];
+                join(uw, E.pwin[i]);
+                join(ui, E.pini[i]);
+                join(uf, E.pfin[i]);
             }
             window_tables(A, uw, ui, uf, E.ell, S, tab, true);
             S.nstates = S.mp;
         } else {            // esimpleLoadFast 0x415370 over the states first[r] ..
+            // P->0x858 is the identity over every state (0x407f67): the
+            // walk takes state i for slot i (no unmap beyond 64 states)
             S.nstates = ms;
             S.mp = ms;
             for (int i = 0; i < 64; ++i) S.unmap[i] = i < ms ? i : -1;
             uint64_t* T0 = tab.data() + S.o_T0;
             uint64_t* T2 = tab.data() + S.o_T2;
             for (int c = 0; c < 256; ++c) {
-                const uint64_t bc = A.B[c][0];
-                if (E.etype == 1) {   // 0x4153fa: the pieces, bit r * pl + pp
+                if (E.etype == 1) {   // 0x4153fa: the pieces, bit r * pl + pp (ISSET: every state)
                     for (int r = 0; r <= k; ++r)
                         for (int pp = 0; pp < E.ell; ++pp) {
                             const int st = E.first[r] + E.ell - 1 - pp;
-                            if (st < 64 && ((bc >> st) & 1)) {
+                            if (st < ms && has(A.B[c], st)) {
                                 const uint64_t bit = 1ull << (r * E.ell + pp);
                                 T0[c] |= bit;
                                 if (pp > 0) T2[c] |= bit;
@@ -696,7 +730,7 @@ bool rg_build(const RgTree& t, const uint64_t* B, int W, int npos, int64_t max_l
                 } else {              // simpleLoadFast 0x417561: the window backward
                     for (int r = 0; r < E.ell; ++r) {
                         const int st = E.first[0] + E.ell - 1 - r;
-                        if (st < 64 && ((bc >> st) & 1)) T0[c] |= 1ull << (64 - E.ell + r);
+                        if (st < ms && has(A.B[c], st)) T0[c] |= 1ull << (64 - E.ell + r);
                     }
                 }
             }
@@ -953,9 +987,68 @@ struct RgWalk {
     }
 };
 
-// eregular (k > 0, one word): the scanners and checkMatch of
-// oracle/pm_nrgrep_reg.c over the cluster's text
-template <int KR, int SC>
+// A state set of the eregular verify: NW words (1 up to 64 states, RG_NW
+// beyond)
+template <int NW>
+struct WS {
+    uint64_t w[NW];
+};
+template <int NW>
+__device__ __forceinline__ WS<NW> ws_zero() {
+    WS<NW> r;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r.w[q] = 0;
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ WS<NW> ws_bit(int s) {
+    WS<NW> r;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r.w[q] = q == (s >> 6) ? 1ull << (s & 63) : 0ull;
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ WS<NW> ws_or(const WS<NW>& a, const WS<NW>& b) {
+    WS<NW> r;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r.w[q] = a.w[q] | b.w[q];
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ WS<NW> ws_and(const WS<NW>& a, const WS<NW>& b) {
+    WS<NW> r;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r.w[q] = a.w[q] & b.w[q];
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ bool ws_meets(const WS<NW>& a, const WS<NW>& b) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) x |= a.w[q] & b.w[q];
+    return x != 0;
+}
+template <int NW>
+__device__ __forceinline__ bool ws_any(const WS<NW>& a) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) x |= a.w[q];
+    return x != 0;
+}
+template <int NW>
+__device__ __forceinline__ WS<NW> ws_load(const uint64_t* p) {
+    WS<NW> r;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) r.w[q] = p[q];
+    return r;
+}
+
+// eregular (k > 0): the scanners and checkMatch of oracle/pm_nrgrep_reg.c
+// over the cluster's text.  The scanners run over one word (the window
+// remapped, or esimple's piece bits); checkMatch's rows hold NW words, their
+// transitions through the tables rg_build baked the slice layout into
+// (slice_map: fwdCheck / bwdCheck's regularMakeDet tables indexed by SLICE)
+template <int KR, int SC, int NW>
 struct ErgWalk {
     const RgSlot* S;
     const uint64_t* tab;
@@ -996,6 +1089,7 @@ struct ErgWalk {
     __device__ bool right_ok(uint64_t q, uint64_t lim) const {
         return !((S->anchors & PM_ANCHOR_END) && q < lim && at(q) != (uint8_t)'\n');
     }
+    // the window scanners' one-word transitions
     __device__ static uint64_t tr(const uint64_t* tb, uint64_t d) {
         uint64_t r = 0;
         while (d) {
@@ -1004,16 +1098,33 @@ struct ErgWalk {
         }
         return r;
     }
+    // checkMatch's transitions: row q of tb (NW words) for every state q of d
+    __device__ static WS<NW> trn(const uint64_t* tb, const WS<NW>& d) {
+        WS<NW> r = ws_zero<NW>();
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            uint64_t x = d.w[q];
+            while (x) {
+                const uint64_t* row = tb + (size_t)(q * 64 + __builtin_ctzll(x)) * NW;
+                x &= x - 1;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) r.w[w] |= row[w];
+            }
+        }
+        return r;
+    }
+    __device__ WS<NW> bmask(uint64_t p) const { return ws_load<NW>(tab + S->o_B + (size_t)at(p) * NW); }
     // fwdCheck 0x403310: from state s (it read t[p]) forward; kio: budget in,
     // errors used out
     __device__ uint64_t efwd(uint64_t p, uint64_t lim, int s, int& kio) const {
         const int K = kio, ins = S->errs & PM_ERR_INS, del = S->errs & PM_ERR_DEL, sub = S->errs & PM_ERR_SUB;
         const uint64_t* arr = tab + S->o_arr;
-        const uint64_t* B = tab + S->o_B;
-        const uint64_t F = S->final_[0];
-        uint64_t rows[KR + 1];
-        rows[0] = 1ull << s;
-        if (rows[0] & F) {   // 0x40339d: insertions up to the right context
+        WS<NW> F;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) F.w[q] = S->final_[q];
+        WS<NW> rows[KR + 1];
+        rows[0] = ws_bit<NW>(s);
+        if (ws_meets(rows[0], F)) {   // 0x40339d: insertions up to the right context
             kio = 0;
             for (uint64_t q = p + 1;; ++q) {
                 if (right_ok(q, lim + 1)) return q - 1;
@@ -1026,8 +1137,8 @@ struct ErgWalk {
 #pragma unroll
         for (int j = 1; j <= KR; ++j) {   // 0x4034c0 (rows left unset without OptDel: row 0)
             if (j > kmax) break;
-            rows[j] = del ? rows[j - 1] | tr(arr, rows[j - 1]) : rows[j - 1];
-            if (del && (rows[j] & F) && right_ok(p + 1, lim + 1)) {
+            rows[j] = del ? ws_or(rows[j - 1], trn(arr, rows[j - 1])) : rows[j - 1];
+            if (del && ws_meets(rows[j], F) && right_ok(p + 1, lim + 1)) {
                 kio = j;
                 kmax = j - 1;
                 best = p;
@@ -1036,29 +1147,29 @@ struct ErgWalk {
         if (p == lim) return best;
         for (uint64_t cur = p;;) {
             ++cur;
-            const uint64_t bc = B[at(cur)];
-            const uint64_t n0 = tr(arr, rows[0]) & bc;
-            if ((n0 & F) && right_ok(cur + 1, lim + 1)) {
+            const WS<NW> bc = bmask(cur);
+            const WS<NW> n0 = ws_and(trn(arr, rows[0]), bc);
+            if (ws_meets(n0, F) && right_ok(cur + 1, lim + 1)) {
                 kio = 0;
                 return cur;
             }
-            uint64_t oldp = rows[0], last = n0;
+            WS<NW> oldp = rows[0], last = n0;
             rows[0] = n0;
 #pragma unroll
             for (int j = 1; j <= KR; ++j) {   // 0x4037a0
                 if (j > kmax) break;
-                uint64_t v = del ? tr(arr, last) : 0;
-                if (ins) v |= oldp;
-                if (sub) v |= tr(arr, oldp);
-                v |= tr(arr, rows[j]) & bc;
-                const uint64_t oj = rows[j];
+                WS<NW> v = del ? trn(arr, last) : ws_zero<NW>();
+                if (ins) v = ws_or(v, oldp);
+                if (sub) v = ws_or(v, trn(arr, oldp));
+                v = ws_or(v, ws_and(trn(arr, rows[j]), bc));
+                const WS<NW> oj = rows[j];
                 rows[j] = v;
                 last = v;
-                if ((v & F) && right_ok(cur + 1, lim + 1)) {   // 0x403a01: the fewest errors
+                if (ws_meets(v, F) && right_ok(cur + 1, lim + 1)) {   // 0x403a01: the fewest errors
                     int c = j;
 #pragma unroll
                     for (int d = KR - 1; d >= 0; --d)   // while rows[c - 1] is final: --c
-                        if (d == c - 1 && (rows[d] & F)) c = d;
+                        if (d == c - 1 && ws_meets(rows[d], F)) c = d;
                     if (c == 0) {
                         kio = 0;
                         return cur;
@@ -1070,17 +1181,16 @@ struct ErgWalk {
                 }
                 oldp = oj;
             }
-            if (!last || cur == lim) return best;
+            if (!ws_any(last) || cur == lim) return best;
         }
     }
     // bwdCheck 0x403df0: from state s (it reads t[p - 1]) backward
     __device__ uint64_t ebwd(uint64_t p, uint64_t lim, int s, int& kio) const {
         const int K = kio, ins = S->errs & PM_ERR_INS, del = S->errs & PM_ERR_DEL, sub = S->errs & PM_ERR_SUB;
         const uint64_t* rev = tab + S->o_rev;
-        const uint64_t* B = tab + S->o_B;
-        uint64_t rows[KR + 1];
-        rows[0] = 1ull << s;
-        if (rows[0] & 1) {   // 0x403e71: insertions down to the left context
+        WS<NW> rows[KR + 1];
+        rows[0] = ws_bit<NW>(s);
+        if (rows[0].w[0] & 1) {   // 0x403e71: insertions down to the left context
             kio = 0;
             for (uint64_t q = p;;) {
                 if (left_ok(q, lim)) return q;
@@ -1095,8 +1205,8 @@ struct ErgWalk {
 #pragma unroll
         for (int j = 1; j <= KR; ++j) {   // 0x403f80
             if (j > kmax) break;
-            rows[j] = del ? rows[j - 1] | tr(rev, rows[j - 1]) : rows[j - 1];
-            if (del && (rows[j] & 1) && left_ok(p, lim)) {
+            rows[j] = del ? ws_or(rows[j - 1], trn(rev, rows[j - 1])) : rows[j - 1];
+            if (del && (rows[j].w[0] & 1) && left_ok(p, lim)) {
                 kio = j;
                 kmax = j - 1;
                 best = p;
@@ -1105,29 +1215,29 @@ struct ErgWalk {
         if (p == lim) return best;
         for (uint64_t cur = p;;) {
             --cur;
-            const uint64_t bc = B[at(cur)];
-            const uint64_t n0 = tr(rev, rows[0] & bc);
-            if ((n0 & 1) && left_ok(cur, lim)) {
+            const WS<NW> bc = bmask(cur);
+            const WS<NW> n0 = trn(rev, ws_and(rows[0], bc));
+            if ((n0.w[0] & 1) && left_ok(cur, lim)) {
                 kio = 0;
                 return cur;
             }
-            uint64_t oldp = rows[0], last = n0;
+            WS<NW> oldp = rows[0], last = n0;
             rows[0] = n0;
 #pragma unroll
             for (int j = 1; j <= KR; ++j) {   // 0x404230
                 if (j > kmax) break;
-                uint64_t v = del ? tr(rev, last) : 0;
-                if (ins) v |= oldp;
-                if (sub) v |= tr(rev, oldp);
-                v |= tr(rev, rows[j] & bc);
-                const uint64_t oj = rows[j];
+                WS<NW> v = del ? trn(rev, last) : ws_zero<NW>();
+                if (ins) v = ws_or(v, oldp);
+                if (sub) v = ws_or(v, trn(rev, oldp));
+                v = ws_or(v, trn(rev, ws_and(rows[j], bc)));
+                const WS<NW> oj = rows[j];
                 rows[j] = v;
                 last = v;
-                if ((v & 1) && left_ok(cur, lim)) {
+                if ((v.w[0] & 1) && left_ok(cur, lim)) {
                     int c = j;
 #pragma unroll
                     for (int d = KR - 1; d >= 0; --d)   // while rows[c - 1] is final: --c
-                        if (d == c - 1 && (rows[d] & 1)) c = d;
+                        if (d == c - 1 && (rows[d].w[0] & 1)) c = d;
                     if (c == 0) {
                         kio = 0;
                         return cur;
@@ -1139,40 +1249,62 @@ struct ErgWalk {
                 }
                 oldp = oj;
             }
-            if (!last || cur == lim) return best;
+            if (!ws_any(last) || cur == lim) return best;
         }
     }
-    // checkMatch 0x406010: the states of `match` in order; the first whose
-    // first phase succeeds decides
+    // one state of checkMatch's loop: 1 printed (mb, me), 0 the candidate
+    // fails (a failed second phase), -1 the next state
+    __device__ int attempt(int s, uint64_t pos, uint64_t rb, uint64_t re, uint64_t& mb, uint64_t& me) {
+        int k1 = S->k, k2;
+        uint64_t st, en;
+        if (S->type != 3) {
+            en = efwd(pos, re - 1, s, k1);
+            if (en == RG_NONE) return -1;
+            k2 = S->k - k1;
+            st = ebwd(pos + 1, rb, s, k2);
+        } else {
+            st = ebwd(pos, rb, s, k1);
+            if (st == RG_NONE) return -1;
+            k2 = S->k - k1;
+            en = efwd(pos - 1, re - 1, s, k2);
+        }
+        if (st == RG_NONE || en == RG_NONE) return 0;   // 0x406248: the second phase fails the candidate
+        mb = st;
+        me = en + 1;
+        return 1;
+    }
+    // checkMatch 0x406010: the slots i < P->0x24 whose bit of `match` is set
+    // (`bt`: the bit number mod 64), in order; the first whose first phase
+    // succeeds decides
     __device__ bool check(uint64_t pos, uint64_t match, uint64_t& mb, uint64_t& me) {
         if (S->type == 3 && pos == 0) return false;
         const uint64_t rp = S->type == 3 ? pos - 1 : pos;
         uint64_t rb, re;
         record(rp, rb, re);
         if (rp < rb || rp >= re) return false;
-        if (S->nstates < 64) match &= (1ull << S->nstates) - 1;
-        while (match) {
-            const int i = __builtin_ctzll(match);
-            match &= match - 1;
-            const int s = S->unmap[i];
-            if (s < 0) continue;
-            int k1 = S->k, k2;
-            uint64_t st, en;
-            if (S->type != 3) {
-                en = efwd(pos, re - 1, s, k1);
-                if (en == RG_NONE) continue;
-                k2 = S->k - k1;
-                st = ebwd(pos + 1, rb, s, k2);
-            } else {
-                st = ebwd(pos, rb, s, k1);
-                if (st == RG_NONE) continue;
-                k2 = S->k - k1;
-                en = efwd(pos - 1, re - 1, s, k2);
+        if (S->nstates <= 64) {
+            if (S->nstates < 64) match &= (1ull << S->nstates) - 1;
+            while (match) {
+                const int i = __builtin_ctzll(match);
+                match &= match - 1;
+                const int s = S->unmap[i];
+                if (s < 0) continue;
+                const int r = attempt(s, pos, rb, re, mb, me);
+                if (r >= 0) return r == 1;
             }
-            if (st == RG_NONE || en == RG_NONE) return false;   // 0x406248: the second phase fails the candidate
-            mb = st;
-            me = en + 1;
-            return true;
+            return false;
+        }
+        // class 1 over more than 64 states: slot i = state i (P->0x858 the
+        // identity), tested by bit i mod 64 -- states i, i + 64, ... per bit
+        for (int base = 0; base < S->nstates; base += 64) {
+            uint64_t mm = match;
+            while (mm) {
+                const int s = base + __builtin_ctzll(mm);
+                mm &= mm - 1;
+                if (s >= S->nstates) break;
+                const int r = attempt(s, pos, rb, re, mb, me);
+                if (r >= 0) return r == 1;
+            }
         }
         return false;
     }
@@ -1400,7 +1532,7 @@ struct ErgWalk {
     }
 };
 
-template <int KR, int SC>
+template <int KR, int SC, int NW>
 __global__ __launch_bounds__(WALK_T) void k_erg_walk(XtPrep X, uint64_t* __restrict__ keys, uint32_t* __restrict__ lens,
                                                      const uint64_t* total_d, uint64_t total_h,
                                                      uint8_t* __restrict__ acc, TextView tv) {
@@ -1431,7 +1563,7 @@ __global__ __launch_bounds__(WALK_T) void k_erg_walk(XtPrep X, uint64_t* __restr
                 R0 = tv.reg.t[r];
                 n = tv.reg.e[r];
             }
-            ErgWalk<KR, SC> w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
+            ErgWalk<KR, SC, NW> w{S, tab, tv, n, R0, ~0ull, n, TxtCache{tcbuf, 0, 0}};
             // from the start of first's line, at most span + 4 before it
             // (the scanners' rows then agree with the whole scan's, and no
             // match found before first can start at another cluster's key)
@@ -1548,12 +1680,20 @@ void rg_launch(const XtPrep& X, uint64_t* keys, uint32_t* lens, const uint64_t* 
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(WALK_T), lds, s, X, keys, lens, total_d, total_h, acc, tv);
         };
+        // (and the verify's words: one up to 64 states)
         auto by_k = [&](auto sc) {
             constexpr int SC = decltype(sc)::value;
-            X.k == 1   ? go(k_erg_walk<1, SC>)
-            : X.k == 2 ? go(k_erg_walk<2, SC>)
-            : X.k == 3 ? go(k_erg_walk<3, SC>)
-                       : go(k_erg_walk<PM_MAX_K, SC>);
+            if (X.words == 1) {
+                X.k == 1   ? go(k_erg_walk<1, SC, 1>)
+                : X.k == 2 ? go(k_erg_walk<2, SC, 1>)
+                : X.k == 3 ? go(k_erg_walk<3, SC, 1>)
+                           : go(k_erg_walk<PM_MAX_K, SC, 1>);
+            } else {
+                X.k == 1   ? go(k_erg_walk<1, SC, RG_NW>)
+                : X.k == 2 ? go(k_erg_walk<2, SC, RG_NW>)
+                : X.k == 3 ? go(k_erg_walk<3, SC, RG_NW>)
+                           : go(k_erg_walk<PM_MAX_K, SC, RG_NW>);
+            }
         };
         switch (X.scanner) {
             case 0: by_k(std::integral_constant<int, 0>{}); break;
@@ -1609,11 +1749,12 @@ extern "C" int pm_eregular_plan(int m, int words, const uint64_t* byte_mask, int
         out[2] = E.cls;
         out[3] = E.defined ? 1 : 0;
         out[4] = E.npieces;
-        for (int i = 0; i < E.npieces; ++i) {
-            masks[3 * i] = E.pwin[i];
-            masks[3 * i + 1] = E.pini[i];
-            masks[3 * i + 2] = E.pfin[i];
-        }
-        masks[3 * (PM_MAX_K + 1)] = E.match0;
+        for (int i = 0; i < E.npieces; ++i)
+            for (int q = 0; q < RG_NW; ++q) {
+                masks[(3 * i) * RG_NW + q] = E.pwin[i][q];
+                masks[(3 * i + 1) * RG_NW + q] = E.pini[i][q];
+                masks[(3 * i + 2) * RG_NW + q] = E.pfin[i][q];
+            }
+        masks[3 * (PM_MAX_K + 1) * RG_NW] = E.match0;
     });
 }

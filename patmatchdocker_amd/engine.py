@@ -275,8 +275,6 @@ def route(prog: Program, alphabet: str, k: int, types: str) -> str:
         # (pm_regular.hip)
         raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
                                % (k, prog.min_len))
-    if k > 0 and prog.kind == "regular" and prog.m + 1 > 64:
-        raise UnsupportedOnGPU("nrgrep's eregular report is restated for at most 63 positions (%d)" % prog.m)
     return "nfa"   # automaton kernels: anything else, long oligos and k > 3 included
 
 
@@ -499,12 +497,16 @@ def eregular_plan(prog: Program, k: int) -> dict:
     w, bm, _, _, _ = _nfa_tables(prog)
     tree, tnull = _tree_tables(prog)
     out = np.zeros(5, dtype=np.int32)
-    masks = np.zeros(3 * (_lib.PM_MAX_K + 1) + 1, dtype=np.uint64)
+    nw = 5   # RG_NW: words per state set
+    masks = np.zeros((3 * (_lib.PM_MAX_K + 1) + 1) * nw, dtype=np.uint64)
     check(_lib.load().pm_eregular_plan(prog.m, w, bm.ctypes.data, len(prog.tree), tree.ctypes.data, tnull.ctypes.data,
                                        k, out.ctypes.data, masks.ctypes.data))
-    wins = [(int(masks[3 * i]), int(masks[3 * i + 1]), int(masks[3 * i + 2])) for i in range(int(out[4]))]
+
+    def word_set(j):
+        return sum(int(masks[j * nw + q]) << (64 * q) for q in range(nw))
+    wins = [(word_set(3 * i), word_set(3 * i + 1), word_set(3 * i + 2)) for i in range(int(out[4]))]
     return {"type": int(out[0]), "ell": int(out[1]), "cls": int(out[2]), "defined": bool(out[3]),
-            "windows": wins, "match": int(masks[3 * (_lib.PM_MAX_K + 1)])}
+            "windows": wins, "match": int(masks[3 * (_lib.PM_MAX_K + 1) * nw])}
 
 
 def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",

@@ -64,6 +64,11 @@ QUERIES = [
     ("(CA){2,4}GT", "dna", None, "insertion", "deletion", None, "2", 300),
     ("C(AG){1,3}L", "pep", None, None, None, None, "1", 300),
     ("K(RK){1,2}XXC", "pep", None, None, None, "substitution", "2", 300),
+    # group repeats past 63 positions at k > 0 (round 6: the multi-word
+    # eregular verify, its sliced transition tables included)
+    ("(CA){37,38}G", "dna", None, None, None, None, "1", 300),
+    ("(GATC){8,16}T", "dna", "Both strands", None, None, None, "1", 300),
+    ("(CA){20,40}GT", "dna", None, "insertion", "deletion", None, "1", 300),
     ("AC", "pep", None, None, None, None, None, 500),          # below MIN_TOKEN
     ("EFL", "dna", None, None, None, None, None, 500),        # invalid nucleotide
 ]
@@ -73,7 +78,9 @@ def main():
     tmp = tempfile.mkdtemp()
     try:
         files = {"orf_dna.seq": dna_fasta(101, 12, max_len=2500, noise=True)
-                 + b">orfA orfA desc\nATGAAACCCGGGAATTCTTTTAA\n>orfB\nATGCATGCTAA\n>orfC x\natgtataaaagtaa\n",
+                 + b">orfA orfA desc\nATGAAACCCGGGAATTCTTTTAA\n>orfB\nATGCATGCTAA\n>orfC x\natgtataaaagtaa\n"
+                 + b">orfR repeats\nTT" + b"CA" * 38 + b"GTTA" + b"GATC" * 9 + b"TAA" + b"CA" * 25 + b"GT"
+                 + b"CC" + b"CA" * 18 + b"GCA" + b"CA" * 18 + b"GTT\n",
                  "orf_pep.seq": pep_fasta(102, 60, max_len=500)
                  + b">YPX1 X SGDID:S1, p\nMSKCAACGGGCLNASKDEL*\n>YPX2\nMSKDEL\n"}
         for name, data in files.items():

@@ -119,14 +119,15 @@ def test_route_indels():
     assert engine.error_mask("ids") == 7 and engine.error_mask("d") == 2
     # deletions with k >= the shortest match: class sequences, extended and
     # regular patterns (the esimple / eextended / eregular walks over every
-    # line); more than 63 positions at k > 0 are refused loudly for regular
-    # patterns
+    # line); regular patterns over 63 positions at k > 0 route too (round 6:
+    # the multi-word eregular verify)
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 3, "d") == "nfa"
     assert engine.route(compile_pattern("(RG?D)"), engine.BYTE, 2, "d") == "nfa"
     assert engine.route(compile_pattern("(R(GK)?D)"), engine.BYTE, 2, "d") == "nfa"
-    with pytest.raises(UnsupportedOnGPU):
-        engine.route(compile_pattern("(R(GK)?D" + "A" * 60 + ")"), engine.BYTE, 2, "d")
+    assert engine.route(compile_pattern("(R(GK)?D" + "A" * 60 + ")"), engine.BYTE, 2, "d") == "nfa"
     assert engine.route(compile_pattern("(RGD)"), engine.BYTE, 2, "d") == "nfa"
+    with pytest.raises(UnsupportedOnGPU):   # beyond the automaton kernels' 256 positions
+        engine.route(compile_pattern("(R(GK)?D" + "A" * 260 + ")"), engine.BYTE, 1, "s")
 
 
 def test_flag_values_match_the_header():

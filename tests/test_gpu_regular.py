@@ -205,3 +205,20 @@ def test_long_records_with_errors(engine, oracle_mod):
     text = "".join(recs).encode()
     progs = [compile_pattern(convert("-n", "GA(TC){1,2}A"))]
     assert _check(engine, oracle_mod, text, progs, k=1, types="ids") > 1000
+
+
+@pytest.mark.parametrize("width", [60, None])
+def test_long_group_repeats_at_k_above_zero(engine, oracle_mod, width):
+    """Group repeats past 63 positions (round 6): the eregular verify over
+    several words, the sliced transition tables of fwdCheck / bwdCheck with
+    their word jumps (tests/test_nrgrep_eregular.py LONG_REPEATS) -- the
+    verdict's (GATC){8,16} and (CA){20,40}GT among them -- over tandem
+    repeats long enough to match, -k 1ids / 2ids / 1s / 2d, both layouts."""
+    from tests.test_nrgrep_eregular import _long_progs
+    progs = [p for _, p in _long_progs()]
+    text = tandem_fasta(606, ["CA" * 37 + "G", "CA" * 38 + "GT", "GATC" * 9 + "T", "GATC" * 13, "CA" * 25 + "GT",
+                              "AC" * 31 + "GT", "CA", "GATC", "TG"], n_records=5, rec_len=6000, width=width)
+    total = 0
+    for k, types in [(1, "ids"), (2, "ids"), (1, "s"), (2, "d")]:
+        total += _check(engine, oracle_mod, text, progs, k=k, types=types)
+    assert total > 30

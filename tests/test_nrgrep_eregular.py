@@ -121,3 +121,94 @@ def test_group_repeat_mismatches_converter_patterns(oracle_mod):
     assert len(got) > 5
     for s, e in got:
         assert _approx(prog.source, text, s, e, 1, "ids")
+
+
+# Group repeats past 63 positions (round 6): the eregular verify's rows span
+# several words.  fwdCheck / bwdCheck read the regularMakeDet tables (states
+# t W .. t W + W - 1, W = ceil(m / ceil(m / 16))) by SLICE with an offset that
+# jumps to the next word when a slice would cross one (0x403530), so where W
+# does not divide 64 the states past the jump take other states' transitions
+# (oracle etab).  With W = 16 the verify is the automaton's own.
+LONG_REPEATS = [
+    ("-n", "(CA){37,38}G"),      # 78 states, W = 16: exact
+    ("-n", "(CA){37,38}GT"),     # 79 states, W = 16
+    ("-n", "(GATC){8,16}T"),     # 66 states, W = 14: a jump over states 56 .. 63
+    ("-c", "(GATC){8,16}"),      # 65 states, W = 13
+    ("-n", "(CA){20,40}GT"),     # 83 states, W = 14
+    ("-c", "(CA){20,40}GT"),
+    ("-c", "AC(GT){30,35}"),     # 73 states
+]
+
+
+def _long_progs():
+    out = []
+    for strand, pat in LONG_REPEATS:
+        src = convert("-n", pat) if strand == "-n" else convert("-c", convert("-n", pat))
+        prog = compile_pattern(src)
+        assert prog.kind == "regular" and prog.m + 1 > 64, (strand, pat, prog.kind, prog.m)
+        out.append(((strand, pat), prog))
+    return out
+
+
+def _slice_width(states):
+    nt0 = (states + 15) // 16
+    return (states + nt0 - 1) // nt0
+
+
+def test_long_plan_library_equals_oracle(oracle_mod):
+    for name, prog in _long_progs():
+        for k in (1, 2, 3):
+            want = oracle_mod.eregular_plan(prog, k)
+            got = engine.eregular_plan(prog, k)
+            for key in ("type", "ell", "cls", "defined", "windows", "match"):
+                assert got[key] == want[key], (name, k, key)
+            assert want["states"] == prog.m + 1 if want["cls"] == 1 else want["states"] <= 64
+
+
+def _planted(rng, units, lines=30):
+    def mutate(s, n):
+        s = list(s)
+        for _ in range(n):
+            i, op = rng.randrange(len(s)), rng.randrange(3)
+            if op == 0:
+                s[i] = rng.choice("ACGT")
+            elif op == 1:
+                del s[i]
+            else:
+                s.insert(i, rng.choice("ACGT"))
+        return "".join(s)
+    out = []
+    for r in range(lines):
+        line = "".join(rng.choice("ACGT") for _ in range(rng.randint(5, 30)))
+        line += mutate(rng.choice(units), rng.randint(0, 2)) + "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 9)))
+        out.append(">s%d\n%s\n" % (r, line))
+    return "".join(out).encode()
+
+
+def test_long_repeats_with_aligned_slices_print_approximate_occurrences(oracle_mod):
+    """W = 16: every slice is one word's, the verify follows the automaton:
+    every print is an occurrence with <= k errors, prints never overlap."""
+    rng = random.Random(606)
+    for (strand, pat), prog in _long_progs()[:2]:
+        assert _slice_width(prog.m + 1) == 16
+        text = _planted(rng, ["CA" * 37 + "G", "CA" * 38 + "GT", "CA" * 36 + "G", "CA" * 40])
+        for k, types in [(1, "ids"), (2, "ids"), (1, "s"), (2, "d")]:
+            got = oracle_mod.scan_reported(text, prog, k, types, bufsize=0)
+            assert len(got) >= 5, (pat, k, types)
+            last = -1
+            for s, e in got:
+                assert s >= last and _approx(prog.source, text, s, e, k, types), (pat, k, types, s, e)
+                last = e
+
+
+def test_long_repeat_whose_slices_jump_prints_nothing(oracle_mod):
+    """(CA){20,40}GT: 83 states, W = 14, the fifth slice jumps from state 56
+    to 64; states 56 .. 63 take no transition in fwdCheck, the piece
+    candidates' forward phase dies there, nothing is printed (the restated
+    binary; parity unpinned)."""
+    rng = random.Random(607)
+    (_, prog) = _long_progs()[4]
+    text = _planted(rng, ["CA" * 20 + "GT", "CA" * 30 + "GT", "CA" * 40 + "GT"])
+    assert oracle_mod.scan_py_reported(text[:3000], prog, 1, "ids")   # real occurrences exist
+    for k, types in [(1, "ids"), (2, "ids"), (1, "s")]:
+        assert oracle_mod.scan_reported(text, prog, k, types, bufsize=0) == []

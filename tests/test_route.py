@@ -38,11 +38,13 @@ def test_refusals_left():
     assert engine.route(prog("ACG"), engine.NUC, 3, "ids") == "nfa"
     assert engine.route(prog("AC?G"), engine.NUC, 2, "ids") == "nfa"
     assert engine.route(prog("A(TC)?G"), engine.NUC, 2, "ids") == "nfa"
-    # the eregular restatement covers automata of at most 64 states
+    # the eregular restatement covers more than 64 states too (round 6)
     assert engine.route(prog("A(TC)?G" + "A" * 59), engine.NUC, 1, "ids") == "nfa"
     assert engine.route(prog("A(TC)?G" + "A" * 60), engine.NUC, 0, "") == "nfa"
-    with pytest.raises(_lib.UnsupportedOnGPU):
-        engine.route(prog("A(TC)?G" + "A" * 60), engine.NUC, 1, "ids")
+    assert engine.route(prog("A(TC)?G" + "A" * 60), engine.NUC, 1, "ids") == "nfa"
+    assert engine.route(prog("A(TC)?G" + "A" * 200), engine.NUC, 7, "ids") == "nfa"
+    with pytest.raises(_lib.UnsupportedOnGPU):   # 4 words: at most 7 errors
+        engine.route(prog("A(TC)?G" + "A" * 200), engine.NUC, 8, "ids")
 
 
 def test_nfa_words():

@@ -29,9 +29,8 @@ def svc(tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [
-    dict(pattern="A(TC){0,1}G" + "A" * 62, seqtype="dna", mismatch="1"),    # a group, 66 positions, k > 0
-    dict(pattern="A(TC){0,1}G" + "A" * 62, seqtype="dna", mismatch="2", deletion="d"),
     dict(pattern="A" * 300, seqtype="dna", mismatch="1"),             # 300 automaton positions
+    dict(pattern="A(TC){0,1}G" + "A" * 200, seqtype="dna", mismatch="8"),   # 4 words: at most 7 errors
     dict(pattern="A" * 40, seqtype="dna", mismatch="16", substitution="s"),   # 16 errors
 ])
 def test_refused_shapes_answer_with_an_error(svc, kw):
@@ -47,3 +46,6 @@ def test_supported_shapes_reach_the_database(svc):
         svc.run_patmatch(FakeRequest(pattern="ACG", seqtype="dna", mismatch="3"), "t3")
     with pytest.raises(AssertionError, match="must not be opened"):   # a range: the eextended walk
         svc.run_patmatch(FakeRequest(pattern="AN{0,1}G", seqtype="dna", mismatch="2"), "t4")
+    for i, kw in enumerate([dict(mismatch="1"), dict(mismatch="2", deletion="d")]):   # a group, 66 positions, k > 0
+        with pytest.raises(AssertionError, match="must not be opened"):   # (round 6: the multi-word eregular walk)
+            svc.run_patmatch(FakeRequest(pattern="A(TC){0,1}G" + "A" * 62, seqtype="dna", **kw), "t5%d" % i)

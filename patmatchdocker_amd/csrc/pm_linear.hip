@@ -192,6 +192,7 @@ struct OthersArgs {
     uint32_t nwg, tiles_per_wg;
     int items_per_wave;  // k_linear_others: 1, 2 or 4 (2 * maxlen - 1 <= 64 / items_per_wave)
     int n_classes;       // k_linear_others<true>: classes staged in LDS (<= 256)
+    uint64_t jall;       // skip_ok: bit j = some pattern's jsel entry is j (j >= 1)
 };
 
 // Phase 1, one thread per candidate word: the exception bits that can own a
@@ -221,19 +222,17 @@ __device__ inline uint32_t select_bits(const OthersArgs& a, uint64_t t, uint64_t
         // The build-time index (xint/xedge) drops the run interiors for
         // any jsel <= RUN_SKIP; this query's jsel also drops most of the
         // RUN_SKIP edge words at a run's end.
-        // (no early exits: the loads of all (pattern, jsel) words are issued
-        // together instead of as a dependent chain)
+        // Dead for every pattern of the chunk: the AND over the patterns p
+        // of (m0 & the "other" words at p's jsel positions) is m0 & the AND
+        // of those words over the DISTINCT positions of all patterns (`jall`,
+        // a few for any batch): one load per distinct position instead of
+        // one per (pattern, jsel) entry -- 256 patterns at configs[4] made
+        // this pass 2.0 ms beside the scan (round 6)
         const uint32_t m0 = prev & a.xoth[idx];
         if (m0) {
             uint32_t m = m0;
-            for (int p = 0; p < a.P; ++p) {   // dead for every pattern of the chunk
-                uint32_t mp = m0;
-                for (int t2 = 0; t2 <= a.k; ++t2) {
-                    const uint32_t j = a.jsel[p * 4 + t2];
-                    mp &= j ? a.nuc.bo[phys_word(tile, lw + j)].y : ~0u;
-                }
-                m &= mp;
-            }
+            for (uint64_t jm = a.jall; jm; jm &= jm - 1)
+                m &= a.nuc.bo[phys_word(tile, lw + (uint32_t)__builtin_ctzll(jm))].y;
             ot &= ~m;
         }
     }
@@ -1964,6 +1963,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                           reinterpret_cast<OtherSel*>(ws + 256), reinterpret_cast<uint32_t*>(ws),
                           sb.out, sb.cnt, sb.slot_base, sb.slot_cap, (uint32_t)nout, (uint32_t)(tiles_per_out), 1,
                           n_classes};
+            oa.jall = 0;
+            for (int p = ch.base; p < ch.base + ch.P; ++p)
+                for (int t = 0; t <= k; ++t)
+                    if (const int j = jsel[(size_t)p * 4 + t]) oa.jall |= 1ull << j;
             const int span = 2 * oa.maxlen - 1;
             oa.items_per_wave = span <= 16 ? 4 : span <= 32 ? 2 : 1;
             // phase 1: one thread per candidate word selects the

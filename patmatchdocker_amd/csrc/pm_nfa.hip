@@ -32,6 +32,9 @@ struct NfaArgs {
     NucView nuc;
     const uint8_t* bytes;       // BYTE alphabet (headers stored as '\n')
     const uint8_t* bytes_raw;   // BYTE alphabet, the file's own bytes (cross mode)
+    const uint32_t* p5;         // BYTE alphabet: the 5-bit residue planes (p5[q * nw5 + w], pm_db.hip)
+    uint64_t nw5;
+    const uint64_t* bmask5;     // [32][W]: positions accepting each residue code (0 header, 1 '\n': none)
     const uint64_t* prec;       // [nt][2^S][W] positions preceding a slice value
     const uint64_t* follow;     // [nt][2^S][W] positions following it
     const uint64_t* bmask;      // [256][W]
@@ -222,11 +225,28 @@ __device__ inline void load_tables(uint64_t* s_tab, uint64_t* s_b, const uint64_
 template <int W>
 constexpr int tab_words() { return W == 1 ? 8 * 256 : 16 * W * 16 * W; }
 
-template <int K, int W, bool NUC>
+// The text a start pass reads: the nucleotide planes, the byte copy, or
+// (a BYTE database with residue planes, line-bounded scans) the 5-bit
+// residue codes -- north_star's 5-bit-packed database: 0.625 B per residue
+// instead of 1 (round 6; PM_SCAN_BYTES keeps the byte copy, A/B)
+constexpr int SRC_NUC = 0, SRC_BYTE = 1, SRC_P5 = 2;
+
+// the residue code of position p (< n): bit q from plane q
+__device__ inline uint32_t p5_code(const NfaArgs& a, uint64_t p) {
+    const uint64_t w = p >> 5;
+    const uint32_t i = (uint32_t)p & 31u;
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) c |= ((a.p5[(uint64_t)q * a.nw5 + w] >> i) & 1u) << q;
+    return c;
+}
+
+template <int K, int W, int SRC>
 __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
+    constexpr bool NUC = SRC == SRC_NUC;
     __shared__ uint64_t s_prec[tab_words<W>()];
     __shared__ uint64_t s_b[256 * W];
-    load_tables<W>(s_prec, s_b, a.prec, a.bmask, a.nt);
+    load_tables<W>(s_prec, s_b, a.prec, SRC == SRC_P5 ? a.bmask5 : a.bmask, a.nt);
     const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool live = gid < a.nchunks;
     const uint64_t chunk_id = live ? gid : a.nchunks - 1;
@@ -253,6 +273,32 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
             bool kill;
             const uint8_t ch = char_at<NUC>(a, p, kill);
             step(p, ch, kill);
+        }
+    } else if constexpr (SRC == SRC_P5) {
+        // 32 positions per word of each plane: the word's five plane words
+        // are loaded when p enters it, the word below's are in flight; a
+        // code <= 1 (a header byte, '\n') or a position past the file kills
+        auto load = [&](uint64_t w, uint32_t (&v)[5]) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) v[q] = w < a.nw5 ? a.p5[(uint64_t)q * a.nw5 + w] : 0u;
+        };
+        uint64_t w = (top - 1) >> 5;
+        uint32_t cur[5], nxt[5];
+        load(w, cur);
+        load(w - 1, nxt);   // (w = 0: wraps past nw5, reads nothing)
+        for (uint64_t p = top; p-- > c0;) {
+            if ((p >> 5) != w) {
+                --w;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) cur[q] = nxt[q];
+                load(w - 1, nxt);
+            }
+            const uint32_t i = (uint32_t)p & 31u;
+            uint32_t c = 0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) c |= ((cur[q] >> i) & 1u) << q;
+            const bool kill = p >= a.n || c <= P5_NL;
+            step(p, (uint8_t)c, kill);
         }
     } else {
         // the lane's bytes arrive 16 at a time (aligned uint4 loads), the
@@ -294,13 +340,14 @@ __global__ __launch_bounds__(256) void k_nfa_rev(NfaArgs a) {
 // (at most the chunks per record; a record break kills every state, so
 // patterns that die quickly converge in 1-2 rounds).  Chunks whose input did
 // not change since the previous round copy their old output.
-template <int K, int W, bool NUC>
+template <int K, int W, int SRC>
 __global__ __launch_bounds__(256) void k_nfa_carry(NfaArgs a, const uint64_t* __restrict__ st_old,
                                                    uint64_t* __restrict__ st_new, const uint64_t* __restrict__ in_seen,
                                                    uint64_t* __restrict__ in_now, uint32_t* changed) {
+    constexpr bool NUC = SRC == SRC_NUC;
     __shared__ uint64_t s_prec[tab_words<W>()];
     __shared__ uint64_t s_b[256 * W];
-    load_tables<W>(s_prec, s_b, a.prec, a.bmask, a.nt);
+    load_tables<W>(s_prec, s_b, a.prec, SRC == SRC_P5 ? a.bmask5 : a.bmask, a.nt);
     const uint64_t gid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (gid >= a.nchunks) return;
     const uint64_t c0 = gid * a.chunk, c1 = c0 + a.chunk;
@@ -323,7 +370,13 @@ __global__ __launch_bounds__(256) void k_nfa_carry(NfaArgs a, const uint64_t* __
     }
     for (uint64_t p = c1; p-- > c0;) {
         bool kill;
-        const uint8_t ch = char_at<NUC>(a, p, kill);
+        uint8_t ch;
+        if constexpr (SRC == SRC_P5) {
+            ch = p < a.n ? (uint8_t)p5_code(a, p) : 0;
+            kill = ch <= P5_NL;
+        } else {
+            ch = char_at<NUC>(a, p, kill);
+        }
         nfa_rev_step<K, W>(R, bits_of<W>(s_b + ch * W), !kill, s_prec, a);
     }
     bool diff = false;
@@ -428,21 +481,21 @@ int kernel_rows(int k) { return k <= 3 ? k : k <= 7 ? 7 : 15; }
 int kernel_words(int m) { return m <= 64 ? 1 : m <= 128 ? 2 : 4; }
 bool nfa_supported(int k, int m) { return k <= PM_MAX_K && m <= PM_MAX_POSITIONS && !(kernel_words(m) == 4 && k > 7); }
 
-template <bool NUC>
+template <int SRC>
 void launch_nfa_rev(int K, int W, const NfaArgs& a, uint32_t blocks, hipStream_t s) {
 #define PM_X(KK, WW) \
-    if (K == KK && W == WW) { hipLaunchKernelGGL((k_nfa_rev<KK, WW, NUC>), dim3(blocks), dim3(256), 0, s, a); return; }
+    if (K == KK && W == WW) { hipLaunchKernelGGL((k_nfa_rev<KK, WW, SRC>), dim3(blocks), dim3(256), 0, s, a); return; }
     PM_NFA_KW(PM_X)
 #undef PM_X
     throw failure(PM_E_UNSUPPORTED, "no NFA kernel for these rows/words");
 }
 
-template <bool NUC>
+template <int SRC>
 void launch_nfa_carry(int K, int W, const NfaArgs& a, uint32_t blocks, hipStream_t s, const uint64_t* o, uint64_t* n,
                       const uint64_t* seen, uint64_t* now, uint32_t* changed) {
 #define PM_X(KK, WW)                                                                                          \
     if (K == KK && W == WW) {                                                                                 \
-        hipLaunchKernelGGL((k_nfa_carry<KK, WW, NUC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); \
+        hipLaunchKernelGGL((k_nfa_carry<KK, WW, SRC>), dim3(blocks), dim3(256), 0, s, a, o, n, seen, now, changed); \
         return;                                                                                               \
     }
     PM_NFA_KW(PM_X)
@@ -524,7 +577,7 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
               const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
               pm_hits** out, const RgTree* rgt = nullptr) {
     require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES |
-                       PM_ESIMPLE | PM_EXTENDED | PM_REGULAR)) == 0,
+                       PM_ESIMPLE | PM_EXTENDED | PM_REGULAR | PM_SCAN_BYTES)) == 0,
             "bad flags");
     require(!(flags & PM_REGULAR) || rgt != nullptr, "PM_REGULAR needs nrgrep's tree (pm_scan_nfa_tree)");
     require(db != nullptr, "db is NULL");
@@ -631,6 +684,14 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     const size_t o_f = up.add(tf.data(), tf.size() * 8);
     const size_t o_p = up.add(tp.data(), tp.size() * 8);
     const size_t o_b = up.add(bm.data(), bm.size() * 8);
+    // residue code -> positions (the byte copy's folded byte of the code; 0
+    // a header byte or padding, 1 '\n': none)
+    std::vector<uint64_t> bm5((size_t)32 * W, 0);
+    if (db->alphabet == PM_ALPHA_BYTE && db->n_codes > 0)
+        for (int b = 0; b < 256; ++b)
+            if (db->code_of[b] > P5_NL)
+                for (int q = 0; q < W; ++q) bm5[(size_t)db->code_of[b] * W + q] = bm[(size_t)b * W + q];
+    const size_t o_b5 = up.add(bm5.data(), bm5.size() * 8);
     EsBuild esb;
     EsUpload esu;
     if (esimple) {
@@ -742,6 +803,14 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     a.nchunks = std::max<uint64_t>(1, (db->n + chunk - 1) / chunk);
     a.st_stride = (k + 1) * W;
     const bool nuc = db->alphabet == PM_ALPHA_NUC;
+    // a peptide file's start pass reads the 5-bit residue planes (0.625 B per
+    // residue) when it has them and the scan is line-bounded
+    const bool p5 = !nuc && db->p5 && db->n_codes > 0 && !cross && !(flags & PM_SCAN_BYTES);
+    if (p5) {
+        a.p5 = db->p5;
+        a.nw5 = db->nw5;
+        a.bmask5 = reinterpret_cast<const uint64_t*>(d_up + o_b5);
+    }
 
     uint64_t expected = std::max<uint64_t>(db->n / 64, 1 << 16);
     SinkBuffers sb;
@@ -769,8 +838,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         HIPCHK(hipEventRecord(cev.a, s));
         for (uint64_t round = 0; round <= a.nchunks; ++round) {
             HIPCHK(hipMemsetAsync(changed, 0, sizeof(uint32_t), s));
-            if (nuc) launch_nfa_carry<true>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
-            else launch_nfa_carry<false>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+            if (nuc) launch_nfa_carry<SRC_NUC>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+            else if (p5) launch_nfa_carry<SRC_P5>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
+            else launch_nfa_carry<SRC_BYTE>(K, W, a, blocks, s, st[cur], st[cur ^ 1], in_seen, in_now, changed);
             HIPCHK(hipGetLastError());
             std::swap(in_seen, in_now);
             cur ^= 1;
@@ -800,8 +870,9 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
         }
         if (!launched) {
             HIPCHK(hipEventRecord(ev.a, s));
-            if (nuc) launch_nfa_rev<true>(K, W, a, blocks, s);
-            else launch_nfa_rev<false>(K, W, a, blocks, s);
+            if (nuc) launch_nfa_rev<SRC_NUC>(K, W, a, blocks, s);
+            else if (p5) launch_nfa_rev<SRC_P5>(K, W, a, blocks, s);
+            else launch_nfa_rev<SRC_BYTE>(K, W, a, blocks, s);
             HIPCHK(hipEventRecord(ev.b, s));
         }
         HIPCHK(hipGetLastError());

@@ -216,3 +216,41 @@ def test_many_patterns_one_batch(engine, oracle_mod):
                 assert _pairs(r) == oracle_mod.scan_reported(text, prog, k, "s", skip_headers=True), (prog.source, k)
     finally:
         db.close()
+
+
+NFA_PATTERNS = ["C-x(2,4)-C-x(3)-[LIVMFYWC]", "CX{1,3}CK", "C(AG){1,3}L", "KX{2,}C", "N-{P}-[ST]-{P}",
+                "[RK](2)-x-[ST]", "C-x(10,60)-C", "GXGXXG", "<M-x(0,5)-K", "KDEL>"]
+
+
+@pytest.mark.parametrize("k,types", [(0, ""), (1, "ids"), (2, "s"), (1, "d")])
+def test_automaton_start_pass_on_the_planes(engine, oracle_mod, k, types):
+    """The automaton kernels' start pass (k_nfa_rev; k_nfa_carry for
+    unbounded patterns) reads the residue planes of a peptide file (round 6):
+    every candidate (PM_REPORT_ALL, headers kept) equals the byte copy's
+    (PM_SCAN_BYTES), and the reported matches equal the oracle's, for ranges,
+    group repeats, an unbounded range, a 62-position range (two state words)
+    and anchors."""
+    rng = random.Random(90 + k)
+    text = proteome(rng, n_records=50)
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.BYTE, device=0)
+    try:
+        assert db.residue_codes()[0] > 0
+        total = 0
+        for p in NFA_PATTERNS:
+            prog = compile_pattern(convert("-p", p))
+            if prog.linear and k == 0:
+                continue   # the fixed-length kernels (tested above)
+            base = _lib.PM_REPORT_ALL | _lib.PM_KEEP_HEADERS
+            try:
+                planes = engine.scan_nfa(db, prog, k, types=types or "s", flags=base)
+                direct = engine.scan_nfa(db, prog, k, types=types or "s", flags=base | _lib.PM_SCAN_BYTES)
+            except _lib.UnsupportedOnGPU:
+                continue
+            got = list(zip(planes.beg.tolist(), planes.end.tolist()))
+            assert got == list(zip(direct.beg.tolist(), direct.end.tolist())), (p, k, types)
+            total += len(got)
+            res, _ = engine.scan(db, [prog], k=k, types=types)
+            assert _pairs(res[0]) == oracle_mod.scan_reported(text, prog, k, types, skip_headers=True), (p, k, types)
+        assert total > 100
+    finally:
+        db.close()

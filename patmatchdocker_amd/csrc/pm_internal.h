@@ -452,6 +452,8 @@ struct pm_pending {
     std::vector<int32_t> lengths;
     std::vector<uint8_t> pos_class, class_acgt, class_is_any;
     std::vector<uint32_t> class_bytes;
+    uint64_t* clk = nullptr;          // PM_JIT_CLOCK: the launch's per-workgroup clock samples
+    uint64_t clk_nwg = 0;
     ~pm_pending();
 };
 

@@ -997,6 +997,7 @@ struct JArgs {
     // to groupB workgroups (nA, nA + 1, ...) of tpwB tiles (the last fewer)
     u32 nA, tpwB, groupB, tpo;
     u64 tilesA;
+    u64* clk;               // PM_JIT_CLOCK builds: per workgroup {shader cycles, 100 MHz ticks, start tick}
 };
 #define STREAM 2048u
 #define TILE_POS 65536ull
@@ -1026,6 +1027,7 @@ struct JArgsHost {           // must match JArgs in kJitCommon
     uint32_t rcap, tiles_per_wg;
     uint32_t nA, tpwB, groupB, tpo;
     uint64_t tilesA;
+    uint64_t* clk = nullptr;
 };
 constexpr int JIT_REC_LDS = 96;       // hit records staged per wave in LDS (3 workgroups per CU)
 // workgroups resident per CU (4: two 16.5 KiB tile slots each fit the LDS)
@@ -1222,6 +1224,58 @@ bool jit_rotate() {
     return !(e && e[0] == '0');
 }
 
+// PM_JIT_CLOCK=1 (measurement only): every workgroup of pm_linear_jit reads
+// the shader clock counter (s_memtime) and the 100 MHz real-time counter
+// (s_memrealtime) at its start and end, and the library prints per launch
+// the effective shader clock of the launch (cycles / real time over the
+// workgroups) on stderr -- whether a slower dispatch ran at a lower clock
+// (tools/clock_trace.py)
+bool jit_clock() {
+    static const bool on = [] {
+        const char* e = getenv("PM_JIT_CLOCK");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// PM_JIT_CLOCK: a ring of per-launch sample buffers (a pipelined query is
+// resolved after the next one launched), and the report of one launch
+uint64_t* clock_buffer(int device, uint64_t nwg) {
+    static std::mutex mu;
+    static std::map<int, std::pair<std::vector<uint64_t*>, size_t>> rings;   // device -> (buffers, next)
+    std::lock_guard<std::mutex> lk(mu);
+    auto& r = rings[device];
+    constexpr size_t N = 16, CAP = 3 * 65536;   // workgroups per launch at most (nwg <= 256 CUs x 4 x 8 x ...)
+    require(nwg <= 65536, "PM_JIT_CLOCK: too many workgroups");
+    if (r.first.empty()) {
+        r.first.resize(N);
+        for (auto& p : r.first) HIPCHK(hipMalloc(&p, CAP * sizeof(uint64_t)));
+    }
+    uint64_t* p = r.first[r.second];
+    r.second = (r.second + 1) % N;
+    return p;
+}
+
+void clock_report(const uint64_t* d, uint64_t nwg, double kms) {
+    std::vector<uint64_t> h(3 * nwg);
+    HIPCHK(hipMemcpy(h.data(), d, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    double cyc = 0, ticks = 0, lo = 1e9, hi = 0;
+    uint64_t t_first = ~0ull, t_last = 0;
+    for (uint64_t i = 0; i < nwg; ++i) {
+        if (!h[3 * i + 1]) continue;
+        cyc += (double)h[3 * i];
+        ticks += (double)h[3 * i + 1];
+        const double g = (double)h[3 * i] / (double)h[3 * i + 1] * 0.1;   // 100 MHz ticks -> GHz
+        lo = std::min(lo, g);
+        hi = std::max(hi, g);
+        t_first = std::min(t_first, h[3 * i + 2]);
+        t_last = std::max(t_last, h[3 * i + 2] + h[3 * i + 1]);
+    }
+    fprintf(stderr, "PM_JIT_CLOCK nwg=%llu kernel_ms=%.4f clock_ghz=%.4f min=%.3f max=%.3f span_ms=%.4f t0_tick=%llu\n",
+            (unsigned long long)nwg, kms, ticks > 0 ? cyc / ticks * 0.1 : 0.0, lo, hi,
+            (double)(t_last - t_first) * 1e-5, (unsigned long long)t_first);
+}
+
 std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_t* pos_class,
                               const uint8_t* class_acgt, const uint8_t* class_is_any, int waves, int parts) {
     const int PARTS = parts;                     // waves per workgroup
@@ -1236,7 +1290,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     std::ostringstream o;
     o << kJitCommon;
     o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define STEPS "
-      << JIT_STEPS << "\n#define NW " << PARTS << "\n";
+      << JIT_STEPS << "\n#define NW " << PARTS << "\n#define JIT_CLOCK " << (jit_clock() ? 1 : 0) << "\n";
     auto word_off = [&](int i) {   // physical word of logical word 32 lane + i, relative to the tile
         std::ostringstream s;
         if (i < LANE_WORDS) s << (i * 64) << " + lane";
@@ -1418,6 +1472,9 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  __shared__ uint2 rst[NW][REC_LDS];\n"
          "  const int lane = threadIdx.x & 63;\n"
          "  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+         "#if JIT_CLOCK\n"
+         "  const u64 clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();\n"
+         "#endif\n"
          "  // halo word offsets (logical words 32 lane + 32 g + r, r < 32)\n"
          "  const u32 hb1 = lane + 1 < 64 ? lane + 1 : 32u * lane + 32u, hs1 = lane + 1 < 64 ? 64u : 1u;\n"
          "  const u32 hb2 = lane + 2 < 64 ? lane + 2 : 32u * lane + 64u, hs2 = lane + 2 < 64 ? 64u : 1u;\n"
@@ -1486,6 +1543,14 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    slot = slot == RING - 1 ? 0 : slot + 1;\n  }\n"
          "  if (scnt) flush_records(st, scnt, grec, gcnt, a.rcap, lane);\n"
          "  if (lane == 0) a.rec_cnt[(u64)blockIdx.x * NW + wid] = gcnt + scnt;\n"
+         "#if JIT_CLOCK\n"
+         "  if (threadIdx.x == 0 && a.clk) {\n"
+         "    const u64 c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();\n"
+         "    a.clk[3 * (u64)blockIdx.x] = c1 - clk_c0;\n"
+         "    a.clk[3 * (u64)blockIdx.x + 1] = r1 - clk_r0;\n"
+         "    a.clk[3 * (u64)blockIdx.x + 2] = clk_r0;\n"
+         "  }\n"
+         "#endif\n"
          "}\n";
     return o.str();
 }
@@ -1552,6 +1617,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
     const auto key = std::make_pair(device, std::to_string(parts) + (jit_rotate() ? "r/" : "f/") +
+                                                (jit_clock() ? "c/" : "") +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);
@@ -2266,6 +2332,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     nospec = g_nospec.count({db, cap_key}) != 0;
                 }
                 const bool spec_async = async && sb.nbins <= 4096 && attempt == 0 && !nospec;
+                uint64_t* clk = nullptr;   // PM_JIT_CLOCK samples of the launch
                 // expansion, exception pass and sort run on the scan's stream
                 // (overlapping them with the next scan on a second stream
                 // measured no faster: the chip is at its power limit)
@@ -2273,6 +2340,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 for (const Chunk& ch : chunks) {
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw,
                                  (uint32_t)nA, (uint32_t)tpwB, (uint32_t)groupB, (uint32_t)tpo, tilesA};
+                    if (jit_clock() && chunks.size() == 1) {
+                        ja.clk = clock_buffer(db->device, nwg);
+                        clk = ja.clk;
+                    }
                     void* params[] = {&ja};
                     jev.emplace_back(new EventPair());
                     // the events take the dispatch's own start/end timestamps
@@ -2323,6 +2394,8 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                         HIPCHK(hipEventRecord(pd->counted, xs));
                     }
                     pd->jev = std::move(jev);
+                    pd->clk = clk;
+                    pd->clk_nwg = nwg;
                     pd->hint_key = cap_key;
                     pd->slot_caps = slot_caps;
                     pd->rcap = rcap;
@@ -2346,6 +2419,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     spec = sink_sort_speculative(db, sb, reinterpret_cast<const int32_t*>(d_up + o_len), nullptr, s);
                 bool overflow = false;
                 total = sink_total(db, sb, counts, overflow);   // synchronizes the stream
+                if (clk) clock_report(clk, nwg, jev.empty() ? 0.0 : jev[0]->ms());
                 const uint32_t rec_need = sb.aux;
                 if (!overflow && rec_need == 0) {
                     done = true;
@@ -2462,6 +2536,7 @@ void hits_finalize(pm_hits* h) {
         double kms = 0.0;
         for (auto& e : pd->jev) kms += e->ms();
         h->kernel_ms = kms;
+        if (pd->clk) clock_report(pd->clk, pd->clk_nwg, kms);
         std::lock_guard<std::mutex> lk(g_cap_mu);
         if (g_cap_hint.size() > 256) g_cap_hint.clear();
         g_cap_hint[{db, pd->hint_key}] = {pd->slot_caps, pd->rcap};

@@ -49,7 +49,7 @@ def main():
         sc = sum((b - mc) ** 2 for b in c) ** 0.5
         summary["timed_corr_kernel_ms_vs_clock"] = round(cov / (sk * sc), 3) if sk and sc else None
         # cycles per launch: duration x clock (constant if the clock explains the duration)
-        summary["timed_gcycles_mean"] = round(statistics.mean(a * b * 1e-3 for a, b in zip(k, c)), 4)
+        summary["timed_mcycles_mean"] = round(statistics.mean(a * b for a, b in zip(k, c)), 4)
     json.dump({"launches": rows, "summary": summary}, sys.stdout, indent=1)
     print()
 

@@ -1238,6 +1238,20 @@ bool jit_clock() {
     return on;
 }
 
+// PM_JIT_PREFETCH=<bytes> (A/B): besides the LDS DMA of the next tile, each
+// workgroup touches the tile after it -- one 4-byte read per `bytes` of it
+// (64 or 128), landing in a 256-byte dummy LDS row -- so two tiles per
+// workgroup are in flight from HBM instead of one, with no extra LDS ring
+// slot; the DMA of that tile an iteration later then hits L2 / MALL.  0: off
+int jit_prefetch() {
+    static const int v = [] {
+        const char* e = getenv("PM_JIT_PREFETCH");
+        const int b = e ? atoi(e) : 0;
+        return b == 64 || b == 128 || b == 256 ? b : 0;
+    }();
+    return v;
+}
+
 // PM_JIT_CLOCK: a ring of per-launch sample buffers (a pipelined query is
 // resolved after the next one launched), and the report of one launch
 uint64_t* clock_buffer(int device, uint64_t nwg) {
@@ -1424,7 +1438,7 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     const int LOAD_PIECES = (LOAD_BYTES + 1023) / 1024;
     (void)DMA_PIECES;
     o << "#define RING " << RING << "\n#define LDS_TILE " << LDS_TILE << "\n#define DMA_PIECES " << LOAD_PIECES
-      << "\n#define LOAD_BYTES " << LOAD_BYTES << "\n";
+      << "\n#define LOAD_BYTES " << LOAD_BYTES << "\n#define PF_STRIDE " << jit_prefetch() << "\n";
     o << R"JIT(// Raw barrier: __syncthreads()'s release fence would wait vmcnt(0) and
 // drain the tile prefetch in flight.  LDS writes are complete at
 // lgkmcnt(0); the empty asm statements keep the compiler from moving memory
@@ -1456,6 +1470,26 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
                  : "=&s"(keep) : "v"(voff), "s"(pb), "s"(dst) : "memory");
   }
 }
+#if PF_STRIDE
+// PM_JIT_PREFETCH: one dword per PF_STRIDE bytes of tile t into the dummy
+// row at LDS byte address `dst` (no VGPR destination; waited for with the
+// DMAs by the loop's vmcnt(0))
+__device__ __forceinline__ void prefetch(const JArgs& a, u32 dst, u64 tile, u64 tend, u32 wid, int lane) {
+  if (tile >= tend) return;
+  const unsigned char* tb = reinterpret_cast<const unsigned char*>(a.hl + tile * TILE_WORDS);
+  constexpr int LINES = (LOAD_BYTES + PF_STRIDE - 1) / PF_STRIDE;
+  const u32 d = __builtin_amdgcn_readfirstlane(dst);
+#pragma unroll
+  for (int q = 0; q * 64 < LINES; q += NW) {
+    if ((q + (int)wid) * 64 >= LINES) break;
+    if ((q + (int)wid) * 64 + lane >= LINES) continue;
+    const u32 voff = (u32)(((q + (int)wid) * 64 + lane) * PF_STRIDE);
+    u32 keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(tb), "s"(d) : "memory");
+  }
+}
+#endif
 // Moves the wave's staged records to its global segment.  Rare; ends with
 // vmcnt(0), so the DMA wait arithmetic of the main loop stays exact whatever
 // order stores and loads retire in.
@@ -1497,6 +1531,11 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "  if (a.aux_zero && blockIdx.x == 0 && threadIdx.x == 0) *a.aux_zero = 0u;   // read by k_linear_expand (after)\n"
          "  stage(a, lds_base, t0, tend, wid, lane);\n"
          "  stage(a, lds_base + LDS_TILE, t0 + 1, tend, wid, lane);\n"
+         "#if PF_STRIDE\n"
+         "  __shared__ u32 pfd[64];\n"
+         "  const u32 pf_base = (u32)reinterpret_cast<u64>(pfd);\n"
+         "  prefetch(a, pf_base, t0 + RING, tend, wid, lane);\n"
+         "#endif\n"
          "  u32 slot = 0;\n"
          "  for (u64 tile = t0; tile < tend; ++tile) {\n"
          "    // wait for this tile's pieces (own DMAs), then the barrier makes\n"
@@ -1504,6 +1543,9 @@ __device__ __noinline__ void flush_records(const lds_uint2* st, u32 n, glb_uint2
          "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
          "    BARRIER();\n"
          "    stage(a, lds_base + (slot == 0 ? RING - 1 : slot - 1) * LDS_TILE, tile + RING - 1, tend, wid, lane);\n"
+         "#if PF_STRIDE\n"
+         "    prefetch(a, pf_base, tile + RING, tend, wid, lane);\n"
+         "#endif\n"
          "    const uint2* sw = reinterpret_cast<const uint2*>(lds + slot * LDS_TILE);\n"
          "    u32 dd[STEPS + XS][P];   // dead windows per slot and pattern (every path writes all of them)\n";
     // The parts rotate over the waves from tile to tile: part 0 (the words
@@ -1617,7 +1659,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
     const auto key = std::make_pair(device, std::to_string(parts) + (jit_rotate() ? "r/" : "f/") +
-                                                (jit_clock() ? "c/" : "") +
+                                                (jit_clock() ? "c/" : "") + "pf" + std::to_string(jit_prefetch()) + "/" +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);

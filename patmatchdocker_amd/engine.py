@@ -266,15 +266,12 @@ def route(prog: Program, alphabet: str, k: int, types: str) -> str:
         raise UnsupportedOnGPU("patterns longer than %d positions are not supported" % _lib.PM_MAX_POSITIONS)
     if k > _lib.PM_MAX_K or (nfa_words(prog.m) == 4 and k > 7):
         raise UnsupportedOnGPU("k=%d errors is not supported by the GPU kernels for %d positions" % (k, prog.m))
-    if indel and "d" in types and prog.min_len <= k and prog.kind not in ("simple", "extended", "regular"):
-        # a class sequence runs nrgrep's esimple report, whose walk takes
-        # every position of every line then (pm_esimple.hip,
-        # es_all_positions); an extended pattern nrgrep's eextended report,
-        # whose walk takes every line (pm_eextended.hip, ee_add_lines); a
-        # regular one nrgrep's eregular report, every line a cluster
-        # (pm_regular.hip)
-        raise UnsupportedOnGPU("deletions with k=%d >= the shortest match (%d) are not supported by the GPU scan"
-                               % (k, prog.min_len))
+    # deletions with k >= the shortest match route too: a class sequence runs
+    # nrgrep's esimple report, whose walk then takes every position of every
+    # line (pm_esimple.hip, es_all_positions); an extended pattern its
+    # eextended report, every line a cluster (pm_eextended.hip,
+    # ee_add_lines); a regular one its eregular report, likewise
+    # (pm_regular.hip) -- every engine kind, so no shape is refused here
     return "nfa"   # automaton kernels: anything else, long oligos and k > 3 included
 
 

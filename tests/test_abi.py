@@ -104,9 +104,9 @@ def test_specialized_kernel_shares_strand_blocks(tmp_path, monkeypatch):
 
 
 def test_route_indels():
-    """-k with insertions/deletions routes to the Glushkov kernels; deletions
-    with k >= the shortest match of a non-simple pattern are refused loudly
-    (no CPU fallback)."""
+    """-k with insertions/deletions routes to the Glushkov kernels, deletions
+    with k >= the shortest match included; only sizes past the automaton
+    kernels' limits are refused, loudly (no CPU fallback)."""
     from patmatchdocker_amd import engine
     from patmatchdocker_amd._lib import UnsupportedOnGPU
     from patmatchdocker_amd.regex import compile_pattern

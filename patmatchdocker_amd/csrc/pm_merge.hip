@@ -23,7 +23,7 @@ constexpr uint32_t MERGE_T = 1024;
 struct Parts {
     uint64_t beg[MERGE_MAX_PARTS];   // part r = keys[beg[r], beg[r] + len[r])
     uint64_t len[MERGE_MAX_PARTS];
-    uint64_t out0[MERGE_MAX_PARTS + 1];   // prefix of len: part r's first compacted index
+    uint32_t blk0[MERGE_MAX_PARTS + 1];   // prefix of the move's blocks per part
     int n;
 };
 
@@ -72,22 +72,53 @@ __global__ __launch_bounds__(MERGE_T) void k_merge_bases(const uint64_t* __restr
     }
 }
 
-// one thread per key: part by the compacted prefix, destination = base of
-// its (part, pattern) slice + its absolute index
-__global__ void k_merge_move(const uint64_t* __restrict__ keys, const int32_t* __restrict__ lens, Parts parts,
-                             uint32_t P, const int64_t* __restrict__ base, const int32_t* __restrict__ len_of,
-                             uint64_t total, uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_lens) {
-    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (j >= total) return;
+// The move: a block takes MOVE_KEYS consecutive keys of ONE part (its part
+// from the blocks' prefix, blk0, wave-uniform), stages that part's base row
+// and the pattern lengths in LDS when the batch has <= MOVE_STAGE_P
+// patterns, and each thread moves MOVE_PER keys at stride MOVE_T: the loads
+// and (within a pattern's slice) the stores coalesce, and each thread has
+// MOVE_PER independent loads in flight.  (Round 6's first form, one thread
+// per key with a per-key search over the parts' prefix: 1.71 ms for 8 x
+// 30.7 M keys, ~2.9 TB/s of its 4.9 GB.)
+constexpr uint32_t MOVE_T = 256, MOVE_PER = 8, MOVE_KEYS = MOVE_T * MOVE_PER;
+constexpr uint32_t MOVE_STAGE_P = 512;    // (a block re-reads the staged row: 4 KB at most)
+
+template <bool STAGE>
+__global__ __launch_bounds__(MOVE_T) void k_merge_move(const uint64_t* __restrict__ keys, const int32_t* __restrict__ lens,
+                                                       Parts parts, uint32_t P, const int64_t* __restrict__ base,
+                                                       const int32_t* __restrict__ len_of, uint64_t* __restrict__ out_keys,
+                                                       int32_t* __restrict__ out_lens) {
+    __shared__ int64_t s_base[STAGE ? MOVE_STAGE_P : 1];
+    __shared__ int32_t s_len[STAGE ? MOVE_STAGE_P : 1];
     int r = 0;
-    while (r + 1 < parts.n && j >= parts.out0[r + 1]) ++r;
-    const uint64_t i = parts.beg[r] + (j - parts.out0[r]);
-    const uint64_t key = keys[i];
-    const uint32_t p = (uint32_t)(key >> 48);
-    if (p >= P) return;   // the caller's pattern count is too small: checked on the host
-    const uint64_t dst = (uint64_t)(base[r * P + p] + (int64_t)i);
-    out_keys[dst] = key;
-    if (out_lens) out_lens[dst] = lens ? lens[i] : len_of[p];
+    while (r + 1 < parts.n && blockIdx.x >= parts.blk0[r + 1]) ++r;   // block-uniform
+    const uint64_t c0 = (uint64_t)(blockIdx.x - parts.blk0[r]) * MOVE_KEYS;
+    const uint64_t n = parts.len[r] > c0 ? umin64(parts.len[r] - c0, MOVE_KEYS) : 0;
+    const int64_t* brow = base + (uint64_t)r * P;
+    if constexpr (STAGE) {
+        for (uint32_t p = threadIdx.x; p < P; p += MOVE_T) {
+            s_base[p] = brow[p];
+            if (out_lens && !lens) s_len[p] = len_of[p];
+        }
+        __syncthreads();
+    }
+    const uint64_t i0 = parts.beg[r] + c0;
+    uint64_t k[MOVE_PER];
+#pragma unroll
+    for (uint32_t u = 0; u < MOVE_PER; ++u) {
+        const uint64_t q = threadIdx.x + (uint64_t)u * MOVE_T;
+        k[u] = q < n ? keys[i0 + q] : ~0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < MOVE_PER; ++u) {
+        const uint64_t q = threadIdx.x + (uint64_t)u * MOVE_T;
+        const uint32_t p = (uint32_t)(k[u] >> 48);
+        if (q >= n || p >= P) continue;   // (p >= P: the caller's pattern count is too small, checked on the host)
+        const uint64_t i = i0 + q;
+        const uint64_t dst = (uint64_t)((STAGE ? s_base[p] : brow[p]) + (int64_t)i);
+        out_keys[dst] = k[u];
+        if (out_lens) out_lens[dst] = lens ? lens[i] : (STAGE ? s_len[p] : len_of[p]);
+    }
 }
 
 }  // namespace
@@ -118,14 +149,16 @@ int pm_merge_parts(const uint64_t* keys, const int32_t* lens, const uint64_t* pa
         require(!out_lens || lens || len_of_pattern, "out_lens needs lens or len_of_pattern");
         Parts parts{};
         parts.n = nparts;
-        uint64_t total = 0;
+        uint64_t total = 0, blocks = 0;
         for (int r = 0; r < nparts; ++r) {
             parts.beg[r] = part_beg[r];
             parts.len[r] = part_len[r];
-            parts.out0[r] = total;
+            parts.blk0[r] = (uint32_t)blocks;
             total += part_len[r];
+            blocks += (part_len[r] + MOVE_KEYS - 1) / MOVE_KEYS;
         }
-        parts.out0[nparts] = total;
+        parts.blk0[nparts] = (uint32_t)blocks;
+        require(blocks < (1ull << 31), "pm_merge_parts: too many keys");
         if (total == 0) return;
         require(keys != nullptr, "keys is NULL");
         DeviceGuard g(device);
@@ -138,8 +171,8 @@ int pm_merge_parts(const uint64_t* keys, const int32_t* lens, const uint64_t* pa
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_merge_bases, dim3(1), dim3(MERGE_T), 0, s, start, parts, P, base);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_merge_move, dim3(blocks_for(total, 256)), dim3(256), 0, s, keys, lens, parts, P, base,
-                           len_of_pattern, total, out_keys, out_lens);
+        hipLaunchKernelGGL(P <= MOVE_STAGE_P ? k_merge_move<true> : k_merge_move<false>, dim3((uint32_t)blocks),
+                           dim3(MOVE_T), 0, s, keys, lens, parts, P, base, len_of_pattern, out_keys, out_lens);
         HIPCHK(hipGetLastError());
         if (!stream) HIPCHK(hipStreamSynchronize(s));
     });

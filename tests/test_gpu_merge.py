@@ -45,6 +45,7 @@ def _buffer(parts, pad, dev, dtype=torch.int64, fill=-1):
     ([0, 3000, 0, 4000, 1], 7, (3,)),
     ([20000] * 8, 256, (0, 255, 17)),
     ([1], 1, ()),
+    ([3000, 0, 9000, 2047, 2049], 1000, (5,)),   # more patterns than the move stages in LDS
 ])
 def test_merge_equals_a_sort_with_fixed_lengths(dev, sizes, npat, absent):
     from patmatchdocker_amd import shards

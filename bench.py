@@ -53,7 +53,7 @@ sys.path.insert(0, ROOT)
 
 MOTIF = "TGCTGASTCAGCANW"          # 15 nt, degenerate (S, N, W)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8.0 TB/s spec
-ROUND = "r05"   # committed PMC traffic run (profiles/r05_traffic.json)
+ROUND = "r06"   # committed PMC traffic run (profiles/r06_traffic.json)
 # flags that change the headline workload: with none of them the run also
 # measures the extra workloads (configs4, north_star_100gbp)
 WORKLOAD_FLAGS = ("--config", "--gbp", "--rec-len", "--motif", "--k", "--types", "--serial", "--batch")

@@ -315,14 +315,14 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
         for (int u = 0; u < VU; ++u) {
             const bool ok = base + u * blockDim.x + threadIdx.x < total;
             const uint32_t code = alignb(e[u].w, e[u].z, 2u * a.omax) & ((1u << (2 * BQ)) - 1u);
+            co[u] = 0u;
             if constexpr (HASH) {
-                co[u] = 0u;
                 if (ok)   // a candidate's code is present: the probe ends there (an empty slot: none)
                     for (uint32_t h = bq_hash(code);; h = (h + 1) & (BQ_HASH_SLOTS - 1)) {
                         const uint64_t sl = s_hash[h];
                         if (sl == ~0ull) break;
                         if ((uint32_t)(sl & 0xFFFFFu) == code) {
-                            co[u] = (uint32_t)((sl >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl >> 44);
+                            co[u] = bq_slot_entry(sl);
                             break;
                         }
                     }
@@ -334,13 +334,20 @@ __global__ __launch_bounds__(1024) void k_batch_verify(BatchVerifyArgs a) {
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             const uint32_t lo = co[u] >> 8;
-            h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
-            mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+            if (co[u] & BQ_CO_ONE) {   // a one-entry code: the entry from the slot, the masks by pattern
+                const uint32_t w0 = co[u] & ~BQ_CO_ONE;
+                h[u] = make_uint4(w0, bq_len_mask(w0 >> 24), 0u, 0u);
+                mk[u] = a.pmask[w0 & 0xFFFFu];
+            } else {
+                h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
+                mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+            }
         }
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             if (!co[u]) continue;
             verify_entry(a, tend, vs, e[u], lf[u], h[u], mk[u]);
+            if (co[u] & BQ_CO_ONE) continue;   // its one entry came from the slot
             const uint32_t lo = co[u] >> 8, hi = lo + (co[u] & 255u);
             for (uint32_t t = lo + 1; t < hi; ++t) verify_entry(a, tend, vs, e[u], lf[u], a.ents[2 * t], a.ents[2 * t + 1]);
         }
@@ -367,9 +374,15 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
     __shared__ uint64_t s_hash[HASH ? BQ_HASH_SLOTS : 1];
     __shared__ uint32_t s_n[BATCH_MAX_WPO + 1];   // prefix of the waves' candidate counts
     __shared__ uint32_t s_hist[HIST ? BATCH_VERIFY_WAVES : 1][HIST ? ORD_HIST_MAX_P : 1];
+    // HIST (<= ORD_HIST_MAX_P patterns): the patterns' class masks in LDS too,
+    // so a one-entry code (the slot holds its entry) is verified with no
+    // global load after the candidate's (round 6)
+    __shared__ uint4 s_pmask[HASH && HIST ? ORD_HIST_MAX_P : 1];
     const uint32_t og = blockIdx.x;
     if constexpr (HIST)
         for (uint32_t i = threadIdx.x; i < BATCH_VERIFY_WAVES * ORD_HIST_MAX_P; i += blockDim.x) (&s_hist[0][0])[i] = 0u;
+    if constexpr (HASH && HIST)
+        for (uint32_t p = threadIdx.x; p < (uint32_t)a.P; p += blockDim.x) s_pmask[p] = a.pmask[p];
     if constexpr (HASH)
         for (uint32_t i = threadIdx.x; i < BQ_HASH_SLOTS; i += blockDim.x) s_hash[i] = a.hash[i];
     // (the bins of the exception pass, xkeys and first starts are zeroed by
@@ -456,14 +469,27 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
                     hh[u] = (hh[u] + 1) & (BQ_HASH_SLOTS - 1);
                     sl[u] = s_hash[hh[u]];
                 }
-                if (sl[u] != ~0ull) co[u] = (uint32_t)((sl[u] >> 20) & 0xFFFFFFu) << 8 | (uint32_t)(sl[u] >> 44);
+                if (sl[u] != ~0ull) co[u] = bq_slot_entry(sl[u]);
             }
         }
+        // HASH && HIST: a one-entry code's entry is its slot's and its masks
+        // are in LDS, so nothing is loaded ahead (and no h / mk registers are
+        // held across the round); a code with more entries (rare) loads them
+        // where it is verified.  Otherwise the entries load here, together.
+        constexpr bool LATE = HASH && HIST;
+        if constexpr (!LATE) {
 #pragma unroll
-        for (int u = 0; u < VU; ++u) {
-            const uint32_t lo = co[u] >> 8;
-            h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
-            mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+            for (int u = 0; u < VU; ++u) {
+                const uint32_t lo = co[u] >> 8;
+                if (co[u] & BQ_CO_ONE) {   // a one-entry code: the entry from the slot, the masks by pattern
+                    const uint32_t w0 = co[u] & ~BQ_CO_ONE;
+                    h[u] = make_uint4(w0, bq_len_mask(w0 >> 24), 0u, 0u);
+                    mk[u] = a.pmask[w0 & 0xFFFFu];
+                } else {
+                    h[u] = co[u] ? a.ents[2 * lo] : make_uint4(0u, 0u, 0u, 0u);
+                    mk[u] = co[u] ? a.ents[2 * lo + 1] : make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
@@ -481,8 +507,17 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
                 }
             };
             if (co[u]) {
-                take(h[u], mk[u]);
-                const uint32_t lo = co[u] >> 8, hi = lo + (co[u] & 255u);
+                const uint32_t lo = co[u] >> 8, hi = (co[u] & BQ_CO_ONE) ? 0u : lo + (co[u] & 255u);
+                if constexpr (LATE) {
+                    if (co[u] & BQ_CO_ONE) {
+                        const uint32_t w0 = co[u] & ~BQ_CO_ONE;
+                        take(make_uint4(w0, bq_len_mask(w0 >> 24), 0u, 0u), s_pmask[w0 & 0xFFFFu]);
+                    } else {
+                        take(a.ents[2 * lo], a.ents[2 * lo + 1]);
+                    }
+                } else {
+                    take(h[u], mk[u]);
+                }
                 for (uint32_t t = lo + 1; t < hi; ++t) take(a.ents[2 * t], a.ents[2 * t + 1]);
             }
             if (bad) atomicOr(a.ord_bad, 1u);
@@ -625,7 +660,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
             bi.table[c >> 5] |= 1u << (c & 31);
             bi.code_off[c] = (uint32_t)i << 8;
         }
-        if ((bi.code_off[c] & 255u) == 255u || i >= (1u << 24)) return false;
+        if ((bi.code_off[c] & 255u) == 255u || i >= (1u << 23)) return false;
         ++bi.code_off[c];
         uint32_t* e = &bi.ents[i * BATCH_ENT_WORDS];
         e[0] = p | op << 16 | (uint32_t)lengths[p] << 24;
@@ -643,7 +678,14 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
             for (const auto& cf : codes) {
                 uint32_t h = bq_hash(cf.first);
                 while (bi.hash[h] != ~0ull) h = (h + 1) & (BQ_HASH_SLOTS - 1);
-                bi.hash[h] = (uint64_t)cf.first | (uint64_t)cf.second << 20 | (uint64_t)(bi.code_off[cf.first] & 255u) << 44;
+                // a code with one entry carries the entry's first word in
+                // the slot (the verify then needs no entry load: pattern,
+                // offset and length from the slot, the class masks per
+                // pattern), else its first entry's index
+                const uint64_t cnt = bi.code_off[cf.first] & 255u;
+                const uint64_t mid = cnt == 1 ? (uint64_t)bi.ents[(size_t)cf.second * BATCH_ENT_WORDS]
+                                              : (uint64_t)cf.second;
+                bi.hash[h] = (uint64_t)cf.first | mid << 20 | cnt << 52;
             }
         }
     }

@@ -582,8 +582,10 @@ struct BatchIndex {
     std::vector<uint32_t> pmask;      // [P][4]: bit 2j + 1 = position j accepts A / C / G / T
     std::vector<uint32_t> popt;       // [P]: o_p, the indexed piece's offset
     // [BQ_HASH_SLOTS] open-addressing table of the codes present, for the
-    // verify's LDS (empty when there are too many codes): code | first entry
-    // << 20 | entries << 44, ~0 = empty slot
+    // verify's LDS (empty when there are too many codes): code | x << 20 |
+    // entries << 52, ~0 = empty slot; x = the entry's first word (p | o_p <<
+    // 16 | len << 24) for a code with one entry, else its first entry's index
+    // (bq_slot_entry)
     std::vector<uint64_t> hash;
     // device image (ws_batch): table | code_off | ents | pmask | popt | hash
     size_t o_table = 0, o_code = 0, o_ents = 0, o_pmask = 0, o_popt = 0, o_hash = 0, bytes = 0;
@@ -595,6 +597,20 @@ __host__ __device__ inline uint32_t bq_hash(uint32_t code) { return (code * 0x9E
 // one verification entry (two uint4): {p | o_p << 16 | len << 24, length mask
 // (bits 2j + 1), 0, 0}, {mA, mC, mG, mT}
 constexpr int BATCH_ENT_WORDS = 8;
+// a hash slot -> co: first entry << 8 | entries (entries >= 2; 0: absent),
+// or, for a one-entry code, that entry's first word | BQ_CO_ONE (the slot
+// holds it: p | o_p << 16 | len << 24, len < 32 leaves bit 31 free; entry
+// indices stay below 2^23, build_batch_index)
+constexpr uint32_t BQ_CO_ONE = 1u << 31;
+__host__ __device__ inline uint32_t bq_slot_entry(uint64_t sl) {
+    const uint32_t cnt = (uint32_t)(sl >> 52) & 255u;
+    if (cnt == 1) return (uint32_t)(sl >> 20) | BQ_CO_ONE;
+    return (uint32_t)((sl >> 20) & 0xFFFFFFu) << 8 | cnt;
+}
+// the length mask of a pattern of `len` positions (bits 2j + 1, j < len)
+__host__ __device__ inline uint32_t bq_len_mask(uint32_t len) {
+    return 0xAAAAAAAAu & (len >= 16 ? ~0u : (1u << (2 * len)) - 1u);
+}
 // false: the batch is not for the filter (lengths outside [BQ, BATCH_MAX_LEN],
 // too many patterns or expansions, a code shared by more than 255 patterns)
 bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, const uint8_t* class_acgt,

@@ -568,7 +568,7 @@ void free_db(pm_db* db) {
         quiet(hipStreamSynchronize(db->exc));
         quiet(hipStreamDestroy(db->exc));
     }
-    for (hipEvent_t e : {db->exc_fork, db->exc_join})
+    for (hipEvent_t e : {db->exc_fork, db->exc_join, db->scan_ev, db->join_ev})
         if (e) quiet(hipEventDestroy(e));
     void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
                     db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->hdr_end, db->bytes, db->bytes_raw, db->ws_post.p,
@@ -616,9 +616,33 @@ void lane_end(pm_db* db, hipStream_t s) {
 
 void switch_lane(pm_db* db) { std::swap(static_cast<pm_lane&>(*db), db->alt); }
 
+int post_mode() {
+    static const int v = [] {
+        const char* e = getenv("PM_POST_STREAM");
+        return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+    }();
+    return v;
+}
+
 hipStream_t post_stream(pm_db* db) {
-    if (!db->post) HIPCHK(hipStreamCreateWithFlags(&db->post, hipStreamNonBlocking));
+    if (!db->post) {
+        if (post_mode() == 2) {
+            int least = 0, greatest = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIPCHK(hipStreamCreateWithPriority(&db->post, hipStreamNonBlocking, greatest));
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&db->post, hipStreamNonBlocking));
+        }
+        HIPCHK(hipEventCreateWithFlags(&db->scan_ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&db->join_ev, hipEventDisableTiming));
+    }
     return db->post;
+}
+
+void post_join(pm_db* db) {
+    if (!db->post) return;
+    HIPCHK(hipEventRecord(db->join_ev, db->post));
+    HIPCHK(hipStreamWaitEvent(db->stream, db->join_ev, 0));
 }
 
 hipStream_t exc_stream(pm_db* db) {
@@ -758,6 +782,7 @@ void set_regions(pm_db* db, const std::vector<uint64_t>& t, const std::vector<ui
         throw;
     }
     HIPCHK(hipStreamSynchronize(db->stream));   // queued scans may still read the old table
+    if (db->post) HIPCHK(hipStreamSynchronize(db->post));   // (and their post-processing)
     for (void* p : {(void*)db->reg_t, (void*)db->reg_e, (void*)db->reg_lut, (void*)db->reg_near})
         if (p) HIPCHK(hipFree(p));
     db->reg_t = static_cast<uint64_t*>(nt[0]);

@@ -410,6 +410,9 @@ struct pm_db : pm_lane {
     // inherited pm_lane is the active one, `alt` the other; switch_lane swaps)
     hipStream_t post = nullptr;
     pm_lane alt;
+    bool lane_flip = false;          // PM_POST_STREAM: the next pipelined scan takes `alt`
+    hipEvent_t scan_ev = nullptr;    // PM_POST_STREAM: a scan's end, waited for by `post`
+    hipEvent_t join_ev = nullptr;    // post_join: `post`'s queued work, waited for by `stream`
     // the exception pass (k_linear_others) runs on `exc`, concurrently with
     // the specialized scan: forked from the scan stream after the counters
     // are zeroed, joined before the sort
@@ -500,6 +503,13 @@ void lane_begin(pm_db* db);
 void lane_end(pm_db* db, hipStream_t s);
 void switch_lane(pm_db* db);
 hipStream_t post_stream(pm_db* db);
+// PM_POST_STREAM (A/B, round 6): 0 (default) the expansion, exception pass,
+// sort and report of a pipelined scan run on the scan's own stream; 1 on
+// `post` with the workspaces double-buffered (lane_flip), so scan i+1 runs
+// while scan i is post-processed; 2 the same with `post` at high priority
+int post_mode();
+// every other user of a database's workspaces waits for `post` first
+void post_join(pm_db* db);
 hipStream_t exc_stream(pm_db* db);   // creates exc, exc_fork and exc_join on first use
 void* reserve(pm_db* db, pm_devbuf& b, size_t bytes);
 // Per-device pool of hit-list buffers (sizes rounded to powers of two):

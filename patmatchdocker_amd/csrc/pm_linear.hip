@@ -2022,6 +2022,27 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             chunks.push_back({base, P, fn});
             base += P;
         }
+        // PM_POST_STREAM (A/B): a pipelined single-launch scan post-processes
+        // on `post` in its own workspace lane (alternating), everything else
+        // waits for `post` first
+        const bool post2 = async && jit && !batch && chunks.size() == 1 && post_mode() > 0;
+        struct LaneBack {
+            pm_db* db;
+            bool on;
+            ~LaneBack() {
+                if (on) switch_lane(db);
+            }
+        } lane_back{db, false};
+        if (post2) {
+            post_stream(db);
+            if (db->lane_flip) {
+                switch_lane(db);
+                lane_back.on = true;
+            }
+            db->lane_flip = !db->lane_flip;
+        } else {
+            post_join(db);
+        }
         lane_begin(db);
         uint8_t* d_up = up.commit(db);
         const EsPrep esp = esimple ? es_bind(esu, d_up, es_gap(esb)) : EsPrep{};
@@ -2377,8 +2398,9 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                 uint64_t* clk = nullptr;   // PM_JIT_CLOCK samples of the launch
                 // expansion, exception pass and sort run on the scan's stream
                 // (overlapping them with the next scan on a second stream
-                // measured no faster: the chip is at its power limit)
-                const hipStream_t xs = s;
+                // measured no faster in round 4: the chip is at its power
+                // limit; PM_POST_STREAM re-measures it, round 6)
+                const hipStream_t xs = post2 && spec_async ? db->post : s;
                 for (const Chunk& ch : chunks) {
                     JArgsHost ja{db->hl, d_rec, d_rcnt, ch.base == 0 ? d_over : nullptr, db->ntiles, rcap, (uint32_t)tpw,
                                  (uint32_t)nA, (uint32_t)tpwB, (uint32_t)groupB, (uint32_t)tpo, tilesA};
@@ -2392,6 +2414,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                     // (no marker packets around the launch; sizes in threads)
                     HIPCHK(hipExtModuleLaunchKernel(ch.jit, (uint32_t)(nwg * 64 * parts), 1, 1, (uint32_t)(64 * parts), 1, 1, 0, s, params,
                                                     nullptr, jev.back()->a, jev.back()->b, 0));
+                    if (xs != s) {   // the post stream starts where the scan ends
+                        HIPCHK(hipEventRecord(db->scan_ev, s));
+                        HIPCHK(hipStreamWaitEvent(xs, db->scan_ev, 0));
+                    }
                     ExpandArgs xa{db->bo, db->lflag, d_rec, d_rcnt, d_over, rcap, db->ntiles, db->n,
                                   reinterpret_cast<const int32_t*>(d_up + o_len) + ch.base, ch.P, ch.base, sb.out, sb.cnt,
                                   sb.slot_base, sb.slot_cap, (uint32_t)nwg, (uint32_t)nout, (uint32_t)group,

@@ -582,6 +582,8 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     require(!(flags & PM_REGULAR) || rgt != nullptr, "PM_REGULAR needs nrgrep's tree (pm_scan_nfa_tree)");
     require(db != nullptr, "db is NULL");
     std::lock_guard<std::recursive_mutex> lk(db->mu);
+    DeviceGuard pj(db->device);
+    post_join(db);   // a pipelined scan's post-processing may still read the workspaces
     require(out != nullptr && byte_mask && follow && first && last, "null argument");
     require(m >= 1 && m <= PM_MAX_POSITIONS, "m out of range", PM_E_UNSUPPORTED);
     require(W == kernel_words(m), "words must be ceil(m / 64), at most 4");

@@ -859,7 +859,18 @@ __global__ __launch_bounds__(64) void k_p5_cross_fix(P5FixArgs a) {   // one wav
 // wave per whole tile reading the rows straight from global memory (19 %
 // fewer VALU instructions, no LDS) measured slower still, 0.546 vs 0.473 ms:
 // each row load's latency is exposed at 3 waves per SIMD (r04w A/B).
-int jit_parts() { return 4; }
+// waves per workgroup = parts of a tile's 32 window words (PM_JIT_PARTS, A/B:
+// 1, 2 or 4; default 4).  Each wave derives the class words of its steps'
+// rows plus the Lmax - 1 rows its last windows reach into: fewer parts
+// derive fewer rows twice, more parts keep more waves per SIMD
+int jit_parts() {
+    static const int v = [] {
+        const char* e = getenv("PM_JIT_PARTS");
+        const int p = e ? atoi(e) : 4;
+        return p == 1 || p == 2 || p == 4 ? p : 4;
+    }();
+    return v;
+}
 // the graded tail (scan_linear), on unless PM_JIT_GRADED=0: kernel -1.4 %
 // at 10 Gbp (frac 0.704 vs 0.694) with the same step time, -3 % kernel and
 // step at 100 Gbp (round 4, gpu_envab.sh; tests/test_gpu_graded.py checks

@@ -478,6 +478,16 @@ __global__ __launch_bounds__(256) void k_others_lane(LaneArgs a) {
 constexpr int OTH_BATCH_THREADS = 256;
 constexpr int OTH_BATCH_MAX_CLASSES = 32;
 
+// TWO (spans of <= 32 positions: every q-gram batch, patterns <= 16): the
+// wave takes two selected words at a time, one per 32-lane half -- lane
+// 32 h + i gathers position i of half h's span, the ballots carry both
+// spans side by side (half h at bits 32 h ..), and the class vectors and
+// the per-pattern window tests run on both at once: a window of half 0
+// reads bits < 31 and one of half 1 bits 32 .. 62, so the shifts that carry
+// bits across the halves only reach bits no window start of the other half
+// uses.  Half as many serial (gather, ballots, tests) rounds per exception
+// (round 6).
+template <bool TWO>
 __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a) {
     __shared__ uint4 s_cls[BATCH_MAX_P];                          // 16 class ids per pattern
     __shared__ uint32_t s_cm[OTH_BATCH_MAX_CLASSES][8];           // byte membership per class
@@ -506,19 +516,39 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int half = TWO ? lane >> 5 : 0, hl = TWO ? lane & 31 : lane;   // this lane's half, its lane in it
     uint64_t* const mv = s_mv[wid];
     const int ML = a.maxlen, span = 2 * ML - 1;
     const uint32_t nsel = *a.nsel;
-    for (uint32_t it = blockIdx.x * (OTH_BATCH_THREADS / 64) + wid; it < nsel; it += gridDim.x * (OTH_BATCH_THREADS / 64)) {
-        const OtherSel sv = a.sel[it];
-        const uint64_t tile = sv.word / TILE_WORDS;
-        const uint32_t lw = logical_word((uint32_t)(sv.word % TILE_WORDS));
-        for (uint32_t bits = sv.bits; bits; bits &= bits - 1) {
-            const uint64_t e = pos_of(tile, lw, __builtin_ctz(bits));
-            if (e >= a.n) continue;   // wave-uniform
+    constexpr uint32_t WPI = TWO ? 2 : 1;   // selected words per wave round
+    for (uint32_t it = (blockIdx.x * (OTH_BATCH_THREADS / 64) + wid) * WPI; it < nsel;
+         it += gridDim.x * (OTH_BATCH_THREADS / 64) * WPI) {
+        OtherSel sv[2];
+        uint32_t bits[2], lw[2];
+        uint64_t tile[2];
+#pragma unroll
+        for (uint32_t h = 0; h < WPI; ++h) {
+            sv[h] = it + h < nsel ? a.sel[it + h] : OtherSel{0, 0u, 0u};
+            bits[h] = sv[h].bits;
+            tile[h] = sv[h].word / TILE_WORDS;
+            lw[h] = logical_word((uint32_t)(sv[h].word % TILE_WORDS));
+        }
+        while (bits[0] | (TWO ? bits[1] : 0u)) {   // wave-uniform
+            // each half's next exception bit (a half without one idles: e = n)
+            uint64_t eh[2] = {a.n, a.n};
+#pragma unroll
+            for (uint32_t h = 0; h < WPI; ++h)
+                if (bits[h]) {
+                    eh[h] = pos_of(tile[h], lw[h], __builtin_ctz(bits[h]));
+                    bits[h] &= bits[h] - 1;
+                }
+            const bool live0 = eh[0] < a.n, live1 = TWO && eh[1] < a.n;
+            if (!live0 && !live1) continue;   // wave-uniform
+            const uint64_t e = TWO && half ? eh[1] : eh[0];
+            const bool live = TWO && half ? live1 : live0;
             const int64_t q0 = (int64_t)e - (ML - 1);
-            const int64_t q = q0 + lane;
-            const bool in_span = lane < span, in_file = in_span && q >= 0 && (uint64_t)q < a.n;
+            const int64_t q = q0 + hl;
+            const bool in_span = live && hl < span, in_file = in_span && q >= 0 && (uint64_t)q < a.n;
             uint32_t h = 0, l = 0, br = 0, ot = 0;
             if (in_file) {   // 1-2 words of the position-contiguous planes for the whole span
                 const uint4 v = a.nuc.lin[(uint64_t)q >> 5];
@@ -535,8 +565,18 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
             const uint64_t EXN = OT & ~BR & H;   // N (NUC_N_MARK)
             const uint64_t EXL = EX & ~EXN;       // bytes compared by value
             const uint64_t KILL = OUT | (a.cross ? 0ull : BR);
-            const uint64_t before = (OT | BR) & ((1ull << (ML - 1)) - 1);
-            const uint64_t owned = before ? ~0ull >> __builtin_clzll(before) : 0ull;
+            // windows that also hold an earlier exception of the span are its
+            // (per half: below the last exception before e)
+            const uint64_t bm = (1ull << (ML - 1)) - 1;
+            const uint64_t before = (OT | BR) & (TWO ? (bm | bm << 32) : bm);
+            uint64_t owned;
+            if constexpr (TWO) {
+                const uint32_t b0 = (uint32_t)before, b1 = (uint32_t)(before >> 32);
+                owned = (b0 ? 0xFFFFFFFFull >> __builtin_clz(b0) : 0ull) |
+                        ((b1 ? 0xFFFFFFFFull >> __builtin_clz(b1) : 0ull) << 32);
+            } else {
+                owned = before ? ~0ull >> __builtin_clzll(before) : 0ull;
+            }
             // the lane's byte when it is compared by value (N: its mark)
             uint8_t ch = 'N';
             const bool byval = ((EXN | EXL) >> lane) & 1;
@@ -549,12 +589,14 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
                 if (lane == c) mv[c] = (~vec_mismatch(H, L, s_csub[c]) & ~EX) | vb;
             }
             wave_lds_sync();
+            const int64_t q00 = (int64_t)eh[0] - (ML - 1), q01 = (int64_t)eh[1] - (ML - 1);
             for (int p = lane; p < a.P; p += 64) {
                 const int len = a.lengths[p];
                 const uint4 cl = s_cls[p];
                 const uint32_t cw[4] = {cl.x, cl.y, cl.z, cl.w};
-                // starts u whose window holds e: u in [ML - len, ML - 1]
-                uint64_t alive = (((1ull << len) - 1) << (ML - len)) & ~owned;
+                // starts u whose window holds e: u in [ML - len, ML - 1] (per half)
+                const uint64_t r = ((1ull << len) - 1) << (ML - len);
+                uint64_t alive = ((live0 ? r : 0ull) | (TWO && live1 ? r << 32 : 0ull)) & ~owned;
                 if (KILL) {   // wave-uniform; rare with the simple engine (off-file positions only)
                     uint64_t kw = 0;
                     for (int j = 0; j < len; ++j) kw |= KILL >> j;
@@ -580,7 +622,8 @@ __global__ __launch_bounds__(OTH_BATCH_THREADS) void k_others_batch(OthersArgs a
                     alive &= ~dead;
                 }
                 for (; alive; alive &= alive - 1) {
-                    const uint64_t s0 = (uint64_t)(q0 + __builtin_ctzll(alive));
+                    const int b = __builtin_ctzll(alive);
+                    const uint64_t s0 = TWO && b >= 32 ? (uint64_t)(q01 + (b - 32)) : (uint64_t)(q00 + b);
                     const uint32_t slot = (uint32_t)(a.pattern_base + p);
                     const uint64_t og = (uint32_t)(s0 / TILE_POS) / (uint32_t)a.tiles_per_wg;   // 32-bit division
                     const uint32_t o = atomicAdd(&a.seg_cnt[(uint64_t)slot * a.nwg + og], 1u);
@@ -2126,8 +2169,10 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
             HIPCHK(hipMemsetAsync(oa.nsel, 0, sizeof(uint32_t), os));
             hipLaunchKernelGGL(k_others_select, dim3(blocks_for(words, OTH_SELECT_T)), dim3(OTH_SELECT_T), 0, os, oa);
             HIPCHK(hipGetLastError());
+            // PM_OTH_TWO=0: one exception per wave round (A/B)
+            static const bool two_env = !(getenv("PM_OTH_TWO") && getenv("PM_OTH_TWO")[0] == '0');
             if (batch_form)
-                hipLaunchKernelGGL(k_others_batch,
+                hipLaunchKernelGGL(two_env && span <= 32 ? k_others_batch<true> : k_others_batch<false>,
                                    dim3((uint32_t)std::min<uint64_t>(OTH_BLOCKS, blocks_for(words * 64, OTH_BATCH_THREADS))),
                                    dim3(OTH_BATCH_THREADS), 0, os, oa);
             else

@@ -96,3 +96,26 @@ def test_two_rank_bench_config4_batch(tmp_path):
     assert line["n_gpus"] == 2 and line["config"]["patterns"] == 256
     progs = [compile_pattern(convert("-n", m)) for m in bench.batch_patterns(256)]
     _same(line, k, ln, _local_hits(0, "", progs))
+
+
+def test_two_rank_bench_with_the_extras(tmp_path):
+    """The default run's extras at N = 2 (the driver's multi-GPU runs print
+    them too): configs4 and north_star_100gbp sub-objects from both ranks'
+    timed loops, whole-job values, no CPU baseline above one rank."""
+    env = dict(os.environ, PM_BENCH_REHEARSE="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--gbp", str(GBP), "--rec-len", str(REC_LEN), "--no-cpu-baseline", "--extras", "on",
+           "--cfg4-gbp", "0.07", "--north-gbp", "0.07"]   # >= 64 Mi positions: the specialized kernels
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    for key, kern in (("configs4", "k_batch_scan"), ("north_star_100gbp", "pm_linear_jit")):
+        sub = line[key]
+        assert sub["value"] > 0 and sub["ms_per_step"] > 0 and sub["hits"] > 0, (key, sub)
+        assert sub["roofline"]["kernel"].startswith(kern) and sub["roofline"]["kernel_ms"] > 0
+        assert sub["cpu_baseline"] is None
+    assert "over 2 GPUs" in line["configs4"]["workload"]

@@ -491,6 +491,40 @@ __global__ __launch_bounds__(1024) void k_batch_verify_ord(BatchVerifyArgs a) {
                 }
             }
         }
+        // LATE: when every candidate of the round has one entry or none
+        // (wave-uniform; a batch of distinct motifs almost always), each has
+        // at most one match, and a single ballot places them -- no match
+        // list, no bit-sliced prefix
+        bool fast = false;
+        if constexpr (LATE) {
+            bool multi = false;
+#pragma unroll
+            for (int u = 0; u < VU; ++u) multi |= co[u] != 0u && !(co[u] & BQ_CO_ONE);
+            fast = __builtin_amdgcn_ballot_w64(multi) == 0;
+        }
+        if (fast) {
+#pragma unroll
+            for (int u = 0; u < VU; ++u) {
+                uint64_t key = 0;
+                bool hit = false;
+                if (co[u]) {
+                    const uint32_t w0 = co[u] & ~BQ_CO_ONE;
+                    hit = verify_key(a, tend, e[u], lf[u], make_uint4(w0, bq_len_mask(w0 >> 24), 0u, 0u),
+                                     s_pmask[w0 & 0xFFFFu], key) == 1;
+                }
+                const uint64_t bb = __builtin_amdgcn_ballot_w64(hit);
+                if (bb) {   // wave-uniform
+                    const uint32_t at0 =
+                        wcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+                    if (hit) {
+                        if (at0 < a.ord_cap) out[at0] = key;
+                        if constexpr (HIST) atomicAdd(&s_hist[wv][(uint32_t)(key >> 48)], 1u);
+                    }
+                    wcnt += (uint32_t)__builtin_popcountll(bb);
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < VU; ++u) {
             uint64_t hk[VH];

@@ -121,3 +121,11 @@ json.dump({"pm_linear_jit (configs[2], k=2 substitutions)": lin, "pm_ids_rev (co
           open(os.path.join(prof, "%s_pmc.json" % rnd), "w"), indent=1)
 print(json.dumps({"traffic": traffic, "alg": alg, "lin_valu": lin.get("SQ_INSTS_VALU"),
                   "ids_valu": ids.get("SQ_INSTS_VALU"), "cal": cal.get("FETCH_SIZE")}))
+# the steady-state dispatch means of the three workloads from the default
+# run's kernel trace (tools/steady_state.py)
+trace, line = os.path.join(root, "prof", "run_kernel_trace.csv"), os.path.join(root, "prof.json")
+if os.path.exists(trace) and os.path.exists(line):
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "steady_state.py"),
+                          trace, line, "20"], capture_output=True, text=True, check=True).stdout
+    open(os.path.join(prof, "%s_steady_state.json" % rnd), "w").write(out)

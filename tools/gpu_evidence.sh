@@ -9,7 +9,8 @@
 #   FETCH_SIZE calibration on known-byte reads (tools/micro/calib_read)
 #   configs[0]/[1]/[3] timings with bit-exact checks (tools/config_times.py)
 #   a kernel trace of configs[3]'s queries (tools/cfg3_prof.py)
-# then: python3 tools/evidence_summary.py gpurun_out/<tag> <round> (host side)
+# then: python3 tools/evidence_summary.py gpurun_out/<tag> <round> (host side; also
+# writes the steady-state summary, tools/steady_state.py)
 # Usage: bash tools/gpu_evidence.sh <tag> [a|b]   (a: benches + headline PMC, b: the rest;
 # default both -- two gpurun calls keep each under its time limit)
 set -o pipefail

@@ -302,6 +302,29 @@ __global__ void k_lane_flags(uint64_t ntiles, const uint2* __restrict__ bo, uint
     if (lane == 0) lflag[t] = bal;
 }
 
+// hflag[t] bit l: a position of lane l's own words of tile t (logical words
+// [32 l, 32 l + 32), every stream) is a header byte -- a break whose raw byte
+// is not '\n' (nuc_is_header).  The report pass's header check (rep_keep)
+// settles a start whose lane and predecessor's lane have none from this
+// word.  One wave per tile.
+__global__ void k_header_flags(uint64_t ntiles, const uint2* __restrict__ bo, const uint32_t* __restrict__ sbflag,
+                               const uint32_t* __restrict__ sbbase, const uint8_t* __restrict__ xbytes,
+                               uint64_t* __restrict__ hflag) {
+    const uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (t >= ntiles) return;
+    bool any = false;
+    for (uint32_t i = 0; i < LANE_WORDS && !any; ++i) {
+        const uint64_t pw = phys_word(t, lane * LANE_WORDS + i);
+        for (uint32_t brk = bo[pw].x; brk && !any; brk &= brk - 1) {
+            const uint32_t idx = exception_index(sbflag, sbbase, pw);
+            any = xbytes[(uint64_t)idx * 32 + __builtin_ctz(brk)] != (uint8_t)'\n';
+        }
+    }
+    const uint64_t bal = __ballot(any);
+    if (lane == 0) hflag[t] = bal;
+}
+
 // The position-contiguous copy (lin): lin[p / 32] holds bit p % 32 of the
 // hi, lo, brk and oth planes of positions p..  One block per tile: the
 // tile's 2048 physical words of hl and bo in LDS, then every lin word of the
@@ -451,6 +474,7 @@ void alloc_planes(pm_db* db) {
     db->hl = dalloc<uint2>(db, db->nwords + 128);   // + LDS-DMA over-read of the last tile
     db->bo = dalloc<uint2>(db, db->nwords);
     db->lflag = dalloc<uint64_t>(db, db->ntiles);
+    db->hflag = dalloc<uint64_t>(db, db->ntiles);
 }
 
 // halo words, flags, compacted exception side tables, lane flags
@@ -470,10 +494,10 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     HIPCHK(hipGetLastError());
     size_t tmp_bytes = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
-    clear_stale_capture_status("rocPRIM call (pm_db)");   // (rocPRIM's stale capture status, as below)
+    clear_stale_capture_status("rocPRIM call (pm_db)");   // (a check after the call, pm_internal.h)
     void* tmp = tmp_alloc<uint8_t>(owned, tmp_bytes);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sbcnt, db->sbbase, (int)db->nsb, s));
-    clear_stale_capture_status("rocPRIM call (pm_db)");   // rocPRIM leaves a stale "stream is capturing" status behind
+    clear_stale_capture_status("rocPRIM call (pm_db)");   // (fails on any status but a caller's capture code)
     uint32_t* h = static_cast<uint32_t*>(reserve_host(db, db->pin_down, 16));
     HIPCHK(hipMemcpyAsync(h, db->sbbase + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h + 1, sbcnt + db->nsb - 1, 4, hipMemcpyDeviceToHost, s));
@@ -494,6 +518,9 @@ void finish_nuc(pm_db* db, std::vector<void*>& owned, const uint8_t* d_raw, uint
     db->n_oth_words = h[0];   // 0: scans skip the "other byte" pass
     hipLaunchKernelGGL(k_lane_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
                        db->lflag);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_header_flags, dim3(blocks_for(db->ntiles * 64, 256)), dim3(256), 0, s, db->ntiles, db->bo,
+                       db->sbflag, db->sbbase, db->xbytes, db->hflag);
     HIPCHK(hipGetLastError());
     db->lin = dalloc<uint4>(db, db->ntiles * STREAM);   // 0.5 byte per position
     hipLaunchKernelGGL(k_build_lin, dim3((uint32_t)std::min<uint64_t>(db->ntiles, 8192)), dim3(256), 0, s, db->ntiles,
@@ -571,7 +598,7 @@ void free_db(pm_db* db) {
     for (hipEvent_t e : {db->exc_fork, db->exc_join, db->scan_ev, db->join_ev})
         if (e) quiet(hipEventDestroy(e));
     void* ptrs[] = {db->hdr, db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->hl, db->bo, db->lin, db->sbflag, db->sbbase, db->xbrk, db->xoth, db->xword, db->xbytes,
-                    db->lflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->hdr_end, db->bytes, db->bytes_raw, db->ws_post.p,
+                    db->lflag, db->hflag, db->xint, db->xedge, db->xedge_oth, db->xlist, db->p5, db->hdr_end, db->bytes, db->bytes_raw, db->ws_post.p,
                     db->ws_batch.p};
     for (void* p : ptrs)
         if (p) quiet(hipFree(p));

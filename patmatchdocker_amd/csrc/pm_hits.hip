@@ -945,11 +945,14 @@ __device__ inline bool rep_keep(const RepArgs& a, uint64_t key) {
     if (!a.hdr) return true;
     const uint64_t s = key & POS_MASK;
     if (a.tv.nuc_layout) {
-        // positions whose lane holds no exception at all (lflag: 1.5 MB per
-        // 12.5 Gbp, cache-resident) are no header byte: most reported starts
-        // then cost one cached load instead of two random plane reads
+        // positions whose lane holds no header byte (hflag: 1.5 MB per 12.5
+        // Gbp, cache-resident) settle with one cached load.  (Until round 6
+        // this was lflag, the lanes with ANY exception -- N runs, IUPAC
+        // letters, every line break of a wrapped file: ~5 % of a synthetic
+        // database's lanes and nearly all of a real genome's, each such start
+        // then paying the exception-table chain of nuc_is_header)
         auto clean = [&](uint64_t p) {
-            return !((a.tv.lflag[p / TILE_POS] >> ((uint32_t)(p % STREAM) >> 5)) & 1ull);
+            return !((a.tv.hflag[p / TILE_POS] >> ((uint32_t)(p % STREAM) >> 5)) & 1ull);
         };
         if (clean(s) && (s == 0 || clean(s - 1))) return true;
     }
@@ -1292,7 +1295,7 @@ void retire_buffers(pm_hits* h, hipStream_t s) {
 }  // namespace
 
 TextView text_view(const pm_db* db) {
-    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->lflag,
+    return TextView{nuc_view(db), db->bytes, db->bytes_raw, db->n, db->alphabet == PM_ALPHA_NUC ? 1 : 0, db->hflag,
                     Regions{db->reg_t, db->reg_e, db->reg_lut, db->reg_near, db->nreg}};
 }
 

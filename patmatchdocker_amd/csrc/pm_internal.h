@@ -365,6 +365,7 @@ struct pm_db : pm_lane {
     uint8_t* xbytes = nullptr;
     uint64_t* xword = nullptr;   // NUC: physical word of each flagged word
     uint64_t* lflag = nullptr;   // NUC: per tile, lanes with exceptions
+    uint64_t* hflag = nullptr;   // NUC: per tile, lanes whose own words hold a header byte (k_header_flags)
     uint4* lin = nullptr;        // NUC: {hi, lo, brk, oth} bits of positions 32 q .. 32 q + 31 (k_build_lin)
     // NUC, runs of N: per flagged word, the bits whose position is preceded
     // by an exception and followed by RUN_SKIP more "other" bytes (xint);
@@ -812,7 +813,7 @@ struct TextView {
     const uint8_t* raw;     // BYTE layout, the file's own bytes
     uint64_t n;
     int nuc_layout;
-    const uint64_t* lflag;  // NUC: per tile, the lanes with an exception (a clean lane holds no header byte)
+    const uint64_t* hflag;  // NUC: per tile, the lanes whose own words hold a header byte (pm_db::hflag)
     Regions reg;
 };
 TextView text_view(const pm_db* db);

@@ -225,13 +225,12 @@ __device__ __forceinline__ int verify_key(const BatchVerifyArgs& a, uint64_t ten
     const uint64_t pos = pos_of(tile, w, st);
     if (tile >= a.ntiles || pos + (uint64_t)len > a.n) return 0;
     if ((lf >> (w >> 5)) & 1) {   // an exception near: windows over it are the others pass's
-        uint32_t kill = 0;
-        for (int j = 0; j < len; ++j) {
-            const Loc l = loc_of(pos + j);
-            const uint2 b = a.bo[l.word];
-            kill |= ((b.x | b.y) >> l.bit) & 1u;
-        }
-        if (kill) return 0;
+        // the window's break | other bits from the position-contiguous
+        // planes: 1-2 words (round 6; a load per position before)
+        const uint64_t q = pos >> 5;
+        const uint4 v0 = a.lin[q], v1 = a.lin[q + 1];   // (lin has a word past every position)
+        const uint64_t ex = ((uint64_t)(v1.z | v1.w) << 32 | (v0.z | v0.w)) >> (pos & 31);
+        if (ex & ((1ull << len) - 1)) return 0;
     }
     key = ((uint64_t)p << 48) | pos;
     if (tile < tend) return 1;

@@ -668,6 +668,7 @@ struct BatchVerifyArgs {
     uint32_t ord_cap = 0;
     uint32_t sink_segs = 0;   // segments per pattern of the bins k_batch_fixup fills (0: nout)
     uint32_t* ord_hist = nullptr;   // [P][nout * BATCH_VERIFY_WAVES] keys per (pattern, list); null: none
+    const uint4* lin = nullptr;     // the position-contiguous planes: a window's exception bits in 1-2 loads
 };
 // k_batch_scan (timed by ev_a / ev_b), k_batch_verify, k_batch_fixup on s
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,

@@ -2280,6 +2280,7 @@ void scan_linear_impl(pm_db* db, int n_patterns, const int32_t* lengths, const u
                                    (uint32_t)xcap};
                 uint32_t* d_ocnt = reinterpret_cast<uint32_t*>(rbase + o_ocnt);
                 va.sink_segs = (uint32_t)snout;
+                va.lin = db->lin;
                 // the exception pass's segment of a start: all in one with snout 1
                 const uint64_t oth_tiles = ordered ? (uint64_t)UINT32_MAX : tpw * wpo;
                 if (ordered) {

@@ -448,22 +448,37 @@ struct EsText {
                 for (uint32_t q = 0; q < cnt; ++q) es_lds[r.base + ((uint32_t)(b + q) & r.mask)] = 0;
                 r.hi = b + cnt;
             } else if (tv.nuc_layout) {
-                const uint4 v = tv.nuc.lin[b >> 5];
-                const uint64_t e = umin64(((b >> 5) + 1) << 5, upto);   // through the word's end (or upto)
-                for (uint64_t p = b; p < e; ++p) {
-                    const uint32_t i = (uint32_t)(p & 31);
-                    uint8_t c;
-                    if (p >= n || ((v.z >> i) & 1)) {   // a break or past the end
-                        c = 0;
-                    } else if ((v.w >> i) & 1) {
-                        c = cmap[nuc_char_at(tv.nuc, p)];
-                    } else {
-                        const uint32_t code = (((v.x >> i) & 1) << 1) | ((v.y >> i) & 1);
-                        c = cmap[(0x54474341u >> (8 * code)) & 0xff];
+                // the whole 32-position word, four codes per 32-bit LDS store
+                // (a word's slots never wrap: win >= 64 is a power of two);
+                // positions of the word before b get the codes they hold
+                // already, or sit below the ring (round 6: one byte store
+                // and a table read per position before)
+                const uint64_t wb = b & ~31ull;
+                const uint4 v = tv.nuc.lin[wb >> 5];
+                const uint32_t acgt4 = (uint32_t)cmap['A'] | (uint32_t)cmap['C'] << 8 | (uint32_t)cmap['G'] << 16 |
+                                       (uint32_t)cmap['T'] << 24;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(es_lds + r.base + ((uint32_t)wb & r.mask));
+#pragma unroll
+                for (uint32_t g = 0; g < 8; ++g) {
+                    uint32_t o = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint32_t bit = 4 * g + i;
+                        const uint32_t code = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1);
+                        const uint32_t c = ((v.z >> bit) & 1) ? 0u : (acgt4 >> (8 * code)) & 0xffu;   // a break: 0
+                        o |= c << (8 * i);
                     }
-                    es_lds[r.base + ((uint32_t)p & r.mask)] = c;
+                    dst[g] = o;
                 }
-                r.hi = e;
+                // "other" bytes (N, IUPAC letters) from the side tables; past
+                // the end of the text every position is a break (0)
+                for (uint32_t ex = v.w & ~v.z; ex; ex &= ex - 1) {
+                    const uint64_t p = wb + (uint32_t)__builtin_ctz(ex);
+                    es_lds[r.base + ((uint32_t)p & r.mask)] = p < n ? cmap[nuc_char_at(tv.nuc, p)] : (uint8_t)0;
+                }
+                if (wb + 32 > n)
+                    for (uint64_t p = umax64(wb, n); p < wb + 32; ++p) es_lds[r.base + ((uint32_t)p & r.mask)] = 0;
+                r.hi = wb + 32;
             } else {
                 const uint32_t cnt = (uint32_t)umin64(ES_CHUNK, upto - b);
                 uint8_t c[ES_CHUNK];

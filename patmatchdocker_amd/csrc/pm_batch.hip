@@ -80,9 +80,6 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
 // consecutive pieces per pattern measured: scan 3.0 -> 2.16 ms, but the two
 // pieces' expansions raise the candidates and verify 2.08 -> 2.74 ms, 10.6
 // vs 9.9 ms per configs[4] step; round 2.)
-// NOWRITE (PM_BATCH_SCAN_NOWRITE=1, timing only -- no candidates leave):
-// the probes without the candidate write-out, to price the write-out
-template <bool NOWRITE>
 __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
     __shared__ uint32_t s_tab[BQ_TABLE_WORDS];   // 128 KB: one workgroup per CU
     for (uint32_t i = threadIdx.x; i < BQ_TABLE_WORDS; i += BATCH_THREADS) s_tab[i] = a.table[i];
@@ -163,10 +160,6 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             // this LDS-bound kernel, measured 3.0 -> 3.48 ms; an LDS staging
             // of the entries 3.67 ms), a round or two at ~0.26 per lane
             uint32_t m = acc;
-            if constexpr (NOWRITE) {
-                ccnt ^= m;   // keeps the probes live
-                continue;
-            }
             if (__builtin_amdgcn_ballot_w64(m != 0u)) {   // wave-uniform
                 const uint32_t cnt = (uint32_t)__builtin_popcount(m);
                 uint32_t q = 0, tot = 0;
@@ -190,13 +183,7 @@ __global__ __launch_bounds__(BATCH_THREADS) void k_batch_scan(BatchScanArgs a) {
             }
         }
     }
-    if constexpr (NOWRITE) {
-        // no candidates (the probes stay live through the xor: a count of 1
-        // only if lane 0's xor hits the constant)
-        if (lane == 0) a.cand_cnt[wave] = ccnt == 0x9E3779B9u ? 1u : 0u;
-    } else if (lane == 0) {
-        a.cand_cnt[wave] = ccnt;
-    }
+    if (lane == 0) a.cand_cnt[wave] = ccnt;
 }
 
 // Slot tables of the block's hit lists, staged in LDS.
@@ -749,9 +736,7 @@ bool build_batch_index(int P, const int32_t* lengths, const uint8_t* pos_class, 
 void batch_launch(const BatchScanArgs& sa, const BatchVerifyArgs& va, uint32_t nblocks, hipStream_t s,
                   hipEvent_t ev_a, hipEvent_t ev_b) {
     // the kernel's own dispatch timestamps (no marker packets)
-    static const bool nowrite = getenv("PM_BATCH_SCAN_NOWRITE") && getenv("PM_BATCH_SCAN_NOWRITE")[0] == '1';
-    hipExtLaunchKernelGGL(nowrite ? k_batch_scan<true> : k_batch_scan<false>, dim3(nblocks), dim3(BATCH_THREADS), 0, s,
-                          ev_a, ev_b, 0u, sa);
+    hipExtLaunchKernelGGL(k_batch_scan, dim3(nblocks), dim3(BATCH_THREADS), 0, s, ev_a, ev_b, 0u, sa);
     HIPCHK(hipGetLastError());
     // PM_BATCH_HASH=0: the code_off array (A/B)
     static const bool hash_on = !(getenv("PM_BATCH_HASH") && getenv("PM_BATCH_HASH")[0] == '0');

@@ -663,7 +663,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                                                      (int)total, 0, pack ? (int)(pos_bits + slot_bits) : 64, s));
         if (!inline_off)
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counted, (uint64_t*)nullptr, (int)sb.nbins, s));
-        clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status, size queries too (see the scan below)
+        clear_stale_capture_status("rocPRIM call (pm_hits)");   // (status check after the size queries too, see the scan below)
         Carve c;
         const size_t o_off = c.take(sb.nbins * sizeof(uint64_t));
         const size_t o_scan = c.take(scan_bytes);
@@ -678,9 +678,9 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
         uint64_t* d_off = reinterpret_cast<uint64_t*>(base + o_off);
         if (!inline_off) {
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + o_scan, scan_bytes, counted, d_off, (int)sb.nbins, s));
-            // rocPRIM's scan leaves a stale "stream is capturing" status from
-            // its capture query behind (the call itself succeeded): clear it so
-            // the next launch check does not report it
+            // (a status check after the library call: any status but a
+            // caller's capture code fails here, pm_internal.h -- round 6's
+            // probe found none of these rocPRIM calls leaves one)
             clear_stale_capture_status("rocPRIM call (pm_hits)");
         }
         if (whole) {
@@ -690,7 +690,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
             HIPCHK(hipGetLastError());
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_tmp, sort_bytes, unsorted, h->keys, (int)total, 0,
                                                      pack ? (int)(pos_bits + slot_bits) : 64, s));
-            clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (see the scan above)
+            clear_stale_capture_status("rocPRIM call (pm_hits)");   // (status check, see the scan above)
             if (pack) {
                 hipLaunchKernelGGL(k_unpack_keys, dim3(blocks_for(total, 256)), dim3(256), 0, s, h->keys, total,
                                    pos_bits);
@@ -729,7 +729,7 @@ pm_hits* sink_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uint32
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipcub::DeviceRadixSort::SortKeys(base + o_hsort, hsort_bytes, hin, hout, (int)nhuge, 0,
                                                          pack ? (int)(pos_bits + slot_bits) : 64, s));
-                clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (see the scan above)
+                clear_stale_capture_status("rocPRIM call (pm_hits)");   // (status check, see the scan above)
                 hipLaunchKernelGGL(k_scatter_huge, dim3((uint32_t)huge.size()), dim3(1024), 0, s, hout, sh, d_hb,
                                    h->keys, slot_len, h->lens, pb);
                 HIPCHK(hipGetLastError());
@@ -801,7 +801,7 @@ pm_hits* ordered_to_hits(pm_db* db, const SinkBuffers& sb, const std::vector<uin
             if (hs)
                 HIPCHK(rocprim::merge(nullptr, merge_bytes, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
                                       (uint64_t*)nullptr, (size_t)t1, (size_t)sink_total, rocprim::less<uint64_t>(), s));
-            clear_stale_capture_status("rocPRIM call (pm_hits)");   // rocPRIM's stale capture status (sink_to_hits)
+            clear_stale_capture_status("rocPRIM call (pm_hits)");   // (status check, see sink_to_hits)
             Carve c;
             const size_t o_off = c.take(d_hist ? nh * sizeof(uint32_t) : nlists * sizeof(uint64_t));
             const size_t o_scan = c.take(scan_bytes);

@@ -453,6 +453,7 @@ struct pm_pending {
     int n_patterns = 0, n_classes = 0, k = 0;
     uint32_t flags = 0;               // PM_REPORT_* / PM_ANCHOR_*
     bool reported = false;            // counts_h[nbins + 1] holds the reported count
+    bool count_only = false;          // a pipelined batch: counts_h[0] is the reported count, nothing else pends
     std::vector<int32_t> lengths;
     std::vector<uint8_t> pos_class, class_acgt, class_is_any;
     std::vector<uint32_t> class_bytes;

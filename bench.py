@@ -372,16 +372,22 @@ def run_workload(ctx, config, motif, k, types, gbp, rec_len, n_batch, serial, st
         return out, ms
 
     def ids_step():
+        # both strands launched before either is collected (PM_PIPELINED:
+        # strand 1's scan queues behind strand 0's report pass, no host wait
+        # between them), as engine.scan does
         parts_k, parts_l, ms = [], [], 0.0
-        for pid, prog in enumerate(progs):
-            h = engine.nfa_launch(db, prog, k, pid, types)
-            try:   # keys pid << 48 | beg, copied on the device
+        handles = []
+        try:
+            for pid, prog in enumerate(progs):
+                handles.append(engine.nfa_launch(db, prog, k, pid, types, pipelined=not serial))
+            for h in handles:   # keys pid << 48 | beg, copied on the device
                 keys, lens = shards.hits_to_tensors(h, device)
                 ms += engine.kernel_ms(h)
-            finally:
+                parts_k.append(keys)
+                parts_l.append(lens)
+        finally:
+            for h in handles:
                 engine.destroy_hits(h)
-            parts_k.append(keys)
-            parts_l.append(lens)
         keys = shards.to_global(torch.cat(parts_k), offset)
         out = shards.gather_hits(keys, torch.cat(parts_l))
         return out, ms / len(progs)   # per launch (one strand)
@@ -610,7 +616,7 @@ def main():
                        "k_mismatches": args.k, "patterns": len(progs),
                        "strands": 2 if args.config == 2 else 1, "gbp_per_gpu": args.gbp, "record_len": args.rec_len,
                        "hits": n_hits, "parallelism": "shard-by-record x%d + RCCL hit gather" % world,
-                       "error_types": args.types if args.k else "", "pipelined": not (args.serial or indel)},
+                       "error_types": args.types if args.k else "", "pipelined": not args.serial},
             "roofline": roof,
         }
         if args.config == 4:

@@ -122,6 +122,11 @@ int pm_db_decode(pm_db* db, uint64_t beg, uint32_t len, uint8_t* out);
 /* pm_scan_linear on a BYTE database: scan the byte copy instead of the
  * 5-bit residue planes (A/B and tests; same hits).                        */
 #define PM_SCAN_BYTES 256
+/* pm_scan_nfa_errs / _wide / _tree: return once the report pass is queued
+ * (no host wait for it); the list's count resolves on first use, as for
+ * pm_scan_linear_async, so a caller launches its next scan (the other
+ * strand) while this one's report runs.  Same results.                  */
+#define PM_PIPELINED 1024
 /* The pattern is a class sequence (nrgrep's detClass() == 1) searched with
  * k > 0 errors: nrgrep_coords runs its "esimple" engine (searchPreproc
  * 0x402710), whose own candidate order and two-phase verification decide

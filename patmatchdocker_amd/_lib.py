@@ -28,6 +28,7 @@ PM_SCAN_BYTES = 256           # BYTE databases: scan the byte copy, not the 5-bi
 PM_ESIMPLE = 64               # a class sequence at k > 0: nrgrep's esimple report
 PM_EXTENDED = 128             # classes with '?*+': nrgrep's extended / eextended report
 PM_REGULAR = 512              # '|' / repeated groups: nrgrep's regular report (pm_scan_nfa_tree)
+PM_PIPELINED = 1024           # automaton scans: the report pass is queued, the count resolves on first use
 
 # every symbol declared in include/patmatch_hip.h
 EXPORTED = (

@@ -577,8 +577,12 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
               const uint64_t* last, int max_len, int min_len, int k, int errs, int pattern_id, int flags,
               pm_hits** out, const RgTree* rgt = nullptr) {
     require((flags & ~(PM_REPORT_NRGREP | PM_ANCHOR_START | PM_ANCHOR_END | PM_KEEP_HEADERS | PM_CROSS_LINES |
-                       PM_ESIMPLE | PM_EXTENDED | PM_REGULAR | PM_SCAN_BYTES)) == 0,
+                       PM_ESIMPLE | PM_EXTENDED | PM_REGULAR | PM_SCAN_BYTES | PM_PIPELINED)) == 0,
             "bad flags");
+    // PM_PIPELINED: the report pass is queued and the count resolves on
+    // first use (hits_finalize); the report kernels never see the bit
+    const bool pipelined = (flags & PM_PIPELINED) != 0;
+    flags &= ~PM_PIPELINED;
     require(!(flags & PM_REGULAR) || rgt != nullptr, "PM_REGULAR needs nrgrep's tree (pm_scan_nfa_tree)");
     require(db != nullptr, "db is NULL");
     std::lock_guard<std::recursive_mutex> lk(db->mu);
@@ -912,14 +916,33 @@ void scan_nfa(pm_db* db, int m, int W, const uint64_t* byte_mask, const uint64_t
     // record, e.g. extended checkMatch 0x411b1d): no candidate starts on a
     // header line, the pass only selects what nrgrep reports; the simple
     // engine (cross) also drops the windows starting on a header line
-    if (esimple) {
-        // the walk replaces the lengths; until it runs they are unset
-        report_sync(db, h, (uint32_t)flags, total, false, &esp);
-    } else if (extended || regular) {
-        report_sync(db, h, (uint32_t)flags, total, false, nullptr, &xtp);
-    } else if (report_needed(db, (uint32_t)flags, cross)) {
-        report_sync(db, h, (uint32_t)flags, total, cross);
+    // (esimple: the walk replaces the lengths; until it runs they are unset)
+    const bool walk = esimple || extended || regular;
+    const bool rep = walk || report_needed(db, (uint32_t)flags, cross);
+    const EsPrep* rep_es = esimple ? &esp : nullptr;
+    const XtPrep* rep_xt = (extended || regular) ? &xtp : nullptr;
+    if (pipelined && rep && total && !every_pos) {
+        // the report pass is queued behind the scan and its kept count lands
+        // in pinned memory with the pass's last dispatch: the caller launches
+        // its next scan (the other strand) while this one's walk runs --
+        // between the two strands of a `-k 2ids` query the GPU idled ~0.1 ms
+        // for the host's wait, copy and next launch (round 6)
+        std::unique_ptr<pm_pending> pd(new pm_pending());
+        pd->db = db;
+        pd->count_only = true;
+        pd->counts_h = static_cast<uint32_t*>(pinned_get(8, &pd->counts_cap));
+        pd->counts_h[0] = 0u;
+        const ReportWs ws = report_ws(db, h->keys_cap / 8);
+        if (!h->ready) HIPCHK(hipEventCreate(&h->ready));
+        report_enqueue_ws(db, h, (uint32_t)flags, ws, false, total, pd->counts_h, s, h->ready, !walk && cross, rep_es,
+                          rep_xt);
+        lane_end(db, s);
+        h->pending = pd.release();
+        db->pending.insert(h);
+        *out = h;
+        return;
     }
+    if (rep) report_sync(db, h, (uint32_t)flags, total, !walk && cross, rep_es, rep_xt);
     HIPCHK(hipStreamSynchronize(s));
     hits_ready(db, h);
     *out = h;

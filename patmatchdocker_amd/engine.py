@@ -507,12 +507,17 @@ def eregular_plan(prog: Program, k: int) -> dict:
 
 
 def nfa_launch(db: SequenceDatabase, prog: Program, k: int, pattern_id: int = 0, types: str = "s",
-               flags: int = None):
+               flags: int = None, pipelined: bool = False):
     """pm_scan_nfa_wide; returns the raw pm_hits handle (caller destroys),
-    keys ``pattern_id << 48 | beg`` -- see :func:`scan_nfa`."""
+    keys ``pattern_id << 48 | beg`` -- see :func:`scan_nfa`.
+    ``pipelined`` (PM_PIPELINED): returns once the report pass is queued;
+    the list's count resolves on first use, so the caller can launch its
+    next scan (the other strand) before collecting this one."""
     w, bm, fol, first, last = _nfa_tables(prog)
     errs = error_mask(types) if k else _lib.PM_ERR_SUB
     flags = report_flags(prog) if flags is None else flags
+    if pipelined:
+        flags |= _lib.PM_PIPELINED
     if k == 0 and prog.linear and any(10 in c for c in prog.classes):
         flags |= _lib.PM_CROSS_LINES
     if k > 0 and prog.linear and prog.kind == "simple":
@@ -580,11 +585,28 @@ def scan(db: SequenceDatabase, progs: Sequence[Program], k: int = 0, types: str 
         total_ms += hits.kernel_ms
         for slot, i in enumerate(linear_ids):
             results[i] = hits.for_pattern(slot)
-    for i in range(len(progs)):
-        if routes[i] == "nfa" and canonical[i] == i:
-            hits = scan_nfa(db, progs[i], k, 0, types, report_flags(progs[i], report, keep_headers, start_anchor))
-            total_ms += hits.kernel_ms
-            results[i] = (hits.beg, hits.end)
+    # the automaton scans are all launched before the first is collected
+    # (PM_PIPELINED): each one's report pass runs while the host launches
+    # the next scan
+    nfa_ids = [i for i in range(len(progs)) if routes[i] == "nfa" and canonical[i] == i]
+    handles = []
+    try:
+        for i in nfa_ids:
+            handles.append(nfa_launch(db, progs[i], k, 0, types,
+                                      report_flags(progs[i], report, keep_headers, start_anchor), pipelined=True))
+    except BaseException:
+        for h in handles:
+            destroy_hits(h)
+        raise
+    for j, i in enumerate(nfa_ids):
+        try:
+            hits = _collect(handles[j])
+        except BaseException:
+            for h in handles[j + 1:]:
+                destroy_hits(h)
+            raise
+        total_ms += hits.kernel_ms
+        results[i] = (hits.beg, hits.end)
     for i in range(len(progs)):
         if results[i] is None:
             results[i] = results[canonical[i]]

@@ -105,3 +105,39 @@ def test_ids_pass_classes_that_take_n(engine, oracle_mod, monkeypatch):
             assert list(zip(r.beg.tolist(), r.end.tolist())) == want, src
     finally:
         db.close()
+
+
+def test_pipelined_scans_equal_synchronous(engine, monkeypatch):
+    """PM_PIPELINED (engine.scan's automaton scans, bench --types ids): the
+    report pass is queued and the count resolves on first use.  Several
+    scans of every report kind are launched before any is collected, some
+    are destroyed uncollected, and each collected list equals the same
+    query run synchronously."""
+    from patmatchdocker_amd import _lib
+    monkeypatch.setenv("PM_IDS_JIT", "1")
+    text = TEXTS["dna"]()
+    db = engine.SequenceDatabase.from_bytes(text, alphabet=engine.NUC)
+    try:
+        cases = []
+        for src, k, types in [(convert("-n", "TGCTGASTCAGCANW"), 2, "ids"),
+                              (convert("-c", convert("-n", "TGCTGASTCAGCANW")), 2, "ids"),
+                              ("GA*TTC+A", 1, "ids"), ("(GATC){2,3}A", 0, ""), ("(CA|GT)TTG", 1, "s"),
+                              ("TATA[AT]A", 1, "ids")]:
+            prog = compile_pattern(src, ignore_case=True)
+            for report in ("nrgrep", "all"):
+                cases.append((prog, k, types, engine.report_flags(prog, report)))
+        want = []
+        for prog, k, types, flags in cases:
+            r = engine.scan_nfa(db, prog, k, 0, types or "s", flags)
+            want.append(_pairs((r.beg, r.end)))
+        handles = [engine.nfa_launch(db, prog, k, 0, types or "s", flags, pipelined=True)
+                   for prog, k, types, flags in cases]
+        for i, h in enumerate(handles):
+            if i % 3 == 1:
+                engine.destroy_hits(h)   # never collected
+                continue
+            r = engine._collect(h)
+            assert _pairs((r.beg, r.end)) == want[i], (cases[i][0].source, cases[i][1], cases[i][3])
+        assert _lib.PM_PIPELINED == 1024
+    finally:
+        db.close()

@@ -371,15 +371,23 @@ def run_workload(ctx, config, motif, k, types, gbp, rec_len, n_batch, serial, st
         out = shards.gather_hits(keys, lens, fixed_len=[p.m for p in progs])
         return out, ms
 
-    def ids_step():
-        # both strands launched before either is collected (PM_PIPELINED:
-        # strand 1's scan queues behind strand 0's report pass, no host wait
-        # between them), as engine.scan does
-        parts_k, parts_l, ms = [], [], 0.0
+    def ids_launch():
+        # both strands' automaton scans (PM_PIPELINED unless --serial: each
+        # returns once its report pass is queued, so strand 1's scan queues
+        # behind strand 0's report with no host wait between them)
         handles = []
         try:
             for pid, prog in enumerate(progs):
                 handles.append(engine.nfa_launch(db, prog, k, pid, types, pipelined=not serial))
+        except BaseException:
+            for h in handles:
+                engine.destroy_hits(h)
+            raise
+        return handles
+
+    def ids_collect(handles):
+        parts_k, parts_l, ms = [], [], 0.0
+        try:
             for h in handles:   # keys pid << 48 | beg, copied on the device
                 keys, lens = shards.hits_to_tensors(h, device)
                 ms += engine.kernel_ms(h)
@@ -393,20 +401,21 @@ def run_workload(ctx, config, motif, k, types, gbp, rec_len, n_batch, serial, st
         return out, ms / len(progs)   # per launch (one strand)
 
     # pipelined (default): a step launches query i+1 (pm_scan_linear_async,
-    # no host sync) and then collects query i, so the host-side collection
-    # and the next launch overlap the GPU scan.  The query launched before
-    # the timed region finishes before t0 (synchronize below); the timed
-    # region holds K launches whose GPU work all completes inside it.
-    pending = [batch.launch(db, k, pipelined=True)] if not (serial or indel) else []
+    # no host sync; '-k <k>ids': both strands' automaton scans) and then
+    # collects query i, so the host-side collection and the next launch
+    # overlap the GPU scan.  The query launched before the timed region
+    # finishes before t0 (synchronize below); the timed region holds K
+    # launches whose GPU work all completes inside it.
+    pending = []
+    if not serial:
+        pending.append(ids_launch() if indel else batch.launch(db, k, pipelined=True))
 
     def step():
-        if indel:
-            return ids_step()
         if serial:
-            return collect(batch.launch(db, k))
-        nxt = batch.launch(db, k, pipelined=True)
+            return ids_collect(ids_launch()) if indel else collect(batch.launch(db, k))
+        nxt = ids_launch() if indel else batch.launch(db, k, pipelined=True)
         h, pending[0] = pending[0], nxt
-        return collect(h)
+        return ids_collect(h) if indel else collect(h)
 
     for _ in range(warmup):
         step()
@@ -423,8 +432,9 @@ def run_workload(ctx, config, motif, k, types, gbp, rec_len, n_batch, serial, st
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if pending:
-        engine.destroy_hits(pending[0])   # the query launched by the last step (its work is done)
+    if pending:   # the query launched by the last step (its work is done)
+        for h in pending[0] if indel else pending:
+            engine.destroy_hits(h)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if ctx.rehearse else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/pipe
-timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_ids.py tests/test_gpu_esimple.py tests/test_gpu_extended.py tests/test_gpu_eextended.py tests/test_gpu_regular.py tests/test_service_gpu.py > gpurun_out/pipe/tests.txt 2>&1 || { tail -30 gpurun_out/pipe/tests.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_ids.py tests/test_gpu_bench_ranks.py > gpurun_out/pipe/tests.txt 2>&1 || { tail -30 gpurun_out/pipe/tests.txt; exit 1; }
 tail -2 gpurun_out/pipe/tests.txt
 for i in 1 2; do
 timeout -k 10 200 python bench.py --types ids --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/pipe/p$i.json 2> gpurun_out/pipe/p$i.err || exit 1

@@ -1,7 +1,10 @@
 #!/bin/bash
 # A/B (round 6): configs[4]'s post-verify work (ordered lists' sort, scatter,
 # merge, report) on the post stream while the next query scans
-# (PM_POST_STREAM=1 / 2) vs on the scan's stream (0, default); parity first
+# (PM_POST_STREAM=1 / 2) vs on the scan's stream (0, default); parity first.
+# The batch half of the knob was measured slower and removed again
+# (profiles/r06af_cfg4_post_stream_ab.txt): this script now runs the same
+# code three times.
 set -o pipefail
 out=gpurun_out/postb
 mkdir -p $out

@@ -407,6 +407,8 @@ constexpr int ES_CHUNK = 16;     // positions staged per refill of a thread's wi
 constexpr int ES_THREADS = 256;  // walk threads per block (4 waves: the block's tables in LDS serve them all)
 constexpr int ES_SPAN = 16;      // window starts whose pieces one shift-and pass finds
 constexpr size_t ES_TAB_LDS = 16 << 10;   // compact tables kept in LDS up to this size
+constexpr size_t ES_SLOTS_LDS = 4 << 10;  // slots kept in LDS up to this size
+static_assert(sizeof(EsSlot) % 8 == 0, "k_es_walk copies the slots in 8-byte words");
 
 // A thread's text window: the codes (es_upload) of the line-bounded bytes of
 // positions [lo, hi) in an LDS ring of win (a power of two) bytes.  The walk
@@ -818,6 +820,15 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         for (uint32_t q = threadIdx.x; q < P.tab_words; q += blockDim.x) lt[q] = P.tab[q];
         tab = lt;
     }
+    // the slots too (a few hundred bytes each): every cluster's walk reads
+    // its slot's fields, a chain of global loads otherwise
+    const EsSlot* slots = P.slots;
+    if (P.slots_lds) {
+        uint64_t* ls = reinterpret_cast<uint64_t*>(es_lds + P.slots_off);
+        const uint64_t* gs = reinterpret_cast<const uint64_t*>(P.slots);
+        for (uint32_t q = threadIdx.x; q < (uint32_t)P.nslots * (uint32_t)(sizeof(EsSlot) / 8); q += blockDim.x) ls[q] = gs[q];
+        slots = reinterpret_cast<const EsSlot*>(ls);
+    }
     __syncthreads();
     // the thread's rank lane * waves + wave: consecutive entries of a block
     // go to different waves
@@ -832,7 +843,7 @@ __global__ __launch_bounds__(ES_THREADS) void k_es_walk(EsPrep P, uint64_t* __re
         uint64_t nout = 0;
         const int64_t slot = (int64_t)pid - P.pid_base;
         if (slot >= 0 && slot < P.nslots) {
-            const EsSlot& S = P.slots[slot];
+            const EsSlot& S = slots[slot];
             // the cluster's region [R0, n): its search starts at R0 and the
             // text ends at n for it (reads past it see a break)
             uint64_t R0 = 0, n = tv.n;
@@ -1055,13 +1066,17 @@ void es_launch(const EsPrep& P0, uint64_t* keys, uint32_t* lens, const uint64_t*
     while (win < (uint32_t)P.gap_max + ES_SPAN + 32) win <<= 1;
     // wider patterns read memory directly (a block's rings, piece words and
     // tables stay within the CU's LDS)
-    P.win = (size_t)ES_THREADS * win + (size_t)ES_THREADS * ES_SPAN * 8 + ES_TAB_LDS + 256 <= (160u << 10) ? win : 0;
+    P.win = (size_t)ES_THREADS * win + (size_t)ES_THREADS * ES_SPAN * 8 + ES_TAB_LDS + 256 + ES_SLOTS_LDS <= (160u << 10) ? win : 0;
     P.dl_off = ES_THREADS * P.win;  // then ES_SPAN piece words per thread
     // then the compact tables (up to ES_TAB_LDS bytes) and the code map
     P.tab_off = P.dl_off + ES_THREADS * ES_SPAN * 8;
     P.tab_lds = (size_t)P.tab_words * 8 <= ES_TAB_LDS ? 1 : 0;
     P.map_off = P.tab_off + (P.tab_lds ? P.tab_words * 8 : 0);
-    const size_t lds = P.map_off + 256;
+    // then the slots, when they are few (PM_ES_SLOTS_LDS=0: global, A/B)
+    static const bool slots_env = !(getenv("PM_ES_SLOTS_LDS") && getenv("PM_ES_SLOTS_LDS")[0] == '0');
+    P.slots_off = P.map_off + 256;
+    P.slots_lds = slots_env && (size_t)P.nslots * sizeof(EsSlot) <= ES_SLOTS_LDS ? 1 : 0;
+    const size_t lds = P.slots_off + (P.slots_lds ? (size_t)P.nslots * sizeof(EsSlot) : 0);
     // a cluster's walk is a chain of dependent steps, so as many waves as
     // the registers allow: blocks of ES_THREADS share the tables in LDS, all
     // resident, striding over the walk list (its length is on the device)

@@ -1082,6 +1082,8 @@ struct EsPrep {
     uint32_t win = 0;       // k_es_walk's per-thread text ring (bytes, a power of two; 0: none)
     uint32_t tab_off = 0, map_off = 0;   // k_es_walk's LDS: the compact tables, the code map
     int tab_lds = 0;        // the tables are read from LDS
+    uint32_t slots_off = 0; // k_es_walk's LDS copy of the slots (slots_lds)
+    int slots_lds = 0;      // the slots are read from LDS
 };
 // Deletions with k >= m (the whole pattern may be deleted): every position
 // can be reported, so the walk takes every position as a key and each line

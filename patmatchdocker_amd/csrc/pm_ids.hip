@@ -161,6 +161,17 @@ bool ids_keep() {
     return e && e[0] == '1';
 }
 
+// PM_IDS_BRKSPLIT=0 (A/B): a step whose words hold an exception masks every
+// new state register with the break mask (45 more VALU ops at the bench's
+// m = 15, k = 2) whether or not a line break is among them.  Default: that
+// step tests the wave's break bits first and takes the masked update only
+// when some lane's word holds a break (rare: N runs and IUPAC letters are
+// the common exceptions; breaks come once per line)
+bool ids_brk_split() {
+    static const bool on = !(getenv("PM_IDS_BRKSPLIT") && getenv("PM_IDS_BRKSPLIT")[0] == '0');
+    return on;
+}
+
 // The kernel's source and its cache signature (everything the source
 // depends on); with want_source false only the signature (a query's cache
 // lookup: generating the source cost ~0.1 ms per query).
@@ -187,7 +198,8 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     std::ostringstream sg;
     const int WPL = ids_wpl(WU);
     const bool keep = sp.keep && WPL == 32 && WU >= 1;   // lane c's warm-up column is lane c + 1's
-    sg << "ids12:" << WPL << ":" << (keep ? 1 : 0) << ":" << m << ":" << k << ":" << sp.errs << ":";
+    const bool brk_split = ids_brk_split();
+    sg << "ids13:" << WPL << ":" << (keep ? 1 : 0) << ":" << (brk_split ? 1 : 0) << ":" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) {
         sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
         if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
@@ -291,6 +303,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
               << in << "    const uint2* " << pv << " = pn + (long)((u_ & 31u) * s1 + (u_ >> 5) * s2);\n";
         o << in << "    const u32 sl_ = sl;\n";
         o << in << "    ++qs; sl = sl + 1u == IDS_SLOTS ? 0u : sl + 1u; snx = snx + 1u == IDS_SLOTS ? 0u : snx + 1u;\n";
+        if (brk_split) o << in << "    bool killed_ = false;\n";
         for (size_t c = 0; c < rep.size(); ++c) {
             const PosClass& p = pc[rep[c]];
             if (p.any) o << in << "    u32 M" << c << " = 0xffffffffu;\n";
@@ -321,10 +334,24 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
               << c << " & ~(1u << b));\n";
         o << in << "            }\n";
         o << in << "        }\n";
-        update(o, src, dst, true, in + "        ");
-        o << in << "    } else {\n";
-        update(o, src, dst, false, in + "        ");
-        o << in << "    }\n";
+        if (brk_split) {
+            // only a break kills: without one in any lane's word the
+            // exception step takes the plain update below with the adjusted
+            // classes (one copy of each update, as without the split)
+            o << in << "        if (__builtin_amdgcn_ballot_w64(e.x != 0u)) {   // wave-uniform: a line break\n";
+            update(o, src, dst, true, in + "            ");
+            o << in << "            killed_ = true;\n";
+            o << in << "        }\n";
+            o << in << "    }\n";
+            o << in << "    if (!killed_) {\n";
+            update(o, src, dst, false, in + "        ");
+            o << in << "    }\n";
+        } else {   // (the round-5 form)
+            update(o, src, dst, true, in + "        ");
+            o << in << "    } else {\n";
+            update(o, src, dst, false, in + "        ");
+            o << in << "    }\n";
+        }
         if (emit) {
             o << in << "    u32 em = 0u";
             for (int j = 0; j <= k; ++j) o << " | " << V(dst, j, 0);

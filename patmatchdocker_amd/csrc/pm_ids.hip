@@ -69,11 +69,19 @@ __device__ inline u64 phys(u64 tile, u32 w) {
 // lds + 4 lane, the lo plane's at lds + 256 + 4 lane (no VGPR destination;
 // waited for with vmcnt).  Inline asm, so that the compiler's own wait
 // bookkeeping does not drain the loads in flight.
+#if IDS_M0_CLOBBER
+// m0 declared clobbered: the compiler keeps nothing in it across the DMA
+// (no save / restore around each of a step's four DMAs)
+__device__ __forceinline__ void dma_dword(u64 ga, u32 lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" : : "v"(ga), "s"(lds) : "memory", "m0");
+}
+#else
 __device__ __forceinline__ void dma_dword(u64 ga, u32 lds) {
     u32 keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(ga), "s"(lds) : "memory");
 }
+#endif
 // a step's word of both planes: {hi, lo} at lds, lds + 256 and the
 // exception plane's {brk, oth} at lds + 512, lds + 768 (4 lane-linear dwords).
 // A row with no break or "other" byte in any lane (`ex` false, wave-uniform)
@@ -167,6 +175,13 @@ bool ids_keep() {
 // step tests the wave's break bits first and takes the masked update only
 // when some lane's word holds a break (rare: N runs and IUPAC letters are
 // the common exceptions; breaks come once per line)
+// PM_IDS_M0=0 (A/B): each LDS-DMA saves and restores m0 around itself (the
+// round-5 form); default: m0 is a declared clobber of the DMA's asm
+bool ids_m0_clobber() {
+    static const bool on = !(getenv("PM_IDS_M0") && getenv("PM_IDS_M0")[0] == '0');
+    return on;
+}
+
 bool ids_brk_split() {
     static const bool on = !(getenv("PM_IDS_BRKSPLIT") && getenv("PM_IDS_BRKSPLIT")[0] == '0');
     return on;
@@ -199,7 +214,8 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     const int WPL = ids_wpl(WU);
     const bool keep = sp.keep && WPL == 32 && WU >= 1;   // lane c's warm-up column is lane c + 1's
     const bool brk_split = ids_brk_split();
-    sg << "ids13:" << WPL << ":" << (keep ? 1 : 0) << ":" << (brk_split ? 1 : 0) << ":" << m << ":" << k << ":" << sp.errs << ":";
+    const bool m0c = ids_m0_clobber();
+    sg << "ids13:" << WPL << ":" << (keep ? 1 : 0) << ":" << (brk_split ? 1 : 0) << (m0c ? "c" : "s") << ":" << m << ":" << k << ":" << sp.errs << ":";
     for (int i = 0; i < m; ++i) {
         sg << (pc[i].any ? '.' : (char)('a' + pc[i].acgt));
         if (!pc[i].any && ((sp.byte_mask[(uint8_t)'N'] >> i) & 1)) sg << 'N';   // the class takes N
@@ -365,6 +381,7 @@ std::string gen_ids_source(const IdsSpec& sp, std::string* sig, bool want_source
     };
 
     std::ostringstream o;
+    o << "#define IDS_M0_CLOBBER " << (m0c ? 1 : 0) << "\n";
     o << kIdsCommon;
     o << "#define WU " << WU << "\n";
     // keep: the warm-up words' planes stay in LDS for the lane that owns

@@ -1278,6 +1278,13 @@ bool jit_rotate() {
     return !(e && e[0] == '0');
 }
 
+// PM_JIT_M0=0 (A/B): the tile DMAs save and restore m0 around themselves
+// (the round-5 form); default: m0 is a declared clobber of the DMA's asm
+bool jit_m0() {
+    static const bool on = !(getenv("PM_JIT_M0") && getenv("PM_JIT_M0")[0] == '0');
+    return on;
+}
+
 // PM_JIT_CLOCK=1 (measurement only): every workgroup of pm_linear_jit reads
 // the shader clock counter (s_memtime) and the 100 MHz real-time counter
 // (s_memrealtime) at its start and end, and the library prints per launch
@@ -1358,7 +1365,8 @@ std::string gen_linear_source(int P, int K, const int32_t* lengths, const uint8_
     std::ostringstream o;
     o << kJitCommon;
     o << "#define P " << P << "\n#define K " << K << "\n#define REC_LDS " << JIT_REC_LDS << "\n#define STEPS "
-      << JIT_STEPS << "\n#define NW " << PARTS << "\n#define JIT_CLOCK " << (jit_clock() ? 1 : 0) << "\n";
+      << JIT_STEPS << "\n#define NW " << PARTS << "\n#define JIT_CLOCK " << (jit_clock() ? 1 : 0)
+      << "\n#define JIT_M0_CLOBBER " << (jit_m0() ? 1 : 0) << "\n";
     auto word_off = [&](int i) {   // physical word of logical word 32 lane + i, relative to the tile
         std::ostringstream s;
         if (i < LANE_WORDS) s << (i * 64) << " + lane";
@@ -1519,9 +1527,14 @@ __device__ __forceinline__ void stage(const JArgs& a, u32 dst0, u64 tile, u64 te
     if ((q + (int)wid + 1) * 1024 > LOAD_BYTES && lane * 16 >= LOAD_BYTES % 1024) continue;   // partial last piece
     const u32 dst = __builtin_amdgcn_readfirstlane(dst0 + (q + wid) * 1024);
     const unsigned char* pb = tb + (q + wid) * 1024;
+#if JIT_M0_CLOBBER   // m0 a declared clobber: no save / restore around the DMA
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(pb), "s"(dst)
+                 : "memory", "m0");
+#else
     u32 keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(pb), "s"(dst) : "memory");
+#endif
   }
 }
 #if PF_STRIDE
@@ -1713,7 +1726,7 @@ hipFunction_t jit_function(int device, int P, int K, const int32_t* lengths, con
                            const uint8_t* class_acgt, const uint8_t* class_is_any) {
     const int parts = jit_parts();
     const auto key = std::make_pair(device, std::to_string(parts) + (jit_rotate() ? "r/" : "f/") +
-                                                (jit_clock() ? "c/" : "") + "pf" + std::to_string(jit_prefetch()) + "/" +
+                                                (jit_clock() ? "c/" : "") + (jit_m0() ? "" : "m0s/") + "pf" + std::to_string(jit_prefetch()) + "/" +
                                                 jit_signature(P, K, lengths, pos_class, class_acgt, class_is_any));
     std::lock_guard<std::mutex> lk(g_jit_mu);
     auto it = g_jit_cache.find(key);

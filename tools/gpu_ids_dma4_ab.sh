@@ -1,4 +1,6 @@
 #!/bin/bash
+# (The PM_IDS_DMA4 generator form was measured slower and removed again,
+# profiles/r06ak_ids_dma4_ab.txt: this script now runs the same code.)
 # A/B (round 6): pm_ids_rev's own-column steps fed by one row DMA
 # (PM_IDS_DMA4=1, with PM_IDS_BRKSPLIT=0: 121 VGPRs; with the split it
 # spills) vs the default (dword DMAs, break split) vs neither; parity tests

@@ -135,6 +135,6 @@ def test_flag_values_match_the_header():
     text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                              "patmatch_hip.h")).read()
     for name in ("PM_REPORT_NRGREP", "PM_KEEP_HEADERS", "PM_CROSS_LINES", "PM_ESIMPLE", "PM_EXTENDED",
-                 "PM_SCAN_BYTES"):
+                 "PM_SCAN_BYTES", "PM_REGULAR", "PM_PIPELINED"):
         m = re.search(r"#define %s (\d+)" % name, text)
         assert m and int(m.group(1)) == getattr(_lib, name), name
